@@ -1,0 +1,83 @@
+"""Readers for the golden fixtures in tests/golden/ (written by make_golden.py)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+AGENT_KEYS = ["old_rep", "this_rep", "smooth_rep", "na_row", "participation_rows",
+              "relative_part", "reporter_bonus", "scores"]
+EVENT_KEYS = ["adj_first_loadings", "outcomes_raw", "consensus_reward", "certainty",
+              "NAs Filled", "participation_columns", "author_bonus",
+              "outcomes_adjusted", "outcomes_final"]
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
+
+
+def split_cases(flat):
+    """{'case/key': v} -> {case: {key: v}}"""
+    out = {}
+    for k, v in flat.items():
+        c, kk = k.split("/", 1)
+        out.setdefault(c, {})[kk] = v
+    return out
+
+
+def unstack(st, b):
+    return {k: v[b] for k, v in st.items()}
+
+
+def kat():
+    return split_cases(load("kat.npz"))
+
+
+def mixed():
+    return split_cases(load("synth_mixed.npz"))
+
+
+def synth():
+    return load("synth_50x20.npz")
+
+
+def c2():
+    return load("c2_1000x100.npz")
+
+
+def oracle_args(case):
+    """Constructor kwargs equivalent to the ones the reference was run with."""
+    R = case["in_reports"]
+    if bool(case["in_int_dtype"]):
+        R = R.astype(np.int64)
+    kw = dict(reports=R)
+    if bool(case["in_has_bounds"]):
+        kw["event_bounds"] = [{"scaled": bool(s), "min": float(a), "max": float(b)}
+                              for s, a, b in zip(case["in_scaled"], case["in_lo"], case["in_hi"])]
+    if bool(case["in_has_rep"]):
+        kw["reputation"] = case["in_reputation"]
+    kw["catch_tolerance"] = float(case["in_catch_tolerance"])
+    kw["alpha"] = float(case["in_alpha"])
+    kw["algorithm"] = str(case["in_algorithm"])
+    return kw
+
+
+def flat_result(res):
+    """Result dict -> {key: float64 array}, same keys as the fixtures."""
+    f = lambda v: np.asarray(np.ma.filled(np.ma.asarray(v, dtype=np.float64), np.nan), dtype=np.float64)
+    d = {"original": f(res["original"]), "filled": f(np.asarray(res["filled"]))}
+    for k in AGENT_KEYS:
+        d["agents." + k] = f(res["agents"][k])
+    for k in EVENT_KEYS:
+        d["events." + k] = f(res["events"][k])
+    d["participation"] = f(res["participation"])
+    d["avg_certainty"] = f(res["avg_certainty"])
+    d["convergence"] = np.array(bool(res["convergence"]))
+    d["components"] = np.array(int(res["components"]))
+    return d
+
+
+# keys whose sign follows the eigenvector sign (LAPACK-defined, quirk Q8)
+SIGNED_KEYS = ("agents.scores", "events.adj_first_loadings")
