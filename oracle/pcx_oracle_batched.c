@@ -1,0 +1,555 @@
+/*
+ * pcx_oracle_batched.c -- CPU restatement of the batched consensus round.
+ *
+ * TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.  Built into
+ * oracle/lib/libpcx_oracle.so and loaded (ctypes) only by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg.  libpcx never links it.
+ *
+ * It restates, one round at a time, pyconsensus Oracle(...).consensus() with the
+ * default algorithm="PCA" (pyconsensus/__init__.py:102-611), with the arithmetic
+ * order written down explicitly (SPEC comments) so that the GPU batched kernel
+ * (pyconsensus_amd/csrc/pcx_batched.hip) can be checked against it bit for bit:
+ *
+ *   - where the reference's order is defined by Python/numpy (sequential Python
+ *     loops, builtin sum, numpy pairwise add.reduce, elementwise ops) this file
+ *     replays that exact order, so those steps agree bit-for-bit with the
+ *     reference too;
+ *   - where the reference calls BLAS (np.dot, dgemm) or LAPACK (svd) the order is
+ *     OpenBLAS/LAPACK-internal; here it is a fixed sequential-FMA order and the
+ *     leading eigenvector comes from power iteration.  Those steps agree with the
+ *     reference to rounding (checked against tests/golden/ with tolerances, and
+ *     near-tie rounds reported separately).
+ *
+ * Compiled with -ffp-contract=off: every fma() below is deliberate.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+
+#include "../include/pcx.h"
+
+#define NMAX 64
+#define EMAX 64
+#define ES (EMAX + 1)
+
+/* power iteration constants -- must equal pcx_batched.hip */
+#define PI_TOL 1e-14
+#define PI_MAXIT 256
+#define PI_PRESQUARE 3
+#define PI_SQUARE_EVERY 32
+#define PI_MAX_SQUARINGS 8
+#define PI_POLISH 4
+
+/* numpy pairwise summation (umath loops_utils pairwise_sum, PW_BLOCKSIZE 128),
+ * as np.add.reduce uses it for a contiguous 1-D array of <= 8192 elements. */
+static double pw_sum(const double* a, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; i++) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int k = 0; k < 8; k++) r[k] = a[k];
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int k = 0; k < 8; k++) r[k] += a[i + k];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_sum(a, n2) + pw_sum(a + n2, n - n2);
+}
+
+/* SPEC tree64: butterfly over 64 slots (zero padded), xor distance 32..1. */
+static double tree64(const double* a, int n) {
+    double t[64], u[64];
+    for (int i = 0; i < 64; i++) t[i] = i < n ? a[i] : 0.0;
+    for (int s = 32; s >= 1; s >>= 1) {
+        for (int i = 0; i < 64; i++) u[i] = t[i] + t[i ^ s];
+        memcpy(t, u, sizeof t);
+    }
+    return t[0];
+}
+
+/* SPEC dot2: compensated dot product (Ogita-Rump-Oishi Dot2: TwoProduct by fma,
+ * TwoSum), summed in index order.  Used for the GEMVs whose results feed the
+ * discontinuous decisions (ranks, catch): the reference's np.dot is OpenBLAS
+ * dgemv, whose summation order is BLAS-internal; a nearly correctly rounded dot
+ * reproduces every decision that does not hinge on BLAS rounding. */
+static double dot2(const double* a, int sa, const double* b, int sb, int n) {
+    double s = 0.0, c = 0.0;
+    for (int i = 0; i < n; i++) {
+        double x = a[(int64_t)i * sa], y = b[(int64_t)i * sb];
+        double p = x * y;
+        double pe = fma(x, y, -p);
+        double t = s + p;
+        double z = t - s;
+        double se = (s - (t - z)) + (p - z);
+        s = t;
+        c = c + (pe + se);
+    }
+    return s + c;
+}
+
+static double catch_(double x, double tol) {  /* __init__.py:251-258 */
+    if (x < 1.5 - tol) return 1.0;
+    if (x > 1.5 + tol) return 2.0;
+    return 1.5;
+}
+
+static void normalize_(const double* v, int n, double* out) {  /* __init__.py:244-249 */
+    double a[NMAX > EMAX ? NMAX : EMAX];
+    for (int i = 0; i < n; i++) a[i] = fabs(v[i]);
+    double s = pw_sum(a, n);
+    if (s == 0) {
+        for (int i = 0; i < n; i++) a[i] += 1.0;
+        s = pw_sum(a, n);
+    }
+    for (int i = 0; i < n; i++) out[i] = a[i] / s;
+}
+
+/* weightedstats.weighted_median restated (see oracle/pcx_oracle.py). */
+static double wmedian(const double* x, const double* w, int n) {
+    double W = 0.0;
+    for (int i = 0; i < n; i++) W += w[i];
+    double mid = 0.5 * W;
+    int dom = 0;
+    for (int i = 0; i < n; i++) dom |= w[i] > mid;
+    if (dom) {
+        double m = w[0];
+        for (int i = 1; i < n; i++) if (w[i] > m) m = w[i];
+        for (int i = 0; i < n; i++) if (w[i] == m) return x[i];
+        return NAN;
+    }
+    int pos = 0;
+    for (int i = 0; i < n; i++) pos |= w[i] > 0;
+    if (!pos) return NAN;
+    double xs[NMAX], ws[NMAX];
+    for (int i = 0; i < n; i++) {  /* stable rank by (x, w) */
+        int r = 0;
+        for (int m = 0; m < n; m++) {
+            int lt = (x[m] < x[i]) || (x[m] == x[i] && w[m] < w[i]);
+            int eq = (x[m] == x[i]) && (w[m] == w[i]);
+            r += lt || (eq && m < i);
+        }
+        xs[r] = x[i];
+        ws[r] = w[i];
+    }
+    double cum = 0.0;
+    int k = 0;
+    while (cum <= mid) {
+        if (k == n) return NAN; /* the reference raises IndexError here */
+        cum += ws[k];
+        k++;
+    }
+    double before = cum - ws[k - 1];
+    if (fabs(before - mid) < DBL_EPSILON) {
+        if (k >= 2) return (xs[k - 2] + xs[k - 1]) / 2.0;
+        if (n == 1) return xs[0] / 1.0;
+        return NAN; /* empty slice: ZeroDivisionError in the reference */
+    }
+    return xs[k - 1];
+}
+
+static void rank_avg(const double* v, int n, double* r) {  /* scipy.stats.rankdata 'average' */
+    for (int j = 0; j < n; j++) {
+        int lt = 0, eq = 0;
+        for (int k = 0; k < n; k++) {
+            lt += v[k] < v[j];
+            eq += v[k] == v[j];
+        }
+        r[j] = (double)lt + (double)(eq + 1) * 0.5;
+    }
+}
+
+/* SPEC: M <- (M*M) / max|M*M|, products as sequential fma over the inner index */
+static void square_scaled(double (*M)[ES], int E) {
+    static __thread double T[EMAX][ES];
+    double mx = 0.0;
+    for (int j = 0; j < E; j++)
+        for (int k = 0; k < E; k++) {
+            double acc = 0.0;
+            for (int l = 0; l < E; l++) acc = fma(M[j][l], M[l][k], acc);
+            T[j][k] = acc;
+            double a = fabs(acc);
+            if (a > mx) mx = a;
+        }
+    for (int j = 0; j < E; j++)
+        for (int k = 0; k < E; k++) M[j][k] = mx > 0.0 ? T[j][k] / mx : T[j][k];
+}
+
+static void matvec_unit(const double (*M)[ES], int E, const double* x, double* y) {
+    double sq[EMAX];
+    for (int j = 0; j < E; j++) {
+        double acc = 0.0;
+        for (int k = 0; k < E; k++) acc = fma(M[j][k], x[k], acc);
+        y[j] = acc;
+        sq[j] = acc * acc;
+    }
+    double nrm = sqrt(tree64(sq, E));
+    for (int j = 0; j < E; j++) y[j] = y[j] / nrm;
+}
+
+/* SPEC power iteration -> unit leading eigenvector of C (replaces svd(C)[0][:,0],
+ * __init__.py:330).  Returns steps taken; sets flags. */
+static int power_iter(const double (*C)[ES], int E, double* v, int* flags) {
+    int finite = 1, nonzero = 0;
+    for (int j = 0; j < E; j++)
+        for (int k = 0; k < E; k++) {
+            finite &= isfinite(C[j][k]) != 0;
+            nonzero |= C[j][k] != 0.0;
+        }
+    if (!finite) {  /* LAPACK raises -> H = ones (:331-333) */
+        for (int j = 0; j < E; j++) v[j] = 1.0;
+        *flags |= PCX_FLAG_SVD_FAIL;
+        return 0;
+    }
+    if (!nonzero) {  /* svd(0) returns U = I: first column e_0 */
+        for (int j = 0; j < E; j++) v[j] = j == 0 ? 1.0 : 0.0;
+        *flags |= PCX_FLAG_ZERO_COV;
+        return 0;
+    }
+    static __thread double M[EMAX][ES];
+    int kd = 0;
+    for (int j = 1; j < E; j++) if (C[j][j] > C[kd][kd]) kd = j;
+    double x[EMAX], y[EMAX], sq[EMAX];
+    for (int j = 0; j < E; j++) {
+        x[j] = C[j][kd];
+        sq[j] = x[j] * x[j];
+    }
+    double nrm = sqrt(tree64(sq, E));
+    for (int j = 0; j < E; j++) x[j] = x[j] / nrm;
+    for (int j = 0; j < E; j++) memcpy(M[j], C[j], sizeof(double) * E);
+    int sqn = 0;
+    for (; sqn < PI_PRESQUARE; sqn++) square_scaled(M, E);
+    int it = 0, since = 0;
+    for (;;) {
+        matvec_unit((const double (*)[ES])M, E, x, y);
+        double d = 0.0;
+        for (int j = 0; j < E; j++) {
+            double a = fabs(y[j] - x[j]);
+            if (a > d) d = a;
+            x[j] = y[j];
+        }
+        it++;
+        since++;
+        if (d <= PI_TOL) break;
+        if (it >= PI_MAXIT) {
+            *flags |= PCX_FLAG_PI_MAXIT;
+            break;
+        }
+        if (since >= PI_SQUARE_EVERY && sqn < PI_MAX_SQUARINGS) {
+            square_scaled(M, E);
+            sqn++;
+            since = 0;
+        }
+    }
+    for (int p = 0; p < PI_POLISH; p++) {
+        matvec_unit(C, E, x, y);
+        memcpy(x, y, sizeof(double) * E);
+    }
+    /* SPEC sign (the reference's is whatever LAPACK gesdd returns): measured on
+     * the golden set, U[:,0] has its first nonzero component negative, except
+     * when it is a unit vector e_k, which LAPACK returns as +e_k. */
+    {
+        int f = -1, nnz = 0;
+        for (int j = 0; j < E; j++)
+            if (x[j] != 0.0) {
+                nnz++;
+                if (f < 0) f = j;
+            }
+        int neg = nnz == 1 ? x[f] < 0.0 : x[f] > 0.0;
+        if (neg)
+            for (int j = 0; j < E; j++) x[j] = -x[j];
+    }
+    memcpy(v, x, sizeof(double) * E);
+    return it + PI_POLISH + sqn;
+}
+
+#define OUT(p, idx, val) do { if (p) (p)[idx] = (val); } while (0)
+
+static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
+    const int N = (int)in->n_reporters, E = (int)in->n_events;
+    const double* Rin = in->reports + b * N * E;
+    const int has_bounds = in->scaled != NULL;
+    const int64_t bo = in->bounds_shared ? 0 : b * E;
+    double X[NMAX][ES], F[NMAX][ES];
+    double rep[NMAX], tok[NMAX];
+    unsigned char isnan_[NMAX][EMAX], iszero[NMAX][EMAX];
+    int scaled[EMAX];
+    double lo[EMAX], hi[EMAX];
+    for (int j = 0; j < E; j++) {
+        scaled[j] = has_bounds ? in->scaled[bo + j] != 0 : 0;
+        lo[j] = has_bounds ? in->lo[bo + j] : 0.0;
+        hi[j] = has_bounds ? in->hi[bo + j] : 0.0;
+    }
+    /* --- a1: reputation (__init__.py:138-146) --- */
+    if (in->reputation) {
+        const double* rr = in->reputation + b * N;
+        double tot = pw_sum(rr, N);
+        for (int i = 0; i < N; i++) rep[i] = rr[i] / tot;
+    } else {
+        for (int i = 0; i < N; i++) rep[i] = 1.0 / (double)N;
+    }
+    double sumtok = 0.0;
+    for (int i = 0; i < N; i++) {
+        tok[i] = trunc(rep[i] * 1e6);
+        sumtok += tok[i];
+    }
+    const double denom = sumtok - 1.0;
+    /* --- a2: rescale (:266-269), NA detection (:278) --- */
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < E; j++) {
+            double x = Rin[(int64_t)i * E + j];
+            if (scaled[j]) {
+                x = (x - lo[j]) / (hi[j] - lo[j]);
+                if (in->int_dtype) x = trunc(x);
+            }
+            X[i][j] = x;
+            isnan_[i][j] = isnan(x) != 0;
+            iszero[i][j] = x == 0.0;
+            OUT(out->original, (b * N + i) * E + j, x);
+        }
+    /* --- a3: interpolate (:284-313) --- */
+    for (int i = 0; i < N; i++) memcpy(F[i], X[i], sizeof(double) * E);
+    for (int j = 0; j < E; j++) {
+        int nmiss = 0;
+        for (int i = 0; i < N; i++) nmiss += isnan_[i][j] | iszero[i][j];
+        if (!nmiss) continue;
+        double tot = 0.0;
+        int np_ = 0;
+        double xp[NMAX], wp[NMAX];
+        for (int i = 0; i < N; i++)
+            if (!(isnan_[i][j] | iszero[i][j])) {
+                tot += rep[i];
+                xp[np_++] = X[i][j];
+            }
+        double g;
+        if (scaled[j]) {
+            int m = 0;
+            for (int i = 0; i < N; i++)
+                if (!(isnan_[i][j] | iszero[i][j])) wp[m++] = rep[i] / tot;
+            g = wmedian(xp, wp, np_);
+        } else {
+            g = 0.0;
+            int m = 0;
+            for (int i = 0; i < N; i++)
+                if (!(isnan_[i][j] | iszero[i][j])) g += (rep[i] / tot) * xp[m++];
+            g = catch_(g, in->catch_tolerance);
+        }
+        if (in->int_dtype) g = trunc(g);
+        for (int i = 0; i < N; i++)
+            if (isnan_[i][j] | iszero[i][j]) F[i][j] = g;
+    }
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < E; j++) OUT(out->filled, (b * N + i) * E + j, F[i][j]);
+
+    double loading[EMAX], s[NMAX], nc[NMAX];
+    int flags = 0, iters = 0, branch = PCX_BRANCH_NONE;
+    double old[EMAX];
+    for (int j = 0; j < E; j++) old[j] = dot2(rep, 1, &F[0][j], ES, N);  /* np.dot(rep, F) */
+    if (in->algorithm == 0) {
+        /* --- a5: weighted mean (np.ma.average, :317-319) --- */
+        double mu[EMAX];
+        double den = pw_sum(rep, N);
+        for (int j = 0; j < E; j++) {
+            double acc;
+            if (E == 1) {
+                double p[NMAX];
+                for (int i = 0; i < N; i++) p[i] = F[i][j] * rep[i];
+                acc = pw_sum(p, N);
+            } else {
+                acc = F[0][j] * rep[0];
+                for (int i = 1; i < N; i++) acc = acc + F[i][j] * rep[i];
+            }
+            mu[j] = acc / den;
+        }
+        /* --- a6: token-weighted covariance (:326), lower triangle, mirrored --- */
+        static __thread double C[EMAX][ES];
+        for (int j = 0; j < E; j++)
+            for (int k = 0; k <= j; k++) {
+                double acc = 0.0;
+                for (int i = 0; i < N; i++) acc = fma((F[i][j] - mu[j]) * tok[i], F[i][k] - mu[k], acc);
+                C[j][k] = acc / denom;
+                C[k][j] = C[j][k];
+            }
+        /* --- a7: leading eigenvector (:330-336), scores (:337) --- */
+        double v[EMAX], sq[EMAX];
+        iters = power_iter((const double (*)[ES])C, E, v, &flags);
+        for (int j = 0; j < E; j++) sq[j] = v[j] * v[j];
+        double nv = sqrt(pw_sum(sq, E));
+        for (int j = 0; j < E; j++) loading[j] = v[j] / nv;
+        for (int i = 0; i < N; i++) {
+            double acc = 0.0;
+            for (int j = 0; j < E; j++) acc = fma(F[i][j] - mu[j], loading[j], acc);
+            s[i] = acc;
+        }
+        /* --- a8/a9: nonconformity_rank (:487-500), tie -> nonconformity (:475-485) --- */
+        double mn = s[0], mx = s[0];
+        for (int i = 1; i < N; i++) {  /* NaN propagates like np.min / np.max */
+            if (isnan(s[i]) || s[i] < mn) mn = isnan(mn) ? mn : s[i];
+            if (isnan(s[i]) || s[i] > mx) mx = isnan(mx) ? mx : s[i];
+        }
+        double set1[NMAX], set2[NMAX], n1[NMAX], n2[NMAX];
+        for (int i = 0; i < N; i++) {
+            set1[i] = s[i] + fabs(mn);
+            set2[i] = s[i] - mx;
+        }
+        normalize_(set1, N, n1);
+        normalize_(set2, N, n2);
+        double d1[EMAX], d2[EMAX], new1[EMAX], new2[EMAX], r0[EMAX], r1[EMAX], r2[EMAX];
+        for (int j = 0; j < E; j++) {
+            double a1 = dot2(n1, 1, &F[0][j], ES, N);
+            double a2 = dot2(n2, 1, &F[0][j], ES, N);
+            d1[j] = a1;
+            d2[j] = a2;
+            double t = 0.01 * old[j];
+            new1[j] = a1 + t;
+            new2[j] = a2 + t;
+        }
+        rank_avg(old, E, r0);
+        rank_avg(new1, E, r1);
+        rank_avg(new2, E, r2);
+        double e1[EMAX], e2[EMAX];
+        for (int j = 0; j < E; j++) {
+            e1[j] = fabs(r1[j] - r0[j]);
+            e2[j] = fabs(r2[j] - r0[j]);
+        }
+        double ref = pw_sum(e1, E) - pw_sum(e2, E);
+        int pick1;
+        if (ref == 0) {
+            for (int j = 0; j < E; j++) {
+                double a = d1[j] - old[j], c = d2[j] - old[j];
+                e1[j] = a * a;
+                e2[j] = c * c;
+            }
+            double ref2 = pw_sum(e1, E) - pw_sum(e2, E);
+            pick1 = ref2 <= 0;
+            branch = pick1 ? PCX_BRANCH_TIE_SET1 : PCX_BRANCH_TIE_SET2;
+        } else {
+            pick1 = ref < 0;
+            branch = pick1 ? PCX_BRANCH_SET1 : PCX_BRANCH_SET2;
+        }
+        for (int i = 0; i < N; i++) nc[i] = pick1 ? set1[i] : set2[i];
+    } else {  /* "absolute": nc = 0, no loading (Q13) */
+        for (int j = 0; j < E; j++) loading[j] = 0.0;
+        for (int i = 0; i < N; i++) s[i] = nc[i] = 0.0;
+    }
+    /* --- a10: reputation update (:460-472) --- */
+    double meanrep = pw_sum(rep, N) / (double)N;
+    double u[NMAX], this_[NMAX], smooth[NMAX];
+    for (int i = 0; i < N; i++) u[i] = nc[i] * (rep[i] / meanrep);
+    normalize_(u, N, this_);
+    const double a = in->alpha, oma = 1.0 - in->alpha;
+    for (int i = 0; i < N; i++) smooth[i] = a * this_[i] + oma * rep[i];
+    /* --- a12/a13: outcomes (:510-538) --- */
+    double raw[EMAX], adj[EMAX], fin[EMAX], cert[EMAX];
+    for (int j = 0; j < E; j++) {
+        raw[j] = dot2(smooth, 1, &F[0][j], ES, N);
+        if (scaled[j]) {
+            double col[NMAX];
+            for (int i = 0; i < N; i++) col[i] = F[i][j];
+            raw[j] = wmedian(col, smooth, N);
+            adj[j] = raw[j];
+            fin[j] = adj[j] * (hi[j] - lo[j]);
+            fin[j] = fin[j] + lo[j];
+        } else {
+            adj[j] = catch_(raw[j], in->catch_tolerance);
+            fin[j] = adj[j];
+        }
+    }
+    /* --- a14: certainty (:540-546) --- */
+    for (int j = 0; j < E; j++) {
+        double sel[NMAX];
+        int m = 0;
+        for (int i = 0; i < N; i++)
+            if (F[i][j] == adj[j]) sel[m++] = smooth[i];
+        cert[j] = m ? pw_sum(sel, m) : NAN;
+    }
+    double reward[EMAX];
+    normalize_(cert, E, reward);
+    double avg_cert = pw_sum(cert, E) / (double)E;
+    /* --- a15: participation and bonuses (:549-581) --- */
+    double pc[EMAX], pr[NMAX], narow[NMAX], rel[NMAX], relc[EMAX];
+    for (int j = 0; j < E; j++) {
+        double na[NMAX];
+        int nz = 0;
+        for (int i = 0; i < N; i++) {
+            na[i] = (isnan_[i][j] | iszero[i][j]) ? 1.0 : 0.0;
+            nz += iszero[i][j];
+        }
+        pc[j] = 1.0 - dot2(smooth, 1, na, 1, N);
+        OUT(out->nas_filled, b * E + j, (double)nz);
+    }
+    for (int i = 0; i < N; i++) {
+        int nz = 0;
+        for (int j = 0; j < E; j++) nz += iszero[i][j];
+        narow[i] = (double)nz;
+        pr[i] = 1.0 - narow[i] / (double)E;
+    }
+    double pna = 1.0 - pw_sum(pc, E) / (double)E;
+    /* A reporter whose every report is NaN has a fully MASKED row in na_mat, so its
+     * participation_rows entry is masked: np.sum skips it, and masked arithmetic
+     * keeps the first operand's data -- relative_part = |pr| undivided and
+     * reporter_bonus = relative_part (quirk Q15, __init__.py:567,576-577). */
+    int rowmasked[NMAX];
+    for (int i = 0; i < N; i++) {
+        int nn = 0;
+        for (int j = 0; j < E; j++) nn += isnan_[i][j];
+        rowmasked[i] = nn == E;
+    }
+    {
+        double a2[NMAX];
+        for (int i = 0; i < N; i++) a2[i] = rowmasked[i] ? 0.0 : fabs(pr[i]);
+        double S = pw_sum(a2, N);
+        int bump = S == 0;
+        if (bump) {
+            for (int i = 0; i < N; i++) a2[i] = rowmasked[i] ? 0.0 : fabs(pr[i]) + 1.0;
+            S = pw_sum(a2, N);
+        }
+        for (int i = 0; i < N; i++) rel[i] = rowmasked[i] ? fabs(pr[i]) : a2[i] / S;
+    }
+    normalize_(pc, E, relc);
+    for (int i = 0; i < N; i++) {
+        const int64_t o = b * N + i;
+        OUT(out->old_rep, o, rep[i]);
+        OUT(out->this_rep, o, this_[i]);
+        OUT(out->smooth_rep, o, smooth[i]);
+        OUT(out->scores, o, s[i]);
+        OUT(out->na_row, o, narow[i]);
+        OUT(out->participation_rows, o, pr[i]);
+        OUT(out->relative_part, o, rel[i]);
+        OUT(out->reporter_bonus, o, rowmasked[i] ? rel[i] : rel[i] * pna + smooth[i] * (1.0 - pna));
+    }
+    for (int j = 0; j < E; j++) {
+        const int64_t o = b * E + j;
+        OUT(out->adj_first_loadings, o, loading[j]);
+        OUT(out->outcomes_raw, o, raw[j]);
+        OUT(out->outcomes_adjusted, o, adj[j]);
+        OUT(out->outcomes_final, o, fin[j]);
+        OUT(out->certainty, o, cert[j]);
+        OUT(out->consensus_reward, o, reward[j]);
+        OUT(out->participation_columns, o, pc[j]);
+        OUT(out->author_bonus, o, relc[j] * pna + reward[j] * (1.0 - pna));
+    }
+    OUT(out->participation, b, 1.0 - pna);
+    OUT(out->avg_certainty, b, avg_cert);
+    OUT(out->branch, b, branch);
+    OUT(out->flags, b, flags);
+    OUT(out->pi_iters, b, iters);
+}
+
+/* Host-memory restatement of pcx_consensus_batched_f64 (same structs). */
+int pcxo_consensus_batched_f64(const pcx_batch* in, pcx_batch_result* out, int n_threads) {
+    if (!in || !out || in->n_reporters < 1 || in->n_reporters > NMAX || in->n_events < 1 ||
+        in->n_events > EMAX || in->n_rounds < 0)
+        return PCX_EINVAL;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(n_threads > 0 ? n_threads : 1)
+    for (int64_t b = 0; b < in->n_rounds; b++) one_round(in, out, b);
+    return PCX_OK;
+}

@@ -1,0 +1,70 @@
+"""ctypes front-end of the C oracle (oracle/lib/libpcx_oracle.so).
+
+TEST INFRASTRUCTURE -- used only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  Same structs as the product ABI (include/pcx.h), host memory.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from pyconsensus_amd._abi import BATCH_OUTPUTS, Batch, BatchResult, out_shape, ALGORITHMS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "lib", "libpcx_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.pcxo_consensus_batched_f64.argtypes = [C.POINTER(Batch), C.POINTER(BatchResult), C.c_int]
+        _lib.pcxo_consensus_batched_f64.restype = C.c_int
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_tolerance=0.1,
+            alpha=0.1, int_dtype=False, algorithm="PCA", threads=1, want=None):
+    """Run B rounds; returns {name: array} for every output in ``want`` (default: all)."""
+    R = np.ascontiguousarray(reports, dtype=np.float64)
+    B, N, E = R.shape
+    shared = scaled is not None and np.ndim(scaled) == 1
+    keep = []
+    def cont(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a
+    sc = cont(scaled, np.uint8)
+    lo_ = cont(lo, np.float64)
+    hi_ = cont(hi, np.float64)
+    rp = cont(reputation, np.float64)
+    inp = Batch(B, N, E, _ptr(R), _ptr(rp), _ptr(sc), _ptr(lo_), _ptr(hi_), int(shared), int(bool(int_dtype)),
+                float(catch_tolerance), float(alpha), ALGORITHMS[algorithm])
+    outs = {}
+    res = BatchResult()
+    for name, kind, dt in BATCH_OUTPUTS:
+        if want is not None and name not in want:
+            continue
+        a = np.empty(out_shape(kind, B, N, E), dtype=dt)
+        outs[name] = a
+        setattr(res, name, a.ctypes.data)
+    rc = lib().pcxo_consensus_batched_f64(C.byref(inp), C.byref(res), int(threads))
+    if rc != 0:
+        raise ValueError("oracle rejected the batch (rc=%d)" % rc)
+    return outs

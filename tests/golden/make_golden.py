@@ -91,7 +91,7 @@ def _normalize(v):
     return v / np.sum(v)
 
 
-def _rank_decision(s, F, rep, dot):
+def _rank_vectors(s, F, rep, dot):
     from scipy.stats import rankdata
 
     set1 = s + abs(s.min())
@@ -100,8 +100,49 @@ def _rank_decision(s, F, rep, dot):
     r0 = rankdata(old)
     r1 = rankdata(dot(_normalize(set1), F) + 0.01 * old)
     r2 = rankdata(dot(_normalize(set2), F) + 0.01 * old)
+    return r0, r1, r2
+
+
+def _rank_decision(s, F, rep, dot):
+    r0, r1, r2 = _rank_vectors(s, F, rep, dot)
     ri = np.sum(np.abs(r1 - r0)) - np.sum(np.abs(r2 - r0))
     return 0 if ri == 0 else (1 if ri < 0 else 2)
+
+
+def _decision_full(s, F, rep, dot):
+    """1/2: rank rule picks set1/set2; 3/4: exact rank tie, continuous rule picks set1/set2."""
+    d = _rank_decision(s, F, rep, dot)
+    if d:
+        return d
+    set1 = s + abs(s.min())
+    set2 = s - s.max()
+    old = dot(rep, F)
+    e1 = dot(_normalize(set1), F) - old
+    e2 = dot(_normalize(set2), F) - old
+    if dot is _dot_exact:
+        ref = math.fsum(e1 ** 2) - math.fsum(e2 ** 2)
+    else:
+        ref = np.sum(e1 ** 2) - np.sum(e2 ** 2)
+    return 3 if ref <= 0 else 4
+
+
+def _rank_neartie(s, F, rep):
+    """The sign-choice rule depends on rounding: the three rank vectors from np.dot
+    differ from those of correctly rounded (fsum) dots, or the decision flips when
+    the dots are summed in another order."""
+    a = _rank_vectors(s, F, rep, np.dot)
+    b = _rank_vectors(s, F, rep, _dot_exact)
+    if any(not np.array_equal(x, y) for x, y in zip(a, b)):
+        return True
+    dec = _decision_full(s, F, rep, np.dot)
+    if any(_decision_full(s, F, rep, f) != dec for f in (_dot_exact, _dot_rev)):
+        return True
+    # scores are themselves BLAS/LAPACK output: the decision must survive score
+    # perturbations at the 1e-13 level, and scores rounded to 12 digits (which
+    # restores exact ties that rounding broke)
+    rng = np.random.default_rng(0)
+    trials = [np.round(s, 12)] + [s * (1.0 + 1e-13 * rng.standard_normal(s.shape)) for _ in range(6)]
+    return any(_decision_full(t, F, rep, _dot_exact) != dec for t in trials)
 
 
 def _dot_exact(w, F):
@@ -195,12 +236,15 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
     # diagnostics + near-tie flags (parity reports separate these rounds)
     if "s" in cap:
         s, F, rep = cap["s"], cap["F"], cap["rep"]
-        dec = _rank_decision(s, F, rep, np.dot)
-        alt = {_rank_decision(s, F, rep, _dot_exact), _rank_decision(s, F, rep, _dot_rev)}
-        d["branch"] = np.array(dec if not cap["fallback"] else 3)
-        d["neartie_rank"] = np.array(bool(alt != {dec}))
+        dec = _decision_full(s, F, rep, np.dot)
+        assert (dec >= 3) == cap["fallback"]
+        d["branch"] = np.array(dec)
+        # the same decision in exact arithmetic (correctly rounded dots)
+        d["branch_exact"] = np.array(_decision_full(s, F, rep, _dot_exact))
+        d["neartie_rank"] = np.array(bool(_rank_neartie(s, F, rep)))
     else:
-        d["branch"] = np.array(-1)
+        d["branch"] = np.array(5)
+        d["branch_exact"] = np.array(5)
         d["neartie_rank"] = np.array(False)
     raw = d["events.outcomes_raw"]
     tol = float(kw.get("catch_tolerance", 0.1))
@@ -208,6 +252,15 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
     scaled = d.get("in_scaled", np.zeros(E, bool))
     bin_raw = raw[~scaled]
     d["neartie_catch"] = np.array(bool(bin_raw.size and np.min(np.abs(bin_raw[:, None] - thr[None, :])) < 1e-12))
+    if "s" in cap:  # interpolation guesses of binary columns (sequential weighted means)
+        X, Fm = d["original"], cap["F"]
+        miss = np.isnan(X) | (X == 0.0)
+        for j in np.nonzero(miss.any(axis=0) & ~scaled)[0]:
+            pres = ~miss[:, j]
+            if pres.any():
+                g = math.fsum(cap["rep"][pres] * X[pres, j]) / math.fsum(cap["rep"][pres])
+                if np.min(np.abs(g - thr)) < 1e-12:
+                    d["neartie_catch"] = np.array(True)
     F = d["filled"]
     sm = d["agents.smooth_rep"]
     margins = [_median_margin(F[:, j], sm) for j in np.nonzero(scaled)[0]]
@@ -359,7 +412,8 @@ def main():
         rows.append(d)
     st = _stack(rows)
     np.savez_compressed(os.path.join(HERE, "synth_50x20.npz"), **st)
-    print("synth_50x20: branch counts", np.bincount(st["branch"].astype(int) + 1),
+    print("synth_50x20: branch counts", np.bincount(st["branch"].astype(int)),
+          "exact-arith branch differs", int(np.sum(st["branch"] != st["branch_exact"])),
           "near-ties rank/catch/median", st["neartie_rank"].sum(), st["neartie_catch"].sum(),
           st["neartie_median"].sum())
 

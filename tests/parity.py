@@ -1,0 +1,93 @@
+"""Parity comparison of a consensus result against a golden (reference) case.
+
+Tolerances (BASELINE.json north_star): discrete outputs exact; reputations,
+smooth_rep, scaled outcomes and every other continuous output within 1e-9
+relative (atol 1e-12 for entries that are ~0).  ``scores`` and
+``adj_first_loadings`` follow the eigenvector sign, which the reference takes from
+LAPACK (quirk Q8): they are compared after aligning one global sign, and sign
+agreement is reported separately.
+
+Rounds flagged ``neartie_*`` in the fixture are those whose discrete decisions
+depend on rounding inside the reference's BLAS/LAPACK calls (see
+tests/golden/make_golden.py); callers count them separately.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+RTOL = 1e-9
+ATOL = 1e-12
+
+# golden key -> result key of the ABI / flat dict
+ABI_NAME = {
+    "agents.old_rep": "old_rep", "agents.this_rep": "this_rep", "agents.smooth_rep": "smooth_rep",
+    "agents.scores": "scores", "agents.na_row": "na_row",
+    "agents.participation_rows": "participation_rows", "agents.relative_part": "relative_part",
+    "agents.reporter_bonus": "reporter_bonus",
+    "events.adj_first_loadings": "adj_first_loadings", "events.outcomes_raw": "outcomes_raw",
+    "events.outcomes_adjusted": "outcomes_adjusted", "events.outcomes_final": "outcomes_final",
+    "events.certainty": "certainty", "events.consensus_reward": "consensus_reward",
+    "events.NAs Filled": "nas_filled", "events.participation_columns": "participation_columns",
+    "events.author_bonus": "author_bonus", "participation": "participation",
+    "avg_certainty": "avg_certainty", "filled": "filled", "original": "original",
+}
+EXACT = {"agents.na_row", "agents.participation_rows", "events.NAs Filled",
+         "events.outcomes_adjusted", "events.outcomes_final", "filled", "original"}
+SIGNED = {"agents.scores", "events.adj_first_loadings"}
+
+# cases the GPU path does not reproduce by design (documented in DESIGN.md):
+# a scaled event with no present report makes the reference fill NaN, its SVD
+# fail, and every later output depend on numpy.ma masked-data internals.
+EXCLUDED = {"q_all_missing_scaled_col"}
+
+
+def is_neartie(case):
+    return bool(case.get("neartie_rank", False)) or bool(case.get("neartie_catch", False)) \
+        or bool(case.get("neartie_median", False))
+
+
+def compare(case, ours, keys=None):
+    """Return (mismatches, sign_agrees).  ``ours`` maps ABI names to 1-round arrays."""
+    bad = []
+    L_ref = np.asarray(case["events.adj_first_loadings"], float)
+    L_our = np.asarray(ours["adj_first_loadings"], float)
+    dot = float(np.nansum(L_ref * L_our))
+    sign = -1.0 if dot < 0 else 1.0
+    for gk, ok in ABI_NAME.items():
+        if keys is not None and gk not in keys:
+            continue
+        if gk not in case or ok not in ours:
+            continue
+        a = np.asarray(ours[ok], float)
+        b = np.asarray(case[gk], float)
+        if gk in SIGNED:
+            a = a * sign
+        if a.shape != b.shape:
+            bad.append((gk, "shape", a.shape, b.shape))
+            continue
+        if not np.array_equal(np.isnan(a), np.isnan(b)):
+            bad.append((gk, "nan-pattern"))
+            continue
+        m = ~np.isnan(a)
+        if gk in EXACT:
+            if not np.array_equal(a[m], b[m]):
+                bad.append((gk, "exact", float(np.max(np.abs(a[m] - b[m])))))
+        else:
+            err = np.abs(a[m] - b[m])
+            tol = ATOL + RTOL * np.abs(b[m])
+            if np.any(err > tol):
+                k = int(np.argmax(err - tol))
+                bad.append((gk, "tol", float(err[k]), float(b[m][k])))
+    return bad, sign > 0
+
+
+_FLIP = {1: 2, 2: 1, 3: 4, 4: 3, 5: 5}
+
+
+def branch_matches(case, ours, sign_agrees):
+    """Branch codes name set1/set2 relative to the eigenvector sign; with the
+    opposite sign, set1 and set2 swap roles (and so do the codes)."""
+    b = int(ours["branch"])
+    if not sign_agrees:
+        b = _FLIP.get(b, b)
+    return b == int(case["branch"])
