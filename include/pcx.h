@@ -73,7 +73,7 @@ int      pcx_synchronize(pcx_ctx* ctx);
 /* wavefront (Simulator.jl-style Monte Carlo, README.rst:52-56).  Each round is */
 /* the complete Oracle(reports, event_bounds, reputation).consensus() of       */
 /* __init__.py:102-611.                                                          */
-/* Limits: 1 <= N <= 64, 1 <= E <= 64.                                          */
+/* Limits: 1 <= N <= 64, 1 <= E <= 32.                                          */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     int64_t n_rounds;             /* B                                           */

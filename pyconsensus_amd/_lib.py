@@ -1,0 +1,81 @@
+"""ctypes binding of libpcx.so (include/pcx.h).
+
+The library is built in-tree (``pyconsensus_amd/libpcx.so``, see csrc/Makefile)
+and is the ONLY compute path of this package: if it cannot be loaded, or no GPU is
+visible, every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from . import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpcx.so")
+
+_lock = threading.Lock()
+_lib = None
+
+
+class PcxError(RuntimeError):
+    """An error reported by libpcx (the message is pcx_last_error())."""
+
+
+def _declare(lib):
+    lib.pcx_abi_version.restype = C.c_int
+    lib.pcx_last_error.restype = C.c_char_p
+    lib.pcx_create.argtypes = [C.c_int]
+    lib.pcx_create.restype = C.c_void_p
+    lib.pcx_destroy.argtypes = [C.c_void_p]
+    lib.pcx_destroy.restype = None
+    lib.pcx_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    lib.pcx_set_stream.restype = C.c_int
+    lib.pcx_synchronize.argtypes = [C.c_void_p]
+    lib.pcx_synchronize.restype = C.c_int
+    lib.pcx_consensus_batched_f64.argtypes = [C.c_void_p, C.POINTER(_abi.Batch), C.POINTER(_abi.BatchResult)]
+    lib.pcx_consensus_batched_f64.restype = C.c_int
+
+
+def lib():
+    """Load (once) and return the ctypes handle of libpcx.so; raise if missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise PcxError("libpcx.so is not built (%s); run `make -C pyconsensus_amd/csrc` "
+                               "or __graft_entry__.build()" % LIB_PATH)
+            h = C.CDLL(LIB_PATH)
+            _declare(h)
+            v = h.pcx_abi_version()
+            if v != _abi.ABI_VERSION:
+                raise PcxError("libpcx ABI version %d, expected %d" % (v, _abi.ABI_VERSION))
+            _lib = h
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise PcxError("libpcx error %d: %s" % (rc, lib().pcx_last_error().decode(errors="replace")))
+
+
+_ctx = {}
+
+
+def context(device_index):
+    """The per-(thread, device) pcx_ctx handle."""
+    key = (threading.get_ident(), int(device_index))
+    h = _ctx.get(key)
+    if h is None:
+        h = lib().pcx_create(int(device_index))
+        if not h:
+            raise PcxError("pcx_create(%d) failed: %s" % (device_index, lib().pcx_last_error().decode()))
+        _ctx[key] = h
+    return h
+
+
+def bind_stream(device_index, stream_handle):
+    h = context(device_index)
+    check(lib().pcx_set_stream(h, C.c_void_p(stream_handle)))
+    return h

@@ -1,0 +1,127 @@
+// pcx_api.cpp -- the extern "C" boundary of libpcx (declared in include/pcx.h).
+// Host-side validation, context/stream management and kernel launches; no
+// compute happens here.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/pcx.h"
+#include "pcx_internal.h"
+
+struct pcx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(PCX_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+extern "C" {
+
+int pcx_abi_version(void) { return PCX_ABI_VERSION; }
+
+const char* pcx_last_error(void) { return g_err.c_str(); }
+
+pcx_ctx* pcx_create(int device_id) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || device_id < 0 || device_id >= n) {
+        g_err = "pcx_create: no HIP device " + std::to_string(device_id);
+        return nullptr;
+    }
+    pcx_ctx* c = new (std::nothrow) pcx_ctx;
+    if (!c) {
+        g_err = "pcx_create: out of host memory";
+        return nullptr;
+    }
+    c->device = device_id;
+    return c;
+}
+
+void pcx_destroy(pcx_ctx* ctx) { delete ctx; }
+
+int pcx_set_stream(pcx_ctx* ctx, void* s) {
+    if (!ctx) return fail(PCX_EINVAL, "pcx_set_stream: null context");
+    ctx->stream = reinterpret_cast<hipStream_t>(s);
+    return PCX_OK;
+}
+
+int pcx_synchronize(pcx_ctx* ctx) {
+    if (!ctx) return fail(PCX_EINVAL, "pcx_synchronize: null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? PCX_OK : hip_fail(e, "pcx_synchronize");
+}
+
+int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_result* out) {
+    if (!ctx || !in || !out) return fail(PCX_EINVAL, "pcx_consensus_batched_f64: null argument");
+    if (in->n_rounds < 0 || in->n_rounds > 0x7fffffff)
+        return fail(PCX_EINVAL, "batched: n_rounds must be in [0, 2^31)");
+    if (in->n_reporters < 1 || in->n_reporters > 64)
+        return fail(PCX_EINVAL, "batched: n_reporters must be in [1, 64]");
+    if (in->n_events < 1 || in->n_events > 32) return fail(PCX_EINVAL, "batched: n_events must be in [1, 32]");
+    if (!in->reports) return fail(PCX_EINVAL, "batched: reports is NULL");
+    if (in->scaled && (!in->lo || !in->hi)) return fail(PCX_EINVAL, "batched: scaled given without lo/hi");
+    if (in->algorithm != 0 && in->algorithm != 1) return fail(PCX_EINVAL, "batched: algorithm must be 0 (PCA) or 1");
+    if (!std::isfinite(in->catch_tolerance) || !std::isfinite(in->alpha))
+        return fail(PCX_EINVAL, "batched: catch_tolerance/alpha must be finite");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    pcx::BatchArgs a{};
+    a.B = in->n_rounds;
+    a.N = (int)in->n_reporters;
+    a.E = (int)in->n_events;
+    a.ES = a.E | 1;
+    a.reports = in->reports;
+    a.reputation = in->reputation;
+    a.scaled = in->scaled;
+    a.lo = in->lo;
+    a.hi = in->hi;
+    a.bounds_shared = in->bounds_shared;
+    a.int_dtype = in->int_dtype;
+    a.algorithm = in->algorithm;
+    a.catch_tol = in->catch_tolerance;
+    a.alpha = in->alpha;
+    a.old_rep = out->old_rep;
+    a.this_rep = out->this_rep;
+    a.smooth_rep = out->smooth_rep;
+    a.scores = out->scores;
+    a.na_row = out->na_row;
+    a.participation_rows = out->participation_rows;
+    a.relative_part = out->relative_part;
+    a.reporter_bonus = out->reporter_bonus;
+    a.adj_first_loadings = out->adj_first_loadings;
+    a.outcomes_raw = out->outcomes_raw;
+    a.outcomes_adjusted = out->outcomes_adjusted;
+    a.outcomes_final = out->outcomes_final;
+    a.certainty = out->certainty;
+    a.consensus_reward = out->consensus_reward;
+    a.nas_filled = out->nas_filled;
+    a.participation_columns = out->participation_columns;
+    a.author_bonus = out->author_bonus;
+    a.participation = out->participation;
+    a.avg_certainty = out->avg_certainty;
+    a.branch = out->branch;
+    a.flags = out->flags;
+    a.pi_iters = out->pi_iters;
+    a.original = out->original;
+    a.filled = out->filled;
+    e = pcx::launch_batched(a, ctx->stream);
+    return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,751 @@
+// pcx_batched.hip -- batched oracle rounds on MI355X (gfx950): one wavefront per
+// independent round (Simulator.jl-style Monte Carlo, README.rst:52-56).
+//
+// Each workgroup is ONE wave64 that runs a complete
+// Oracle(reports, event_bounds, reputation).consensus()
+// (pyconsensus/__init__.py:102-611, algorithm="PCA") for one N x E round held in
+// LDS (N <= 64 reporters: one lane per reporter row; E <= 32 events: one lane per
+// event column).  All arithmetic is IEEE fp64; the file is compiled with
+// -ffp-contract=off and every fma() is deliberate.  The arithmetic order is the
+// one written down in oracle/pcx_oracle_batched.c (the "SPEC"), so results are
+// bit-identical to that CPU restatement; see there for which steps replay the
+// reference's numpy order exactly and which use compensated dots / power
+// iteration in place of OpenBLAS / LAPACK.
+//
+// Lane roles per phase:
+//   row phase    lane i = reporter i      (rescale, fill, scores, bonuses)
+//   column phase lane j = event j         (sequential column sums, GEMV^T, ranks)
+//   entry phase  lane o = matrix entry o  (covariance, matrix squaring)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pcx_internal.h"
+
+namespace pcx {
+
+namespace {
+
+constexpr int W = 64;        // wavefront
+constexpr int NMAX = 64;  // reporters per round (one lane each)
+constexpr int EMAX = 32;
+static_assert(NMAX == W, "one reporter per lane");
+
+// power iteration constants (SPEC; equal to oracle/pcx_oracle_batched.c)
+constexpr double PI_TOL = 1e-14;
+constexpr int PI_MAXIT = 256;
+constexpr int PI_PRESQUARE = 3;
+constexpr int PI_SQUARE_EVERY = 32;
+constexpr int PI_MAX_SQUARINGS = 8;
+constexpr int PI_POLISH = 4;
+constexpr double DBL_EPS = 2.220446049250313080847e-16;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
+
+__device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, W); }
+
+// SPEC tree64: butterfly, xor distance 32..1 (every lane ends with the same sum)
+__device__ __forceinline__ double tree_sum(double v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v = v + __shfl_xor(v, s, W);
+    return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v = fmax(v, __shfl_xor(v, s, W));
+    return v;
+}
+
+__device__ __forceinline__ double catch_(double x, double tol) {  // __init__.py:251-258
+    if (x < 1.5 - tol) return 1.0;
+    if (x > 1.5 + tol) return 2.0;
+    return 1.5;
+}
+
+// numpy pairwise add.reduce (n <= 128 branch: 8 accumulators) of the lanes that
+// have `sel` set, taken in lane order.  All 64 lanes call it; every lane gets the
+// result.  `scr` is a 64-double LDS scratch owned by this wave.
+__device__ double wave_pw_sum(double v, bool sel, double* scr) {
+    const int l = lane_id();
+    const uint64_t m = ballot(sel);
+    const int n = popc(m);
+    const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    wsync();
+    if (sel) scr[pos] = v;
+    wsync();
+    double res = 0.0;
+    if (n < 8) {
+        if (l == 0)
+            for (int t = 0; t < n; t++) res += scr[t];
+    } else {
+        const int n8 = n - (n % 8);
+        double r = 0.0;
+        if (l < 8) {
+            r = scr[l];
+            for (int t = l + 8; t < n8; t += 8) r += scr[t];
+        }
+        const double r0 = bcast(r, 0), r1 = bcast(r, 1), r2 = bcast(r, 2), r3 = bcast(r, 3);
+        const double r4 = bcast(r, 4), r5 = bcast(r, 5), r6 = bcast(r, 6), r7 = bcast(r, 7);
+        if (l == 0) {
+            res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+            for (int t = n8; t < n; t++) res += scr[t];
+        }
+    }
+    return bcast(res, 0);
+}
+
+// SPEC dot2 over rows i < N of column-strided data: a[i] * b[i*bs]
+__device__ __forceinline__ double dot2(const double* a, const double* b, int bs, int n) {
+    double s = 0.0, c = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double x = a[i], y = b[i * bs];
+        const double p = x * y;
+        const double pe = fma(x, y, -p);
+        const double t = s + p;
+        const double z = t - s;
+        const double se = (s - (t - z)) + (p - z);
+        s = t;
+        c = c + (pe + se);
+    }
+    return s + c;
+}
+
+// weightedstats.weighted_median restated (oracle/pcx_oracle.py): lane i holds the
+// pair (x, w) if `sel`; W is the builtin sequential sum of the selected weights in
+// lane order (computed by the caller).  Scratch: sx, sw (64 doubles each).
+__device__ double wave_wmedian(double x, double w, bool sel, double W, double* sx, double* sw) {
+    const int l = lane_id();
+    const double mid = 0.5 * W;
+    const uint64_t dom = ballot(sel && w > mid);
+    if (dom) {
+        // Python max(weights) then .index(): the first maximal weight
+        double mx = wave_max(sel ? w : -__builtin_inf());
+        const uint64_t at = ballot(sel && w == mx);
+        return bcast(x, __builtin_ctzll(at));
+    }
+    if (!ballot(sel && w > 0.0)) return __builtin_nan("");
+    const uint64_t selm = ballot(sel);
+    const int n = popc(selm);
+    wsync();
+    sx[l] = x;
+    sw[l] = w;
+    wsync();
+    int r = 0;
+    if (sel) {  // stable rank by (x, w)
+        uint64_t rest = selm;
+        while (rest) {
+            const int mrow = __builtin_ctzll(rest);
+            rest &= rest - 1;
+            const double xm = sx[mrow], wm = sw[mrow];
+            const bool lt = (xm < x) || (xm == x && wm < w);
+            const bool eq = (xm == x) && (wm == w);
+            r += (lt || (eq && mrow < l)) ? 1 : 0;
+        }
+    }
+    wsync();
+    if (sel) {
+        sx[r] = x;
+        sw[r] = w;
+    }
+    wsync();
+    double res = 0.0;
+    if (l == 0) {
+        double cum = 0.0;
+        int k = 0;
+        bool fail = false;
+        while (cum <= mid) {
+            if (k == n) {
+                fail = true;
+                break;
+            }
+            cum += sw[k];
+            k++;
+        }
+        if (fail) {
+            res = __builtin_nan("");
+        } else {
+            const double before = cum - sw[k - 1];
+            if (fabs(before - mid) < DBL_EPS) {
+                if (k >= 2)
+                    res = (sx[k - 2] + sx[k - 1]) / 2.0;
+                else
+                    res = n == 1 ? sx[0] / 1.0 : __builtin_nan("");
+            } else {
+                res = sx[k - 1];
+            }
+        }
+    }
+    return bcast(res, 0);
+}
+
+// scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
+__device__ __forceinline__ double rank_avg(const double* v, int E) {
+    const int l = lane_id();
+    double r = 0.0;
+    if (l < E) {
+        const double x = v[l];
+        int lt = 0, eq = 0;
+        for (int k = 0; k < E; k++) {
+            const double y = v[k];
+            lt += y < x;
+            eq += y == x;
+        }
+        r = (double)lt + (double)(eq + 1) * 0.5;
+    }
+    return r;
+}
+
+struct Smem {
+    double* F;      // [N][ES] rescaled, then filled reports
+    double* C;      // [E][ES] covariance
+    double* M;      // [E][ES] power-iteration working matrix
+    double* rep;    // [64]
+    double* tok;    // [64]
+    double* s;      // [64] scores
+    double* n1;     // [64] normalize(set1)
+    double* n2;     // [64] normalize(set2)
+    double* smooth; // [64]
+    double* sx;     // [64] scratch
+    double* sw;     // [64] scratch
+    double* scr;    // [64] scratch
+    double* mu;     // [32]
+    double* guess;  // [32]
+    double* x;      // [32] power-iteration vector
+    double* ld;     // [32] loading
+    double* old;    // [32]
+    double* nv1;    // [32]
+    double* nv2;    // [32]
+    double* adj;    // [32]
+    uint64_t* nanm; // [32] bit i = report (i, j) is NaN
+    uint64_t* zerm; // [32] bit i = report (i, j) == 0.0
+};
+
+__device__ Smem carve(double* base, int N, int E, int ES) {
+    Smem s;
+    double* p = base;
+    s.F = p; p += N * ES;
+    s.C = p; p += E * ES;
+    s.M = p; p += E * ES;
+    s.rep = p; p += 64;
+    s.tok = p; p += 64;
+    s.s = p; p += 64;
+    s.n1 = p; p += 64;
+    s.n2 = p; p += 64;
+    s.smooth = p; p += 64;
+    s.sx = p; p += 64;
+    s.sw = p; p += 64;
+    s.scr = p; p += 64;
+    s.mu = p; p += 32;
+    s.guess = p; p += 32;
+    s.x = p; p += 32;
+    s.ld = p; p += 32;
+    s.old = p; p += 32;
+    s.nv1 = p; p += 32;
+    s.nv2 = p; p += 32;
+    s.adj = p; p += 32;
+    s.nanm = reinterpret_cast<uint64_t*>(p); p += 32;
+    s.zerm = reinterpret_cast<uint64_t*>(p); p += 32;
+    return s;
+}
+
+// y = normalize(M x) for lane j < E, x in LDS; returns y_j (0 on other lanes)
+__device__ __forceinline__ double matvec_unit(const double* M, int ES, const double* x, int E) {
+    const int l = lane_id();
+    double y = 0.0;
+    if (l < E) {
+        double acc = 0.0;
+        const double* row = M + l * ES;
+        for (int k = 0; k < E; k++) acc = fma(row[k], x[k], acc);
+        y = acc;
+    }
+    const double nrm = sqrt(tree_sum(l < E ? y * y : 0.0));
+    return l < E ? y / nrm : 0.0;
+}
+
+// M <- (M M) / max|M M| (SPEC square_scaled)
+__device__ void square_scaled(double* M, int ES, int E) {
+    const int l = lane_id();
+    double t[EMAX * EMAX / W];
+    double mx = 0.0;
+    const int tot = E * E;
+#pragma unroll
+    for (int q = 0; q < EMAX * EMAX / W; q++) {
+        const int o = l + q * W;
+        t[q] = 0.0;
+        if (o < tot) {
+            const int j = o / E, k = o - j * E;
+            double acc = 0.0;
+            for (int m = 0; m < E; m++) acc = fma(M[j * ES + m], M[m * ES + k], acc);
+            t[q] = acc;
+            mx = fmax(mx, fabs(acc));
+        }
+    }
+    mx = wave_max(mx);
+    wsync();
+#pragma unroll
+    for (int q = 0; q < EMAX * EMAX / W; q++) {
+        const int o = l + q * W;
+        if (o < tot) {
+            const int j = o / E, k = o - j * E;
+            M[j * ES + k] = mx > 0.0 ? t[q] / mx : t[q];
+        }
+    }
+    wsync();
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int N = a.N, E = a.E, ES = a.ES;
+    const int l = lane_id();
+    const int64_t b = blockIdx.x;
+    Smem S = carve(smem, N, E, ES);
+    const bool row = l < N, col = l < E;
+    const int64_t bo = a.bounds_shared ? 0 : b * E;
+    const bool has_bounds = a.scaled != nullptr;
+
+    // ---- load the round -------------------------------------------------
+    const double* Rg = a.reports + b * (int64_t)N * E;
+    for (int idx = l; idx < N * E; idx += W) {
+        const int i = idx / E, j = idx - i * E;
+        S.F[i * ES + j] = Rg[idx];
+    }
+    bool scj = false;
+    double loj = 0.0, hij = 0.0;
+    if (col && has_bounds) {
+        scj = a.scaled[bo + l] != 0;
+        loj = a.lo[bo + l];
+        hij = a.hi[bo + l];
+    }
+    const uint64_t scaled_mask = ballot(col && scj);
+
+    // ---- a1: reputation (__init__.py:138-146) -----------------------------
+    double raw = row && a.reputation ? a.reputation[b * N + l] : 0.0;
+    double rep;
+    if (a.reputation) {
+        const double tot = wave_pw_sum(raw, row, S.scr);
+        rep = raw / tot;
+    } else {
+        rep = 1.0 / (double)N;
+    }
+    const double tok = trunc(rep * 1e6);
+    if (row) {
+        S.rep[l] = rep;
+        S.tok[l] = tok;
+    }
+    const double denom = tree_sum(row ? tok : 0.0) - 1.0;  // exact integer sum
+    wsync();
+
+    // ---- a2: rescale (:266-269) + NA masks (:278) -------------------------
+    for (int j = 0; j < E; j++) {
+        const bool sc = (scaled_mask >> j) & 1;
+        const double lo = bcast(loj, j), hi = bcast(hij, j);
+        double x = 0.0;
+        if (row) {
+            x = S.F[l * ES + j];
+            if (sc) {
+                x = (x - lo) / (hi - lo);
+                if (a.int_dtype) x = trunc(x);
+                S.F[l * ES + j] = x;
+            }
+            if (a.original) a.original[(b * N + l) * E + j] = x;
+        }
+        const uint64_t nm = ballot(row && __builtin_isnan(x));
+        const uint64_t zm = ballot(row && x == 0.0);
+        if (l == 0) {
+            S.nanm[j] = nm;
+            S.zerm[j] = zm;
+        }
+    }
+    wsync();
+
+    // ---- a3: interpolation guesses (:284-313), column phase ----------------
+    uint64_t miss_j = 0;
+    double Wj = 0.0;
+    if (col) {
+        miss_j = S.nanm[l] | S.zerm[l];
+        if (miss_j) {
+            double tot = 0.0;
+            for (int i = 0; i < N; i++)
+                if (!((miss_j >> i) & 1)) tot += S.rep[i];
+            double g = 0.0;
+            if (scj) {
+                for (int i = 0; i < N; i++)
+                    if (!((miss_j >> i) & 1)) Wj += S.rep[i] / tot;
+            } else {
+                for (int i = 0; i < N; i++)
+                    if (!((miss_j >> i) & 1)) g += (S.rep[i] / tot) * S.F[i * ES + l];
+                g = catch_(g, a.catch_tol);
+                if (a.int_dtype) g = trunc(g);
+                S.guess[l] = g;
+            }
+            S.mu[l] = tot;  // stash the present-reputation total for the median phase
+        }
+    }
+    wsync();
+    // scaled columns with missing reports: weighted median of the present values
+    {
+        uint64_t todo = ballot(col && scj && miss_j != 0);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t mj = S.nanm[j] | S.zerm[j];
+            const bool present = row && !((mj >> l) & 1);
+            const double tot = S.mu[j];
+            const double x = row ? S.F[l * ES + j] : 0.0;
+            const double w = present ? S.rep[l] / tot : 0.0;
+            const double Wsum = bcast(Wj, j);
+            double g = wave_wmedian(x, w, present, Wsum, S.sx, S.sw);
+            if (a.int_dtype) g = trunc(g);
+            if (l == 0) S.guess[j] = g;
+            wsync();
+        }
+    }
+    wsync();
+    // fill (row phase)
+    if (row) {
+        for (int j = 0; j < E; j++) {
+            const uint64_t mj = S.nanm[j] | S.zerm[j];
+            if ((mj >> l) & 1) S.F[l * ES + j] = S.guess[j];
+        }
+    }
+    wsync();
+    if (a.filled && row)
+        for (int j = 0; j < E; j++) a.filled[(b * N + l) * E + j] = S.F[l * ES + j];
+
+    // ---- old = rep . F (np.dot) -------------------------------------------
+    double oldj = col ? dot2(S.rep, S.F + l, ES, N) : 0.0;
+    if (col) S.old[l] = oldj;
+
+    double sc_i = 0.0, nc_i = 0.0, ld_j = 0.0;
+    int branch = 5, flags = 0, iters = 0;
+    if (a.algorithm == 0) {
+        // ---- a5: weighted mean, np.ma.average (:317-319) -------------------
+        const double den = wave_pw_sum(rep, row, S.scr);
+        double muj = 0.0;
+        if (E == 1) {
+            const double p = row ? S.F[l * ES] * rep : 0.0;
+            const double acc = wave_pw_sum(p, row, S.scr);
+            muj = acc / den;
+        } else if (col) {
+            double acc = S.F[l] * S.rep[0];
+            for (int i = 1; i < N; i++) acc = acc + S.F[i * ES + l] * S.rep[i];
+            muj = acc / den;
+        }
+        wsync();
+        if (col) S.mu[l] = muj;
+        wsync();
+
+        // ---- a6: token-weighted covariance (:326), lower triangle ----------
+        const int ntri = E * (E + 1) / 2;
+        bool nonzero = false, finite = true;
+        for (int o = l; o < ntri; o += W) {
+            int j = 0;
+            while ((j + 1) * (j + 2) / 2 <= o) j++;
+            const int k = o - j * (j + 1) / 2;
+            const double mj = S.mu[j], mk = S.mu[k];
+            double acc = 0.0;
+            for (int i = 0; i < N; i++)
+                acc = fma((S.F[i * ES + j] - mj) * S.tok[i], S.F[i * ES + k] - mk, acc);
+            const double c = acc / denom;
+            S.C[j * ES + k] = c;
+            S.C[k * ES + j] = c;
+            S.M[j * ES + k] = c;
+            S.M[k * ES + j] = c;
+            nonzero |= c != 0.0;
+            finite &= __builtin_isfinite(c) != 0;
+        }
+        const bool any_nz = ballot(nonzero) != 0;
+        const bool all_fin = ballot(!finite) == 0;
+        wsync();
+
+        // ---- a7: leading eigenvector by power iteration (:330-336) -------
+        double xv = 0.0;
+        if (!all_fin) {
+            xv = col ? 1.0 : 0.0;
+            flags |= 2;
+        } else if (!any_nz) {
+            xv = l == 0 ? 1.0 : 0.0;
+            flags |= 1;
+        } else {
+            // start: the column with the largest diagonal entry (first max)
+            int kd = 0;
+            for (int j = 1; j < E; j++)
+                if (S.C[j * ES + j] > S.C[kd * ES + kd]) kd = j;
+            double x0 = col ? S.C[l * ES + kd] : 0.0;
+            const double n0 = sqrt(tree_sum(x0 * x0));
+            xv = col ? x0 / n0 : 0.0;
+            int sqn = 0;
+            for (; sqn < PI_PRESQUARE; sqn++) square_scaled(S.M, ES, E);
+            if (col) S.x[l] = xv;
+            wsync();
+            int it = 0, since = 0;
+            for (;;) {
+                const double y = matvec_unit(S.M, ES, S.x, E);
+                const double d = wave_max(col ? fabs(y - xv) : 0.0);
+                xv = y;
+                wsync();
+                if (col) S.x[l] = xv;
+                wsync();
+                it++;
+                since++;
+                if (d <= PI_TOL) break;
+                if (it >= PI_MAXIT) {
+                    flags |= 4;
+                    break;
+                }
+                if (since >= PI_SQUARE_EVERY && sqn < PI_MAX_SQUARINGS) {
+                    square_scaled(S.M, ES, E);
+                    sqn++;
+                    since = 0;
+                }
+            }
+            for (int p = 0; p < PI_POLISH; p++) {
+                xv = matvec_unit(S.C, ES, S.x, E);
+                wsync();
+                if (col) S.x[l] = xv;
+                wsync();
+            }
+            // SPEC sign: first nonzero component negative; a unit vector e_k is +e_k
+            const uint64_t nzm = ballot(col && xv != 0.0);
+            if (nzm) {
+                const double xf = bcast(xv, __builtin_ctzll(nzm));
+                const bool neg = popc(nzm) == 1 ? xf < 0.0 : xf > 0.0;
+                if (neg) xv = -xv;
+            }
+            iters = it + PI_POLISH + sqn;
+        }
+        // loading = v / sqrt(sum(v**2)) with numpy's pairwise sum (:336)
+        const double nv = sqrt(wave_pw_sum(xv * xv, col, S.scr));
+        ld_j = col ? xv / nv : 0.0;
+        wsync();
+        if (col) S.ld[l] = ld_j;
+        wsync();
+        // scores s = wcd . loading (:337), row phase
+        if (row) {
+            double acc = 0.0;
+            for (int j = 0; j < E; j++) acc = fma(S.F[l * ES + j] - S.mu[j], S.ld[j], acc);
+            sc_i = acc;
+        }
+        // ---- a8/a9: nonconformity_rank (:487-500) / nonconformity (:475-485)
+        const bool any_nan = ballot(row && __builtin_isnan(sc_i)) != 0;
+        double mn = wave_max(row ? -sc_i : -__builtin_inf());
+        mn = -mn;
+        double mx = wave_max(row ? sc_i : -__builtin_inf());
+        if (any_nan) {
+            mn = __builtin_nan("");
+            mx = __builtin_nan("");
+        }
+        const double set1 = sc_i + fabs(mn);
+        const double set2 = sc_i - mx;
+        double a1 = fabs(set1), a2 = fabs(set2);
+        double S1 = wave_pw_sum(a1, row, S.scr);
+        if (S1 == 0) {
+            a1 += 1.0;
+            S1 = wave_pw_sum(a1, row, S.scr);
+        }
+        double S2 = wave_pw_sum(a2, row, S.scr);
+        if (S2 == 0) {
+            a2 += 1.0;
+            S2 = wave_pw_sum(a2, row, S.scr);
+        }
+        if (row) {
+            S.n1[l] = a1 / S1;
+            S.n2[l] = a2 / S2;
+            S.s[l] = sc_i;
+        }
+        wsync();
+        double d1 = 0.0, d2 = 0.0;
+        if (col) {
+            d1 = dot2(S.n1, S.F + l, ES, N);
+            d2 = dot2(S.n2, S.F + l, ES, N);
+            const double t = 0.01 * oldj;
+            S.nv1[l] = d1 + t;
+            S.nv2[l] = d2 + t;
+        }
+        wsync();
+        const double r0 = rank_avg(S.old, E);
+        const double r1 = rank_avg(S.nv1, E);
+        const double r2 = rank_avg(S.nv2, E);
+        const double e1 = fabs(r1 - r0), e2 = fabs(r2 - r0);
+        const double ref = wave_pw_sum(e1, col, S.scr) - wave_pw_sum(e2, col, S.scr);
+        bool pick1;
+        if (ref == 0) {
+            const double q1 = d1 - oldj, q2 = d2 - oldj;
+            const double ref2 = wave_pw_sum(q1 * q1, col, S.scr) - wave_pw_sum(q2 * q2, col, S.scr);
+            pick1 = ref2 <= 0;
+            branch = pick1 ? 3 : 4;
+        } else {
+            pick1 = ref < 0;
+            branch = pick1 ? 1 : 2;
+        }
+        nc_i = pick1 ? set1 : set2;
+    }
+
+    // ---- a10: reputation update (:460-472) --------------------------------
+    const double meanrep = wave_pw_sum(rep, row, S.scr) / (double)N;
+    double u = fabs(nc_i * (rep / meanrep));
+    double Su = wave_pw_sum(u, row, S.scr);
+    if (Su == 0) {
+        u += 1.0;
+        Su = wave_pw_sum(u, row, S.scr);
+    }
+    const double this_i = u / Su;
+    const double smooth_i = a.alpha * this_i + (1.0 - a.alpha) * rep;
+    wsync();
+    if (row) S.smooth[l] = smooth_i;
+    wsync();
+
+    // ---- a12/a13: outcomes (:510-538) -------------------------------------
+    double rawj = col ? dot2(S.smooth, S.F + l, ES, N) : 0.0;
+    if (scaled_mask) {
+        const double Wsm = [&] {  // builtin sequential sum of smooth_rep (weightedstats)
+            double w = 0.0;
+            if (l == 0)
+                for (int i = 0; i < N; i++) w += S.smooth[i];
+            return bcast(w, 0);
+        }();
+        uint64_t todo = scaled_mask;
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const double x = row ? S.F[l * ES + j] : 0.0;
+            const double m = wave_wmedian(x, smooth_i, row, Wsm, S.sx, S.sw);
+            if (l == j) rawj = m;
+            wsync();
+        }
+    }
+    double adjj = 0.0, finj = 0.0;
+    if (col) {
+        if (scj) {
+            adjj = rawj;
+            finj = adjj * (hij - loj);
+            finj = finj + loj;
+        } else {
+            adjj = catch_(rawj, a.catch_tol);
+            finj = adjj;
+        }
+        S.adj[l] = adjj;
+    }
+    wsync();
+
+    // ---- a14: certainty (:540-546): pairwise sum of the matching smooth_rep --
+    double certj = 0.0;
+    for (int j = 0; j < E; j++) {
+        const double aj = S.adj[j];
+        const bool hit = row && S.F[l * ES + j] == aj;
+        const uint64_t hm = ballot(hit);
+        const double c = hm ? wave_pw_sum(smooth_i, hit, S.scr) : __builtin_nan("");
+        if (l == j) certj = c;
+    }
+    // normalize(certainty), mean(certainty)
+    double ac = fabs(certj);
+    double Sc = wave_pw_sum(ac, col, S.scr);
+    if (Sc == 0) {
+        ac += 1.0;
+        Sc = wave_pw_sum(ac, col, S.scr);
+    }
+    const double reward = ac / Sc;
+    const double avg_cert = wave_pw_sum(certj, col, S.scr) / (double)E;
+
+    // ---- a15: participation and bonuses (:549-581) -------------------------
+    double pcj = 0.0, nzj = 0.0;
+    if (col) {
+        const uint64_t nam = S.nanm[l] | S.zerm[l];
+        // dot2(smooth, na) with na in {0,1}
+        double s = 0.0, c = 0.0;
+        for (int i = 0; i < N; i++) {
+            const double x = S.smooth[i], y = ((nam >> i) & 1) ? 1.0 : 0.0;
+            const double p = x * y;
+            const double pe = fma(x, y, -p);
+            const double t = s + p;
+            const double z = t - s;
+            const double se = (s - (t - z)) + (p - z);
+            s = t;
+            c = c + (pe + se);
+        }
+        pcj = 1.0 - (s + c);
+        nzj = (double)popc(S.zerm[l]);
+    }
+    double narow = 0.0;
+    int nnan = 0;
+    if (row) {
+        int nz = 0;
+        for (int j = 0; j < E; j++) {
+            nz += (S.zerm[j] >> l) & 1;
+            nnan += (S.nanm[j] >> l) & 1;
+        }
+        narow = (double)nz;
+    }
+    const bool rowmasked = row && nnan == E;
+    const double pr = 1.0 - narow / (double)E;
+    const double pna = 1.0 - wave_pw_sum(pcj, col, S.scr) / (double)E;
+    double ar = rowmasked ? 0.0 : fabs(pr);
+    double Sr = wave_pw_sum(ar, row, S.scr);
+    if (Sr == 0) {
+        ar = rowmasked ? 0.0 : fabs(pr) + 1.0;
+        Sr = wave_pw_sum(ar, row, S.scr);
+    }
+    const double rel = rowmasked ? fabs(pr) : ar / Sr;
+    double apc = fabs(pcj);
+    double Spc = wave_pw_sum(apc, col, S.scr);
+    if (Spc == 0) {
+        apc += 1.0;
+        Spc = wave_pw_sum(apc, col, S.scr);
+    }
+    const double relc = apc / Spc;
+
+    // ---- write the round ---------------------------------------------------
+    if (row) {
+        const int64_t o = b * N + l;
+        if (a.old_rep) a.old_rep[o] = rep;
+        if (a.this_rep) a.this_rep[o] = this_i;
+        if (a.smooth_rep) a.smooth_rep[o] = smooth_i;
+        if (a.scores) a.scores[o] = sc_i;
+        if (a.na_row) a.na_row[o] = narow;
+        if (a.participation_rows) a.participation_rows[o] = pr;
+        if (a.relative_part) a.relative_part[o] = rel;
+        if (a.reporter_bonus) a.reporter_bonus[o] = rowmasked ? rel : rel * pna + smooth_i * (1.0 - pna);
+    }
+    if (col) {
+        const int64_t o = b * E + l;
+        if (a.adj_first_loadings) a.adj_first_loadings[o] = ld_j;
+        if (a.outcomes_raw) a.outcomes_raw[o] = rawj;
+        if (a.outcomes_adjusted) a.outcomes_adjusted[o] = adjj;
+        if (a.outcomes_final) a.outcomes_final[o] = finj;
+        if (a.certainty) a.certainty[o] = certj;
+        if (a.consensus_reward) a.consensus_reward[o] = reward;
+        if (a.nas_filled) a.nas_filled[o] = nzj;
+        if (a.participation_columns) a.participation_columns[o] = pcj;
+        if (a.author_bonus) a.author_bonus[o] = relc * pna + reward * (1.0 - pna);
+    }
+    if (l == 0) {
+        if (a.participation) a.participation[b] = 1.0 - pna;
+        if (a.avg_certainty) a.avg_certainty[b] = avg_cert;
+        if (a.branch) a.branch[b] = branch;
+        if (a.flags) a.flags[b] = flags;
+        if (a.pi_iters) a.pi_iters[b] = iters;
+    }
+}
+
+size_t batched_lds_bytes(int N, int E) {
+    const int ES = E | 1;
+    const size_t doubles = (size_t)N * ES + 2 * (size_t)E * ES + 9 * 64 + 8 * 32 + 2 * 32;
+    return doubles * sizeof(double);
+}
+
+hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
+    const size_t lds = batched_lds_bytes(a.N, a.E);
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(batched_round_kernel, dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace pcx

@@ -1,0 +1,35 @@
+// pcx_internal.h -- declarations shared by the libpcx translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pcx {
+
+// Kernel arguments of the batched round kernel (by value).
+struct BatchArgs {
+    int64_t B;
+    int N, E, ES;
+    const double* reports;
+    const double* reputation;
+    const uint8_t* scaled;
+    const double* lo;
+    const double* hi;
+    int bounds_shared;
+    int int_dtype;
+    int algorithm;
+    double catch_tol;
+    double alpha;
+    double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
+        *reporter_bonus;
+    double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
+        *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
+    double *participation, *avg_certainty;
+    int32_t *branch, *flags, *pi_iters;
+    double *original, *filled;
+};
+
+size_t batched_lds_bytes(int N, int E);
+hipError_t launch_batched(const BatchArgs& a, hipStream_t stream);
+
+}  // namespace pcx

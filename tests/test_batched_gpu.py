@@ -1,0 +1,124 @@
+"""GPU parity of the batched round kernel (one wavefront per round).
+
+* bit-for-bit against the C oracle (oracle/pcx_oracle_batched.c) on the full C3
+  workload: 65,536 seeded 50 x 20 rounds, every output;
+* against the reference's golden vectors (KATs, mixed shapes, 600 synthetic
+  rounds) with the north_star tolerances (tests/parity.py).
+"""
+import numpy as np
+import pytest
+
+import golden_cases as G
+import parity as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(outs):
+    return {k: v.cpu().numpy() for k, v in outs.items() if not k.startswith("_")}
+
+
+def _run_gpu(case_list):
+    """Rounds of one shape in one launch; case_list: list of golden dicts."""
+    from pyconsensus_amd.batched import consensus_batched
+
+    R = np.stack([c["in_reports"] for c in case_list])
+    c0 = case_list[0]
+    kw = {}
+    if bool(c0["in_has_bounds"]):
+        kw.update(scaled=np.stack([c["in_scaled"] for c in case_list]),
+                  lo=np.stack([c["in_lo"] for c in case_list]), hi=np.stack([c["in_hi"] for c in case_list]))
+    if bool(c0["in_has_rep"]):
+        kw["reputation"] = np.stack([c["in_reputation"] for c in case_list])
+    return _np(consensus_batched(R, catch_tolerance=float(c0["in_catch_tolerance"]),
+                                 alpha=float(c0["in_alpha"]), int_dtype=bool(c0["in_int_dtype"]),
+                                 filled=True, original=True, **kw))
+
+
+def _score(cases, outs):
+    stats = dict(n=0, neartie=0, neartie_match=0, sign=0)
+    fails = []
+    for b, (name, case) in enumerate(cases):
+        ours = {k: v[b] for k, v in outs.items()}
+        bad, sign = P.compare(case, ours)
+        stats["n"] += 1
+        stats["sign"] += sign
+        ok = not bad and P.branch_matches(case, ours, sign)
+        if P.is_neartie(case):
+            stats["neartie"] += 1
+            stats["neartie_match"] += ok
+        elif not ok:
+            fails.append((name, int(ours["branch"]), int(case["branch"]), bad[:3]))
+    return stats, fails
+
+
+def test_golden_synth_50x20(gpu_lib):
+    st = G.synth()
+    cases = [(b, G.unstack(st, b)) for b in range(st["branch"].shape[0])]
+    outs = _run_gpu([c for _, c in cases])
+    stats, fails = _score(cases, outs)
+    print("synth_50x20", stats)
+    assert not fails, fails[:5]
+    assert stats["neartie"] <= 0.08 * stats["n"]
+
+
+def test_golden_kat_and_mixed(gpu_lib):
+    allc = list(G.kat().items()) + list(G.mixed().items())
+    fails = []
+    tot = dict(n=0, neartie=0, neartie_match=0, sign=0)
+    for name, case in allc:
+        N, E = case["in_reports"].shape
+        if name in P.EXCLUDED or N > 64 or E > 32:
+            continue
+        stats, f = _score([(name, case)], _run_gpu([case]))
+        fails += f
+        for k in tot:
+            tot[k] += stats[k]
+    print("kat+mixed", tot)
+    assert not fails, fails[:5]
+
+
+def test_bitexact_vs_c_oracle_c3(gpu_lib):
+    """Full C3 workload (65,536 x 50 x 20, seed 20261015): GPU == C oracle, bit for bit."""
+    from oracle import pcx_oracle_c as OC
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, sc, lo, hi, rep = synthetic.rounds(65536, 50, 20, seed=20261015)
+    g = _np(consensus_batched(R, rep, sc, lo, hi, filled=True))
+    c = OC.batched(R, sc, lo, hi, rep, threads=16)
+    for k, v in g.items():
+        if k == "original":
+            continue
+        a, b = v, c[k]
+        same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+        nbad = int(np.size(same) - np.count_nonzero(same))
+        assert nbad == 0, (k, nbad)
+
+
+@pytest.mark.parametrize("variant", ["uniform_rep", "shared_bounds", "no_bounds", "int_dtype",
+                                     "absolute", "E1", "N1", "N64_E32"])
+def test_variants_bitexact_vs_c_oracle(gpu_lib, variant):
+    from oracle import pcx_oracle_c as OC
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    N, E = {"E1": (30, 1), "N1": (1, 6), "N64_E32": (64, 32)}.get(variant, (50, 20))
+    R, sc, lo, hi, rep = synthetic.rounds(512, N, E, seed=5)
+    kw = dict(reputation=rep, scaled=sc, lo=lo, hi=hi)
+    if variant == "uniform_rep":
+        kw["reputation"] = None
+    if variant == "shared_bounds":
+        kw.update(scaled=sc[0], lo=lo[0], hi=hi[0])
+    if variant == "no_bounds":
+        kw.update(scaled=None, lo=None, hi=None)
+    if variant == "int_dtype":
+        R = np.where(np.isnan(R), 0.0, np.trunc(R))
+        kw["int_dtype"] = True
+    if variant == "absolute":
+        kw["algorithm"] = "absolute"
+    g = _np(consensus_batched(R, filled=True, original=True, **kw))
+    c = OC.batched(R, **kw, threads=8)
+    for k, v in g.items():
+        same = (v == c[k]) | (np.isnan(v) & np.isnan(c[k])) if v.dtype.kind == "f" else (v == c[k])
+        assert np.all(same), (variant, k, int(np.size(same) - np.count_nonzero(same)))
