@@ -156,8 +156,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md 8(d) generator: 10% NaN, 25% scaled events, 70/30 honest/liar, "
-                    "integer reputation; seed %d + rank)" % SEED,
+            "data": ("synthetic (SURVEY.md 8(d) generator: 10%% NaN, 25%% scaled events, 70/30 honest/liar, "
+                     "integer reputation; seed %d + rank)") % SEED,
             "config": {"workload": "C3: %d independent 50x20 oracle rounds per GPU per step (one wavefront "
                                    "per round), inputs resident in HBM" % B,
                        "rounds_per_gpu": B, "reporters": N_REP, "events": N_EV,
