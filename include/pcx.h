@@ -124,6 +124,104 @@ typedef struct {
 
 int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_result* out);
 
+/* ------------------------------------------------------------------------ */
+/* Single-matrix regime: one N x E report matrix, optionally sharded by        */
+/* reporter rows over several GPUs (one process per GPU).  The consensus is a   */
+/* fixed sequence of stages (pcx_mat_stage); between some stages the host       */
+/* combines per-rank partial buffers across ranks (pyconsensus_amd/pipeline.py, */
+/* torch.distributed over RCCL).  Every buffer is caller-allocated device memory */
+/* sized as documented in pipeline.py (MatWorkspace).                           */
+/* ------------------------------------------------------------------------ */
+enum pcx_mat_stage_id {
+    PCX_M_REPUTATION = 1,    /* rep, tokens (__init__.py:138-146)                    */
+    PCX_M_COLSTATS = 2,      /* rescale + NA + present sums per event (:266-299)     */
+    PCX_M_GUESS = 3,         /* binary fills (:304-309), median setup (:300-303)     */
+    PCX_M_MEAN = 4,          /* weighted mean mu, old = rep . F (:317-319, 490)     */
+    PCX_M_COV = 5,           /* token-weighted covariance partial tiles, fp64 MFMA (:326) */
+    PCX_M_COV_REDUCE = 6,    /* sum split-K slabs into this rank's partial C         */
+    PCX_M_COV_FINISH = 7,    /* C = partial / (sum tokens - 1), symmetric            */
+    PCX_M_POWER = 8,         /* leading eigenvector by power iteration (:330-336)    */
+    PCX_M_SCORES = 9,        /* scores = wcd . loading (:337), row NA counts         */
+    PCX_M_NCSUMS = 10,       /* sums of |set1|, |set2| (:488-489, normalize)         */
+    PCX_M_GEMV2 = 11,        /* normalize(set1/2) . F (:492-493)                     */
+    PCX_M_DECIDE = 12,       /* rank rule / continuous fallback (:491-498, 475-485)  */
+    PCX_M_REPU = 13,         /* nc * rep / mean(rep) and its sum (:460-462)          */
+    PCX_M_SMOOTH = 14,       /* this_rep, smooth_rep (:460-472)                      */
+    PCX_M_OUTCOMES = 15,     /* smooth . F, participation, certainty bins (:510, 559, 542) */
+    PCX_M_EVENTS = 16,       /* catch/unscale binary events (:526-538)               */
+    PCX_M_SCALED_CERT = 17,  /* certainty of scaled events (:540-546)                */
+    PCX_M_FINAL = 18,        /* reward, author bonus, participation (:545-581)      */
+    PCX_M_ROWSUMS = 19,      /* participation_rows normalisation sums (:567-576)     */
+    PCX_M_AGENTS = 20,       /* per-reporter outputs (:576-577, 586-595)             */
+    PCX_M_MATRICES = 21,     /* result["original"] / result["filled"] (:584-585)     */
+    PCX_M_SEL_INIT = 30,     /* weighted median (:303, :520): totals, key range, max weight */
+    PCX_M_SEL_START = 31,    /*   dominance test, first histogram range              */
+    PCX_M_SEL_ARGMAX = 32,   /*   first row with the dominant weight                 */
+    PCX_M_SEL_VALUE = 33,    /*   value at that row                                  */
+    PCX_M_SEL_HIST = 34,     /*   exact weight histogram over the current key range  */
+    PCX_M_SEL_STEP = 35,     /*   narrow the range; converged columns get their result */
+    PCX_M_SEL_FINISH = 36,   /*   results into guess (phase 1) / outcomes_raw (phase 2) */
+};
+
+typedef struct {
+    /* shape and parameters */
+    int64_t n_rows;               /* rows held by this rank                       */
+    int64_t n_events;             /* E                                            */
+    int64_t n_total;              /* N over all ranks                             */
+    int64_t row_offset;           /* global index of this rank's first row        */
+    int32_t world, rank;
+    int32_t int_dtype, algorithm;
+    double  catch_tolerance, alpha;
+    int32_t n_scaled;             /* number of scaled events                      */
+    int32_t sel_phase;            /* 1: interpolation medians, 2: outcome medians */
+    int32_t col_blocks;           /* row chunks of the column passes (G)          */
+    int32_t cov_tiles, cov_kslices;
+    /* inputs */
+    const double*  reports;       /* [n_rows][E]                                  */
+    const uint8_t* scaled;        /* [E] or NULL (event_bounds None)              */
+    const double*  lo;            /* [E]                                          */
+    const double*  hi;            /* [E]                                          */
+    const double*  rep_raw;       /* [n_total] raw reputation, or NULL = uniform   */
+    const int32_t* scaled_cols;   /* [n_scaled] event index of each scaled event   */
+    const int32_t* scaled_index;  /* [E] position of event j among scaled events, -1 if binary */
+    /* workspace */
+    double*   rep;                /* [n_rows]                                     */
+    double*   tok;                /* [n_rows]                                     */
+    double*   T;                  /* [n_scaled][n_rows] rescaled scaled events, NaN = missing */
+    double*   part;               /* [col_blocks][E][8][2] column-pass block partials */
+    double*   mpart;              /* [col_blocks][E][4] block max/min partials     */
+    double*   cstat;              /* [world][E][16][2] per-rank column sums (dd)   */
+    double*   cmax;               /* [world][E][4] per-rank max rep / argmax / min / max */
+    double*   scal;               /* [world][16][2] per-rank scalar sums (dd)      */
+    double*   spart;              /* [4096][4][2] row-pass block partials          */
+    double*   ev;                 /* [16][E] event vectors (guess, mu, old, ...)   */
+    double*   cslab;              /* [cov_kslices][E][E] covariance partial tiles  */
+    double*   C;                  /* [E][E] covariance                             */
+    double*   pvec;               /* [4][E + 64] power-iteration scratch           */
+    double*   rowv;               /* [6][n_rows] scores, this, smooth, u, ...       */
+    uint32_t* rowstat;            /* [n_rows][2] NaN / zero counts per row         */
+    uint64_t* skey;               /* [world][4] score min/max keys, flags          */
+    int64_t*  info;               /* [16] host-visible status (branch, iterations, active columns) */
+    /* weighted-median selection state (per scaled event) */
+    uint64_t* sel_sum;            /* [world][n_scaled][256][4] limb sums + counts  */
+    uint64_t* sel_min;            /* [world][n_scaled][256][2] min key, min weight bits */
+    uint64_t* sel_max;            /* [world][n_scaled][256] max key                */
+    uint64_t* sel_state;          /* [n_scaled][16] range, sums, flags             */
+    double*   sel_val;            /* [world][n_scaled][4] max weight, value, result */
+    /* outputs ([E] events, [n_rows] agents of this rank) */
+    double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
+        *reporter_bonus;
+    double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
+        *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
+    double* scalars;              /* [4]: participation, avg_certainty, branch, flags */
+    double* original;             /* [n_rows][E] rescaled reports (PCX_M_MATRICES), optional */
+    double* filled;               /* [n_rows][E] filled reports (PCX_M_MATRICES), optional   */
+} pcx_mat;
+
+/* Run one stage on the context's stream (PCX_M_POWER and the selection steps may
+ * synchronise the stream to read convergence state). */
+int pcx_mat_stage(pcx_ctx* ctx, pcx_mat* m, int stage);
+
 #ifdef __cplusplus
 }
 #endif

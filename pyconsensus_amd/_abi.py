@@ -50,3 +50,38 @@ class BatchResult(C.Structure):
 
 def out_shape(kind, B, N, E):
     return {"N": (B, N), "E": (B, E), "1": (B,), "NE": (B, N, E)}[kind]
+
+
+# ---------------------------------------------------------------- single-matrix stages
+M_REPUTATION, M_COLSTATS, M_GUESS, M_MEAN, M_COV, M_COV_REDUCE, M_COV_FINISH, M_POWER = 1, 2, 3, 4, 5, 6, 7, 8
+M_SCORES, M_NCSUMS, M_GEMV2, M_DECIDE, M_REPU, M_SMOOTH, M_OUTCOMES, M_EVENTS = 9, 10, 11, 12, 13, 14, 15, 16
+M_SCALED_CERT, M_FINAL, M_ROWSUMS, M_AGENTS, M_MATRICES = 17, 18, 19, 20, 21
+M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH = 30, 31, 32, 33, 34, 35, 36
+M_ZERO_LOADING = 99
+
+# info[] slots (pcx_matrix.hip info_slot)
+INFO_BRANCH, INFO_PI_ITERS, INFO_FLAGS, INFO_SEL_ACTIVE, INFO_SEL_ARGMAX, INFO_PICK1 = 0, 1, 2, 3, 4, 5
+
+MAT_OUTPUT_AGENTS = ["old_rep", "this_rep", "smooth_rep", "scores", "na_row", "participation_rows",
+                     "relative_part", "reporter_bonus"]
+MAT_OUTPUT_EVENTS = ["adj_first_loadings", "outcomes_raw", "outcomes_adjusted", "outcomes_final",
+                     "certainty", "consensus_reward", "nas_filled", "participation_columns", "author_bonus"]
+
+_vp = C.c_void_p
+
+
+class Mat(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64), ("n_events", C.c_int64), ("n_total", C.c_int64), ("row_offset", C.c_int64),
+        ("world", C.c_int32), ("rank", C.c_int32), ("int_dtype", C.c_int32), ("algorithm", C.c_int32),
+        ("catch_tolerance", C.c_double), ("alpha", C.c_double),
+        ("n_scaled", C.c_int32), ("sel_phase", C.c_int32), ("col_blocks", C.c_int32),
+        ("cov_tiles", C.c_int32), ("cov_kslices", C.c_int32),
+        ("reports", _vp), ("scaled", _vp), ("lo", _vp), ("hi", _vp), ("rep_raw", _vp),
+        ("scaled_cols", _vp), ("scaled_index", _vp),
+        ("rep", _vp), ("tok", _vp), ("T", _vp), ("part", _vp), ("mpart", _vp), ("cstat", _vp),
+        ("cmax", _vp), ("scal", _vp), ("spart", _vp), ("ev", _vp), ("cslab", _vp), ("C", _vp),
+        ("pvec", _vp), ("rowv", _vp), ("rowstat", _vp), ("skey", _vp), ("info", _vp),
+        ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
+    ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),
+                                                                   ("filled", _vp)]

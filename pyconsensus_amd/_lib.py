@@ -36,6 +36,8 @@ def _declare(lib):
     lib.pcx_synchronize.restype = C.c_int
     lib.pcx_consensus_batched_f64.argtypes = [C.c_void_p, C.POINTER(_abi.Batch), C.POINTER(_abi.BatchResult)]
     lib.pcx_consensus_batched_f64.restype = C.c_int
+    lib.pcx_mat_stage.argtypes = [C.c_void_p, C.POINTER(_abi.Mat), C.c_int]
+    lib.pcx_mat_stage.restype = C.c_int
 
 
 def lib():

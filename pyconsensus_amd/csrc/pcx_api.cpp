@@ -124,4 +124,19 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");
 }
 
+int pcx_mat_stage(pcx_ctx* ctx, pcx_mat* m, int stage) {
+    if (!ctx || !m) return fail(PCX_EINVAL, "pcx_mat_stage: null argument");
+    if (m->n_rows < 1 || m->n_events < 1 || m->n_total < m->n_rows || !m->reports)
+        return fail(PCX_EINVAL, "pcx_mat_stage: bad shape or missing reports");
+    if (m->n_events > 65536) return fail(PCX_EINVAL, "pcx_mat_stage: n_events > 65536");
+    if (m->n_rows > 0x7fffffffll) return fail(PCX_EINVAL, "pcx_mat_stage: n_rows >= 2^31 per rank");
+    if (m->rank < 0 || m->rank >= m->world) return fail(PCX_EINVAL, "pcx_mat_stage: bad rank/world");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    std::string err;
+    e = pcx::mat_stage(*m, stage, ctx->stream, err);
+    if (!err.empty()) return fail(PCX_EINVAL, err);
+    return e == hipSuccess ? PCX_OK : hip_fail(e, "pcx_mat_stage");
+}
+
 }  // extern "C"

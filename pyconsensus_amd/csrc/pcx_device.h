@@ -51,8 +51,7 @@ struct acc2 {
         s = t.hi;
         c = c + (pe + t.lo);
     }
-    __device__ __forceinline__ dd get() const { return fast_two_sum_safe(s, c); }
-    __device__ __forceinline__ static dd fast_two_sum_safe(double a, double b) { return two_sum(a, b); }
+    __device__ __forceinline__ dd get() const { return two_sum(s, c); }
 };
 
 __device__ __forceinline__ double dd_to_double(dd a) { return a.hi + a.lo; }

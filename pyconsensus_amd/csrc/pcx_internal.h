@@ -4,6 +4,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
+#include "../../include/pcx.h"
+
 namespace pcx {
 
 // Kernel arguments of the batched round kernel (by value).
@@ -31,5 +35,8 @@ struct BatchArgs {
 
 size_t batched_lds_bytes(int N, int E);
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream);
+
+// single-matrix path: launch one stage (pcx_matrix.hip)
+hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t stream, std::string& err);
 
 }  // namespace pcx

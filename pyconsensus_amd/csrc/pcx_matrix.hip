@@ -1,0 +1,1507 @@
+// pcx_matrix.hip -- the single-matrix consensus path on MI355X (gfx950).
+//
+// One N x E report matrix (row-major fp64, NaN = missing), optionally sharded by
+// reporter rows over several GPUs.  The stages of pcx_mat_stage() (include/pcx.h)
+// restate pyconsensus Oracle.consensus(), algorithm="PCA"
+// (pyconsensus/__init__.py:102-611):
+//
+//   * every pass over the matrix recomputes the element transform on the fly
+//     (rescale of scaled events :266-269, NA test :278, fill :310-312, centring
+//     :322) instead of materialising rescaled / filled / centred copies;
+//   * column sums (np.dot(v, F) and the interpolation sums) are compensated
+//     (double-double) so they are within an ulp of exact -- the reference's own
+//     order is OpenBLAS-internal or a sequential Python loop;
+//   * the covariance wcd^T diag(tokens) wcd (:326) runs on fp64 MFMA
+//     (v_mfma_f64_16x16x4_f64) with LDS-staged 128x128 tiles, split-K over rows;
+//   * the leading eigenvector (svd, :330) comes from power iteration;
+//   * weighted medians (weightedstats, :303, :520) are exact weighted selections
+//     over an order-preserving integer key of the values, with weights summed as
+//     exact fixed-point limbs (order-independent, identical on any GPU count).
+//
+// Per-rank partial results are written into slot [rank] of [world][...] buffers;
+// the host all-reduces (SUM) them between stages and the next stage combines the
+// ranks in rank order, so results do not depend on the communication algorithm.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pcx.h"
+#include "pcx_device.h"
+#include "pcx_internal.h"
+
+namespace pcx {
+namespace {
+
+constexpr int CS = 16;           // dd slots per column in cstat
+constexpr int SS = 16;           // dd slots in scal
+constexpr int NB = 256;          // selection buckets
+constexpr int SELS = 16;         // sel_state words per scaled event
+constexpr int BT = 256;          // threads per block for row/column passes
+
+enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
+               EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
+enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH };
+enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP };
+enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1 };
+
+// ------------------------------------------------------------------ element transform
+struct ColParam {
+    bool scaled;
+    double lo, range, guess, mu;
+};
+
+__device__ __forceinline__ double rescale(double r, const ColParam& p, int int_dtype) {
+    if (!p.scaled) return r;
+    double x = (r - p.lo) / p.range;
+    if (int_dtype) x = trunc(x);
+    return x;
+}
+
+__device__ __forceinline__ bool missing(double x) { return __builtin_isnan(x) || x == 0.0; }
+
+__device__ __forceinline__ ColParam col_param(const pcx_mat& m, int c, bool with_fill) {
+    ColParam p;
+    p.scaled = m.scaled && m.scaled[c];
+    p.lo = p.scaled ? m.lo[c] : 0.0;
+    p.range = p.scaled ? (m.hi[c] - m.lo[c]) : 1.0;
+    p.guess = with_fill ? m.ev[EV_GUESS * m.n_events + c] : 0.0;
+    p.mu = with_fill ? m.ev[EV_MU * m.n_events + c] : 0.0;
+    return p;
+}
+
+// filled value F_ic (:310-312)
+__device__ __forceinline__ double filled(double r, const ColParam& p, int int_dtype) {
+    const double x = rescale(r, p, int_dtype);
+    return missing(x) ? p.guess : x;
+}
+
+// ------------------------------------------------------------------ block reductions
+template <int NT>
+__device__ dd block_sum_dd(dd v, dd* lds) {
+    v = wave_sum_dd(v);
+    const int w = threadIdx.x / WAVE, l = threadIdx.x % WAVE;
+    __syncthreads();
+    if (l == 0) lds[w] = v;
+    __syncthreads();
+    dd r{0.0, 0.0};
+    if (threadIdx.x == 0)
+        for (int i = 0; i < NT / WAVE; i++) r = dd_add(r, lds[i]);
+    __syncthreads();
+    return r;  // valid on thread 0
+}
+
+__device__ __forceinline__ dd ld_dd(const double* p) { return {p[0], p[1]}; }
+__device__ __forceinline__ void st_dd(double* p, dd v) {
+    p[0] = v.hi;
+    p[1] = v.lo;
+}
+
+// sum over ranks (rank order) of a [world][stride] dd buffer at offset
+__device__ __forceinline__ dd rank_sum(const double* buf, int world, int64_t stride, int64_t off) {
+    dd r{0.0, 0.0};
+    for (int w = 0; w < world; w++) r = dd_add(r, ld_dd(buf + w * stride + off));
+    return r;
+}
+
+// ------------------------------------------------------------------ limbs (exact sums)
+struct L3 {
+    uint64_t a, b, c;  // value = a*2^-35 + b*2^-78 + c*2^-121
+};
+
+__device__ __forceinline__ L3 l3_norm(L3 x) {  // carry so that b, c < 2^43
+    const uint64_t M = (1ull << 43) - 1;
+    x.b += x.c >> 43;
+    x.c &= M;
+    x.a += x.b >> 43;
+    x.b &= M;
+    return x;
+}
+__device__ __forceinline__ L3 l3_add(L3 x, L3 y) { return l3_norm({x.a + y.a, x.b + y.b, x.c + y.c}); }
+__device__ __forceinline__ L3 l3_twice(L3 x) { return l3_norm({x.a * 2, x.b * 2, x.c * 2}); }
+__device__ __forceinline__ int l3_cmp(L3 x, L3 y) {  // both normalised
+    if (x.a != y.a) return x.a < y.a ? -1 : 1;
+    if (x.b != y.b) return x.b < y.b ? -1 : 1;
+    if (x.c != y.c) return x.c < y.c ? -1 : 1;
+    return 0;
+}
+__device__ __forceinline__ L3 l3_of(double w) {
+    const limbs3 t = to_limbs(w);
+    return {t.l0, t.l1, t.l2};
+}
+__device__ __forceinline__ double l3_to_double(L3 x) {
+    return ldexp((double)x.a, -35) + (ldexp((double)x.b, -78) + ldexp((double)x.c, -121));
+}
+
+// ================================================================== PCX_M_REPUTATION
+__global__ void __launch_bounds__(1024) k_rep_total(pcx_mat m) {
+    __shared__ dd lds[16];
+    acc2 a;
+    for (int64_t i = threadIdx.x; i < m.n_total; i += blockDim.x) a.add(m.rep_raw[i]);
+    dd v = block_sum_dd<1024>(a.get(), lds);
+    if (threadIdx.x == 0) {
+        m.pvec[0] = dd_to_double(v);  // total reputation (np.sum, :144)
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
+    __shared__ dd lds[8];
+    acc2 at, ar;
+    const double tot = m.rep_raw ? m.pvec[0] : 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double r = m.rep_raw ? m.rep_raw[m.row_offset + i] / tot : 1.0 / (double)m.n_total;
+        const double t = trunc(r * 1e6);
+        m.rep[i] = r;
+        m.tok[i] = t;
+        at.add(t);
+        ar.add(r);
+    }
+    dd st = block_sum_dd<BT>(at.get(), lds);
+    dd sr = block_sum_dd<BT>(ar.get(), lds);
+    if (threadIdx.x == 0) {
+        st_dd(m.spart + blockIdx.x * 8 + 0, st);
+        st_dd(m.spart + blockIdx.x * 8 + 2, sr);
+    }
+}
+
+// reduce spart[nblk][4 dd] into scal[rank][slot0 .. slot0+k)
+__global__ void __launch_bounds__(64) k_spart_finish(pcx_mat m, int nblk, int k, int slot0) {
+    const int j = threadIdx.x;
+    if (j >= k) return;
+    dd r{0.0, 0.0};
+    for (int b = 0; b < nblk; b++) r = dd_add(r, ld_dd(m.spart + b * 8 + 2 * j));
+    st_dd(m.scal + ((int64_t)m.rank * SS + slot0 + j) * 2, r);
+}
+
+// ================================================================== column passes
+// grid (ceil(E/BT), G): thread = one event column, loop over a chunk of rows.
+__device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t& r1) {
+    const int64_t per = (m.n_rows + gridDim.y - 1) / gridDim.y;
+    r0 = (int64_t)blockIdx.y * per;
+    r1 = r0 + per < m.n_rows ? r0 + per : m.n_rows;
+}
+
+// PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
+// min/max present value; writes the scaled columns (column-major) into T.
+__global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c >= m.n_events) return;
+    const int E = (int)m.n_events;
+    const ColParam p = col_param(m, c, false);
+    const int si = m.scaled_index ? m.scaled_index[c] : -1;
+    double* Tc = si >= 0 ? m.T + (int64_t)si * m.n_rows : nullptr;
+    int64_t r0, r1;
+    row_range(m, r0, r1);
+    acc2 sr, srx;
+    double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+    for (int64_t i = r0; i < r1; i++) {
+        const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
+        const bool isn = __builtin_isnan(x);
+        const bool z = x == 0.0;
+        if (Tc) Tc[i] = (isn || z) ? __builtin_nan("") : x;
+        nz += z ? 1.0 : 0.0;
+        if (isn || z) continue;
+        const double r = m.rep[i];
+        cnt += 1.0;
+        sr.add(r);
+        srx.add_prod(r, x);
+        if (r > mx) {
+            mx = r;
+            arg = (double)(m.row_offset + i);
+        }
+        mn_x = fmin(mn_x, x);
+        mx_x = fmax(mx_x, x);
+    }
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, {cnt, 0.0});
+    st_dd(pp + 2, sr.get());
+    st_dd(pp + 4, srx.get());
+    st_dd(pp + 6, {nz, 0.0});
+    double* mp = m.mpart + ((int64_t)blockIdx.y * E + c) * 4;
+    mp[0] = mx;
+    mp[1] = arg;
+    mp[2] = mn_x;
+    mp[3] = mx_x;
+}
+
+// reduce part[G][E][k] over G (in order) into cstat[rank][E][base + k]; optional max partials
+__global__ void __launch_bounds__(BT) k_col_finish(pcx_mat m, int G, int k, int base, int with_max) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    for (int j = 0; j < k; j++) {
+        dd r{0.0, 0.0};
+        for (int g = 0; g < G; g++) r = dd_add(r, ld_dd(m.part + ((int64_t)g * E + c) * 16 + 2 * j));
+        st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + base + j) * 2, r);
+    }
+    if (with_max) {
+        double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+        for (int g = 0; g < G; g++) {
+            const double* mp = m.mpart + ((int64_t)g * E + c) * 4;
+            if (mp[0] > mx) {
+                mx = mp[0];
+                arg = mp[1];
+            }
+            mn_x = fmin(mn_x, mp[2]);
+            mx_x = fmax(mx_x, mp[3]);
+        }
+        double* o = m.cmax + ((int64_t)m.rank * E + c) * 4;
+        o[0] = mx;
+        o[1] = arg;
+        o[2] = mn_x;
+        o[3] = mx_x;
+    }
+}
+
+__device__ __forceinline__ dd cst(const pcx_mat& m, int c, int slot) {
+    return rank_sum(m.cstat, m.world, m.n_events * CS * 2, ((int64_t)c * CS + slot) * 2);
+}
+__device__ __forceinline__ dd scl(const pcx_mat& m, int slot) {
+    return rank_sum(m.scal, m.world, SS * 2, (int64_t)slot * 2);
+}
+
+// PCX_M_GUESS: interpolation fills of binary events; mark scaled events that need a median
+__global__ void __launch_bounds__(BT) k_guess(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    const dd cnt = cst(m, c, 0);
+    const dd S_r = cst(m, c, 1);
+    const dd S_rx = cst(m, c, 2);
+    const double present = dd_to_double(cnt);
+    const double miss = (double)m.n_total - present;
+    double mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+    for (int w = 0; w < m.world; w++) {
+        mn_x = fmin(mn_x, m.cmax[((int64_t)w * E + c) * 4 + 2]);
+        mx_x = fmax(mx_x, m.cmax[((int64_t)w * E + c) * 4 + 3]);
+    }
+    m.ev[EV_MINX * E + c] = mn_x;
+    m.ev[EV_MAXX * E + c] = mx_x;
+    m.ev[EV_MISS * E + c] = miss;
+    m.ev[EV_NZERO * E + c] = dd_to_double(cst(m, c, 3));
+    const bool sc = m.scaled && m.scaled[c];
+    double g = 0.0;
+    if (!sc) {
+        // sequential weighted mean of the present reports, then catch (:304-309)
+        g = present > 0 ? catch_value(dd_div(S_rx, S_r), m.catch_tolerance) : catch_value(0.0, m.catch_tolerance);
+        if (m.int_dtype) g = trunc(g);
+    }
+    m.ev[EV_GUESS * E + c] = g;  // scaled events: phase-1 median (PCX_M_SEL_*)
+}
+
+// PCX_M_MEAN: mu = rep . F / sum(rep) (np.ma.average, :317-319); old = rep . F (:490)
+__global__ void __launch_bounds__(BT) k_mean(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    const dd S_r = cst(m, c, 1);
+    const dd S_rx = cst(m, c, 2);
+    const dd R_tot = scl(m, SC_REP);
+    const double g = m.ev[EV_GUESS * E + c];
+    const dd miss_w = dd_sub(R_tot, S_r);  // reputation of the filled cells
+    const dd num = m.ev[EV_MISS * E + c] > 0 ? dd_add(S_rx, dd_mul_d(miss_w, g)) : S_rx;
+    m.ev[EV_OLD * E + c] = dd_to_double(num);
+    m.ev[EV_MU * E + c] = dd_div(num, R_tot);
+}
+
+// ================================================================== covariance (fp64 MFMA)
+typedef double d4 __attribute__((ext_vector_type(4)));
+constexpr int CT = 128;          // C tile edge
+constexpr int KB = 16;           // rows staged per step
+constexpr int LDP = CT + 16;     // padded LDS row (bank-conflict-free b64 fragment reads)
+
+__device__ __forceinline__ void tri_index(int t, int& I, int& J) {
+    int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) i++;
+    while (i * (i + 1) / 2 > t) i--;
+    I = i;
+    J = t - i * (i + 1) / 2;
+}
+
+// one work item = (lower-triangle tile (I,J), row slice ks).  C_part[p][q] over the slice's
+// rows of (tok_i * wcd_ip) * wcd_iq, with wcd = F - mu computed on the fly.
+__global__ void __launch_bounds__(256) k_cov(pcx_mat m) {
+    __shared__ __attribute__((aligned(16))) double As[KB][LDP];
+    __shared__ __attribute__((aligned(16))) double Bs[KB][LDP];
+    __shared__ double prm[2][5][CT];  // side, {scaled, lo, range, guess, mu}
+    const int E = (int)m.n_events;
+    const int ntiles = m.cov_tiles, nks = m.cov_kslices;
+    const int item = blockIdx.x;
+    const int ks = item / ntiles, t = item % ntiles;
+    int I, J;
+    tri_index(t, I, J);
+    const bool diag = I == J;
+    const int64_t per = (m.n_rows + nks - 1) / nks;
+    const int64_t rb = (int64_t)ks * per;
+    const int64_t re = rb + per < m.n_rows ? rb + per : m.n_rows;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    for (int s = 0; s < 2; s++)
+        for (int q = tid; q < CT; q += 256) {
+            const int c = (s == 0 ? I : J) * CT + q;
+            double sc = 0, lo = 0, rg = 1, g = 0, mu = 0;
+            if (c < E) {
+                const ColParam p = col_param(m, c, true);
+                sc = p.scaled ? 1.0 : 0.0;
+                lo = p.lo;
+                rg = p.range;
+                g = p.guess;
+                mu = p.mu;
+            }
+            prm[s][0][q] = sc;
+            prm[s][1][q] = lo;
+            prm[s][2][q] = rg;
+            prm[s][3][q] = g;
+            prm[s][4][q] = mu;
+        }
+    __syncthreads();
+    d4 acc[4][4];
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int sr = tid >> 4;        // staged row 0..15
+    const int scg = (tid & 15) * 8; // staged column group
+    double va[8], vb[8];
+    auto load = [&](int64_t i0) {
+        const int64_t i = i0 + sr;
+        const bool rowok = i < re;
+        const double tk = rowok ? m.tok[i] : 0.0;
+        for (int s = 0; s < (diag ? 1 : 2); s++) {
+            const int cb = (s == 0 ? I : J) * CT;
+            for (int k = 0; k < 8; k++) {
+                const int q = scg + k;
+                const int c = cb + q;
+                double w = 0.0;
+                if (rowok && c < E) {
+                    double x = m.reports[i * E + c];
+                    if (prm[s][0][q] != 0.0) {
+                        x = (x - prm[s][1][q]) / prm[s][2][q];
+                        if (m.int_dtype) x = trunc(x);
+                    }
+                    if (missing(x)) x = prm[s][3][q];
+                    w = x - prm[s][4][q];
+                }
+                if (s == 0) {
+                    va[k] = w * tk;  // np.ma.multiply(wcd.T, tokens): product rounded first
+                    if (diag) vb[k] = w;
+                } else {
+                    vb[k] = w;
+                }
+            }
+        }
+    };
+    auto store = [&]() {
+        for (int k = 0; k < 8; k++) {
+            As[sr][scg + k] = va[k];
+            Bs[sr][scg + k] = vb[k];
+        }
+    };
+    if (rb < re) load(rb);
+    for (int64_t i0 = rb; i0 < re; i0 += KB) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (i0 + KB < re) load(i0 + KB);  // prefetch the next rows under the MFMAs
+#pragma unroll
+        for (int kk = 0; kk < KB / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr][wr * 64 + a * 16 + (lane & 15)];
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[kr][wc * 64 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
+    double* slab = m.cslab + (int64_t)ks * E * E;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++)
+            for (int r = 0; r < 4; r++) {
+                const int p = I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
+                const int q = J * CT + wc * 64 + b * 16 + (lane & 15);
+                if (p < E && q < E) slab[(int64_t)p * E + q] = acc[a][b][r];
+            }
+}
+
+// PCX_M_COV_REDUCE: C = sum of slabs over the lower triangle, mirrored (unnormalised)
+__global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
+    const int64_t E = m.n_events;
+    const int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x;
+    if (idx >= E * E) return;
+    const int64_t p = idx / E, q = idx % E;
+    if (q > p) return;
+    double s = 0.0;
+    for (int k = 0; k < m.cov_kslices; k++) s += m.cslab[(int64_t)k * E * E + p * E + q];
+    m.C[p * E + q] = s;
+    m.C[q * E + p] = s;
+}
+
+// PCX_M_COV_FINISH: divide by (sum tokens - 1) (:326)
+__global__ void __launch_bounds__(BT) k_cov_finish(pcx_mat m) {
+    const int64_t E = m.n_events;
+    const int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x;
+    if (idx >= E * E) return;
+    const double denom = dd_to_double(scl(m, SC_TOK)) - 1.0;
+    m.C[idx] = m.C[idx] / denom;
+}
+
+// ================================================================== power iteration
+// pvec layout: [0..E) x, [E+64 .. 2E+64) y, scalars at pvec[3*(E+64) + k]
+__device__ __forceinline__ double* pv_x(const pcx_mat& m) { return m.pvec; }
+__device__ __forceinline__ double* pv_y(const pcx_mat& m) { return m.pvec + (m.n_events + 64); }
+__device__ __forceinline__ double* pv_s(const pcx_mat& m) { return m.pvec + 3 * (m.n_events + 64); }
+
+__global__ void __launch_bounds__(BT) k_pi_check(pcx_mat m) {
+    const int64_t E = m.n_events;
+    int nonfinite = 0, nonzero = 0;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < E * E; i += (int64_t)gridDim.x * BT) {
+        const double c = m.C[i];
+        nonfinite |= !__builtin_isfinite(c);
+        nonzero |= c != 0.0;
+    }
+    if (__any(nonfinite) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&m.info[IN_FLAGS], 2ull);
+    if (__any(nonzero) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&m.info[IN_FLAGS], 8ull);
+}
+
+// start vector: column of C with the largest diagonal entry (first), normalised
+__global__ void __launch_bounds__(1024) k_pi_start(pcx_mat m) {
+    __shared__ double sv[1024];
+    __shared__ int si[1024];
+    __shared__ dd lds[16];
+    const int E = (int)m.n_events;
+    double best = -__builtin_inf();
+    int bi = 0;
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        const double d = m.C[(int64_t)j * E + j];
+        if (d > best) {
+            best = d;
+            bi = j;
+        }
+    }
+    sv[threadIdx.x] = best;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int s = 512; s >= 1; s >>= 1) {
+        if (threadIdx.x < s) {
+            const double o = sv[threadIdx.x + s];
+            const int oi = si[threadIdx.x + s];
+            if (o > sv[threadIdx.x] || (o == sv[threadIdx.x] && oi < si[threadIdx.x])) {
+                sv[threadIdx.x] = o;
+                si[threadIdx.x] = oi;
+            }
+        }
+        __syncthreads();
+    }
+    const int kd = si[0];
+    acc2 a;
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        const double x = m.C[(int64_t)j * E + kd];
+        a.add(x * x);
+    }
+    const dd n2 = block_sum_dd<1024>(a.get(), lds);
+    __shared__ double nrm;
+    if (threadIdx.x == 0) nrm = sqrt(dd_to_double(n2));
+    __syncthreads();
+    for (int j = threadIdx.x; j < E; j += 1024) pv_x(m)[j] = m.C[(int64_t)j * E + kd] / nrm;
+}
+
+// y = C x, one wavefront per row
+__global__ void __launch_bounds__(BT) k_pi_gemv(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const int row = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    if (row >= E) return;
+    const double* Cr = m.C + (int64_t)row * E;
+    const double* x = pv_x(m);
+    double acc = 0.0;
+    for (int q = lane; q < E; q += WAVE) acc = fma(Cr[q], x[q], acc);
+    acc = wave_sum_d(acc);
+    if (lane == 0) pv_y(m)[row] = acc;
+}
+
+// x <- y / |y|; delta = max |x_new - x_old|  (pv_s[0] = delta)
+__global__ void __launch_bounds__(1024) k_pi_norm(pcx_mat m) {
+    __shared__ dd lds[16];
+    __shared__ double red[1024];
+    __shared__ double nrm;
+    const int E = (int)m.n_events;
+    acc2 a;
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        const double y = pv_y(m)[j];
+        a.add(y * y);
+    }
+    const dd n2 = block_sum_dd<1024>(a.get(), lds);
+    if (threadIdx.x == 0) nrm = sqrt(dd_to_double(n2));
+    __syncthreads();
+    double d = 0.0;
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        const double xn = pv_y(m)[j] / nrm;
+        d = fmax(d, fabs(xn - pv_x(m)[j]));
+        pv_x(m)[j] = xn;
+    }
+    red[threadIdx.x] = d;
+    __syncthreads();
+    for (int s = 512; s >= 1; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) pv_s(m)[0] = red[0];
+}
+
+// loading (:336): sign rule of the batched SPEC, then v / sqrt(sum v^2)
+__global__ void __launch_bounds__(1024) k_pi_finish(pcx_mat m, int mode) {
+    __shared__ dd lds[16];
+    __shared__ int first_nz, nnz;
+    __shared__ double scale;
+    const int E = (int)m.n_events;
+    double* x = pv_x(m);
+    if (threadIdx.x == 0) {
+        first_nz = E;
+        nnz = 0;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        double v = mode == 1 ? 1.0 : (mode == 2 ? (j == 0 ? 1.0 : 0.0) : x[j]);
+        x[j] = v;
+        if (v != 0.0) {
+            atomicMin(&first_nz, j);
+            atomicAdd(&nnz, 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 1.0;
+        if (mode == 0 && first_nz < E) {
+            const double xf = x[first_nz];
+            const bool neg = nnz == 1 ? xf < 0.0 : xf > 0.0;
+            s = neg ? -1.0 : 1.0;
+        }
+        scale = s;
+    }
+    __syncthreads();
+    acc2 a;
+    for (int j = threadIdx.x; j < E; j += 1024) {
+        const double v = x[j] * scale;
+        x[j] = v;
+        a.add(v * v);
+    }
+    const dd n2 = block_sum_dd<1024>(a.get(), lds);
+    __shared__ double nv;
+    if (threadIdx.x == 0) nv = sqrt(dd_to_double(n2));
+    __syncthreads();
+    for (int j = threadIdx.x; j < E; j += 1024) m.ev[EV_LD * E + j] = x[j] / nv;
+}
+
+// ================================================================== row passes
+// PCX_M_SCORES: s_i = sum_j wcd_ij * loading_j (:337), one wavefront per row;
+// per-row NaN / zero counts; min/max keys of the scores.
+__global__ void __launch_bounds__(BT) k_scores(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const int lane = threadIdx.x % WAVE;
+    const int64_t row0 = blockIdx.x * (int64_t)(BT / WAVE) + threadIdx.x / WAVE;
+    uint64_t kmin = ~0ull, kmax = 0;
+    bool anynan = false;
+    for (int64_t i = row0; i < m.n_rows; i += (int64_t)gridDim.x * (BT / WAVE)) {
+        double acc = 0.0;
+        int nn = 0, nz = 0;
+        for (int c = lane; c < E; c += WAVE) {
+            const ColParam p = col_param(m, c, true);
+            const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
+            nn += __builtin_isnan(x) ? 1 : 0;
+            nz += x == 0.0 ? 1 : 0;
+            const double f = missing(x) ? p.guess : x;
+            if (m.algorithm == 0) acc = fma(f - p.mu, m.ev[EV_LD * E + c], acc);
+        }
+        acc = wave_sum_d(acc);
+        for (int s = 32; s >= 1; s >>= 1) {
+            nn += __shfl_xor(nn, s, WAVE);
+            nz += __shfl_xor(nz, s, WAVE);
+        }
+        if (lane == 0) {
+            m.rowv[RV_S * m.n_rows + i] = acc;
+            m.rowstat[2 * i] = nn;
+            m.rowstat[2 * i + 1] = nz;
+        }
+        if (__builtin_isnan(acc)) anynan = true;
+        const uint64_t k = dkey(acc);
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+    }
+    if (lane == 0) {
+        uint64_t* sk = m.skey + (int64_t)m.rank * 4;
+        atomicMin((unsigned long long*)&sk[0], (unsigned long long)kmin);
+        atomicMax((unsigned long long*)&sk[1], (unsigned long long)kmax);
+        if (anynan) atomicOr((unsigned long long*)&sk[2], 1ull);
+    }
+}
+
+__global__ void k_skey_init(pcx_mat m) {
+    uint64_t* sk = m.skey + (int64_t)m.rank * 4;
+    sk[0] = ~0ull;
+    sk[1] = 0;
+    sk[2] = 0;
+    sk[3] = 0;
+}
+
+__device__ __forceinline__ void score_minmax(const pcx_mat& m, double& mn, double& mx) {
+    uint64_t kmin = ~0ull, kmax = 0, nan = 0;
+    for (int w = 0; w < m.world; w++) {
+        const uint64_t* sk = m.skey + (int64_t)w * 4;
+        kmin = sk[0] < kmin ? sk[0] : kmin;
+        kmax = sk[1] > kmax ? sk[1] : kmax;
+        nan |= sk[2];
+    }
+    mn = nan ? __builtin_nan("") : dkey_inv(kmin);
+    mx = nan ? __builtin_nan("") : dkey_inv(kmax);
+}
+
+// PCX_M_NCSUMS: sum |set1|, sum |set1|+1, sum |set2|, sum |set2|+1 (normalize, :244-249)
+__global__ void __launch_bounds__(BT) k_ncsums(pcx_mat m) {
+    __shared__ dd lds[8];
+    double mn, mx;
+    score_minmax(m, mn, mx);
+    acc2 a1, a1p, a2, a2p;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double s = m.rowv[RV_S * m.n_rows + i];
+        const double v1 = fabs(s + fabs(mn)), v2 = fabs(s - mx);
+        a1.add(v1);
+        a1p.add(v1 + 1.0);
+        a2.add(v2);
+        a2p.add(v2 + 1.0);
+    }
+    const dd r0 = block_sum_dd<BT>(a1.get(), lds), r1 = block_sum_dd<BT>(a1p.get(), lds);
+    const dd r2 = block_sum_dd<BT>(a2.get(), lds), r3 = block_sum_dd<BT>(a2p.get(), lds);
+    if (threadIdx.x == 0) {
+        st_dd(m.spart + blockIdx.x * 8 + 0, r0);
+        st_dd(m.spart + blockIdx.x * 8 + 2, r1);
+        st_dd(m.spart + blockIdx.x * 8 + 4, r2);
+        st_dd(m.spart + blockIdx.x * 8 + 6, r3);
+    }
+}
+
+// normalize(set) weight of row i: |v| / sum |v| (or (|v|+1)/sum(|v|+1) when sum |v| == 0)
+__device__ __forceinline__ double nweight(double v, double S, double Sp) {
+    return S == 0.0 ? (v + 1.0) / Sp : v / S;
+}
+
+// PCX_M_GEMV2: d1 = normalize(set1) . F, d2 = normalize(set2) . F  (:492-493)
+__global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    double mn, mx;
+    score_minmax(m, mn, mx);
+    const double S1 = dd_to_double(scl(m, SC_A1)), S1p = dd_to_double(scl(m, SC_A1P));
+    const double S2 = dd_to_double(scl(m, SC_A2)), S2p = dd_to_double(scl(m, SC_A2P));
+    const ColParam p = col_param(m, c, true);
+    int64_t r0, r1;
+    row_range(m, r0, r1);
+    acc2 a1, a2;
+    for (int64_t i = r0; i < r1; i++) {
+        const double f = filled(m.reports[i * E + c], p, m.int_dtype);
+        const double s = m.rowv[RV_S * m.n_rows + i];
+        a1.add_prod(nweight(fabs(s + fabs(mn)), S1, S1p), f);
+        a2.add_prod(nweight(fabs(s - mx), S2, S2p), f);
+    }
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, a1.get());
+    st_dd(pp + 2, a2.get());
+}
+
+// PCX_M_DECIDE: ranks of old, new1, new2 (scipy rankdata 'average') and the rule (:487-500)
+__global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
+    __shared__ dd lds[16];
+    __shared__ double red[1024];
+    const int E = (int)m.n_events;
+    double* old = m.ev + EV_OLD * E;
+    double* n1 = m.ev + EV_D1 * E;   // new1 = normalize(set1) . F + 0.01 * old
+    double* n2 = m.ev + EV_D2 * E;   // new2
+    double* raw1 = m.pvec + 2 * (m.n_events + 64);  // normalize(set1) . F (continuous rule)
+    double* raw2 = pv_y(m);                          // normalize(set2) . F
+    for (int c = threadIdx.x; c < E; c += 1024) {
+        const double a = dd_to_double(cst(m, c, 4));
+        const double b = dd_to_double(cst(m, c, 5));
+        const double t = 0.01 * old[c];
+        n1[c] = a + t;
+        n2[c] = b + t;
+        raw1[c] = a;
+        raw2[c] = b;
+    }
+    __syncthreads();
+    double e1 = 0.0, e2 = 0.0;
+    for (int c = threadIdx.x; c < E; c += 1024) {
+        int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0, lt2 = 0, eq2 = 0;
+        const double o = old[c], a = n1[c], b = n2[c];
+        for (int k = 0; k < E; k++) {
+            const double ok = old[k], ak = n1[k], bk = n2[k];
+            lt0 += ok < o;
+            eq0 += ok == o;
+            lt1 += ak < a;
+            eq1 += ak == a;
+            lt2 += bk < b;
+            eq2 += bk == b;
+        }
+        const double r0 = lt0 + (eq0 + 1) * 0.5, r1 = lt1 + (eq1 + 1) * 0.5, r2 = lt2 + (eq2 + 1) * 0.5;
+        e1 += fabs(r1 - r0);
+        e2 += fabs(r2 - r0);
+    }
+    // half-integer sums are exact in any order
+    red[threadIdx.x] = e1 - e2;
+    __syncthreads();
+    for (int s = 512; s >= 1; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const double ref = red[0];
+    __syncthreads();
+    int branch, pick1;
+    if (ref == 0) {
+        acc2 q1, q2;
+        for (int c = threadIdx.x; c < E; c += 1024) {
+            const double a = raw1[c] - old[c];
+            const double b = raw2[c] - old[c];
+            q1.add(a * a);
+            q2.add(b * b);
+        }
+        const dd s1 = block_sum_dd<1024>(q1.get(), lds);
+        const dd s2 = block_sum_dd<1024>(q2.get(), lds);
+        __shared__ int pk;
+        if (threadIdx.x == 0) pk = dd_to_double(dd_sub(s1, s2)) <= 0 ? 1 : 0;
+        __syncthreads();
+        pick1 = pk;
+        branch = pick1 ? 3 : 4;
+    } else {
+        pick1 = ref < 0;
+        branch = pick1 ? 1 : 2;
+    }
+    if (threadIdx.x == 0) {
+        m.info[IN_BRANCH] = branch;
+        m.info[IN_PICK1] = pick1;
+    }
+}
+
+// PCX_M_REPU: u_i = |nc_i * (rep_i / mean(rep))| and its sums (:460-462)
+__global__ void __launch_bounds__(BT) k_repu(pcx_mat m) {
+    __shared__ dd lds[8];
+    double mn, mx;
+    score_minmax(m, mn, mx);
+    const double mean = dd_to_double(scl(m, SC_REP)) / (double)m.n_total;
+    const int pick1 = (int)m.info[IN_PICK1];
+    acc2 a, ap;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        double nc = 0.0;
+        if (m.algorithm == 0) {
+            const double s = m.rowv[RV_S * m.n_rows + i];
+            nc = pick1 ? s + fabs(mn) : s - mx;
+        }
+        const double u = fabs(nc * (m.rep[i] / mean));
+        m.rowv[RV_U * m.n_rows + i] = u;
+        a.add(u);
+        ap.add(u + 1.0);
+    }
+    const dd r0 = block_sum_dd<BT>(a.get(), lds), r1 = block_sum_dd<BT>(ap.get(), lds);
+    if (threadIdx.x == 0) {
+        st_dd(m.spart + blockIdx.x * 8 + 0, r0);
+        st_dd(m.spart + blockIdx.x * 8 + 2, r1);
+    }
+}
+
+// PCX_M_SMOOTH: this_rep = normalize(u); smooth_rep = alpha*this + (1-alpha)*rep (:460-472)
+__global__ void __launch_bounds__(BT) k_smooth(pcx_mat m) {
+    const double S = dd_to_double(scl(m, SC_U)), Sp = dd_to_double(scl(m, SC_UP));
+    const double a = m.alpha, oma = 1.0 - m.alpha;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double t = nweight(m.rowv[RV_U * m.n_rows + i], S, Sp);
+        m.rowv[RV_THIS * m.n_rows + i] = t;
+        m.rowv[RV_SMOOTH * m.n_rows + i] = a * t + oma * m.rep[i];
+    }
+}
+
+// PCX_M_OUTCOMES: smooth . F (:510), smooth . na (:559), certainty bins for binary events
+__global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    const ColParam p = col_param(m, c, true);
+    int64_t r0, r1;
+    row_range(m, r0, r1);
+    acc2 raw, pc, b1, b15, b2;
+    double n1 = 0, n15 = 0, n2 = 0;
+    for (int64_t i = r0; i < r1; i++) {
+        const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
+        const bool ms = missing(x);
+        const double f = ms ? p.guess : x;
+        const double w = m.rowv[RV_SMOOTH * m.n_rows + i];
+        raw.add_prod(w, f);
+        if (ms) pc.add(w);
+        if (f == 1.0) {
+            b1.add(w);
+            n1 += 1;
+        } else if (f == 1.5) {
+            b15.add(w);
+            n15 += 1;
+        } else if (f == 2.0) {
+            b2.add(w);
+            n2 += 1;
+        }
+    }
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, raw.get());
+    st_dd(pp + 2, pc.get());
+    st_dd(pp + 4, b1.get());
+    st_dd(pp + 6, b15.get());
+    st_dd(pp + 8, b2.get());
+    st_dd(pp + 10, {n1, 0.0});
+    st_dd(pp + 12, {n15, 0.0});
+    st_dd(pp + 14, {n2, 0.0});
+}
+
+// PCX_M_EVENTS: binary outcomes (:526-531), certainty of binary events (:540-546)
+__global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    const bool sc = m.scaled && m.scaled[c];
+    m.ev[EV_PC * E + c] = 1.0 - dd_to_double(cst(m, c, 7));
+    if (sc) return;  // scaled events: phase-2 median
+    const double raw = dd_to_double(cst(m, c, 6));
+    const double adj = catch_value(raw, m.catch_tolerance);
+    const int slot = adj == 1.0 ? 8 : (adj == 1.5 ? 9 : 10);
+    const double cnt = dd_to_double(cst(m, c, slot + 3));
+    m.ev[EV_RAW * E + c] = raw;
+    m.ev[EV_ADJ * E + c] = adj;
+    m.ev[EV_FIN * E + c] = adj;
+    m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, slot)) : __builtin_nan("");
+}
+
+// ================================================================== weighted median selection
+// element (value, weight) of scaled event s at local row i; false = not part of the set
+__device__ __forceinline__ bool sel_elem(const pcx_mat& m, int s, int64_t i, double& x, double& w) {
+    const double t = m.T[(int64_t)s * m.n_rows + i];
+    if (m.sel_phase == 1) {
+        if (__builtin_isnan(t)) return false;
+        x = t;
+        w = m.rep[i];
+    } else {
+        const int c = m.scaled_cols[s];
+        x = __builtin_isnan(t) ? m.ev[EV_GUESS * m.n_events + c] : t;
+        if (__builtin_isnan(x)) return false;
+        w = m.rowv[RV_SMOOTH * m.n_rows + i];
+    }
+    return true;
+}
+
+__device__ __forceinline__ L3 ld_l3(const uint64_t* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ void st_l3(uint64_t* p, L3 v) {
+    p[0] = v.a;
+    p[1] = v.b;
+    p[2] = v.c;
+}
+
+// PCX_M_SEL_INIT: per active scaled event: exact total weight, key range, max weight
+__global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
+    const int s = blockIdx.x;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] == 0) return;
+    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wmaxb;
+    if (threadIdx.x == 0) {
+        la = lb = lc = cnt = 0;
+        kmin = ~0ull;
+        kmax = 0;
+        wmaxb = 0;  // bits of +0.0; weights are >= 0 and order like their bit patterns
+    }
+    __syncthreads();
+    uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0;
+    double wm = -1.0;
+    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
+        double x, w;
+        if (!sel_elem(m, s, i, x, w)) continue;
+        const limbs3 L = to_limbs(w);
+        a += L.l0;
+        b += L.l1;
+        c += L.l2;
+        const uint64_t k = dkey(x);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+        wm = fmax(wm, w);
+        n++;
+    }
+    atomicAdd(&la, (unsigned long long)a);
+    atomicAdd(&lb, (unsigned long long)b);
+    atomicAdd(&lc, (unsigned long long)c);
+    atomicAdd(&cnt, (unsigned long long)n);
+    atomicMin(&kmin, (unsigned long long)mn);
+    atomicMax(&kmax, (unsigned long long)mx);
+    wm = wave_max_d(wm);
+    if ((threadIdx.x & 63) == 0) atomicMax(&wmaxb, (unsigned long long)__double_as_longlong(wm < 0 ? 0.0 : wm));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t o = ((int64_t)m.rank * m.n_scaled + s) * NB;
+        L3 t = l3_norm({la, lb, lc});
+        m.sel_sum[o * 4 + 0] = t.a;
+        m.sel_sum[o * 4 + 1] = t.b;
+        m.sel_sum[o * 4 + 2] = t.c;
+        m.sel_sum[o * 4 + 3] = cnt;
+        m.sel_min[o * 2 + 0] = kmin;
+        m.sel_max[o] = kmax;
+        m.sel_val[((int64_t)m.rank * m.n_scaled + s) * 4 + 0] = cnt ? __longlong_as_double(wmaxb) : -1.0;
+    }
+}
+
+__device__ __forceinline__ int shift_for(uint64_t lo, uint64_t hi) {
+    const uint64_t d = hi - lo;
+    if (d == 0) return 0;
+    const int bits = 64 - __clzll(d);
+    return bits > 8 ? bits - 8 : 0;
+}
+
+// PCX_M_SEL_START: combine ranks; dominance (any w > mid); first range
+__global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] == 0) return;
+    L3 tot{0, 0, 0};
+    uint64_t kmin = ~0ull, kmax = 0, cnt = 0;
+    double wmax = -1.0;
+    for (int w = 0; w < m.world; w++) {
+        const int64_t o = ((int64_t)w * m.n_scaled + s) * NB;
+        tot = l3_add(tot, {m.sel_sum[o * 4], m.sel_sum[o * 4 + 1], m.sel_sum[o * 4 + 2]});
+        cnt += m.sel_sum[o * 4 + 3];
+        kmin = m.sel_min[o * 2] < kmin ? m.sel_min[o * 2] : kmin;
+        kmax = m.sel_max[o] > kmax ? m.sel_max[o] : kmax;
+        wmax = fmax(wmax, m.sel_val[((int64_t)w * m.n_scaled + s) * 4]);
+    }
+    st_l3(st + 7, tot);
+    st_l3(st + 4, {0, 0, 0});
+    st[10] = 0;  // max key below the range (valid if st[11])
+    st[11] = 0;
+    st[13] = __double_as_longlong(wmax);
+    const bool positive = tot.a | tot.b | tot.c;
+    if (cnt == 0 || !positive) {  // weighted_median returns None -> NaN
+        st[0] = 0;
+        st[12] = __double_as_longlong(__builtin_nan(""));
+        return;
+    }
+    // any(w > mid): 2*wmax > total
+    if (l3_cmp(l3_twice(l3_of(wmax)), tot) > 0) {
+        st[0] = 2;  // needs the first row holding wmax
+        atomicAdd((unsigned long long*)&m.info[IN_SEL_ARGMAX], 1ull);
+        return;
+    }
+    st[1] = kmin;
+    st[2] = kmax;
+    st[3] = shift_for(kmin, kmax);
+    if (kmin == kmax) {  // one distinct value: it is the crossing value
+        st[0] = 0;
+        st[12] = __double_as_longlong(dkey_inv(kmin));
+    }
+}
+
+// PCX_M_SEL_ARGMAX: first local row whose weight equals the dominant weight
+__global__ void __launch_bounds__(BT) k_sel_argmax(pcx_mat m) {
+    const int s = blockIdx.x;
+    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] != 2) return;
+    const double wmax = __longlong_as_double(st[13]);
+    __shared__ unsigned long long best;
+    if (threadIdx.x == 0) best = ~0ull;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
+        double x, w;
+        if (sel_elem(m, s, i, x, w) && w == wmax) {
+            atomicMin(&best, (unsigned long long)(m.row_offset + i));
+            break;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) m.sel_val[((int64_t)m.rank * m.n_scaled + s) * 4 + 1] = best == ~0ull ? -1.0 : (double)best;
+}
+
+// PCX_M_SEL_VALUE: the rank owning the first dominant row publishes its value
+__global__ void __launch_bounds__(BT) k_sel_value(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] != 2) return;
+    double first = -1.0;
+    for (int w = 0; w < m.world; w++) {
+        const double v = m.sel_val[((int64_t)w * m.n_scaled + s) * 4 + 1];
+        if (v >= 0 && (first < 0 || v < first)) first = v;
+    }
+    const int64_t gi = (int64_t)first;
+    double* out = m.sel_val + ((int64_t)m.rank * m.n_scaled + s) * 4 + 2;
+    *out = 0.0;
+    if (gi >= m.row_offset && gi < m.row_offset + m.n_rows) {
+        double x, w;
+        sel_elem(m, s, gi - m.row_offset, x, w);
+        *out = x;
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_sel_value_finish(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] != 2) return;
+    double x = 0.0;
+    for (int w = 0; w < m.world; w++) x += m.sel_val[((int64_t)w * m.n_scaled + s) * 4 + 2];
+    st[12] = __double_as_longlong(x);
+    st[0] = 0;
+}
+
+// PCX_M_SEL_HIST: exact weight histogram of the keys inside [lo, hi] (NB buckets)
+__global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
+    const int s = blockIdx.x;
+    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] != 1) return;
+    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB], hw[NB];
+    for (int b = threadIdx.x; b < NB; b += BT) {
+        ha[b] = hb[b] = hc[b] = hn[b] = 0;
+        hmin[b] = ~0ull;
+        hmax[b] = 0;
+        hw[b] = ~0ull;
+    }
+    __syncthreads();
+    const uint64_t lo = st[1], hi = st[2];
+    const int sh = (int)st[3];
+    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
+        double x, w;
+        if (!sel_elem(m, s, i, x, w)) continue;
+        const uint64_t k = dkey(x);
+        if (k < lo || k > hi) continue;
+        const int b = (int)((k - lo) >> sh);
+        const limbs3 L = to_limbs(w);
+        atomicAdd(&ha[b], (unsigned long long)L.l0);
+        atomicAdd(&hb[b], (unsigned long long)L.l1);
+        atomicAdd(&hc[b], (unsigned long long)L.l2);
+        atomicAdd(&hn[b], 1ull);
+        atomicMin(&hmin[b], (unsigned long long)k);
+        atomicMax(&hmax[b], (unsigned long long)k);
+        atomicMin(&hw[b], (unsigned long long)__double_as_longlong(w));
+    }
+    __syncthreads();
+    const int64_t o = ((int64_t)m.rank * m.n_scaled + s) * NB;
+    for (int b = threadIdx.x; b < NB; b += BT) {
+        L3 t = l3_norm({ha[b], hb[b], hc[b]});
+        m.sel_sum[(o + b) * 4 + 0] = t.a;
+        m.sel_sum[(o + b) * 4 + 1] = t.b;
+        m.sel_sum[(o + b) * 4 + 2] = t.c;
+        m.sel_sum[(o + b) * 4 + 3] = hn[b];
+        m.sel_min[(o + b) * 2 + 0] = hmin[b];
+        m.sel_min[(o + b) * 2 + 1] = hw[b];
+        m.sel_max[o + b] = hmax[b];
+    }
+}
+
+// PCX_M_SEL_STEP: walk the buckets (all ranks), keep the one where the prefix crosses
+// half the total; a single-key range is the crossing value (weightedstats semantics)
+__global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] != 1) return;
+    const L3 tot = ld_l3(st + 7);
+    L3 below = ld_l3(st + 4);
+    uint64_t below_max = st[10];
+    bool has_below = st[11] != 0;
+    for (int b = 0; b < NB; b++) {
+        L3 hs{0, 0, 0};
+        uint64_t n = 0, kmin = ~0ull, kmax = 0, wmin = ~0ull;
+        for (int w = 0; w < m.world; w++) {
+            const int64_t o = ((int64_t)w * m.n_scaled + s) * NB + b;
+            hs = l3_add(hs, {m.sel_sum[o * 4], m.sel_sum[o * 4 + 1], m.sel_sum[o * 4 + 2]});
+            n += m.sel_sum[o * 4 + 3];
+            kmin = m.sel_min[o * 2] < kmin ? m.sel_min[o * 2] : kmin;
+            wmin = m.sel_min[o * 2 + 1] < wmin ? m.sel_min[o * 2 + 1] : wmin;
+            kmax = m.sel_max[o] > kmax ? m.sel_max[o] : kmax;
+        }
+        if (n == 0) continue;
+        const L3 upto = l3_add(below, hs);
+        if (l3_cmp(l3_twice(upto), tot) > 0) {
+            // crossing bucket
+            if (kmin == kmax) {
+                const double xs = dkey_inv(kmin);
+                const L3 first = l3_add(below, l3_of(__longlong_as_double(wmin)));
+                const bool at_start = l3_cmp(l3_twice(first), tot) > 0;
+                double res = xs;
+                if (at_start && has_below && l3_cmp(l3_twice(below), tot) == 0)
+                    res = (dkey_inv(below_max) + xs) / 2.0;  // exact half: mean of the pair
+                st[12] = __double_as_longlong(res);
+                st[0] = 0;
+            } else {
+                st[1] = kmin;
+                st[2] = kmax;
+                st[3] = shift_for(kmin, kmax);
+                st_l3(st + 4, below);
+                st[10] = below_max;
+                st[11] = has_below ? 1 : 0;
+                atomicAdd((unsigned long long*)&m.info[IN_SEL_ACTIVE], 1ull);
+            }
+            return;
+        }
+        below = upto;
+        below_max = kmax;
+        has_below = true;
+    }
+    // no crossing (cannot happen with exact sums): give up with NaN
+    st[12] = __double_as_longlong(__builtin_nan(""));
+    st[0] = 0;
+}
+
+// PCX_M_SEL_FINISH: phase 1 -> guess (int dtype truncates, :312); phase 2 -> outcomes
+__global__ void __launch_bounds__(BT) k_sel_finish(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    const int E = (int)m.n_events;
+    const int c = m.scaled_cols[s];
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    const double r = __longlong_as_double(st[12]);
+    if (m.sel_phase == 1) {
+        if (st[15]) m.ev[EV_GUESS * E + c] = m.int_dtype ? trunc(r) : r;
+    } else {
+        m.ev[EV_RAW * E + c] = r;
+        m.ev[EV_ADJ * E + c] = r;
+        double f = r * (m.hi[c] - m.lo[c]);  // :537-538, two roundings
+        f = f + m.lo[c];
+        m.ev[EV_FIN * E + c] = f;
+    }
+}
+
+// phase setup: which scaled events run a selection (phase 1: those with missing reports)
+__global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    const int c = m.scaled_cols[s];
+    const bool need = m.sel_phase == 1 ? m.ev[EV_MISS * m.n_events + c] > 0 : true;
+    for (int k = 0; k < SELS; k++) st[k] = 0;
+    st[0] = need ? 1 : 0;
+    st[15] = need ? 1 : 0;
+}
+
+// PCX_M_SCALED_CERT: sum of smooth_rep over rows whose filled value equals the outcome
+__global__ void __launch_bounds__(BT) k_scaled_cert(pcx_mat m) {
+    __shared__ dd lds[8];
+    __shared__ double cnts[BT];
+    const int s = blockIdx.x;
+    const int E = (int)m.n_events;
+    const int c = m.scaled_cols[s];
+    const double adj = m.ev[EV_ADJ * E + c];
+    acc2 a;
+    double n = 0.0;
+    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
+        const double t = m.T[(int64_t)s * m.n_rows + i];
+        const double f = __builtin_isnan(t) ? m.ev[EV_GUESS * E + c] : t;
+        if (f == adj) {
+            a.add(m.rowv[RV_SMOOTH * m.n_rows + i]);
+            n += 1.0;
+        }
+    }
+    const dd r = block_sum_dd<BT>(a.get(), lds);
+    cnts[threadIdx.x] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tn = 0.0;
+        for (int k = 0; k < BT; k++) tn += cnts[k];
+        st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + 14) * 2, r);
+        st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + 15) * 2, {tn, 0.0});
+    }
+}
+
+// PCX_M_FINAL: certainty of scaled events, consensus_reward, participation, author bonus
+__global__ void __launch_bounds__(1024) k_final(pcx_mat m) {
+    __shared__ dd lds[16];
+    __shared__ double sh[4];
+    const int E = (int)m.n_events;
+    for (int c = threadIdx.x; c < E; c += 1024)
+        if (m.scaled && m.scaled[c]) {
+            const double cnt = dd_to_double(cst(m, c, 15));
+            m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, 14)) : __builtin_nan("");
+        }
+    __syncthreads();
+    acc2 sc, scp, spc, spcp;
+    for (int c = threadIdx.x; c < E; c += 1024) {
+        const double a = fabs(m.ev[EV_CERT * E + c]);
+        sc.add(a);
+        scp.add(a + 1.0);
+        const double p = fabs(m.ev[EV_PC * E + c]);
+        spc.add(p);
+        spcp.add(p + 1.0);
+    }
+    const dd r0 = block_sum_dd<1024>(sc.get(), lds), r1 = block_sum_dd<1024>(scp.get(), lds);
+    const dd r2 = block_sum_dd<1024>(spc.get(), lds), r3 = block_sum_dd<1024>(spcp.get(), lds);
+    acc2 cs, ps;
+    for (int c = threadIdx.x; c < E; c += 1024) {
+        cs.add(m.ev[EV_CERT * E + c]);
+        ps.add(m.ev[EV_PC * E + c]);
+    }
+    const dd r4 = block_sum_dd<1024>(cs.get(), lds), r5 = block_sum_dd<1024>(ps.get(), lds);
+    if (threadIdx.x == 0) {
+        sh[0] = dd_to_double(r0);
+        sh[1] = dd_to_double(r1);
+        sh[2] = dd_to_double(r2);
+        sh[3] = dd_to_double(r3);
+        const double avg_cert = dd_to_double(r4) / (double)E;
+        const double pna = 1.0 - dd_to_double(r5) / (double)E;
+        m.pvec[3 * (m.n_events + 64) + 4] = pna;
+        if (m.scalars) {
+            m.scalars[0] = 1.0 - pna;
+            m.scalars[1] = avg_cert;
+        }
+    }
+    __syncthreads();
+    const double pna = m.pvec[3 * (m.n_events + 64) + 4];
+    for (int c = threadIdx.x; c < E; c += 1024) {
+        const double cert = m.ev[EV_CERT * E + c];
+        const double reward = nweight(fabs(cert), sh[0], sh[1]);
+        const double pc = m.ev[EV_PC * E + c];
+        const double relc = nweight(fabs(pc), sh[2], sh[3]);
+        if (m.adj_first_loadings) m.adj_first_loadings[c] = m.ev[EV_LD * E + c];
+        if (m.outcomes_raw) m.outcomes_raw[c] = m.ev[EV_RAW * E + c];
+        if (m.outcomes_adjusted) m.outcomes_adjusted[c] = m.ev[EV_ADJ * E + c];
+        if (m.outcomes_final) m.outcomes_final[c] = m.ev[EV_FIN * E + c];
+        if (m.certainty) m.certainty[c] = cert;
+        if (m.consensus_reward) m.consensus_reward[c] = reward;
+        if (m.nas_filled) m.nas_filled[c] = m.ev[EV_NZERO * E + c];
+        if (m.participation_columns) m.participation_columns[c] = pc;
+        if (m.author_bonus) m.author_bonus[c] = relc * pna + reward * (1.0 - pna);
+    }
+}
+
+// PCX_M_ROWSUMS: sums for normalize(participation_rows) -- fully-NaN rows are masked (Q15)
+__global__ void __launch_bounds__(BT) k_rowsums(pcx_mat m) {
+    __shared__ dd lds[8];
+    const int E = (int)m.n_events;
+    acc2 a, ap;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const bool masked = (int)m.rowstat[2 * i] == E;
+        const double pr = 1.0 - (double)m.rowstat[2 * i + 1] / (double)E;
+        if (!masked) {
+            a.add(fabs(pr));
+            ap.add(fabs(pr) + 1.0);
+        }
+    }
+    const dd r0 = block_sum_dd<BT>(a.get(), lds), r1 = block_sum_dd<BT>(ap.get(), lds);
+    if (threadIdx.x == 0) {
+        st_dd(m.spart + blockIdx.x * 8 + 0, r0);
+        st_dd(m.spart + blockIdx.x * 8 + 2, r1);
+    }
+}
+
+// PCX_M_AGENTS: per-reporter outputs of this rank (:576-577, 586-595)
+__global__ void __launch_bounds__(BT) k_agents(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const double S = dd_to_double(scl(m, SC_AR)), Sp = dd_to_double(scl(m, SC_ARP));
+    const double pna = m.pvec[3 * (m.n_events + 64) + 4];
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const bool masked = (int)m.rowstat[2 * i] == E;
+        const double narow = (double)m.rowstat[2 * i + 1];
+        const double pr = 1.0 - narow / (double)E;
+        const double rel = masked ? fabs(pr) : nweight(fabs(pr), S, Sp);
+        const double sm = m.rowv[RV_SMOOTH * m.n_rows + i];
+        if (m.old_rep) m.old_rep[i] = m.rep[i];
+        if (m.this_rep) m.this_rep[i] = m.rowv[RV_THIS * m.n_rows + i];
+        if (m.smooth_rep) m.smooth_rep[i] = sm;
+        if (m.scores) m.scores[i] = m.algorithm == 0 ? m.rowv[RV_S * m.n_rows + i] : 0.0;
+        if (m.na_row) m.na_row[i] = narow;
+        if (m.participation_rows) m.participation_rows[i] = pr;
+        if (m.relative_part) m.relative_part[i] = rel;
+        if (m.reporter_bonus) m.reporter_bonus[i] = masked ? rel : rel * pna + sm * (1.0 - pna);
+    }
+}
+
+// PCX_M_MATRICES: rescaled (result["original"]) and filled (result["filled"]) reports
+__global__ void __launch_bounds__(BT) k_matrices(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const int64_t tot = m.n_rows * m.n_events;
+    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < tot; idx += (int64_t)gridDim.x * BT) {
+        const int c = (int)(idx % E);
+        const ColParam p = col_param(m, c, true);
+        const double x = rescale(m.reports[idx], p, m.int_dtype);
+        if (m.original) m.original[idx] = x;
+        if (m.filled) m.filled[idx] = missing(x) ? p.guess : x;
+    }
+}
+
+__global__ void k_info_clear(pcx_mat m, int slot) { m.info[slot] = 0; }
+
+__global__ void k_zero_loading(pcx_mat m) {
+    for (int j = threadIdx.x; j < m.n_events; j += blockDim.x) m.ev[EV_LD * m.n_events + j] = 0.0;
+}
+
+int grid_rows(int64_t n, int per_block) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    return (int)g;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ stage dispatcher
+hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
+    const int E = (int)m.n_events;
+    const int ceb = (E + BT - 1) / BT;
+    const dim3 colgrid(ceb, m.col_blocks);
+    const int rg = grid_rows(m.n_rows, BT);
+    switch (stage) {
+        case PCX_M_REPUTATION:
+            if (m.rep_raw) hipLaunchKernelGGL(k_rep_total, dim3(1), dim3(1024), 0, st, m);
+            hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_TOK);
+            break;
+        case PCX_M_COLSTATS:
+            hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
+            break;
+        case PCX_M_GUESS:
+            hipLaunchKernelGGL(k_guess, dim3(ceb), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_MEAN:
+            hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_COV:
+            hipLaunchKernelGGL(k_cov, dim3(m.cov_tiles * m.cov_kslices), dim3(256), 0, st, m);
+            break;
+        case PCX_M_COV_REDUCE: {
+            const int64_t n = (int64_t)E * E;
+            hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);
+            break;
+        }
+        case PCX_M_COV_FINISH: {
+            const int64_t n = (int64_t)E * E;
+            hipLaunchKernelGGL(k_cov_finish, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);
+            break;
+        }
+        case PCX_M_SCORES:
+            hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
+            hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_NCSUMS:
+            hipLaunchKernelGGL(k_ncsums, dim3(rg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 4, (int)SC_A1);
+            break;
+        case PCX_M_GEMV2:
+            hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
+            break;
+        case PCX_M_DECIDE:
+            hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), 0, st, m);
+            break;
+        case PCX_M_REPU:
+            hipLaunchKernelGGL(k_repu, dim3(rg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_U);
+            break;
+        case PCX_M_SMOOTH:
+            hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_OUTCOMES:
+            hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
+            break;
+        case PCX_M_EVENTS:
+            hipLaunchKernelGGL(k_events, dim3(ceb), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SCALED_CERT:
+            if (m.n_scaled > 0) hipLaunchKernelGGL(k_scaled_cert, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_FINAL:
+            hipLaunchKernelGGL(k_final, dim3(1), dim3(1024), 0, st, m);
+            break;
+        case PCX_M_ROWSUMS:
+            hipLaunchKernelGGL(k_rowsums, dim3(rg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_AR);
+            break;
+        case PCX_M_AGENTS:
+            hipLaunchKernelGGL(k_agents, dim3(rg), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_INIT:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_sel_setup, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_init, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_START:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_SEL_ARGMAX);
+            hipLaunchKernelGGL(k_sel_start, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_ARGMAX:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_sel_argmax, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_VALUE:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_sel_value, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_HIST:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_sel_hist, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_STEP:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_SEL_ACTIVE);
+            hipLaunchKernelGGL(k_sel_step, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_FINISH:
+            if (m.n_scaled == 0) break;
+            hipLaunchKernelGGL(k_sel_value_finish, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_finish, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_POWER: {
+            // replicated on every rank (C is identical everywhere); host loop with polling
+            hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_FLAGS);
+            const int64_t nn = (int64_t)E * E;
+            hipLaunchKernelGGL(k_pi_check, dim3(grid_rows(nn, BT)), dim3(BT), 0, st, m);
+            int64_t flags = 0;
+            hipError_t e = hipMemcpyAsync(&flags, &m.info[IN_FLAGS], sizeof(flags), hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            int mode = 0;
+            int iters = 0;
+            if (flags & 2) {
+                mode = 1;  // non-finite covariance: LAPACK raises, H = ones (:331-333)
+            } else if (!(flags & 8)) {
+                mode = 2;  // zero covariance: svd(0) -> U = I
+            } else {
+                hipLaunchKernelGGL(k_pi_start, dim3(1), dim3(1024), 0, st, m);
+                const int gb = (E + BT / WAVE - 1) / (BT / WAVE);
+                const int maxit = 4000, poll = 8;
+                double delta = 1.0;
+                while (iters < maxit) {
+                    for (int k = 0; k < poll; k++) {
+                        hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m);
+                        hipLaunchKernelGGL(k_pi_norm, dim3(1), dim3(1024), 0, st, m);
+                    }
+                    iters += poll;
+                    e = hipMemcpyAsync(&delta, m.pvec + 3 * (E + 64), sizeof(double), hipMemcpyDeviceToHost, st);
+                    if (e == hipSuccess) e = hipStreamSynchronize(st);
+                    if (e != hipSuccess) return e;
+                    if (delta <= 1e-14) break;
+                }
+                if (delta > 1e-14) mode = 0, flags |= 4;
+            }
+            hipLaunchKernelGGL(k_pi_finish, dim3(1), dim3(1024), 0, st, m, mode);
+            int64_t info2[2] = {iters, (int64_t)((mode == 1 ? 2 : 0) | (mode == 2 ? 1 : 0) | (flags & 4))};
+            e = hipMemcpyAsync(&m.info[IN_PI_ITERS], info2, sizeof(info2), hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            break;
+        }
+        case PCX_M_MATRICES:
+            if (m.original || m.filled)
+                hipLaunchKernelGGL(k_matrices, dim3(grid_rows(m.n_rows * m.n_events, BT)), dim3(BT), 0, st, m);
+            break;
+        case 99:  // "absolute": no loading
+            hipLaunchKernelGGL(k_zero_loading, dim3(1), dim3(256), 0, st, m);
+            break;
+        default:
+            err = "pcx_mat_stage: unknown stage " + std::to_string(stage);
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace pcx

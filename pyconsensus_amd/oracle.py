@@ -1,0 +1,173 @@
+"""Drop-in ``Oracle`` for the PCA consensus path, computed on MI355X.
+
+Same constructor, attributes and ``consensus()`` result dict as the reference
+``pyconsensus.Oracle`` (pyconsensus/__init__.py:100-611).  The host side only
+normalises arguments and assembles the result containers; every number of the
+result is computed by libpcx's HIP kernels:
+
+* rounds with N <= 64 reporters and E <= 32 events run the one-wavefront round
+  kernel (csrc/pcx_batched.hip) -- the same kernel as the batched Monte Carlo
+  regime, with a batch of one;
+* larger matrices run the staged single-matrix pipeline (pipeline.py,
+  csrc/pcx_matrix.hip).
+
+There is no CPU fallback: without the library or a GPU, ``consensus()`` raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .batched import MAX_EVENTS, MAX_REPORTERS, consensus_batched
+
+NO, YES, BAD, NA = 1.0, 2.0, 1.5, 0.0  # __init__.py:65-68
+
+
+class Oracle(object):
+    """``Oracle(reports, event_bounds, reputation, ...).consensus()`` on the GPU.
+
+    Supported ``algorithm`` values: ``"PCA"`` (default, the hot path) and
+    ``"absolute"`` (the reference's unimplemented branch: uniform this_rep,
+    __init__.py:359-362).  The other reference algorithms raise
+    NotImplementedError (scope).
+    """
+
+    def __init__(self, reports=None, event_bounds=None, reputation=None,
+                 catch_tolerance=0.1, alpha=0.1, verbose=False,
+                 aux=None, algorithm="PCA", variance_threshold=0.9,
+                 max_components=5, hierarchy_threshold=0.5, device=None):
+        self.NO, self.YES, self.BAD, self.NA = NO, YES, BAD, NA
+        data = np.ma.getdata(reports) if isinstance(reports, np.ma.MaskedArray) else reports
+        arr = np.asarray(data)
+        if arr.ndim != 2:
+            raise ValueError("reports must be a 2-D reporters x events matrix")
+        # Q2: a float ndarray is rescaled IN PLACE by the reference (:121, :269)
+        self._caller = reports if (isinstance(reports, np.ndarray) and not isinstance(reports, np.ma.MaskedArray)
+                                   and reports.dtype == np.float64) else None
+        self._int_dtype = np.issubdtype(arr.dtype, np.integer)
+        self._data = np.ascontiguousarray(arr, dtype=np.float64)
+        self.reports = np.ma.masked_array(arr, np.isnan(arr.astype(np.float64)))
+        self.num_reports, self.num_events = arr.shape
+        self.event_bounds = event_bounds
+        self.catch_tolerance = catch_tolerance
+        self.alpha = alpha
+        self.verbose = verbose
+        self.algorithm = algorithm
+        self.variance_threshold = variance_threshold
+        self.num_components = -1
+        self.hierarchy_threshold = hierarchy_threshold
+        self.convergence = False
+        self.aux = aux
+        self.max_components = max_components if self.num_events >= max_components else self.num_events
+        self.device = device
+        n = self.num_reports
+        if reputation is None:  # :138-141
+            self.weighted = False
+            self.total_rep = n
+            self.reputation = np.array([1 / float(n)] * n)
+            self._rep_raw = None
+        else:  # :143-145 (the GPU recomputes these from the raw weights)
+            self.weighted = True
+            raw = np.asarray(reputation)
+            self.total_rep = np.sum(raw.ravel())
+            self.reputation = np.asarray(raw, dtype=np.float64).ravel() / float(self.total_rep)
+            self._rep_raw = np.asarray(raw, dtype=np.float64).ravel()
+        self.reptokens = [int(r * 1e6) for r in self.reputation]  # :146
+        self.last_info = {}
+
+    # -- scalar helpers of the reference API (:244-258) ------------------------
+    def normalize(self, v):
+        v = np.abs(v)
+        if np.sum(v) == 0:
+            v = v + 1
+        return v / np.sum(v)
+
+    def catch(self, X):
+        if X < self.BAD - self.catch_tolerance:
+            return self.NO
+        elif X > self.BAD + self.catch_tolerance:
+            return self.YES
+        return self.BAD
+
+    # -- consensus (:502-611) ---------------------------------------------------
+    def _bounds_arrays(self):
+        if self.event_bounds is None:
+            return None, None, None
+        sc = np.array([bool(b["scaled"]) for b in self.event_bounds], dtype=np.uint8)
+        lo = np.array([float(b["min"]) for b in self.event_bounds], dtype=np.float64)
+        hi = np.array([float(b["max"]) for b in self.event_bounds], dtype=np.float64)
+        return sc, lo, hi
+
+    def consensus(self):
+        if self.algorithm not in _abi.ALGORITHMS:
+            raise NotImplementedError("algorithm %r: only 'PCA' (and 'absolute') run on the GPU path"
+                                      % (self.algorithm,))
+        sc, lo, hi = self._bounds_arrays()
+        N, E = self.num_reports, self.num_events
+        if N <= MAX_REPORTERS and E <= MAX_EVENTS:
+            out = consensus_batched(self._data[None], None if self._rep_raw is None else self._rep_raw[None],
+                                    sc, lo, hi, catch_tolerance=self.catch_tolerance, alpha=self.alpha,
+                                    int_dtype=self._int_dtype, algorithm=self.algorithm,
+                                    device=self.device, filled=True, original=True)
+            g = {k: v[0].cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+            participation = float(g["participation"])
+            avg_certainty = float(g["avg_certainty"])
+            self.last_info = {"branch": int(g["branch"]), "flags": int(g["flags"]),
+                              "pi_iters": int(g["pi_iters"]), "path": "batched"}
+        else:
+            from .pipeline import consensus_matrix
+
+            ev, ag, meta = consensus_matrix(self._data, self._rep_raw, sc, lo, hi,
+                                            catch_tolerance=self.catch_tolerance, alpha=self.alpha,
+                                            int_dtype=self._int_dtype, algorithm=self.algorithm,
+                                            device=self.device, matrices=True, n_total=N, row_offset=0)
+            g = {k: v.cpu().numpy() for k, v in list(ev.items()) + list(ag.items())}
+            participation = float(meta["participation"])
+            avg_certainty = float(meta["avg_certainty"])
+            self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
+                              "path": "matrix"}
+        self.convergence = self.algorithm == "PCA"  # :483, :499
+        return self._result(g, participation, avg_certainty)
+
+    def _result(self, g, participation, avg_certainty):
+        original = g["original"]
+        filled = g["filled"]
+        if self._int_dtype:  # int64 storage truncates (Q3)
+            original = original.astype(np.int64)
+            filled = filled.astype(np.int64)
+        if self._caller is not None:  # Q2: the caller's float array carries the rescaled values
+            self._caller[...] = g["original"]
+        self.reports = np.ma.masked_array(original, self.reports.mask)
+        ints = self._int_dtype
+        cnt = (lambda a: [int(x) for x in a]) if ints else (lambda a: [float(x) for x in a])
+        ma = np.ma.masked_array
+        outcomes_adj = [float(x) for x in g["outcomes_adjusted"]]
+        return {
+            "original": original,
+            "filled": filled,
+            "agents": {
+                "old_rep": g["old_rep"],
+                "this_rep": ma(g["this_rep"]),
+                "smooth_rep": ma(g["smooth_rep"]),
+                "na_row": cnt(g["na_row"]),
+                "participation_rows": [float(x) for x in g["participation_rows"]],
+                "relative_part": [float(x) for x in g["relative_part"]],
+                "reporter_bonus": [float(x) for x in g["reporter_bonus"]],
+                "scores": ma(g["scores"]),
+            },
+            "events": {
+                "adj_first_loadings": [float(x) for x in g["adj_first_loadings"]],
+                "outcomes_raw": [float(x) for x in g["outcomes_raw"]],
+                "consensus_reward": g["consensus_reward"],
+                "certainty": g["certainty"],
+                "NAs Filled": cnt(g["nas_filled"]),
+                "participation_columns": [float(x) for x in g["participation_columns"]],
+                "author_bonus": [float(x) for x in g["author_bonus"]],
+                "outcomes_adjusted": outcomes_adj,
+                "outcomes_final": [float(x) for x in g["outcomes_final"]],
+            },
+            "participation": participation,
+            "avg_certainty": avg_certainty,
+            "convergence": self.convergence,
+            "components": self.num_components,
+        }
