@@ -197,6 +197,7 @@ typedef struct {
     double*   ev;                 /* [16][E] event vectors (guess, mu, old, ...)   */
     double*   cslab;              /* [cov_kslices][E][E] covariance partial tiles  */
     double*   C;                  /* [E][E] covariance                             */
+    double*   Mw;                 /* [2][E][E] power-iteration working matrices    */
     double*   pvec;               /* [4][E + 64] power-iteration scratch           */
     double*   rowv;               /* [6][n_rows] scores, this, smooth, u, ...       */
     uint32_t* rowstat;            /* [n_rows][2] NaN / zero counts per row         */

@@ -80,7 +80,7 @@ class Mat(C.Structure):
         ("reports", _vp), ("scaled", _vp), ("lo", _vp), ("hi", _vp), ("rep_raw", _vp),
         ("scaled_cols", _vp), ("scaled_index", _vp),
         ("rep", _vp), ("tok", _vp), ("T", _vp), ("part", _vp), ("mpart", _vp), ("cstat", _vp),
-        ("cmax", _vp), ("scal", _vp), ("spart", _vp), ("ev", _vp), ("cslab", _vp), ("C", _vp),
+        ("cmax", _vp), ("scal", _vp), ("spart", _vp), ("ev", _vp), ("cslab", _vp), ("C", _vp), ("Mw", _vp),
         ("pvec", _vp), ("rowv", _vp), ("rowstat", _vp), ("skey", _vp), ("info", _vp),
         ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
     ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),

@@ -316,24 +316,110 @@ __device__ __forceinline__ void tri_index(int t, int& I, int& J) {
     J = t - i * (i + 1) / 2;
 }
 
-// one work item = (lower-triangle tile (I,J), row slice ks).  C_part[p][q] over the slice's
-// rows of (tok_i * wcd_ip) * wcd_iq, with wcd = F - mu computed on the fly.
-__global__ void __launch_bounds__(256) k_cov(pcx_mat m) {
+// 128x128 tile of A_I^T B_J accumulated over rows [rb, re) on fp64 MFMA
+// (v_mfma_f64_16x16x4_f64): 4 waves in 2x2, each 64x64 = 4x4 MFMA blocks; 16 rows
+// are staged per step through LDS (rows padded to LDP doubles so the b64 fragment
+// reads are bank-conflict free) and the next 16 are prefetched into registers
+// while the MFMAs run.  LOADER fills va (A side) / vb (B side) for 8 columns.
+template <class LOADER>
+__device__ void mfma_tile(LOADER& ld, int I, int J, int64_t rb, int64_t re, d4 (&acc)[4][4]) {
     __shared__ __attribute__((aligned(16))) double As[KB][LDP];
     __shared__ __attribute__((aligned(16))) double Bs[KB][LDP];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int sr = tid >> 4;        // staged row 0..15
+    const int scg = (tid & 15) * 8; // staged column group
+    double va[8], vb[8];
+    if (rb < re) ld.load(rb + sr, re, I, J, scg, va, vb);
+    for (int64_t i0 = rb; i0 < re; i0 += KB) {
+        __syncthreads();
+        for (int k = 0; k < 8; k++) {
+            As[sr][scg + k] = va[k];
+            Bs[sr][scg + k] = vb[k];
+        }
+        __syncthreads();
+        if (i0 + KB < re) ld.load(i0 + KB + sr, re, I, J, scg, va, vb);  // prefetch under the MFMAs
+#pragma unroll
+        for (int kk = 0; kk < KB / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr][wr * 64 + a * 16 + (lane & 15)];
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[kr][wc * 64 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+    }
+}
+
+// D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
+__device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, int I, int J, const d4 (&acc)[4][4]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++)
+            for (int r = 0; r < 4; r++) {
+                const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
+                const int64_t q = (int64_t)J * CT + wc * 64 + b * 16 + (lane & 15);
+                if (p < E && q < E) out[p * ld + q] = acc[a][b][r];
+            }
+}
+
+// covariance loader: wcd = F - mu computed from the raw reports; A side times the tokens
+struct CovLoader {
+    const pcx_mat* m;
+    const double (*prm)[5][CT];
+    bool diag;
+    __device__ void load(int64_t i, int64_t re, int I, int J, int scg, double* va, double* vb) const {
+        const int E = (int)m->n_events;
+        const bool rowok = i < re;
+        const double tk = rowok ? m->tok[i] : 0.0;
+        for (int s = 0; s < (diag ? 1 : 2); s++) {
+            const int cb = (s == 0 ? I : J) * CT;
+            for (int k = 0; k < 8; k++) {
+                const int q = scg + k;
+                const int c = cb + q;
+                double w = 0.0;
+                if (rowok && c < E) {
+                    double x = m->reports[i * E + c];
+                    if (prm[s][0][q] != 0.0) {
+                        x = (x - prm[s][1][q]) / prm[s][2][q];
+                        if (m->int_dtype) x = trunc(x);
+                    }
+                    if (missing(x)) x = prm[s][3][q];
+                    w = x - prm[s][4][q];
+                }
+                if (s == 0) {
+                    va[k] = w * tk;  // np.ma.multiply(wcd.T, tokens): the product is rounded first
+                    if (diag) vb[k] = w;
+                } else {
+                    vb[k] = w;
+                }
+            }
+        }
+    }
+};
+
+// one work item = (lower-triangle tile (I,J), row slice ks): partial
+// C[p][q] = sum over the slice's rows of (tok_i * wcd_ip) * wcd_iq  (:326)
+__global__ void __launch_bounds__(256) k_cov(pcx_mat m) {
     __shared__ double prm[2][5][CT];  // side, {scaled, lo, range, guess, mu}
     const int E = (int)m.n_events;
     const int ntiles = m.cov_tiles, nks = m.cov_kslices;
     const int item = blockIdx.x;
-    const int ks = item / ntiles, t = item % ntiles;
+    const int ks = item / ntiles, t = item % ntiles;  // slice-major: concurrent tiles share rows
     int I, J;
     tri_index(t, I, J);
-    const bool diag = I == J;
     const int64_t per = (m.n_rows + nks - 1) / nks;
     const int64_t rb = (int64_t)ks * per;
     const int64_t re = rb + per < m.n_rows ? rb + per : m.n_rows;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wr = wv >> 1, wc = wv & 1;
+    const int tid = threadIdx.x;
     for (int s = 0; s < 2; s++)
         for (int q = tid; q < CT; q += 256) {
             const int c = (s == 0 ? I : J) * CT + q;
@@ -353,76 +439,55 @@ __global__ void __launch_bounds__(256) k_cov(pcx_mat m) {
             prm[s][4][q] = mu;
         }
     __syncthreads();
+    CovLoader ld{&m, prm, I == J};
     d4 acc[4][4];
-    for (int a = 0; a < 4; a++)
-        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    const int sr = tid >> 4;        // staged row 0..15
-    const int scg = (tid & 15) * 8; // staged column group
-    double va[8], vb[8];
-    auto load = [&](int64_t i0) {
-        const int64_t i = i0 + sr;
-        const bool rowok = i < re;
-        const double tk = rowok ? m.tok[i] : 0.0;
-        for (int s = 0; s < (diag ? 1 : 2); s++) {
-            const int cb = (s == 0 ? I : J) * CT;
-            for (int k = 0; k < 8; k++) {
-                const int q = scg + k;
-                const int c = cb + q;
-                double w = 0.0;
-                if (rowok && c < E) {
-                    double x = m.reports[i * E + c];
-                    if (prm[s][0][q] != 0.0) {
-                        x = (x - prm[s][1][q]) / prm[s][2][q];
-                        if (m.int_dtype) x = trunc(x);
-                    }
-                    if (missing(x)) x = prm[s][3][q];
-                    w = x - prm[s][4][q];
-                }
-                if (s == 0) {
-                    va[k] = w * tk;  // np.ma.multiply(wcd.T, tokens): product rounded first
-                    if (diag) vb[k] = w;
-                } else {
-                    vb[k] = w;
-                }
-            }
-        }
-    };
-    auto store = [&]() {
+    mfma_tile(ld, I, J, rb, re, acc);
+    store_tile(m.cslab + (int64_t)ks * E * E, E, E, I, J, acc);
+}
+
+// plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
+struct GramLoader {
+    const double* A;
+    int E;
+    __device__ void load(int64_t i, int64_t re, int I, int J, int scg, double* va, double* vb) const {
         for (int k = 0; k < 8; k++) {
-            As[sr][scg + k] = va[k];
-            Bs[sr][scg + k] = vb[k];
-        }
-    };
-    if (rb < re) load(rb);
-    for (int64_t i0 = rb; i0 < re; i0 += KB) {
-        __syncthreads();
-        store();
-        __syncthreads();
-        if (i0 + KB < re) load(i0 + KB);  // prefetch the next rows under the MFMAs
-#pragma unroll
-        for (int kk = 0; kk < KB / 4; kk++) {
-            const int kr = kk * 4 + (lane >> 4);
-            double af[4], bf[4];
-#pragma unroll
-            for (int a = 0; a < 4; a++) af[a] = As[kr][wr * 64 + a * 16 + (lane & 15)];
-#pragma unroll
-            for (int b = 0; b < 4; b++) bf[b] = Bs[kr][wc * 64 + b * 16 + (lane & 15)];
-#pragma unroll
-            for (int a = 0; a < 4; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+            const int qa = I * CT + scg + k, qb = J * CT + scg + k;
+            va[k] = (i < re && qa < E) ? A[i * E + qa] : 0.0;
+            vb[k] = (i < re && qb < E) ? A[i * E + qb] : 0.0;
         }
     }
-    // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
-    double* slab = m.cslab + (int64_t)ks * E * E;
+};
+
+// out = A^T A = A A (A symmetric), lower tiles mirrored; atomically tracks max |out| bits
+__global__ void __launch_bounds__(256) k_gram(const double* A, int E, double* out, unsigned long long* maxbits) {
+    int I, J;
+    tri_index(blockIdx.x, I, J);
+    GramLoader ld{A, E};
+    d4 acc[4][4];
+    mfma_tile(ld, I, J, 0, E, acc);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    double mx = 0.0;
     for (int a = 0; a < 4; a++)
         for (int b = 0; b < 4; b++)
             for (int r = 0; r < 4; r++) {
                 const int p = I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
                 const int q = J * CT + wc * 64 + b * 16 + (lane & 15);
-                if (p < E && q < E) slab[(int64_t)p * E + q] = acc[a][b][r];
+                if (p < E && q < E && q <= p) {
+                    const double v = acc[a][b][r];
+                    out[(int64_t)p * E + q] = v;
+                    out[(int64_t)q * E + p] = v;
+                    mx = fmax(mx, fabs(v));
+                }
             }
+    mx = wave_max_d(mx);
+    if (lane == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
+}
+
+__global__ void __launch_bounds__(BT) k_scale(double* M, int64_t n, const unsigned long long* maxbits) {
+    const double mx = __longlong_as_double(*maxbits);
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < n; i += (int64_t)gridDim.x * BT)
+        M[i] = mx > 0.0 ? M[i] / mx : M[i];
 }
 
 // PCX_M_COV_REDUCE: C = sum of slabs over the lower triangle, mirrored (unnormalised)
@@ -507,13 +572,13 @@ __global__ void __launch_bounds__(1024) k_pi_start(pcx_mat m) {
     for (int j = threadIdx.x; j < E; j += 1024) pv_x(m)[j] = m.C[(int64_t)j * E + kd] / nrm;
 }
 
-// y = C x, one wavefront per row
-__global__ void __launch_bounds__(BT) k_pi_gemv(pcx_mat m) {
+// y = M x, one wavefront per row
+__global__ void __launch_bounds__(BT) k_pi_gemv(pcx_mat m, const double* M) {
     const int E = (int)m.n_events;
     const int row = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
     const int lane = threadIdx.x % WAVE;
     if (row >= E) return;
-    const double* Cr = m.C + (int64_t)row * E;
+    const double* Cr = M + (int64_t)row * E;
     const double* x = pv_x(m);
     double acc = 0.0;
     for (int q = lane; q < E; q += WAVE) acc = fma(Cr[q], x[q], acc);
@@ -1468,20 +1533,53 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             } else {
                 hipLaunchKernelGGL(k_pi_start, dim3(1), dim3(1024), 0, st, m);
                 const int gb = (E + BT / WAVE - 1) / (BT / WAVE);
-                const int maxit = 4000, poll = 8;
+                const int nb = (E + CT - 1) / CT;
+                const int ntri = nb * (nb + 1) / 2;
+                const int64_t nn2 = (int64_t)E * E;
+                double* M = m.Mw;
+                double* Tm = m.Mw + nn2;
+                unsigned long long* mxb = (unsigned long long*)&m.info[8];
+                e = hipMemcpyAsync(M, m.C, nn2 * sizeof(double), hipMemcpyDeviceToDevice, st);
+                if (e != hipSuccess) return e;
+                // M <- (M M) / max|M M|: the same leading eigenvector, gap ratio squared
+                auto square = [&]() {
+                    (void)hipMemsetAsync(mxb, 0, sizeof(unsigned long long), st);
+                    hipLaunchKernelGGL(k_gram, dim3(ntri), dim3(256), 0, st, (const double*)M, E, Tm, mxb);
+                    hipLaunchKernelGGL(k_scale, dim3(grid_rows(nn2, BT)), dim3(BT), 0, st, Tm, nn2,
+                                       (const unsigned long long*)mxb);
+                    double* t2 = M;
+                    M = Tm;
+                    Tm = t2;
+                };
+                int sq = 0;
+                const int presq = E <= 1024 ? 3 : 0;  // small E: squaring is cheaper than iterations
+                for (; sq < presq; sq++) square();
+                const int maxit = 2048, poll = 8;
+                int since = 0;
                 double delta = 1.0;
                 while (iters < maxit) {
                     for (int k = 0; k < poll; k++) {
-                        hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m);
+                        hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m, (const double*)M);
                         hipLaunchKernelGGL(k_pi_norm, dim3(1), dim3(1024), 0, st, m);
                     }
                     iters += poll;
+                    since += poll;
                     e = hipMemcpyAsync(&delta, m.pvec + 3 * (E + 64), sizeof(double), hipMemcpyDeviceToHost, st);
                     if (e == hipSuccess) e = hipStreamSynchronize(st);
                     if (e != hipSuccess) return e;
                     if (delta <= 1e-14) break;
+                    if (since >= 32 && sq < 8) {
+                        square();
+                        sq++;
+                        since = 0;
+                    }
                 }
-                if (delta > 1e-14) mode = 0, flags |= 4;
+                if (delta > 1e-14) flags |= 4;
+                for (int k = 0; k < 4; k++) {  // polish with C itself
+                    hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m, (const double*)m.C);
+                    hipLaunchKernelGGL(k_pi_norm, dim3(1), dim3(1024), 0, st, m);
+                }
+                iters += 4 + sq;
             }
             hipLaunchKernelGGL(k_pi_finish, dim3(1), dim3(1024), 0, st, m, mode);
             int64_t info2[2] = {iters, (int64_t)((mode == 1 ? 2 : 0) | (mode == 2 ? 1 : 0) | (flags & 4))};

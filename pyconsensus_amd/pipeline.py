@@ -134,6 +134,7 @@ class MatWorkspace:
         self.ev = z(16, E)
         self.cslab = z(self.cov_kslices, E, E)
         self.C = z(E, E)
+        self.Mw = z(2, E, E)
         self.pvec = z(4, E + 64)
         self.rowv = z(6, n_rows)
         self.rowstat = z(n_rows, 2, dt=t.int32)
@@ -203,7 +204,7 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     m.reports, m.scaled, m.lo, m.hi, m.rep_raw = P(R), P(sc), P(lo_), P(hi_), P(rep)
     m.scaled_cols, m.scaled_index = P(scols), P(sidx)
     for name in ("rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
-                 "pvec", "rowv", "rowstat", "skey", "info", "sel_sum", "sel_min", "sel_max", "sel_state",
+                 "Mw", "pvec", "rowv", "rowstat", "skey", "info", "sel_sum", "sel_min", "sel_max", "sel_state",
                  "sel_val"):
         setattr(m, name, P(getattr(ws, name)))
     for k, v in ws.out.items():
