@@ -161,6 +161,7 @@ enum pcx_mat_stage_id {
     PCX_M_SEL_HIST = 34,     /*   exact weight histogram over the current key range  */
     PCX_M_SEL_STEP = 35,     /*   narrow the range; converged columns get their result */
     PCX_M_SEL_FINISH = 36,   /*   results into guess (phase 1) / outcomes_raw (phase 2) */
+    PCX_M_SEL_EXACT = 37,    /* weighted median replayed with the reference's float order (n <= 8192, 1 rank) */
 };
 
 typedef struct {

@@ -57,6 +57,8 @@ M_REPUTATION, M_COLSTATS, M_GUESS, M_MEAN, M_COV, M_COV_REDUCE, M_COV_FINISH, M_
 M_SCORES, M_NCSUMS, M_GEMV2, M_DECIDE, M_REPU, M_SMOOTH, M_OUTCOMES, M_EVENTS = 9, 10, 11, 12, 13, 14, 15, 16
 M_SCALED_CERT, M_FINAL, M_ROWSUMS, M_AGENTS, M_MATRICES = 17, 18, 19, 20, 21
 M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH = 30, 31, 32, 33, 34, 35, 36
+M_SEL_EXACT = 37
+SEL_EXACT_MAX = 8192
 M_ZERO_LOADING = 99
 
 # info[] slots (pcx_matrix.hip info_slot)

@@ -1235,6 +1235,140 @@ __global__ void __launch_bounds__(BT) k_sel_finish(pcx_mat m) {
     }
 }
 
+// Exact replay of weightedstats.weighted_median with the reference's float arithmetic,
+// for one scaled event whose element count fits the block (n <= SEL_EXACT_MAX; single
+// rank).  Phase 1 (:287-303): weights rep_j / (sequential sum of present rep), over the
+// present reports in row order.  Phase 2 (:520-523): weights smooth_rep over all rows.
+// mid = 0.5 * builtin sum (row order); dominant weight -> first argmax; else bitonic sort
+// by (value, weight) and the sequential walk with the DBL_EPSILON exact-half test.
+constexpr int SEL_EXACT_MAX = 8192;
+
+__global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
+    const int s = blockIdx.x;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[0] == 0) return;
+    __shared__ double xs[SEL_EXACT_MAX];
+    __shared__ double ws[SEL_EXACT_MAX];
+    __shared__ int cnt;
+    __shared__ double mid_s, wmax_s;
+    __shared__ int first_s;
+    const int tid = threadIdx.x;
+    const int n_rows = (int)m.n_rows;
+    if (tid == 0) {
+        // sequential, row order: present total (phase 1), then the weights and their sum
+        double tot = 0.0;
+        if (m.sel_phase == 1)
+            for (int i = 0; i < n_rows; i++) {
+                double x, w;
+                if (sel_elem(m, s, i, x, w)) tot += w;
+            }
+        int k = 0;
+        double W = 0.0;
+        for (int i = 0; i < n_rows; i++) {
+            double x, w;
+            if (!sel_elem(m, s, i, x, w)) continue;
+            if (m.sel_phase == 1) w = w / tot;
+            xs[k] = x;
+            ws[k] = w;
+            W += w;
+            k++;
+        }
+        cnt = k;
+        mid_s = 0.5 * W;
+    }
+    __syncthreads();
+    const int n = cnt;
+    const double mid = mid_s;
+    // dominance: any(w > mid) -> data[first index of max(w)]
+    if (tid == 0) {
+        bool dom = false;
+        double mx = n ? ws[0] : 0.0;
+        for (int k = 0; k < n; k++) {
+            dom |= ws[k] > mid;
+            if (ws[k] > mx) mx = ws[k];
+        }
+        first_s = -1;
+        if (dom)
+            for (int k = 0; k < n; k++)
+                if (ws[k] == mx) {
+                    first_s = k;
+                    break;
+                }
+        bool pos = false;
+        for (int k = 0; k < n; k++) pos |= ws[k] > 0.0;
+        wmax_s = pos ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (first_s >= 0) {
+        if (tid == 0) {
+            st[12] = __double_as_longlong(xs[first_s]);
+            st[0] = 0;
+        }
+        return;
+    }
+    if (wmax_s == 0.0) {  // no positive weight: None
+        if (tid == 0) {
+            st[12] = __double_as_longlong(__builtin_nan(""));
+            st[0] = 0;
+        }
+        return;
+    }
+    // bitonic sort of (x, w) pairs, padded to a power of two with +inf
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int k = n + tid; k < P; k += 1024) {
+        xs[k] = __builtin_inf();
+        ws[k] = __builtin_inf();
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < P / 2; t += 1024) {
+                const int lo = 2 * stride * (t / stride) + (t % stride);
+                const int hi = lo + stride;
+                const bool up = ((lo & size) == 0);
+                const double xa = xs[lo], xb = xs[hi], wa = ws[lo], wb = ws[hi];
+                const bool gt = (xa > xb) || (xa == xb && wa > wb);
+                if (gt == up) {
+                    xs[lo] = xb;
+                    xs[hi] = xa;
+                    ws[lo] = wb;
+                    ws[hi] = wa;
+                }
+            }
+            __syncthreads();
+        }
+    if (tid == 0) {
+        double cum = 0.0;
+        int k = 0;
+        bool fail = false;
+        while (cum <= mid) {
+            if (k == n) {
+                fail = true;
+                break;
+            }
+            cum += ws[k];
+            k++;
+        }
+        double res;
+        if (fail) {
+            res = __builtin_nan("");
+        } else {
+            const double before = cum - ws[k - 1];
+            if (fabs(before - mid) < 2.220446049250313080847e-16) {
+                if (k >= 2)
+                    res = (xs[k - 2] + xs[k - 1]) / 2.0;
+                else
+                    res = n == 1 ? xs[0] / 1.0 : __builtin_nan("");
+            } else {
+                res = xs[k - 1];
+            }
+        }
+        st[12] = __double_as_longlong(res);
+        st[0] = 0;
+    }
+}
+
 // phase setup: which scaled events run a selection (phase 1: those with missing reports)
 __global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
@@ -1487,6 +1621,15 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_sel_setup, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_init, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            break;
+        case PCX_M_SEL_EXACT:
+            if (m.n_scaled == 0) break;
+            if (m.world != 1 || m.n_rows > SEL_EXACT_MAX) {
+                err = "PCX_M_SEL_EXACT needs one rank and n_rows <= 8192";
+                return hipErrorInvalidValue;
+            }
+            hipLaunchKernelGGL(k_sel_setup, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_exact, dim3(m.n_scaled), dim3(1024), 0, st, m);
             break;
         case PCX_M_SEL_START:
             if (m.n_scaled == 0) break;

@@ -297,6 +297,11 @@ def _select(stage, m, ws, comm, phase):
     if m.n_scaled == 0:
         return
     m.sel_phase = phase
+    if comm.world == 1 and m.n_rows <= _abi.SEL_EXACT_MAX:
+        # small matrices: replay the reference's float walk exactly (ties included)
+        stage(_abi.M_SEL_EXACT)
+        stage(_abi.M_SEL_FINISH)
+        return
     for b in (ws.sel_sum, ws.sel_min, ws.sel_max, ws.sel_val):
         comm.clear_slots(b)
     stage(_abi.M_SEL_INIT)

@@ -252,6 +252,7 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
     scaled = d.get("in_scaled", np.zeros(E, bool))
     bin_raw = raw[~scaled]
     d["neartie_catch"] = np.array(bool(bin_raw.size and np.min(np.abs(bin_raw[:, None] - thr[None, :])) < 1e-12))
+    d["neartie_catch_fill"] = np.array(False)
     if "s" in cap:  # interpolation guesses of binary columns (sequential weighted means)
         X, Fm = d["original"], cap["F"]
         miss = np.isnan(X) | (X == 0.0)
@@ -260,11 +261,23 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
             if pres.any():
                 g = math.fsum(cap["rep"][pres] * X[pres, j]) / math.fsum(cap["rep"][pres])
                 if np.min(np.abs(g - thr)) < 1e-12:
-                    d["neartie_catch"] = np.array(True)
+                    d["neartie_catch_fill"] = np.array(True)
     F = d["filled"]
     sm = d["agents.smooth_rep"]
     margins = [_median_margin(F[:, j], sm) for j in np.nonzero(scaled)[0]]
     d["neartie_median"] = np.array(bool(margins and min(margins) < 1e-12))
+    margins = []
+    # interpolation medians (present reports, reputation weights) -- exact ties here are
+    # common with integer reputations (a sorted prefix holding exactly half the weight)
+    if "s" in cap:
+        X = d["original"]
+        miss = np.isnan(X) | (X == 0.0)
+        for j in np.nonzero(miss.any(axis=0) & scaled)[0]:
+            pres = ~miss[:, j]
+            if pres.any():
+                r = cap["rep"][pres]
+                margins.append(_median_margin(X[pres, j], r / math.fsum(r)))
+    d["neartie_median_fill"] = np.array(bool(margins and min(margins) < 1e-12))
     return d
 
 
@@ -414,6 +427,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "synth_50x20.npz"), **st)
     print("synth_50x20: branch counts", np.bincount(st["branch"].astype(int)),
           "exact-arith branch differs", int(np.sum(st["branch"] != st["branch_exact"])),
+          "fill near-ties catch/median", st["neartie_catch_fill"].sum(), st["neartie_median_fill"].sum(),
           "near-ties rank/catch/median", st["neartie_rank"].sum(), st["neartie_catch"].sum(),
           st["neartie_median"].sum())
 

@@ -41,9 +41,23 @@ SIGNED = {"agents.scores", "events.adj_first_loadings"}
 EXCLUDED = {"q_all_missing_scaled_col"}
 
 
-def is_neartie(case):
-    return bool(case.get("neartie_rank", False)) or bool(case.get("neartie_catch", False)) \
-        or bool(case.get("neartie_median", False))
+def is_neartie(case, path="exact"):
+    """Is this round's discrete outcome decided by rounding on ``path``?
+
+    exact:  replays the reference's float order wherever it is defined by Python/numpy
+            (batched kernel, C oracle): only decisions fed by OpenBLAS/LAPACK results
+            are near ties -- the rank rule, catch of outcomes, outcome medians.
+    matrix_small: single-matrix path with N <= 8192 (medians replayed exactly, binary
+            fills from compensated sums): also binary fills at a catch threshold.
+    matrix_large: single-matrix path (exact-arithmetic medians): also fill medians.
+    """
+    f = lambda k: bool(case.get(k, False))
+    nt = f("neartie_rank") or f("neartie_catch") or f("neartie_median")
+    if path in ("matrix_small", "matrix_large"):
+        nt = nt or f("neartie_catch_fill")
+    if path == "matrix_large":
+        nt = nt or f("neartie_median_fill")
+    return nt
 
 
 def compare(case, ours, keys=None):

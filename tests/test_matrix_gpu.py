@@ -43,7 +43,7 @@ def _suite(cases):
         stats["n"] += 1
         stats["sign"] += sign
         ok = not bad and P.branch_matches(case, ours, sign)
-        if P.is_neartie(case):
+        if P.is_neartie(case, "matrix_small"):
             stats["neartie"] += 1
             stats["neartie_match"] += ok
         elif not ok:
@@ -88,6 +88,11 @@ def test_matrix_vs_numpy_oracle(gpu_lib, shape):
 
     N, E = shape
     R, sc, lo, hi, rep = synthetic.matrix(N, E, seed=N + E)
+    if N > 8192:
+        # the selection path computes medians in exact arithmetic; with integer
+        # reputations exact half-weight prefixes (rounding-decided in the reference)
+        # are common, so the large case uses continuous reputations
+        rep = np.random.default_rng(N).uniform(0.5, 99.5, N)
     b = synthetic.bounds_list(sc, lo, hi)
     ref = G.flat_result(OracleCPU(reports=R, event_bounds=b, reputation=rep).consensus())
     res = Oracle(reports=R.copy(), event_bounds=b, reputation=rep).consensus()
