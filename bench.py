@@ -64,6 +64,61 @@ def cpu_baseline(seconds=12.0):
     return out
 
 
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (spec)
+
+
+def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
+    """Config C5: one 1M x 4k report matrix (reputation=None), rows sharded over the
+    ranks; end-to-end consensus latency (inputs resident in HBM, outputs left there)."""
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.pipeline import Comm, consensus_matrix, shard_rows
+
+    per = 8 // world if 8 % world == 0 else None
+    shards = list(range(rank * per, (rank + 1) * per)) if per else None
+    off, cnt = shard_rows(N, world, rank)
+    if shards is None or cnt * world != N:
+        raise ValueError("C5 needs a GPU count dividing 8")
+    R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, shards=shards, device=dev)
+    comm = Comm(world, rank)
+
+    def run(profile=None):
+        return consensus_matrix(R, None, sc, lo, hi, comm=comm, n_total=N, row_offset=off, device=dev,
+                                profile=profile)
+
+    for _ in range(warmup):
+        run()
+    times, prof = [], {}
+    for _ in range(steps):
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev, ag, meta = run(prof)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            m = torch.tensor([el], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(m, op=torch.distributed.ReduceOp.MAX)
+            el = float(m.item())
+        times.append(el)
+    prof = {k: v / steps for k, v in prof.items()}
+    cov_ms = prof.get("M_COV", float("nan"))
+    cov_flops_rank = float(cnt) * E * (E + 1)  # one MAC per unique (j, k<=j) pair per row
+    tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms else None
+    del R
+    return {"metric": "1M x 4k consensus latency", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
+            "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
+            "branch": meta["branch"], "pi_iters": meta["pi_iters"], "flags": meta["flags"],
+            "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
+            "roofline_cov": {"bound": "mfma", "kernel": "k_cov", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
+                             "unit": "TFLOP/s", "frac": (tfs / FP64_MFMA_PEAK_TFS) if tfs else None,
+                             "flops_per_launch": cov_flops_rank},
+            "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
+                    "reputation=None"}
+
+
 def load_traffic():
     """Per-launch HBM bytes from the committed rocprofv3 PMC pass (profiles/), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -81,6 +136,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=ROUNDS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c5-steps", type=int, default=2, help="timed 1M x 4k consensus runs (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -169,6 +225,14 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
+    del Rd, out
+    torch.cuda.empty_cache()
+    c5 = None
+    if args.c5_steps > 0:
+        c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
+    if rank == 0:
+        if c5 is not None:
+            line["c5"] = c5
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

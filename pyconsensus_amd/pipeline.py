@@ -153,7 +153,7 @@ class MatWorkspace:
 
 def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, catch_tolerance=0.1,
                      alpha=0.1, int_dtype=False, algorithm="PCA", comm=None, n_total=None,
-                     row_offset=None, device=None, matrices=False):
+                     row_offset=None, device=None, matrices=False, profile=None):
     """Consensus of one report matrix on the GPU(s).
 
     reports:    this rank's rows, (n_rows, E) float64 (torch tensor on the GPU, or numpy)
@@ -161,6 +161,8 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     scaled/lo/hi: event bounds (E,), or None (every event binary)
     comm:       :class:`Comm` (default: single GPU)
     matrices:   also return this rank's rescaled ("original") and filled reports
+    profile:    optional dict; receives per-stage device milliseconds (HIP events on the
+                launching stream) under the stage names of include/pcx.h
 
     Returns (events, agents, info): event-level tensors (identical on every rank),
     this rank's per-reporter tensors, and a dict of scalars/diagnostics.
@@ -219,8 +221,18 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev))
     lib = _lib.lib()
 
+    names = {v: k for k, v in vars(_abi).items() if k.startswith("M_") and isinstance(v, int)}
+    events = []
+
     def stage(s):
+        if profile is not None:
+            e0 = t.cuda.Event(enable_timing=True)
+            e0.record()
         _lib.check(lib.pcx_mat_stage(h, C.byref(m), int(s)))
+        if profile is not None:
+            e1 = t.cuda.Event(enable_timing=True)
+            e1.record()
+            events.append((names.get(int(s), str(s)), e0, e1))
 
     S = slice
     # a1: reputation, tokens (__init__.py:138-146)
@@ -281,6 +293,10 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
         stage(_abi.M_MATRICES)
 
     info = ws.info.cpu().tolist()
+    if profile is not None:
+        t.cuda.synchronize(dev)
+        for name, e0, e1 in events:
+            profile[name] = profile.get(name, 0.0) + e0.elapsed_time(e1)
     scal = ws.scalars.cpu().tolist()
     events = {k: ws.out[k] for k in _abi.MAT_OUTPUT_EVENTS}
     agents = {k: ws.out[k] for k in _abi.MAT_OUTPUT_AGENTS}
