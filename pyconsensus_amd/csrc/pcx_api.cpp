@@ -8,6 +8,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
+#include <cstdlib>
 
 #include "../../include/pcx.h"
 #include "pcx_internal.h"
@@ -120,7 +122,27 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     a.pi_iters = out->pi_iters;
     a.original = out->original;
     a.filled = out->filled;
+    const char* st_env = getenv("PCX_STAMPS");
+    if (st_env && st_env[0] == '1' && a.B > 0) {  // diagnostic: per-phase clock breakdown
+        long long* d = nullptr;
+        if (hipMalloc(&d, a.B * 16 * sizeof(long long)) == hipSuccess) {
+            (void)hipMemsetAsync(d, 0, a.B * 16 * sizeof(long long), ctx->stream);
+            a.stamps = d;
+        }
+    }
     e = pcx::launch_batched(a, ctx->stream);
+    if (a.stamps) {
+        std::vector<long long> h(a.B * 16);
+        (void)hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(a.stamps);
+        double acc[16] = {0};
+        for (int64_t b = 0; b < a.B; b++)
+            for (int k = 1; k < 13; k++) acc[k] += (double)(h[b * 16 + k] - h[b * 16 + k - 1]);
+        fprintf(stderr, "PCX_STAMPS mean cycles per phase:");
+        for (int k = 1; k < 13; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / (double)a.B);
+        fprintf(stderr, "\n");
+    }
     return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");
 }
 

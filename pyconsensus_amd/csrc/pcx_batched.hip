@@ -41,6 +41,15 @@ constexpr double DBL_EPS = 2.220446049250313080847e-16;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
+// diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
+#define STAMP(k)                                                                  \
+    do {                                                                          \
+        if (a.stamps) {                                                           \
+            const long long t_ = (long long)__builtin_amdgcn_s_memtime();         \
+            if (threadIdx.x == 0) a.stamps[b * 16 + (k)] = t_;                    \
+        }                                                                         \
+    } while (0)
+
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
@@ -311,6 +320,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     const int64_t bo = a.bounds_shared ? 0 : b * E;
     const bool has_bounds = a.scaled != nullptr;
 
+    STAMP(0);
     // ---- load the round -------------------------------------------------
     const double* Rg = a.reports + b * (int64_t)N * E;
     for (int idx = l; idx < N * E; idx += W) {
@@ -343,6 +353,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     const double denom = tree_sum(row ? tok : 0.0) - 1.0;  // exact integer sum
     wsync();
 
+    STAMP(1);
     // ---- a2: rescale (:266-269) + NA masks (:278) -------------------------
     for (int j = 0; j < E; j++) {
         const bool sc = (scaled_mask >> j) & 1;
@@ -366,6 +377,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     }
     wsync();
 
+    STAMP(2);
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
     uint64_t miss_j = 0;
     double Wj = 0.0;
@@ -420,6 +432,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     if (a.filled && row)
         for (int j = 0; j < E; j++) a.filled[(b * N + l) * E + j] = S.F[l * ES + j];
 
+    STAMP(3);
     // ---- old = rep . F (np.dot) -------------------------------------------
     double oldj = col ? dot2(S.rep, S.F + l, ES, N) : 0.0;
     if (col) S.old[l] = oldj;
@@ -443,6 +456,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         if (col) S.mu[l] = muj;
         wsync();
 
+        STAMP(4);
         // ---- a6: token-weighted covariance (:326), lower triangle ----------
         const int ntri = E * (E + 1) / 2;
         bool nonzero = false, finite = true;
@@ -466,6 +480,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         const bool all_fin = ballot(!finite) == 0;
         wsync();
 
+        STAMP(5);
         // ---- a7: leading eigenvector by power iteration (:330-336) -------
         double xv = 0.0;
         if (!all_fin) {
@@ -534,6 +549,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             for (int j = 0; j < E; j++) acc = fma(S.F[l * ES + j] - S.mu[j], S.ld[j], acc);
             sc_i = acc;
         }
+        STAMP(6);
         // ---- a8/a9: nonconformity_rank (:487-500) / nonconformity (:475-485)
         const bool any_nan = ballot(row && __builtin_isnan(sc_i)) != 0;
         double mn = wave_max(row ? -sc_i : -__builtin_inf());
@@ -589,6 +605,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         nc_i = pick1 ? set1 : set2;
     }
 
+    STAMP(7);
     // ---- a10: reputation update (:460-472) --------------------------------
     const double meanrep = wave_pw_sum(rep, row, S.scr) / (double)N;
     double u = fabs(nc_i * (rep / meanrep));
@@ -603,6 +620,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     if (row) S.smooth[l] = smooth_i;
     wsync();
 
+    STAMP(8);
     // ---- a12/a13: outcomes (:510-538) -------------------------------------
     double rawj = col ? dot2(S.smooth, S.F + l, ES, N) : 0.0;
     if (scaled_mask) {
@@ -636,6 +654,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     }
     wsync();
 
+    STAMP(9);
     // ---- a14: certainty (:540-546): pairwise sum of the matching smooth_rep --
     double certj = 0.0;
     for (int j = 0; j < E; j++) {
@@ -655,6 +674,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     const double reward = ac / Sc;
     const double avg_cert = wave_pw_sum(certj, col, S.scr) / (double)E;
 
+    STAMP(10);
     // ---- a15: participation and bonuses (:549-581) -------------------------
     double pcj = 0.0, nzj = 0.0;
     if (col) {
@@ -702,6 +722,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     }
     const double relc = apc / Spc;
 
+    STAMP(11);
     // ---- write the round ---------------------------------------------------
     if (row) {
         const int64_t o = b * N + l;
@@ -733,6 +754,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         if (a.flags) a.flags[b] = flags;
         if (a.pi_iters) a.pi_iters[b] = iters;
     }
+    STAMP(12);
 }
 
 size_t batched_lds_bytes(int N, int E) {

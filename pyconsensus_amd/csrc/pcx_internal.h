@@ -31,6 +31,7 @@ struct BatchArgs {
     double *participation, *avg_certainty;
     int32_t *branch, *flags, *pi_iters;
     double *original, *filled;
+    long long* stamps;  // diagnostic phase clocks [B][16] (PCX_STAMPS), normally NULL
 };
 
 size_t batched_lds_bytes(int N, int E);
