@@ -40,7 +40,9 @@ def test_kat_through_oracle(gpu_lib, name):
     res = Oracle(**G.oracle_args(case)).consensus()
     ours = {P.ABI_NAME[k]: v for k, v in G.flat_result(res).items() if k in P.ABI_NAME}
     bad, sign = P.compare(case, ours)
-    if P.is_neartie(case):
+    if bad and P.is_neartie(case):
+        # the reference's own decision here depends on OpenBLAS/LAPACK rounding (fixture flag);
+        # a near-tie round that matches anyway passes
         pytest.skip("near tie (reference decision depends on BLAS rounding): %s" % (bad[:2],))
     assert not bad, bad
 
