@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=ROUNDS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--c5-steps", type=int, default=2, help="timed 1M x 4k consensus runs (0 = skip)")
+    ap.add_argument("--c5-steps", type=int, default=3, help="timed 1M x 4k consensus runs (0 = skip)")
     args = ap.parse_args()
 
     import torch

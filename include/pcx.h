@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 1
+#define PCX_ABI_VERSION 2
 
 enum pcx_status {
     PCX_OK = 0,
@@ -218,6 +218,11 @@ typedef struct {
     double* scalars;              /* [4]: participation, avg_certainty, branch, flags */
     double* original;             /* [n_rows][E] rescaled reports (PCX_M_MATRICES), optional */
     double* filled;               /* [n_rows][E] filled reports (PCX_M_MATRICES), optional   */
+    /* covariance operands (PCX_M_COV): the centred, filled matrix materialised once */
+    double* wcd;                  /* [wcd_rows][wcd_ld] wcd = F - mu (:322), zero padded          */
+    double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
+    int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
+    int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
 } pcx_mat;
 
 /* Run one stage on the context's stream (PCX_M_POWER and the selection steps may

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
@@ -86,4 +86,5 @@ class Mat(C.Structure):
         ("pvec", _vp), ("rowv", _vp), ("rowstat", _vp), ("skey", _vp), ("info", _vp),
         ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
     ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),
-                                                                   ("filled", _vp)]
+                                                                   ("filled", _vp)] + [
+        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64)]

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/pcx.h"
 #include "pcx_device.h"
 #include "pcx_internal.h"
@@ -371,78 +373,168 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
             }
 }
 
-// covariance loader: wcd = F - mu computed from the raw reports; A side times the tokens
-struct CovLoader {
-    const pcx_mat* m;
-    const double (*prm)[5][CT];
-    bool diag;
-    __device__ void load(int64_t i, int64_t re, int I, int J, int scg, double* va, double* vb) const {
-        const int E = (int)m->n_events;
-        const bool rowok = i < re;
-        const double tk = rowok ? m->tok[i] : 0.0;
-        for (int s = 0; s < (diag ? 1 : 2); s++) {
-            const int cb = (s == 0 ? I : J) * CT;
-            for (int k = 0; k < 8; k++) {
-                const int q = scg + k;
-                const int c = cb + q;
-                double w = 0.0;
-                if (rowok && c < E) {
-                    double x = m->reports[i * E + c];
-                    if (prm[s][0][q] != 0.0) {
-                        x = (x - prm[s][1][q]) / prm[s][2][q];
-                        if (m->int_dtype) x = trunc(x);
-                    }
-                    if (missing(x)) x = prm[s][3][q];
-                    w = x - prm[s][4][q];
-                }
-                if (s == 0) {
-                    va[k] = w * tk;  // np.ma.multiply(wcd.T, tokens): the product is rounded first
-                    if (diag) vb[k] = w;
-                } else {
-                    vb[k] = w;
-                }
+// ---------------------------------------------------------------- covariance operands
+// PCX_M_COV step 1: wcd = F - mu (:317-322) materialised once, [wcd_rows][wcd_ld] with
+// zero padding, plus the tokens zero-padded past n_rows.  The SYRK then streams plain
+// rows (every element is re-read by nb/2 tiles; the transform runs once).
+constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread, 16-byte accesses)
+
+__global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const int64_t ld = m.wcd_ld;
+    const int c0 = blockIdx.y * WCD_COLS + 2 * threadIdx.x;
+    ColParam p[2];
+    bool ok[2];
+    for (int k = 0; k < 2; k++) {
+        ok[k] = c0 + k < E;
+        p[k] = ok[k] ? col_param(m, c0 + k, true) : ColParam{false, 0.0, 1.0, 0.0, 0.0};
+    }
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
+         i += (int64_t)gridDim.x * BT)
+        m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
+    if (c0 >= ld) return;
+    for (int64_t i = blockIdx.x; i < m.wcd_rows; i += gridDim.x) {
+        double w[2] = {0.0, 0.0};
+        if (i < m.n_rows) {
+            const double* r = m.reports + i * E + c0;
+            for (int k = 0; k < 2; k++)
+                if (ok[k]) w[k] = filled(r[k], p[k], m.int_dtype) - p[k].mu;
+        }
+        *(double2*)(m.wcd + i * ld + c0) = double2{w[0], w[1]};
+    }
+}
+
+// PCX_M_COV step 2: partial C = wcd^T diag(tok) wcd (:326) over one row slice, one
+// 128x128 lower-triangle tile per workgroup on fp64 MFMA.  Rows arrive by
+// global_load_lds_dwordx4 (one 1 KB tile row per wave instruction) into a two-stage
+// LDS ring of 16-row stages; one raw barrier per stage, counted vmcnt (the only
+// vector-memory ops in the loop are these DMAs).  75 KB LDS + 208 VGPRs = 2
+// workgroups (2 waves per SIMD) per CU: one wave alone issues an f64 MFMA only every
+// ~128 cycles, two interleave to the 64-cycle rate (tools/covbench, profiles/).
+// The A operand is rounded as tok*w before the MFMA (np.ma.multiply(wcd.T, tokens)).
+constexpr int SY_BK = 16;                       // rows per stage
+constexpr int SY_NBUF = 2;                      // LDS ring depth
+constexpr int SY_LDP = CT + 16;                 // padded LDS row: conflict-free b64 fragment reads
+
+template <bool DIAG>
+struct SyRing {
+    static constexpr int A_OFF = 0;
+    static constexpr int B_OFF = SY_BK * SY_LDP;
+    static constexpr int T_OFF = (DIAG ? 1 : 2) * SY_BK * SY_LDP;
+    static constexpr int STRIDE = T_OFF + 4 * 32;             // doubles per buffer
+    static constexpr int LPW = (DIAG ? SY_BK / 4 : SY_BK / 2) + 1;  // DMAs per wave per stage
+};
+constexpr size_t SY_LDS_BYTES = (size_t)SY_NBUF * SyRing<false>::STRIDE * sizeof(double);
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void syrk_tile(const double* W, const double* tok, int64_t ld, int I, int J, int64_t s0,
+                                          int64_t ns, double* lds, d4 (&acc)[4][4]) {
+    using R = SyRing<DIAG>;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const double* colA = W + I * CT + 2 * lane;
+    const double* colB = W + J * CT + 2 * lane;
+    auto issue = [&](int64_t s, int b) {
+        double* buf = lds + b * R::STRIDE;
+        const int64_t row0 = (s0 + s) * SY_BK;
+#pragma unroll
+        for (int k = 0; k < SY_BK / 4; k++) {
+            const int r = wv + 4 * k;
+            __builtin_amdgcn_global_load_lds((const void*)(colA + (row0 + r) * ld),
+                                             (lds_ptr_t)(buf + R::A_OFF + r * SY_LDP), 16, 0, 0);
+        }
+        if (!DIAG) {
+#pragma unroll
+            for (int k = 0; k < SY_BK / 4; k++) {
+                const int r = wv + 4 * k;
+                __builtin_amdgcn_global_load_lds((const void*)(colB + (row0 + r) * ld),
+                                                 (lds_ptr_t)(buf + R::B_OFF + r * SY_LDP), 16, 0, 0);
             }
         }
+        // 64 dwords = tokens of rows row0 .. row0+31 (tokp is padded) into this wave's slot
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)(tok + row0) + 4 * lane),
+                                         (lds_ptr_t)(buf + R::T_OFF + wv * 32), 4, 0, 0);
+    };
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < SY_NBUF - 1; s++)
+        if (s < ns) issue(s, s);
+    for (int64_t t = 0; t < ns; t++) {
+        if (t + SY_NBUF - 2 < ns)
+            wait_vmcnt<R::LPW * (SY_NBUF - 2)>();
+        else
+            wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + SY_NBUF - 1 < ns) issue(t + SY_NBUF - 1, (int)((t + SY_NBUF - 1) % SY_NBUF));
+        const double* buf = lds + (int)(t % SY_NBUF) * R::STRIDE;
+        const double* As = buf + R::A_OFF;
+        const double* Bs = DIAG ? As : buf + R::B_OFF;
+        const double* Ts = buf + R::T_OFF + wv * 32;
+#pragma unroll
+        for (int kk = 0; kk < SY_BK / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            const double tk = Ts[kr];
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr * SY_LDP + wr * 64 + a * 16 + (lane & 15)] * tk;
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[kr * SY_LDP + wc * 64 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        asm volatile("" ::: "memory");
     }
-};
+}
 
-// one work item = (lower-triangle tile (I,J), row slice ks): partial
-// C[p][q] = sum over the slice's rows of (tok_i * wcd_ip) * wcd_iq  (:326)
-__global__ void __launch_bounds__(256) k_cov(pcx_mat m) {
-    __shared__ double prm[2][5][CT];  // side, {scaled, lo, range, guess, mu}
+// XCD-aware bijective remap: consecutive logical items (the tiles of one row slice)
+// land on one XCD, so their shared rows are fetched into one L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// one work item = (lower-triangle tile (I,J), row slice ks) -> cslab[ks] (lower part)
+__global__ void __launch_bounds__(256) k_syrk(pcx_mat m) {
+    extern __shared__ __attribute__((aligned(16))) double sy_lds[];
     const int E = (int)m.n_events;
     const int ntiles = m.cov_tiles, nks = m.cov_kslices;
-    const int item = blockIdx.x;
-    const int ks = item / ntiles, t = item % ntiles;  // slice-major: concurrent tiles share rows
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / ntiles, t = item % ntiles;
     int I, J;
     tri_index(t, I, J);
-    const int64_t per = (m.n_rows + nks - 1) / nks;
-    const int64_t rb = (int64_t)ks * per;
-    const int64_t re = rb + per < m.n_rows ? rb + per : m.n_rows;
-    const int tid = threadIdx.x;
-    for (int s = 0; s < 2; s++)
-        for (int q = tid; q < CT; q += 256) {
-            const int c = (s == 0 ? I : J) * CT + q;
-            double sc = 0, lo = 0, rg = 1, g = 0, mu = 0;
-            if (c < E) {
-                const ColParam p = col_param(m, c, true);
-                sc = p.scaled ? 1.0 : 0.0;
-                lo = p.lo;
-                rg = p.range;
-                g = p.guess;
-                mu = p.mu;
-            }
-            prm[s][0][q] = sc;
-            prm[s][1][q] = lo;
-            prm[s][2][q] = rg;
-            prm[s][3][q] = g;
-            prm[s][4][q] = mu;
-        }
-    __syncthreads();
-    CovLoader ld{&m, prm, I == J};
+    const int64_t nst = m.wcd_rows / SY_BK;
+    const int64_t per = (nst + nks - 1) / nks;
+    const int64_t s0 = ks * per < nst ? ks * per : nst;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
     d4 acc[4][4];
-    mfma_tile(ld, I, J, rb, re, acc);
-    store_tile(m.cslab + (int64_t)ks * E * E, E, E, I, J, acc);
+    if (I == J)
+        syrk_tile<true>(m.wcd, m.tokp, m.wcd_ld, I, J, s0, s1 - s0, sy_lds, acc);
+    else
+        syrk_tile<false>(m.wcd, m.tokp, m.wcd_ld, I, J, s0, s1 - s0, sy_lds, acc);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    double* out = m.cslab + (int64_t)ks * E * E;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++)
+            for (int r = 0; r < 4; r++) {
+                const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
+                const int64_t q = (int64_t)J * CT + wc * 64 + b * 16 + (lane & 15);
+                if (p < E && q <= p) out[p * E + q] = acc[a][b][r];
+            }
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -1562,9 +1654,25 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case PCX_M_MEAN:
             hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
             break;
-        case PCX_M_COV:
-            hipLaunchKernelGGL(k_cov, dim3(m.cov_tiles * m.cov_kslices), dim3(256), 0, st, m);
+        case PCX_M_COV: {
+            if (!m.wcd || !m.tokp || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
+                m.wcd_ld < m.n_events) {
+                err = "PCX_M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
+                return hipErrorInvalidValue;
+            }
+            const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
+            hipLaunchKernelGGL(k_wcd, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(m.wcd_rows, 4096 / ncb)), ncb),
+                               dim3(BT), 0, st, m);
+            static bool lds_set = false;
+            if (!lds_set) {
+                hipError_t e = hipFuncSetAttribute((const void*)k_syrk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)SY_LDS_BYTES);
+                if (e != hipSuccess) return e;
+                lds_set = true;
+            }
+            hipLaunchKernelGGL(k_syrk, dim3(m.cov_tiles * m.cov_kslices), dim3(256), SY_LDS_BYTES, st, m);
             break;
+        }
         case PCX_M_COV_REDUCE: {
             const int64_t n = (int64_t)E * E;
             hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);

@@ -14,11 +14,13 @@ nonconformity_rank :487-500, lie_detector tail :459-473, consensus :502-611.
 from __future__ import annotations
 
 import ctypes as C
+import threading
 
 from . import _abi, _device, _lib
 
 COL_THREADS = 256
 COV_TILE = 128
+COV_STAGE = 16
 
 
 class Comm:
@@ -64,8 +66,6 @@ class ThreadGroup:
     """Shared state of :class:`ThreadComm` ranks (one thread per virtual shard)."""
 
     def __init__(self, world):
-        import threading
-
         self.world = int(world)
         self.barrier = threading.Barrier(self.world)
         self.bufs = [None] * self.world
@@ -118,9 +118,13 @@ class MatWorkspace:
         self.col_blocks = max(1, min(max(1, 2048 // ceb), (n_rows + 31) // 32, 4096))
         nb = (E + COV_TILE - 1) // COV_TILE
         self.cov_tiles = nb * (nb + 1) // 2
-        ks = max(1, min(16, round(8 * 256 / self.cov_tiles)))
-        ks = max(1, min(ks, n_rows // 1024 if n_rows >= 1024 else 1))
-        self.cov_kslices = ks
+        # covariance operand wcd, materialised [wcd_rows][wcd_ld] (16-row stages, 128-col tiles)
+        self.wcd_rows = (n_rows + COV_STAGE - 1) // COV_STAGE * COV_STAGE
+        self.wcd_ld = nb * COV_TILE
+        # row slices: >= ~16 workgroups per CU slot (2 per CU), each slice >= 8 stages
+        stages = self.wcd_rows // COV_STAGE
+        ks = -(-16 * 2 * 256 // self.cov_tiles)
+        self.cov_kslices = max(1, min(32, ks, stages // 8 if stages >= 8 else 1))
         z = lambda *shape, dt=f64: t.zeros(shape, dtype=dt, device=device)
         self.rep = z(n_rows)
         self.tok = z(n_rows)
@@ -133,6 +137,8 @@ class MatWorkspace:
         self.spart = z(4096, 4, 2)
         self.ev = z(16, E)
         self.cslab = z(self.cov_kslices, E, E)
+        self.wcd = t.empty((self.wcd_rows, self.wcd_ld), dtype=f64, device=device)
+        self.tokp = t.empty((self.wcd_rows + 64,), dtype=f64, device=device)
         self.C = z(E, E)
         self.Mw = z(2, E, E)
         self.pvec = z(4, E + 64)
@@ -146,9 +152,54 @@ class MatWorkspace:
         self.sel_max = z(world, S, 256, dt=u64)
         self.sel_state = z(S, 16, dt=u64)
         self.sel_val = z(world, S, 4)
-        self.out = {k: z(n_rows) for k in _abi.MAT_OUTPUT_AGENTS}
-        self.out.update({k: z(E) for k in _abi.MAT_OUTPUT_EVENTS})
-        self.scalars = z(4)
+
+    # buffers every stage writes in full before reading: not re-zeroed on reuse
+    _NO_RESET = ("wcd", "tokp", "T", "cslab", "C", "Mw")
+
+    def reset(self):
+        """Zero the scratch for another consensus of the same shape (reuse across calls)."""
+        for name, v in vars(self).items():
+            if name not in self._NO_RESET and hasattr(v, "zero_"):
+                v.zero_()
+
+    def new_outputs(self):
+        """Fresh result tensors for one call (results outlive the reused scratch)."""
+        t = _device.torch()
+        z = lambda n: t.zeros(n, dtype=t.float64, device=self.device)
+        out = {k: z(self.n_rows) for k in _abi.MAT_OUTPUT_AGENTS}
+        out.update({k: z(self.E) for k in _abi.MAT_OUTPUT_EVENTS})
+        return out, z(4)
+
+
+_WS_CACHE = {}       # (n_rows, E, n_scaled, world, rank, device) -> MatWorkspace
+_WS_CACHE_MAX = 4
+_WS_LOCK = threading.Lock()
+
+
+def _workspace(n_rows, E, n_scaled, world, rank, device):
+    """Scratch of one rank, reused across calls of the same shape (allocating and first-touching
+    tens of GB per call costs ~0.1 s at C5 sizes).  Least recently used entries are dropped."""
+    key = (int(n_rows), int(E), int(n_scaled), int(world), int(rank), str(device))
+    with _WS_LOCK:
+        ws = _WS_CACHE.pop(key, None)
+        if ws is not None and getattr(ws, "_busy", False):
+            ws = None  # the same key in use on another thread: build a private one
+        if ws is None:
+            while len(_WS_CACHE) >= _WS_CACHE_MAX:
+                _WS_CACHE.pop(next(iter(_WS_CACHE)))
+            ws = MatWorkspace(n_rows, E, n_scaled, world, device)
+        else:
+            ws.reset()
+        ws._busy = True
+        _WS_CACHE[key] = ws
+    return ws
+
+
+def clear_workspace_cache():
+    """Release every cached single-matrix workspace (device memory returns to torch's allocator)."""
+    with _WS_LOCK:
+        _WS_CACHE.clear()
+
 
 
 def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, catch_tolerance=0.1,
@@ -195,23 +246,36 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     if alg is None:
         raise NotImplementedError("algorithm %r is not on the GPU path" % (algorithm,))
 
-    ws = MatWorkspace(n_rows, E, n_scaled, comm.world, dev)
+    ws = _workspace(n_rows, E, n_scaled, comm.world, comm.rank, dev)
+    try:
+        return _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev, catch_tolerance,
+                    alpha, int_dtype, matrices, profile)
+    finally:
+        ws._busy = False
+
+
+def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev, catch_tolerance, alpha,
+         int_dtype, matrices, profile):
+    t = _device.torch()
+    n_rows, E = R.shape
+    out, scalars = ws.new_outputs()
     m = _abi.Mat()
     m.n_rows, m.n_events, m.n_total, m.row_offset = n_rows, E, N, r0
     m.world, m.rank, m.int_dtype, m.algorithm = comm.world, comm.rank, int(bool(int_dtype)), alg
     m.catch_tolerance, m.alpha = float(catch_tolerance), float(alpha)
     m.n_scaled, m.sel_phase, m.col_blocks = n_scaled, 1, ws.col_blocks
     m.cov_tiles, m.cov_kslices = ws.cov_tiles, ws.cov_kslices
+    m.wcd_rows, m.wcd_ld = ws.wcd_rows, ws.wcd_ld
     P = _device.ptr
     m.reports, m.scaled, m.lo, m.hi, m.rep_raw = P(R), P(sc), P(lo_), P(hi_), P(rep)
     m.scaled_cols, m.scaled_index = P(scols), P(sidx)
-    for name in ("rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
+    for name in ("wcd", "tokp", "rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
                  "Mw", "pvec", "rowv", "rowstat", "skey", "info", "sel_sum", "sel_min", "sel_max", "sel_state",
                  "sel_val"):
         setattr(m, name, P(getattr(ws, name)))
-    for k, v in ws.out.items():
+    for k, v in out.items():
         setattr(m, k, P(v))
-    m.scalars = P(ws.scalars)
+    m.scalars = P(scalars)
     mats = {}
     if matrices:
         mats = {"original": t.empty((n_rows, E), dtype=t.float64, device=dev),
@@ -297,9 +361,9 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
         t.cuda.synchronize(dev)
         for name, e0, e1 in events:
             profile[name] = profile.get(name, 0.0) + e0.elapsed_time(e1)
-    scal = ws.scalars.cpu().tolist()
-    events = {k: ws.out[k] for k in _abi.MAT_OUTPUT_EVENTS}
-    agents = {k: ws.out[k] for k in _abi.MAT_OUTPUT_AGENTS}
+    scal = scalars.cpu().tolist()
+    events = {k: out[k] for k in _abi.MAT_OUTPUT_EVENTS}
+    agents = {k: out[k] for k in _abi.MAT_OUTPUT_AGENTS}
     agents.update(mats)
     meta = {"participation": scal[0], "avg_certainty": scal[1],
             "branch": int(info[_abi.INFO_BRANCH]) if pca else _abi.BRANCH_NONE,

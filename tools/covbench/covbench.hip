@@ -1,0 +1,460 @@
+// covbench.hip -- standalone microbenchmark for the token-weighted covariance
+// C = W^T diag(tok) W (pyconsensus/__init__.py:326) on fp64 MFMA, gfx950.
+//
+// W is the centred, filled matrix wcd, materialised [Np][Ep] row-major with zero
+// padding (Np a multiple of the row stage, Ep of 128).  Variants:
+//   peak  : bare v_mfma_f64_16x16x4_f64 loop (operands in registers, random data)
+//   reg   : the round-1 k_cov structure (register-staged 16-row stages, two
+//           __syncthreads per stage) on the materialised W
+//   glds  : global_load_lds_dwordx4 into an NBUF-deep LDS ring, one raw barrier
+//           per stage, counted vmcnt (tile 128x128, 4 waves 2x2, 64x64 per wave)
+// Checks every variant's slab sum against a VALU fp64 reference on a small case.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/covbench/covbench.hip -o tools/covbench/covbench
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);      \
+            exit(1);                                                                            \
+        }                                                                                       \
+    } while (0)
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int CT = 128;
+constexpr int LDP = CT + 16;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void tri_index(int t, int& I, int& J) {
+    int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= t) i++;
+    while (i * (i + 1) / 2 > t) i--;
+    I = i;
+    J = t - i * (i + 1) / 2;
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// ------------------------------------------------------------------ init
+__device__ __forceinline__ double hrand(uint64_t i) {
+    uint64_t z = i * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+
+__global__ void k_init(double* W, int64_t n_rows, int64_t Np, int E, int Ep, double* tok, int tokmode) {
+    const int64_t tot = Np * Ep;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / Ep;
+        const int c = (int)(i % Ep);
+        W[i] = (r < n_rows && c < E) ? hrand(i) : 0.0;
+        if (c == 0) tok[r] = r < n_rows ? (tokmode ? (double)((uint64_t)(hrand(~i) * 1e6) % 4) : 1.0) : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------ peak
+__global__ void __launch_bounds__(256) k_peak(const double* in, double* out, int iters, long long* clk) {
+    const int lane = threadIdx.x & 63;
+    double a = in[lane], b = in[64 + lane];
+    d4 acc[16];
+    for (int k = 0; k < 16; k++) acc[k] = d4{in[k], in[k + 1], in[k + 2], in[k + 3]};
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    const long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    const long long r1 = __builtin_amdgcn_s_memrealtime();
+    double s = 0;
+    for (int k = 0; k < 16; k++) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+    if (threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+// ------------------------------------------------------------------ reference (VALU)
+__global__ void k_ref(const double* W, const double* tok, int64_t Np, int E, int Ep, double* C) {
+    const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)E * E) return;
+    const int p = (int)(idx / E), q = (int)(idx % E);
+    if (q > p) return;
+    double s = 0.0;
+    for (int64_t i = 0; i < Np; i++) s = fma(W[i * Ep + p] * tok[i], W[i * Ep + q], s);
+    C[(int64_t)p * E + q] = s;
+}
+
+__device__ __forceinline__ void store_tile(double* out, int64_t E, int I, int J, const d4 (&acc)[4][4]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++)
+            for (int r = 0; r < 4; r++) {
+                const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
+                const int64_t q = (int64_t)J * CT + wc * 64 + b * 16 + (lane & 15);
+                if (p < E && q < E && q <= p) out[p * E + q] = acc[a][b][r];
+            }
+}
+
+// ------------------------------------------------------------------ variant reg
+template <int KB>
+__global__ void __launch_bounds__(256) k_syrk_reg(const double* W, const double* tok, int64_t Np, int E, int Ep,
+                                                  int ntiles, int nks, double* slab) {
+    __shared__ __attribute__((aligned(16))) double As[KB][LDP];
+    __shared__ __attribute__((aligned(16))) double Bs[KB][LDP];
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / ntiles, t = item % ntiles;
+    int I, J;
+    tri_index(t, I, J);
+    const int64_t nst = Np / KB;
+    const int64_t per = (nst + nks - 1) / nks;
+    const int64_t rb = ks * per * KB;
+    const int64_t re = (ks + 1) * per * KB < Np ? (ks + 1) * per * KB : Np;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    d4 acc[4][4];
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    constexpr int TPR = 256 / KB;     // threads per staged row
+    constexpr int CPT = CT / TPR;     // columns per thread
+    const int sr = tid / TPR, scg = (tid % TPR) * CPT;
+    double va[CPT], vb[CPT];
+    auto load = [&](int64_t i) {
+        const double tk = tok[i];
+        const double* ra = W + i * Ep + I * CT + scg;
+        const double* rbp = W + i * Ep + J * CT + scg;
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            va[k] = ra[k] * tk;
+            vb[k] = rbp[k];
+        }
+    };
+    if (rb < re) load(rb + sr);
+    for (int64_t i0 = rb; i0 < re; i0 += KB) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            As[sr][scg + k] = va[k];
+            Bs[sr][scg + k] = vb[k];
+        }
+        __syncthreads();
+        if (i0 + KB < re) load(i0 + KB + sr);
+#pragma unroll
+        for (int kk = 0; kk < KB / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr][wr * 64 + a * 16 + (lane & 15)];
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[kr][wc * 64 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    store_tile(slab + (int64_t)ks * E * E, E, I, J, acc);
+}
+
+// ------------------------------------------------------------------ variant glds
+// LDS ring: NBUF x { A[BK][LDP], B[BK][LDP] (absent when DIAG), tok[4 waves][32] }
+template <int BK, bool DIAG>
+struct Ring {
+    static constexpr int A_OFF = 0;
+    static constexpr int B_OFF = BK * LDP;
+    static constexpr int T_OFF = (DIAG ? 1 : 2) * BK * LDP;
+    static constexpr int STRIDE = T_OFF + 4 * 32;  // doubles per buffer
+    static constexpr int LPW = (DIAG ? BK / 4 : BK / 2) + 1;  // glds per wave per stage
+};
+
+template <int BK, int NBUF, bool DIAG>
+__device__ __forceinline__ void glds_tile(const double* W, const double* tok, int Ep, int I, int J, int64_t s0,
+                                          int64_t ns, double* lds, d4 (&acc)[4][4]) {
+    using R = Ring<BK, DIAG>;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const double* colA = W + I * CT + 2 * lane;
+    const double* colB = W + J * CT + 2 * lane;
+    // issue stage s (global row block s0+s) into buffer b
+    auto issue = [&](int64_t s, int b) {
+        double* buf = lds + b * R::STRIDE;
+        const int64_t row0 = (s0 + s) * BK;
+#pragma unroll
+        for (int k = 0; k < BK / 4; k++) {
+            const int r = wv + 4 * k;
+            __builtin_amdgcn_global_load_lds((const void*)(colA + (row0 + r) * Ep), (lds_ptr_t)(buf + R::A_OFF + r * LDP),
+                                             16, 0, 0);
+        }
+        if (!DIAG) {
+#pragma unroll
+            for (int k = 0; k < BK / 4; k++) {
+                const int r = wv + 4 * k;
+                __builtin_amdgcn_global_load_lds((const void*)(colB + (row0 + r) * Ep),
+                                                 (lds_ptr_t)(buf + R::B_OFF + r * LDP), 16, 0, 0);
+            }
+        }
+        // 64 dwords = 32 tokens (rows row0 .. row0+31; the buffer is padded) into this wave's slot
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)(tok + row0) + 4 * lane),
+                                         (lds_ptr_t)(buf + R::T_OFF + wv * 32), 4, 0, 0);
+    };
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; s++)
+        if (s < ns) issue(s, s);
+    for (int64_t t = 0; t < ns; t++) {
+        if (t + NBUF - 2 < ns)
+            wait_vm<R::LPW * (NBUF - 2)>();
+        else
+            wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + NBUF - 1 < ns) issue(t + NBUF - 1, (int)((t + NBUF - 1) % NBUF));
+        const double* buf = lds + (int)(t % NBUF) * R::STRIDE;
+        const double* As = buf + R::A_OFF;
+        const double* Bs = DIAG ? As : buf + R::B_OFF;
+        const double* Ts = buf + R::T_OFF + wv * 32;
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            const double tk = Ts[kr];
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr * LDP + wr * 64 + a * 16 + (lane & 15)] * tk;
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[kr * LDP + wc * 64 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
+template <int BK, int NBUF>
+__global__ void __launch_bounds__(256) k_syrk_glds(const double* W, const double* tok, int64_t Np, int E, int Ep,
+                                                   int ntiles, int nks, double* slab) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / ntiles, t = item % ntiles;
+    int I, J;
+    tri_index(t, I, J);
+    const int64_t nst = Np / BK;
+    const int64_t per = (nst + nks - 1) / nks;
+    const int64_t s0 = ks * per;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
+    d4 acc[4][4];
+    if (I == J)
+        glds_tile<BK, NBUF, true>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+    else
+        glds_tile<BK, NBUF, false>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+    store_tile(slab + (int64_t)ks * E * E, E, I, J, acc);
+}
+
+template <int BK, int NBUF>
+size_t glds_lds_bytes() {
+    return (size_t)NBUF * Ring<BK, false>::STRIDE * sizeof(double);
+}
+
+// ------------------------------------------------------------------ host
+__global__ void k_slabsum(const double* slab, int nks, int64_t EE, double* C) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < EE; i += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0;
+        for (int k = 0; k < nks; k++) s += slab[k * EE + i];
+        C[i] = s;
+    }
+}
+
+struct Prob {
+    int64_t N, Np;
+    int E, Ep;
+    double *W, *tok;
+};
+
+static double maxrel(const std::vector<double>& a, const std::vector<double>& b, int E) {
+    double m = 0, scale = 0;
+    for (int p = 0; p < E; p++)
+        for (int q = 0; q <= p; q++) scale = fmax(scale, fabs(b[(size_t)p * E + q]));
+    for (int p = 0; p < E; p++)
+        for (int q = 0; q <= p; q++) m = fmax(m, fabs(a[(size_t)p * E + q] - b[(size_t)p * E + q]));
+    return m / scale;
+}
+
+typedef void (*syrk_fn)(const double*, const double*, int64_t, int, int, int, int, double*);
+
+struct Variant {
+    const char* name;
+    syrk_fn fn;
+    size_t lds;
+    int bk;
+};
+
+static double run_variant(const Variant& v, const Prob& P, int nks, double* slab, int reps, std::vector<double>* out,
+                          double* Cd) {
+    const int nb = P.Ep / CT;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int nwg = ntiles * nks;
+    if (v.lds > 65536) CK(hipFuncSetAttribute((const void*)v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemset(slab, 0, (size_t)nks * P.E * P.E * sizeof(double)));
+    hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(256), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int r = 0; r < reps; r++) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(256), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+    }
+    if (out) {
+        hipLaunchKernelGGL(k_slabsum, dim3(1024), dim3(256), 0, 0, slab, nks, (int64_t)P.E * P.E, Cd);
+        CK(hipDeviceSynchronize());
+        out->resize((size_t)P.E * P.E);
+        CK(hipMemcpy(out->data(), Cd, out->size() * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    double best = 1e30;
+    for (float t : ms) best = fmin(best, t);
+    return best;
+}
+
+int main(int argc, char** argv) {
+    int64_t N = argc > 1 ? atoll(argv[1]) : 1000000;
+    int E = argc > 2 ? atoi(argv[2]) : 4096;
+    int nks = argc > 3 ? atoi(argv[3]) : 8;
+    int reps = argc > 4 ? atoi(argv[4]) : 3;
+    const char* only = argc > 5 ? argv[5] : "";
+
+    // --- peak: bare MFMA loop at 1, 2 and 3 workgroups (4 waves) per CU
+    for (int wpc = 1; wpc <= 3; wpc++) {
+        const int nwg = 256 * wpc, iters = 8000;
+        double *in, *out;
+        long long* clk;
+        CK(hipMalloc(&in, 128 * sizeof(double)));
+        CK(hipMalloc(&out, nwg * 256 * sizeof(double)));
+        CK(hipMalloc(&clk, 2 * nwg * sizeof(long long)));
+        std::vector<double> h(128);
+        for (int i = 0; i < 128; i++) h[i] = 0.5 + 0.001 * i;
+        CK(hipMemcpy(in, h.data(), 128 * sizeof(double), hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int w = 0; w < 3; w++) hipLaunchKernelGGL(k_peak, dim3(nwg), dim3(256), 0, 0, in, out, iters, clk);
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_peak, dim3(nwg), dim3(256), 0, 0, in, out, iters, clk);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        std::vector<long long> hc(2 * nwg);
+        CK(hipMemcpy(hc.data(), clk, hc.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        std::vector<double> ghz, cpm;
+        for (int b = 0; b < nwg; b++) {
+            ghz.push_back((double)hc[2 * b] / (double)hc[2 * b + 1] * 0.1);
+            cpm.push_back((double)hc[2 * b] / (iters * 16.0));
+        }
+        std::sort(ghz.begin(), ghz.end());
+        std::sort(cpm.begin(), cpm.end());
+        const double flops = (double)nwg * 4 * iters * 16 * 2048.0;
+        printf("{\"variant\":\"peak\",\"wg_per_cu\":%d,\"tflops\":%.2f,\"ms\":%.3f,\"clock_ghz_median\":%.3f,"
+               "\"wave_cycles_per_mfma_median\":%.1f}\n",
+               wpc, flops / (ms * 1e-3) / 1e12, ms, ghz[nwg / 2], cpm[nwg / 2]);
+        CK(hipFree(in));
+        CK(hipFree(out));
+        CK(hipFree(clk));
+    }
+
+    // --- problems: small check case and the big case
+    Variant vars[] = {
+        {"reg16", (syrk_fn)k_syrk_reg<16>, 0, 16},
+        {"glds16x3", (syrk_fn)k_syrk_glds<16, 3>, glds_lds_bytes<16, 3>(), 16},
+        {"glds16x2", (syrk_fn)k_syrk_glds<16, 2>, glds_lds_bytes<16, 2>(), 16},
+        {"glds8x4", (syrk_fn)k_syrk_glds<8, 4>, glds_lds_bytes<8, 4>(), 8},
+        {"glds8x3", (syrk_fn)k_syrk_glds<8, 3>, glds_lds_bytes<8, 3>(), 8},
+        {"glds32x2", (syrk_fn)k_syrk_glds<32, 2>, glds_lds_bytes<32, 2>(), 32},
+        {"glds4x6", (syrk_fn)k_syrk_glds<4, 6>, glds_lds_bytes<4, 6>(), 4},
+    };
+    for (int pass = 0; pass < 2; pass++) {
+        Prob P;
+        P.N = pass == 0 ? 3001 : N;
+        P.E = pass == 0 ? 300 : E;
+        P.Ep = (P.E + CT - 1) / CT * CT;
+        const int BKMAX = 32;
+        P.Np = (P.N + BKMAX - 1) / BKMAX * BKMAX;
+        const int nk = pass == 0 ? 3 : nks;
+        CK(hipMalloc(&P.W, (size_t)P.Np * P.Ep * sizeof(double)));
+        CK(hipMalloc(&P.tok, (size_t)(P.Np + 64) * sizeof(double)));
+        CK(hipMemset(P.tok, 0, (size_t)(P.Np + 64) * sizeof(double)));
+        hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, 0, P.W, P.N, P.Np, P.E, P.Ep, P.tok, pass == 0 ? 1 : 0);
+        CK(hipDeviceSynchronize());
+        double *slab, *Cd;
+        CK(hipMalloc(&slab, (size_t)4 * nk * P.E * P.E * sizeof(double)));
+        CK(hipMalloc(&Cd, (size_t)P.E * P.E * sizeof(double)));
+        std::vector<double> ref;
+        if (pass == 0) {
+            CK(hipMemset(Cd, 0, (size_t)P.E * P.E * sizeof(double)));
+            hipLaunchKernelGGL(k_ref, dim3((P.E * P.E + 255) / 256), dim3(256), 0, 0, P.W, P.tok, P.Np, P.E, P.Ep, Cd);
+            CK(hipDeviceSynchronize());
+            ref.resize((size_t)P.E * P.E);
+            CK(hipMemcpy(ref.data(), Cd, ref.size() * sizeof(double), hipMemcpyDeviceToHost));
+        }
+        const double flops = (double)P.N * P.E * (P.E + 1);
+        const int nks_list[3] = {nk, 2 * nk, 4 * nk};
+        for (int ni = 0; ni < (pass == 0 ? 1 : 3); ni++)
+        for (const Variant& v : vars) {
+            if (only[0] && !strstr(only, v.name)) continue;
+            if (pass == 1 && ni > 0 && strcmp(v.name, "glds16x2") && strcmp(v.name, "reg16")) continue;
+            const int nkv = pass == 0 ? nk : nks_list[ni];
+            std::vector<double> got;
+            const double ms = run_variant(v, P, nkv, slab, pass == 0 ? 1 : reps, pass == 0 ? &got : nullptr, Cd);
+            if (pass == 0) {
+                const double err = maxrel(got, ref, P.E);
+                printf("{\"variant\":\"%s\",\"check\":\"%dx%d\",\"max_rel_err\":%.3e,\"ok\":%s}\n", v.name, (int)P.N, P.E,
+                       err, err < 1e-12 ? "true" : "false");
+                if (!(err < 1e-12)) return 3;
+            } else {
+                printf("{\"variant\":\"%s\",\"N\":%lld,\"E\":%d,\"nks\":%d,\"lds\":%zu,\"ms\":%.3f,\"tflops\":%.2f}\n", v.name,
+                       (long long)P.N, P.E, nkv, v.lds, ms, flops / (ms * 1e-3) / 1e12);
+            }
+            fflush(stdout);
+        }
+        CK(hipFree(P.W));
+        CK(hipFree(P.tok));
+        CK(hipFree(slab));
+        CK(hipFree(Cd));
+    }
+    return 0;
+}
