@@ -125,22 +125,28 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     const char* st_env = getenv("PCX_STAMPS");
     if (st_env && st_env[0] == '1' && a.B > 0) {  // diagnostic: per-phase clock breakdown
         long long* d = nullptr;
-        if (hipMalloc(&d, a.B * 16 * sizeof(long long)) == hipSuccess) {
-            (void)hipMemsetAsync(d, 0, a.B * 16 * sizeof(long long), ctx->stream);
+        if (hipMalloc(&d, a.B * 32 * sizeof(long long)) == hipSuccess) {
+            (void)hipMemsetAsync(d, 0, a.B * 32 * sizeof(long long), ctx->stream);
             a.stamps = d;
         }
     }
     e = pcx::launch_batched(a, ctx->stream);
     if (a.stamps) {
-        std::vector<long long> h(a.B * 16);
+        // stamp ids in program order (pcx_batched.hip STAMP(k)); a phase is named by its closing stamp
+        static const int order[] = {0, 1, 2, 13, 14, 3, 4, 5, 6, 7, 8, 15, 16, 9, 10, 11, 12};
+        const int no = (int)(sizeof(order) / sizeof(order[0]));
+        std::vector<long long> h(a.B * 32);
         (void)hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream);
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(a.stamps);
-        double acc[16] = {0};
+        double acc[32] = {0};
         for (int64_t b = 0; b < a.B; b++)
-            for (int k = 1; k < 13; k++) acc[k] += (double)(h[b * 16 + k] - h[b * 16 + k - 1]);
+            for (int k = 1; k < no; k++) {
+                const long long t1 = h[b * 32 + order[k]], t0 = h[b * 32 + order[k - 1]];
+                if (t1 && t0) acc[order[k]] += (double)(t1 - t0);
+            }
         fprintf(stderr, "PCX_STAMPS mean cycles per phase:");
-        for (int k = 1; k < 13; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / (double)a.B);
+        for (int k = 1; k < no; k++) fprintf(stderr, " %d:%.0f", order[k], acc[order[k]] / (double)a.B);
         fprintf(stderr, "\n");
     }
     return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");

@@ -46,7 +46,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x; }
     do {                                                                          \
         if (a.stamps) {                                                           \
             const long long t_ = (long long)__builtin_amdgcn_s_memtime();         \
-            if (threadIdx.x == 0) a.stamps[b * 16 + (k)] = t_;                    \
+            if (threadIdx.x == 0) a.stamps[b * 32 + (k)] = t_;                    \
         }                                                                         \
     } while (0)
 
@@ -193,6 +193,66 @@ __device__ double wave_wmedian(double x, double w, bool sel, double W, double* s
     return bcast(res, 0);
 }
 
+__device__ __forceinline__ double readlane_d(double v, int k) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// The same weighted median as wave_wmedian, without LDS: the selected (x, w) pairs are
+// sorted across the wave by a bitonic network on the total order (x, w, lane) -- which
+// is exactly the stable (x, w) rank order -- and the sequential walk then runs on
+// wave-uniform registers (readlane).  Identical arithmetic: the cumulative weight is
+// the same left-to-right sum, `before` the same subtraction.  NaN keys have no total
+// order, so rounds with a NaN among the selected pairs take wave_wmedian.
+__device__ double wave_wmedian_sorted(double x, double w, bool sel, double Wtot, double* sx, double* sw) {
+    const int l = lane_id();
+    const double mid = 0.5 * Wtot;
+    const uint64_t dom = ballot(sel && w > mid);
+    if (dom) {
+        const double mx = wave_max(sel ? w : -__builtin_inf());
+        const uint64_t at = ballot(sel && w == mx);
+        return bcast(x, __builtin_ctzll(at));
+    }
+    if (!ballot(sel && w > 0.0)) return __builtin_nan("");
+    if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
+    const int n = popc(ballot(sel));
+    double kx = sel ? x : __builtin_inf();
+    double kw = sel ? w : __builtin_inf();
+    int ki = sel ? l : 64 + l;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const double px = __shfl_xor(kx, j, 64);
+            const double pw = __shfl_xor(kw, j, 64);
+            const int pi = __shfl_xor(ki, j, 64);
+            const bool mine_less = (kx < px) || (kx == px && (kw < pw || (kw == pw && ki < pi)));
+            const bool keep_min = ((l & j) == 0) == ((l & k) == 0);
+            if (keep_min != mine_less) {
+                kx = px;
+                kw = pw;
+                ki = pi;
+            }
+        }
+    }
+    // lane r now holds the r-th pair in (x, w) order; walk to half the total weight
+    double cum = 0.0;
+    int k = 0;
+    while (cum <= mid) {
+        if (k == n) return __builtin_nan("");
+        cum += readlane_d(kw, k);
+        k++;
+    }
+    const double before = cum - readlane_d(kw, k - 1);
+    if (fabs(before - mid) < DBL_EPS) {
+        if (k >= 2) return (readlane_d(kx, k - 2) + readlane_d(kx, k - 1)) / 2.0;
+        return n == 1 ? readlane_d(kx, 0) / 1.0 : __builtin_nan("");
+    }
+    return readlane_d(kx, k - 1);
+}
+
 // scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
 __device__ __forceinline__ double rank_avg(const double* v, int E) {
     const int l = lane_id();
@@ -310,9 +370,14 @@ __device__ void square_scaled(double* M, int ES, int E) {
 
 }  // namespace
 
+// NT/ET > 0: the round shape is a compile-time constant (the Monte Carlo shapes the
+// launcher specialises, e.g. the 50 x 20 of config C3): every loop bound is known, so
+// the sequential column/row loops unroll and their LDS reads issue ahead of the
+// dependent adds.  NT = ET = 0: any N <= 64, E <= 32 at run time.  Same arithmetic.
+template <int NT, int ET>
 __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int N = a.N, E = a.E, ES = a.ES;
+    const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? (ET | 1) : a.ES;
     const int l = lane_id();
     const int64_t b = blockIdx.x;
     Smem S = carve(smem, N, E, ES);
@@ -402,6 +467,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         }
     }
     wsync();
+    STAMP(13);
     // scaled columns with missing reports: weighted median of the present values
     {
         uint64_t todo = ballot(col && scj && miss_j != 0);
@@ -414,13 +480,14 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             const double x = row ? S.F[l * ES + j] : 0.0;
             const double w = present ? S.rep[l] / tot : 0.0;
             const double Wsum = bcast(Wj, j);
-            double g = wave_wmedian(x, w, present, Wsum, S.sx, S.sw);
+            double g = wave_wmedian_sorted(x, w, present, Wsum, S.sx, S.sw);
             if (a.int_dtype) g = trunc(g);
             if (l == 0) S.guess[j] = g;
             wsync();
         }
     }
     wsync();
+    STAMP(14);
     // fill (row phase)
     if (row) {
         for (int j = 0; j < E; j++) {
@@ -623,6 +690,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     STAMP(8);
     // ---- a12/a13: outcomes (:510-538) -------------------------------------
     double rawj = col ? dot2(S.smooth, S.F + l, ES, N) : 0.0;
+    STAMP(15);
     if (scaled_mask) {
         const double Wsm = [&] {  // builtin sequential sum of smooth_rep (weightedstats)
             double w = 0.0;
@@ -635,11 +703,12 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const double x = row ? S.F[l * ES + j] : 0.0;
-            const double m = wave_wmedian(x, smooth_i, row, Wsm, S.sx, S.sw);
+            const double m = wave_wmedian_sorted(x, smooth_i, row, Wsm, S.sx, S.sw);
             if (l == j) rawj = m;
             wsync();
         }
     }
+    STAMP(16);
     double adjj = 0.0, finj = 0.0;
     if (col) {
         if (scj) {
@@ -766,7 +835,10 @@ size_t batched_lds_bytes(int N, int E) {
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
     const size_t lds = batched_lds_bytes(a.N, a.E);
     if (a.B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(batched_round_kernel, dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    if (a.N == 50 && a.E == 20 && a.ES == 21)
+        hipLaunchKernelGGL((batched_round_kernel<50, 20>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    else
+        hipLaunchKernelGGL((batched_round_kernel<0, 0>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 
