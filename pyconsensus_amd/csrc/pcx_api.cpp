@@ -147,7 +147,12 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
             }
         fprintf(stderr, "PCX_STAMPS mean cycles per phase:");
         for (int k = 1; k < no; k++) fprintf(stderr, " %d:%.0f", order[k], acc[order[k]] / (double)a.B);
-        fprintf(stderr, "\n");
+        double sort = 0, walk = 0;
+        for (int64_t b = 0; b < a.B; b++) {
+            sort += (double)h[b * 32 + 20];
+            walk += (double)h[b * 32 + 21];
+        }
+        fprintf(stderr, " median_sort:%.0f median_walk:%.0f\n", sort / (double)a.B, walk / (double)a.B);
     }
     return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");
 }

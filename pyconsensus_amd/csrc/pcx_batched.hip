@@ -77,36 +77,67 @@ __device__ __forceinline__ double catch_(double x, double tol) {  // __init__.py
     return 1.5;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int k) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double shr1_d(double v) {  // lane l <- lane l-1 (lane 0 <- 0.0)
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x138, 0xf, 0xf, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x138, 0xf, 0xf, true);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double permute_d(int dst_lane, double v) {  // forward permute
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(dst_lane * 4, (int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(dst_lane * 4, (int)(uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
 // numpy pairwise add.reduce (n <= 128 branch: 8 accumulators) of the lanes that
 // have `sel` set, taken in lane order.  All 64 lanes call it; every lane gets the
-// result.  `scr` is a 64-double LDS scratch owned by this wave.
-__device__ double wave_pw_sum(double v, bool sel, double* scr) {
+// result.  Register-only: element p (p-th selected lane) is permuted to lane
+// 8*(p%8) + p/8, so accumulator k's chain a_k, a_{k+8}, ... sits in lanes 8k..8k+7 and
+// runs as a DPP wave_shr chain (each step recomputes final lanes identically); the
+// accumulators, the fixed tree and the tail are then read back wave-uniformly.
+// Same additions in the same order as numpy (and the C oracle's pw_sum).
+__device__ __forceinline__ double wave_pw_sum(double v, bool sel, double* /*scr*/) {
     const int l = lane_id();
     const uint64_t m = ballot(sel);
     const int n = popc(m);
-    const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    wsync();
-    if (sel) scr[pos] = v;
-    wsync();
-    double res = 0.0;
     if (n < 8) {
-        if (l == 0)
-            for (int t = 0; t < n; t++) res += scr[t];
-    } else {
-        const int n8 = n - (n % 8);
-        double r = 0.0;
-        if (l < 8) {
-            r = scr[l];
-            for (int t = l + 8; t < n8; t += 8) r += scr[t];
+        double res = 0.0;
+        uint64_t mm = m;
+        while (mm) {
+            const int k = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            res += readlane_d(v, k);
         }
-        const double r0 = bcast(r, 0), r1 = bcast(r, 1), r2 = bcast(r, 2), r3 = bcast(r, 3);
-        const double r4 = bcast(r, 4), r5 = bcast(r, 5), r6 = bcast(r, 6), r7 = bcast(r, 7);
-        if (l == 0) {
-            res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-            for (int t = n8; t < n; t++) res += scr[t];
-        }
+        return res;
     }
-    return bcast(res, 0);
+    const int p = sel ? mbcnt64(m) : n + mbcnt64(~m);
+    const double a = permute_d((p & 7) * 8 + (p >> 3), v);
+    const int T = n >> 3;  // full rounds of 8: positions < 8T feed the accumulators
+    double c = a;
+    for (int t = 1; t < T; t++) {
+        const double prev = shr1_d(c);
+        c = (l & 7) == 0 ? a : prev + a;
+    }
+    const double r0 = readlane_d(c, 0 * 8 + T - 1), r1 = readlane_d(c, 1 * 8 + T - 1);
+    const double r2 = readlane_d(c, 2 * 8 + T - 1), r3 = readlane_d(c, 3 * 8 + T - 1);
+    const double r4 = readlane_d(c, 4 * 8 + T - 1), r5 = readlane_d(c, 5 * 8 + T - 1);
+    const double r6 = readlane_d(c, 6 * 8 + T - 1), r7 = readlane_d(c, 7 * 8 + T - 1);
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (int q = 8 * T; q < n; q++) res += readlane_d(a, (q & 7) * 8 + (q >> 3));
+    return res;
 }
 
 // SPEC dot2 over rows i < N of column-strided data: a[i] * b[i*bs]
@@ -128,7 +159,7 @@ __device__ __forceinline__ double dot2(const double* a, const double* b, int bs,
 // weightedstats.weighted_median restated (oracle/pcx_oracle.py): lane i holds the
 // pair (x, w) if `sel`; W is the builtin sequential sum of the selected weights in
 // lane order (computed by the caller).  Scratch: sx, sw (64 doubles each).
-__device__ double wave_wmedian(double x, double w, bool sel, double W, double* sx, double* sw) {
+__device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double W, double* sx, double* sw) {
     const int l = lane_id();
     const double mid = 0.5 * W;
     const uint64_t dom = ballot(sel && w > mid);
@@ -193,21 +224,22 @@ __device__ double wave_wmedian(double x, double w, bool sel, double W, double* s
     return bcast(res, 0);
 }
 
-__device__ __forceinline__ double readlane_d(double v, int k) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// The same weighted median as wave_wmedian, without LDS: the selected (x, w) pairs are
-// sorted across the wave by a bitonic network on the total order (x, w, lane) -- which
-// is exactly the stable (x, w) rank order -- and the sequential walk then runs on
-// wave-uniform registers (readlane).  Identical arithmetic: the cumulative weight is
-// the same left-to-right sum, `before` the same subtraction.  NaN keys have no total
-// order, so rounds with a NaN among the selected pairs take wave_wmedian.
-__device__ double wave_wmedian_sorted(double x, double w, bool sel, double Wtot, double* sx, double* sw) {
+// The same weighted median as wave_wmedian, without LDS scratch or a serial lane:
+//  * rank: every selected lane counts the selected pairs before it in the total order
+//    (x, w, lane) -- exactly the stable (x, w) rank -- against wave-uniform broadcasts
+//    (readlane), one pass over the rows;
+//  * ds_permute moves each pair to lane = rank (unselected lanes fill the tail);
+//  * the left-to-right cumulative weight runs as a DPP wave_shr chain: after t steps
+//    lanes 0..t hold the sequential sums cum_1..cum_{t+1} (already-final lanes recompute
+//    the same value), so it is the SPEC's sequential sum bit for bit;
+//  * the crossing is the first lane with cum > mid; `before` is the same subtraction.
+// NaN keys have no total order: rounds with a NaN among the selected pairs take
+// wave_wmedian.  NR = compile-time row count bound (64 when the shape is dynamic).
+template <int NR>
+__device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* sx, double* sw,
+                                    long long* prof = nullptr) {
     const int l = lane_id();
+    const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
     const double mid = 0.5 * Wtot;
     const uint64_t dom = ballot(sel && w > mid);
     if (dom) {
@@ -217,35 +249,39 @@ __device__ double wave_wmedian_sorted(double x, double w, bool sel, double Wtot,
     }
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
     if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
-    const int n = popc(ballot(sel));
-    double kx = sel ? x : __builtin_inf();
-    double kw = sel ? w : __builtin_inf();
-    int ki = sel ? l : 64 + l;
+    const uint64_t selm = ballot(sel);
+    const int n = popc(selm);
+    // every lane publishes its pair; the comparisons read them back as LDS broadcasts
+    wsync();
+    sx[l] = sel ? x : __builtin_inf();
+    sw[l] = sel ? w : __builtin_inf();
+    wsync();
+    int r = 0;
+    // straight-line body (no per-row branch, non-short-circuit logic) so the broadcast
+    // reads issue ahead of the compares; unselected rows are masked by selm
 #pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const double px = __shfl_xor(kx, j, 64);
-            const double pw = __shfl_xor(kw, j, 64);
-            const int pi = __shfl_xor(ki, j, 64);
-            const bool mine_less = (kx < px) || (kx == px && (kw < pw || (kw == pw && ki < pi)));
-            const bool keep_min = ((l & j) == 0) == ((l & k) == 0);
-            if (keep_min != mine_less) {
-                kx = px;
-                kw = pw;
-                ki = pi;
-            }
-        }
+    for (int m = 0; m < NR; m++) {
+        const double xm = sx[m], wm = sw[m];
+        const bool lt = (xm < x) | ((xm == x) & ((wm < w) | ((wm == w) & (m < l))));
+        r += (lt & (bool)((selm >> m) & 1)) ? 1 : 0;
     }
-    // lane r now holds the r-th pair in (x, w) order; walk to half the total weight
-    double cum = 0.0;
-    int k = 0;
-    while (cum <= mid) {
-        if (k == n) return __builtin_nan("");
-        cum += readlane_d(kw, k);
-        k++;
+    const uint64_t unsel = ~selm;
+    const int upos = __builtin_amdgcn_mbcnt_hi((uint32_t)(unsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)unsel, 0));
+    const int dst = sel ? r : n + upos;
+    const double kx = permute_d(dst, x);
+    const double kw = permute_d(dst, w);
+    if (prof) {
+        const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+        prof[0] += t1 - t0;
+        prof[2] = t1;
     }
-    const double before = cum - readlane_d(kw, k - 1);
+    double cum = l == 0 ? 0.0 + kw : 0.0;
+    for (int t = 1; t < n; t++) cum = shr1_d(cum) + kw;  // after step t lanes 0..t are final
+    const uint64_t over = ballot(l < n && cum > mid);
+    if (prof) prof[1] += (long long)__builtin_amdgcn_s_memtime() - prof[2];
+    if (!over) return __builtin_nan("");
+    const int k = __builtin_ctzll(over) + 1;  // items summed when the walk stops
+    const double before = readlane_d(cum, k - 1) - readlane_d(kw, k - 1);
     if (fabs(before - mid) < DBL_EPS) {
         if (k >= 2) return (readlane_d(kx, k - 2) + readlane_d(kx, k - 1)) / 2.0;
         return n == 1 ? readlane_d(kx, 0) / 1.0 : __builtin_nan("");
@@ -338,7 +374,7 @@ __device__ __forceinline__ double matvec_unit(const double* M, int ES, const dou
 }
 
 // M <- (M M) / max|M M| (SPEC square_scaled)
-__device__ void square_scaled(double* M, int ES, int E) {
+__device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
     const int l = lane_id();
     double t[EMAX * EMAX / W];
     double mx = 0.0;
@@ -385,13 +421,10 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     const int64_t bo = a.bounds_shared ? 0 : b * E;
     const bool has_bounds = a.scaled != nullptr;
 
+    long long mprof[3] = {0, 0, 0};  // diagnostic: median sort / walk cycles (PCX_STAMPS)
     STAMP(0);
     // ---- load the round -------------------------------------------------
     const double* Rg = a.reports + b * (int64_t)N * E;
-    for (int idx = l; idx < N * E; idx += W) {
-        const int i = idx / E, j = idx - i * E;
-        S.F[i * ES + j] = Rg[idx];
-    }
     bool scj = false;
     double loj = 0.0, hij = 0.0;
     if (col && has_bounds) {
@@ -399,10 +432,33 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         loj = a.lo[bo + l];
         hij = a.hi[bo + l];
     }
+    double raw = row && a.reputation ? a.reputation[b * N + l] : 0.0;
+    if constexpr (NT > 0 && ET > 0 && (NT * ET) % 2 == 0) {
+        // every 16-byte load of the round in flight at once, then the LDS scatter
+        constexpr int TOT2 = NT * ET / 2, NV = (TOT2 + W - 1) / W;
+        double2 v[NV];
+#pragma unroll
+        for (int q = 0; q < NV; q++)
+            if (l + W * q < TOT2) v[q] = reinterpret_cast<const double2*>(Rg)[l + W * q];
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            const int idx = 2 * (l + W * q);
+            if (idx < NT * ET) {
+                const int i0 = idx / ET, j0 = idx - i0 * ET;
+                const int i1 = (idx + 1) / ET, j1 = idx + 1 - i1 * ET;
+                S.F[i0 * ES + j0] = v[q].x;
+                S.F[i1 * ES + j1] = v[q].y;
+            }
+        }
+    } else {
+        for (int idx = l; idx < N * E; idx += W) {
+            const int i = idx / E, j = idx - i * E;
+            S.F[i * ES + j] = Rg[idx];
+        }
+    }
     const uint64_t scaled_mask = ballot(col && scj);
 
     // ---- a1: reputation (__init__.py:138-146) -----------------------------
-    double raw = row && a.reputation ? a.reputation[b * N + l] : 0.0;
     double rep;
     if (a.reputation) {
         const double tot = wave_pw_sum(raw, row, S.scr);
@@ -446,20 +502,33 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
     uint64_t miss_j = 0;
     double Wj = 0.0;
-    if (col) {
-        miss_j = S.nanm[l] | S.zerm[l];
-        if (miss_j) {
-            double tot = 0.0;
-            for (int i = 0; i < N; i++)
-                if (!((miss_j >> i) & 1)) tot += S.rep[i];
-            double g = 0.0;
+    if (col) miss_j = S.nanm[l] | S.zerm[l];
+    {
+        // branch-free sequential sums over the present rows (a skipped row keeps the
+        // accumulator as is: the same left-to-right sums as the SPEC loops)
+        constexpr int NR = NT > 0 ? NT : 64;
+        double tot = 0.0;
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            if (i < N) {
+                const double r = S.rep[i];
+                tot = ((miss_j >> i) & 1) ? tot : tot + r;
+            }
+        }
+        double acc = 0.0;  // scaled: sum of rep/tot (weightedstats total); binary: sum of (rep/tot)*F
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            if (i < N) {
+                const double q = S.rep[i] / tot;
+                const double t = scj ? q : q * S.F[i * ES + (col ? l : 0)];
+                acc = ((miss_j >> i) & 1) ? acc : acc + t;
+            }
+        }
+        if (col && miss_j) {
             if (scj) {
-                for (int i = 0; i < N; i++)
-                    if (!((miss_j >> i) & 1)) Wj += S.rep[i] / tot;
+                Wj = acc;
             } else {
-                for (int i = 0; i < N; i++)
-                    if (!((miss_j >> i) & 1)) g += (S.rep[i] / tot) * S.F[i * ES + l];
-                g = catch_(g, a.catch_tol);
+                double g = catch_(acc, a.catch_tol);
                 if (a.int_dtype) g = trunc(g);
                 S.guess[l] = g;
             }
@@ -480,7 +549,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             const double x = row ? S.F[l * ES + j] : 0.0;
             const double w = present ? S.rep[l] / tot : 0.0;
             const double Wsum = bcast(Wj, j);
-            double g = wave_wmedian_sorted(x, w, present, Wsum, S.sx, S.sw);
+            double g = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x, w, present, Wsum, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
             if (a.int_dtype) g = trunc(g);
             if (l == 0) S.guess[j] = g;
             wsync();
@@ -703,7 +772,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const double x = row ? S.F[l * ES + j] : 0.0;
-            const double m = wave_wmedian_sorted(x, smooth_i, row, Wsm, S.sx, S.sw);
+            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x, smooth_i, row, Wsm, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
             if (l == j) rawj = m;
             wsync();
         }
@@ -824,6 +893,10 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         if (a.pi_iters) a.pi_iters[b] = iters;
     }
     STAMP(12);
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[b * 32 + 20] = mprof[0];
+        a.stamps[b * 32 + 21] = mprof[1];
+    }
 }
 
 size_t batched_lds_bytes(int N, int E) {
