@@ -58,16 +58,42 @@ __device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
 
 __device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, W); }
 
+// lane l <- lane l ^ S, by the cheapest cross-lane path for each distance: DPP
+// quad_perm (1, 2) and row_ror:8 (8), ds_swizzle xor mode (4, 16), ds_bpermute (32)
+template <int S>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+    if constexpr (S == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+    else if constexpr (S == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
+    else if constexpr (S == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+    else if constexpr (S == 4 || S == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (S << 10) | 0x1F);
+    else return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ S) * 4), (int)v);
+}
+
+template <int S>
+__device__ __forceinline__ double xor_lane(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = xor_lane32<S>((uint32_t)u), hi = xor_lane32<S>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // SPEC tree64: butterfly, xor distance 32..1 (every lane ends with the same sum)
 __device__ __forceinline__ double tree_sum(double v) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) v = v + __shfl_xor(v, s, W);
+    v = v + xor_lane<32>(v);
+    v = v + xor_lane<16>(v);
+    v = v + xor_lane<8>(v);
+    v = v + xor_lane<4>(v);
+    v = v + xor_lane<2>(v);
+    v = v + xor_lane<1>(v);
     return v;
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) v = fmax(v, __shfl_xor(v, s, W));
+    v = fmax(v, xor_lane<32>(v));
+    v = fmax(v, xor_lane<16>(v));
+    v = fmax(v, xor_lane<8>(v));
+    v = fmax(v, xor_lane<4>(v));
+    v = fmax(v, xor_lane<2>(v));
+    v = fmax(v, xor_lane<1>(v));
     return v;
 }
 
@@ -289,6 +315,84 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     return readlane_d(kx, k - 1);
 }
 
+// K independent weighted medians at once (same steps as wave_wmedian_rank, the K
+// instruction streams interleaved so their dependent latencies overlap).  Only for
+// "regular" medians -- no dominant weight, some positive weight, no NaN -- which the
+// caller checks with wmedian_regular().  scr: K x 128 doubles of LDS scratch.
+__device__ __forceinline__ bool wmedian_regular(double x, double w, bool sel, double Wtot) {
+    const double mid = 0.5 * Wtot;
+    return !ballot(sel && w > mid) && ballot(sel && w > 0.0) &&
+           !ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)));
+}
+
+template <int NR, int K>
+__device__ __forceinline__ void wave_wmedian_rank_k(const double (&x)[K], const double (&w)[K], const bool (&sel)[K],
+                                                    const double (&Wtot)[K], double* scr, double (&out)[K],
+                                                    long long* prof = nullptr) {
+    const int l = lane_id();
+    const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    uint64_t selm[K];
+    int n[K], r[K];
+    wsync();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        selm[k] = ballot(sel[k]);
+        n[k] = popc(selm[k]);
+        r[k] = 0;
+        scr[k * 128 + l] = sel[k] ? x[k] : __builtin_inf();
+        scr[k * 128 + 64 + l] = sel[k] ? w[k] : __builtin_inf();
+    }
+    wsync();
+#pragma unroll 10
+    for (int m = 0; m < NR; m++) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double xm = scr[k * 128 + m], wm = scr[k * 128 + 64 + m];
+            const bool lt = (xm < x[k]) | ((xm == x[k]) & ((wm < w[k]) | ((wm == w[k]) & (m < l))));
+            r[k] += (lt & (bool)((selm[k] >> m) & 1)) ? 1 : 0;
+        }
+    }
+    double kx[K], kw[K], cum[K];
+    int nmax = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int dst = sel[k] ? r[k] : n[k] + mbcnt64(~selm[k]);
+        kx[k] = permute_d(dst, x[k]);
+        kw[k] = permute_d(dst, w[k]);
+        cum[k] = l == 0 ? 0.0 + kw[k] : 0.0;
+        nmax = n[k] > nmax ? n[k] : nmax;
+    }
+    if (prof) {
+        const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+        prof[0] += t1 - t0;
+        prof[2] = t1;
+    }
+    for (int t = 1; t < nmax; t++) {
+#pragma unroll
+        for (int k = 0; k < K; k++) cum[k] = shr1_d(cum[k]) + kw[k];
+    }
+    if (prof) prof[1] += (long long)__builtin_amdgcn_s_memtime() - prof[2];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const double mid = 0.5 * Wtot[k];
+        const uint64_t over = ballot(l < n[k] && cum[k] > mid);
+        if (!over) {
+            out[k] = __builtin_nan("");
+            continue;
+        }
+        const int c = __builtin_ctzll(over) + 1;
+        const double before = readlane_d(cum[k], c - 1) - readlane_d(kw[k], c - 1);
+        if (fabs(before - mid) < DBL_EPS) {
+            if (c >= 2)
+                out[k] = (readlane_d(kx[k], c - 2) + readlane_d(kx[k], c - 1)) / 2.0;
+            else
+                out[k] = n[k] == 1 ? readlane_d(kx[k], 0) / 1.0 : __builtin_nan("");
+        } else {
+            out[k] = readlane_d(kx[k], c - 1);
+        }
+    }
+}
+
 // scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
 __device__ __forceinline__ double rank_avg(const double* v, int E) {
     const int l = lane_id();
@@ -373,33 +477,52 @@ __device__ __forceinline__ double matvec_unit(const double* M, int ES, const dou
     return l < E ? y / nrm : 0.0;
 }
 
-// M <- (M M) / max|M M| (SPEC square_scaled)
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4v mfma_f64(double a, double b, d4v c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// M <- (M M) / max|M M| (SPEC square_scaled) on fp64 MFMA.  v_mfma_f64_16x16x4_f64
+// accumulates exactly like the SPEC's fma chain over m (tools/probes/mfma_f64_order:
+// bitwise equal), and the zero padding of the 32 x 32 tile adds exact zeros, so every
+// entry is bit-identical to the VALU loop.  E <= 32: a 2 x 2 grid of 16 x 16 tiles.
 __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
-    const int l = lane_id();
-    double t[EMAX * EMAX / W];
-    double mx = 0.0;
-    const int tot = E * E;
-#pragma unroll
-    for (int q = 0; q < EMAX * EMAX / W; q++) {
-        const int o = l + q * W;
-        t[q] = 0.0;
-        if (o < tot) {
-            const int j = o / E, k = o - j * E;
-            double acc = 0.0;
-            for (int m = 0; m < E; m++) acc = fma(M[j * ES + m], M[m * ES + k], acc);
-            t[q] = acc;
-            mx = fmax(mx, fabs(acc));
+    const int l = lane_id(), ml = l & 15, kq = l >> 4;
+    const bool two = E > 16;
+    d4v t00 = {0, 0, 0, 0}, t01 = {0, 0, 0, 0}, t10 = {0, 0, 0, 0}, t11 = {0, 0, 0, 0};
+    for (int m0 = 0; m0 < E; m0 += 4) {
+        const int mm = m0 + kq;
+        const bool ok = mm < E;
+        const double a0 = (ok && ml < E) ? M[ml * ES + mm] : 0.0;
+        const double b0 = (ok && ml < E) ? M[mm * ES + ml] : 0.0;
+        t00 = mfma_f64(a0, b0, t00);
+        if (two) {
+            const double a1 = (ok && 16 + ml < E) ? M[(16 + ml) * ES + mm] : 0.0;
+            const double b1 = (ok && 16 + ml < E) ? M[mm * ES + 16 + ml] : 0.0;
+            t01 = mfma_f64(a0, b1, t01);
+            t10 = mfma_f64(a1, b0, t10);
+            t11 = mfma_f64(a1, b1, t11);
         }
+    }
+    double mx = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
+        if (j0 < E && k0 < E) mx = fmax(mx, fabs(t00[r]));
+        if (j0 < E && k1 < E) mx = fmax(mx, fabs(t01[r]));
+        if (j1 < E && k0 < E) mx = fmax(mx, fabs(t10[r]));
+        if (j1 < E && k1 < E) mx = fmax(mx, fabs(t11[r]));
     }
     mx = wave_max(mx);
     wsync();
 #pragma unroll
-    for (int q = 0; q < EMAX * EMAX / W; q++) {
-        const int o = l + q * W;
-        if (o < tot) {
-            const int j = o / E, k = o - j * E;
-            M[j * ES + k] = mx > 0.0 ? t[q] / mx : t[q];
-        }
+    for (int r = 0; r < 4; r++) {
+        const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
+        if (j0 < E && k0 < E) M[j0 * ES + k0] = mx > 0.0 ? t00[r] / mx : t00[r];
+        if (j0 < E && k1 < E) M[j0 * ES + k1] = mx > 0.0 ? t01[r] / mx : t01[r];
+        if (j1 < E && k0 < E) M[j1 * ES + k0] = mx > 0.0 ? t10[r] / mx : t10[r];
+        if (j1 < E && k1 < E) M[j1 * ES + k1] = mx > 0.0 ? t11[r] / mx : t11[r];
     }
     wsync();
 }
@@ -540,18 +663,47 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     // scaled columns with missing reports: weighted median of the present values
     {
         uint64_t todo = ballot(col && scj && miss_j != 0);
+        // the (x, w) pairs of interpolation median j: present reports, rep / tot (:292-303)
+        auto pair_of = [&](int j, double& x, double& w, bool& present, double& Wsum) {
+            const uint64_t mj = S.nanm[j] | S.zerm[j];
+            present = row && !((mj >> l) & 1);
+            const double tot = S.mu[j];
+            x = row ? S.F[l * ES + j] : 0.0;
+            w = present ? S.rep[l] / tot : 0.0;
+            Wsum = bcast(Wj, j);
+        };
+        auto finish = [&](int j, double g) {
+            if (a.int_dtype) g = trunc(g);
+            if (l == 0) S.guess[j] = g;
+        };
+        // two medians at a time while the C/M tiles (dead until the covariance) hold
+        // their scratch; a non-regular median takes the single path
+        // (pairing two medians through wave_wmedian_rank_k measured no faster at 50 x 20:
+        // the rank pass is VALU-throughput bound and the pair raised register pressure)
+        const bool pair_ok = false;
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const uint64_t mj = S.nanm[j] | S.zerm[j];
-            const bool present = row && !((mj >> l) & 1);
-            const double tot = S.mu[j];
-            const double x = row ? S.F[l * ES + j] : 0.0;
-            const double w = present ? S.rep[l] / tot : 0.0;
-            const double Wsum = bcast(Wj, j);
-            double g = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x, w, present, Wsum, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
-            if (a.int_dtype) g = trunc(g);
-            if (l == 0) S.guess[j] = g;
+            double x0, w0, W0;
+            bool p0;
+            pair_of(j, x0, w0, p0, W0);
+            if (pair_ok && todo && wmedian_regular(x0, w0, p0, W0)) {
+                const int j2 = __builtin_ctzll(todo);
+                double x1, w1, W1;
+                bool p1;
+                pair_of(j2, x1, w1, p1, W1);
+                if (wmedian_regular(x1, w1, p1, W1)) {
+                    todo &= todo - 1;
+                    double xs[2] = {x0, x1}, ws[2] = {w0, w1}, Ws[2] = {W0, W1}, g[2];
+                    bool ps[2] = {p0, p1};
+                    wave_wmedian_rank_k<(NT > 0 ? NT : 64), 2>(xs, ws, ps, Ws, S.C, g, a.stamps ? mprof : nullptr);
+                    finish(j, g[0]);
+                    finish(j2, g[1]);
+                    wsync();
+                    continue;
+                }
+            }
+            finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.sx, S.sw, a.stamps ? mprof : nullptr));
             wsync();
         }
     }
@@ -594,23 +746,49 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
 
         STAMP(4);
         // ---- a6: token-weighted covariance (:326), lower triangle ----------
-        const int ntri = E * (E + 1) / 2;
+        // fp64 MFMA, lower tiles of the 2 x 2 grid: entry (j, k), j >= k, accumulates
+        // fma((F_ij - mu_j) * tok_i, F_ik - mu_k, acc) over i ascending -- the SPEC's
+        // chain bit for bit (rows past N and events past E are exact zero padding)
         bool nonzero = false, finite = true;
-        for (int o = l; o < ntri; o += W) {
-            int j = 0;
-            while ((j + 1) * (j + 2) / 2 <= o) j++;
-            const int k = o - j * (j + 1) / 2;
-            const double mj = S.mu[j], mk = S.mu[k];
-            double acc = 0.0;
-            for (int i = 0; i < N; i++)
-                acc = fma((S.F[i * ES + j] - mj) * S.tok[i], S.F[i * ES + k] - mk, acc);
-            const double c = acc / denom;
-            S.C[j * ES + k] = c;
-            S.C[k * ES + j] = c;
-            S.M[j * ES + k] = c;
-            S.M[k * ES + j] = c;
-            nonzero |= c != 0.0;
-            finite &= __builtin_isfinite(c) != 0;
+        {
+            constexpr int NR = NT > 0 ? NT : 64;
+            const int ml = l & 15, kq = l >> 4;
+            const bool two = E > 16;
+            const double mu0 = ml < E ? S.mu[ml] : 0.0, mu1 = 16 + ml < E ? S.mu[16 + ml] : 0.0;
+            d4v c00 = {0, 0, 0, 0}, c10 = {0, 0, 0, 0}, c11 = {0, 0, 0, 0};
+#pragma unroll
+            for (int i0 = 0; i0 < NR; i0 += 4) {
+                if (i0 < N) {
+                    const int i = i0 + kq;
+                    const bool ok = i < N;
+                    const double tk = ok ? S.tok[i] : 0.0;
+                    const bool v0 = ok && ml < E, v1 = ok && 16 + ml < E;
+                    const double d0 = v0 ? S.F[i * ES + ml] - mu0 : 0.0;
+                    const double d1 = v1 ? S.F[i * ES + 16 + ml] - mu1 : 0.0;
+                    const double a0 = v0 ? d0 * tk : 0.0, a1 = v1 ? d1 * tk : 0.0;
+                    c00 = mfma_f64(a0, d0, c00);
+                    if (two) {
+                        c10 = mfma_f64(a1, d0, c10);
+                        c11 = mfma_f64(a1, d1, c11);
+                    }
+                }
+            }
+            auto put = [&](int j, int k, double acc) {
+                const double c = acc / denom;
+                S.C[j * ES + k] = c;
+                S.C[k * ES + j] = c;
+                S.M[j * ES + k] = c;
+                S.M[k * ES + j] = c;
+                nonzero |= c != 0.0;
+                finite &= __builtin_isfinite(c) != 0;
+            };
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
+                if (j0 < E && k0 <= j0) put(j0, k0, c00[r]);
+                if (j1 < E && k0 < E) put(j1, k0, c10[r]);
+                if (j1 < E && k1 <= j1) put(j1, k1, c11[r]);
+            }
         }
         const bool any_nz = ballot(nonzero) != 0;
         const bool all_fin = ballot(!finite) == 0;
@@ -768,11 +946,26 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             return bcast(w, 0);
         }();
         uint64_t todo = scaled_mask;
+        const bool pair_ok = false;  // see phase a3
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const double x = row ? S.F[l * ES + j] : 0.0;
-            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x, smooth_i, row, Wsm, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
+            const double x0 = row ? S.F[l * ES + j] : 0.0;
+            if (pair_ok && todo && wmedian_regular(x0, smooth_i, row, Wsm)) {
+                const int j2 = __builtin_ctzll(todo);
+                const double x1 = row ? S.F[l * ES + j2] : 0.0;
+                if (wmedian_regular(x1, smooth_i, row, Wsm)) {
+                    todo &= todo - 1;
+                    double xs[2] = {x0, x1}, ws[2] = {smooth_i, smooth_i}, Ws[2] = {Wsm, Wsm}, g[2];
+                    bool ps[2] = {row, row};
+                    wave_wmedian_rank_k<(NT > 0 ? NT : 64), 2>(xs, ws, ps, Ws, S.C, g, a.stamps ? mprof : nullptr);
+                    if (l == j) rawj = g[0];
+                    if (l == j2) rawj = g[1];
+                    wsync();
+                    continue;
+                }
+            }
+            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, smooth_i, row, Wsm, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
             if (l == j) rawj = m;
             wsync();
         }
