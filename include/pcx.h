@@ -223,6 +223,7 @@ typedef struct {
     double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
     int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
     int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
+    uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
 } pcx_mat;
 
 /* Run one stage on the context's stream (PCX_M_POWER and the selection steps may

@@ -87,4 +87,4 @@ class Mat(C.Structure):
         ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
     ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),
                                                                    ("filled", _vp)] + [
-        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64)]
+        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64), ("rowpart", _vp)]

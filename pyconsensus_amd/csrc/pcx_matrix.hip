@@ -41,7 +41,7 @@ constexpr int BT = 256;          // threads per block for row/column passes
 
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
                EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
-enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH };
+enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1 };
 
@@ -181,6 +181,42 @@ __device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t
     r1 = r0 + per < m.n_rows ? r0 + per : m.n_rows;
 }
 
+// Row loop of the column passes: U rows' loads are issued before any of them is
+// consumed (the per-row work carries a dependency through the running sums, so
+// without this each thread keeps one 8-byte load in flight -- ~2 TB/s at C5).
+constexpr int ROW_UNROLL = 8;
+
+template <int U, class LOAD, class PROC>
+__device__ __forceinline__ void rows_unrolled(int64_t r0, int64_t r1, LOAD load, PROC proc) {
+    int64_t i = r0;
+    for (; i + U <= r1; i += U) {
+        decltype(load(i)) v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = load(i + u);
+#pragma unroll
+        for (int u = 0; u < U; u++) proc(i + u, v[u]);
+    }
+    for (; i < r1; i++) proc(i, load(i));
+}
+
+// the same over a strided row set i = first, first + stride, ... < n
+template <int U, class LOAD, class PROC>
+__device__ __forceinline__ void rows_strided(int64_t first, int64_t stride, int64_t n, LOAD load, PROC proc) {
+    int64_t i = first;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        decltype(load(i)) v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = load(i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; u++) proc(i + u * stride, v[u]);
+    }
+    for (; i < n; i += stride) proc(i, load(i));
+}
+
+struct XW {
+    double x, w;
+};
+
 // PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
 // min/max present value; writes the scaled columns (column-major) into T.
 __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
@@ -194,24 +230,26 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     row_range(m, r0, r1);
     acc2 sr, srx;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
-    for (int64_t i = r0; i < r1; i++) {
-        const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
-        const bool isn = __builtin_isnan(x);
-        const bool z = x == 0.0;
-        if (Tc) Tc[i] = (isn || z) ? __builtin_nan("") : x;
-        nz += z ? 1.0 : 0.0;
-        if (isn || z) continue;
-        const double r = m.rep[i];
-        cnt += 1.0;
-        sr.add(r);
-        srx.add_prod(r, x);
-        if (r > mx) {
-            mx = r;
-            arg = (double)(m.row_offset + i);
-        }
-        mn_x = fmin(mn_x, x);
-        mx_x = fmax(mx_x, x);
-    }
+    rows_unrolled<ROW_UNROLL>(
+        r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
+        [&](int64_t i, XW v) {
+            const double x = rescale(v.x, p, m.int_dtype);
+            const bool isn = __builtin_isnan(x);
+            const bool z = x == 0.0;
+            if (Tc) Tc[i] = (isn || z) ? __builtin_nan("") : x;
+            nz += z ? 1.0 : 0.0;
+            if (isn || z) return;
+            const double r = v.w;
+            cnt += 1.0;
+            sr.add(r);
+            srx.add_prod(r, x);
+            if (r > mx) {
+                mx = r;
+                arg = (double)(m.row_offset + i);
+            }
+            mn_x = fmin(mn_x, x);
+            mx_x = fmax(mx_x, x);
+        });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, {cnt, 0.0});
     st_dd(pp + 2, sr.get());
@@ -379,10 +417,16 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
 // rows (every element is re-read by nb/2 tiles; the transform runs once).
 constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread, 16-byte accesses)
 
+// Blocks own a contiguous row range of a 512-column block; each wave also counts the
+// NaN / zero rescaled reports of its 128 columns per row (ballots), the block folds its
+// four waves in LDS and writes the counts of 64 rows at a time to rowpart[column block]
+// (k_scores adds the column blocks up: rowstat for na_row / participation, :549-567).
 __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
+    __shared__ uint32_t cnt[4][64][2];
     const int E = (int)m.n_events;
     const int64_t ld = m.wcd_ld;
     const int c0 = blockIdx.y * WCD_COLS + 2 * threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     ColParam p[2];
     bool ok[2];
     for (int k = 0; k < 2; k++) {
@@ -392,15 +436,54 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
         m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
-    if (c0 >= ld) return;
-    for (int64_t i = blockIdx.x; i < m.wcd_rows; i += gridDim.x) {
-        double w[2] = {0.0, 0.0};
-        if (i < m.n_rows) {
-            const double* r = m.reports + i * E + c0;
-            for (int k = 0; k < 2; k++)
-                if (ok[k]) w[k] = filled(r[k], p[k], m.int_dtype) - p[k].mu;
+    const int64_t per = (m.wcd_rows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = blockIdx.x * per, r1 = r0 + per < m.wcd_rows ? r0 + per : m.wcd_rows;
+    const bool in = c0 < ld;
+    uint32_t* part = m.rowpart + (int64_t)blockIdx.y * m.wcd_rows * 2;
+    for (int64_t g0 = r0; g0 < r1; g0 += 64) {
+        const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;
+        for (int u0 = 0; u0 < gn; u0 += 4) {
+            double rv[4][2];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t i = g0 + u0 + u;
+                const bool live = u0 + u < gn && i < m.n_rows;
+                const double* r = m.reports + (live ? i : 0) * E + c0;
+                rv[u][0] = (live && ok[0]) ? r[0] : 0.0;
+                rv[u][1] = (live && ok[1]) ? r[1] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (u0 + u >= gn) break;
+                const int64_t i = g0 + u0 + u;
+                const bool live = i < m.n_rows;
+                double w[2] = {0.0, 0.0};
+                int nn = 0, nz = 0;
+                for (int k = 0; k < 2; k++) {
+                    if (live && ok[k]) {
+                        const double x = rescale(rv[u][k], p[k], m.int_dtype);
+                        nn += __builtin_isnan(x) ? 1 : 0;
+                        nz += x == 0.0 ? 1 : 0;
+                        w[k] = (missing(x) ? p[k].guess : x) - p[k].mu;
+                    }
+                }
+                if (in) *(double2*)(m.wcd + i * ld + c0) = double2{w[0], w[1]};
+                const uint64_t b0 = __ballot(nn >= 1), b1 = __ballot(nn == 2);
+                const uint64_t z0 = __ballot(nz >= 1), z1 = __ballot(nz == 2);
+                if (lane == 0) {
+                    cnt[wv][u0 + u][0] = __popcll(b0) + __popcll(b1);
+                    cnt[wv][u0 + u][1] = __popcll(z0) + __popcll(z1);
+                }
+            }
         }
-        *(double2*)(m.wcd + i * ld + c0) = double2{w[0], w[1]};
+        __syncthreads();
+        if (threadIdx.x < gn) {
+            const int t = threadIdx.x;
+            const uint32_t a = cnt[0][t][0] + cnt[1][t][0] + cnt[2][t][0] + cnt[3][t][0];
+            const uint32_t z = cnt[0][t][1] + cnt[1][t][1] + cnt[2][t][1] + cnt[3][t][1];
+            *(uint2*)(part + (g0 + t) * 2) = uint2{a, z};
+        }
+        __syncthreads();
     }
 }
 
@@ -754,6 +837,48 @@ __global__ void __launch_bounds__(1024) k_pi_finish(pcx_mat m, int mode) {
 // ================================================================== row passes
 // PCX_M_SCORES: s_i = sum_j wcd_ij * loading_j (:337), one wavefront per row;
 // per-row NaN / zero counts; min/max keys of the scores.
+// PCX_M_SCORES (PCA): scores = wcd . loading (:337) from the materialised wcd (the
+// same f - mu values the covariance used), one wave per row, 16-byte loads; row NaN /
+// zero counts from k_wcd's column-block partials.
+__global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
+    const int lane = threadIdx.x % WAVE;
+    const int64_t ld = m.wcd_ld;
+    const int ncb = (int)((ld + WCD_COLS - 1) / WCD_COLS);
+    const double* LD = m.ev + EV_LD * m.n_events;  // zero padded to ld below
+    const int64_t row0 = blockIdx.x * (int64_t)(BT / WAVE) + threadIdx.x / WAVE;
+    uint64_t kmin = ~0ull, kmax = 0;
+    bool anynan = false;
+    for (int64_t i = row0; i < m.n_rows; i += (int64_t)gridDim.x * (BT / WAVE)) {
+        const double* w = m.wcd + i * ld;
+        double acc = 0.0;
+#pragma unroll 4
+        for (int c = 2 * lane; c < ld; c += 2 * WAVE) {
+            const double2 x = *(const double2*)(w + c);
+            const double v0 = c < m.n_events ? LD[c] : 0.0;
+            const double v1 = c + 1 < m.n_events ? LD[c + 1] : 0.0;
+            acc = fma(x.x, v0, acc);
+            acc = fma(x.y, v1, acc);
+        }
+        acc = wave_sum_d(acc);
+        if (lane < 2) {
+            uint32_t t = 0;
+            for (int b = 0; b < ncb; b++) t += m.rowpart[((int64_t)b * m.wcd_rows + i) * 2 + lane];
+            m.rowstat[2 * i + lane] = t;
+        }
+        if (lane == 0) m.rowv[RV_S * m.n_rows + i] = acc;
+        if (__builtin_isnan(acc)) anynan = true;
+        const uint64_t k = dkey(acc);
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+    }
+    if (lane == 0) {
+        uint64_t* sk = m.skey + (int64_t)m.rank * 4;
+        atomicMin((unsigned long long*)&sk[0], (unsigned long long)kmin);
+        atomicMax((unsigned long long*)&sk[1], (unsigned long long)kmax);
+        if (anynan) atomicOr((unsigned long long*)&sk[2], 1ull);
+    }
+}
+
 __global__ void __launch_bounds__(BT) k_scores(pcx_mat m) {
     const int E = (int)m.n_events;
     const int lane = threadIdx.x % WAVE;
@@ -844,51 +969,78 @@ __device__ __forceinline__ double nweight(double v, double S, double Sp) {
 }
 
 // PCX_M_GEMV2: d1 = normalize(set1) . F, d2 = normalize(set2) . F  (:492-493)
-__global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
-    const int c = blockIdx.x * BT + threadIdx.x;
-    const int E = (int)m.n_events;
-    if (c >= E) return;
+// row weights of the two candidate sets, normalize(set1) and normalize(set2) (:488-493),
+// computed once per row (k_gemv2 reads them instead of dividing per element)
+__global__ void __launch_bounds__(BT) k_nweights(pcx_mat m) {
     double mn, mx;
     score_minmax(m, mn, mx);
     const double S1 = dd_to_double(scl(m, SC_A1)), S1p = dd_to_double(scl(m, SC_A1P));
     const double S2 = dd_to_double(scl(m, SC_A2)), S2p = dd_to_double(scl(m, SC_A2P));
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double s = m.rowv[RV_S * m.n_rows + i];
+        m.rowv[RV_N1 * m.n_rows + i] = nweight(fabs(s + fabs(mn)), S1, S1p);
+        m.rowv[RV_N2 * m.n_rows + i] = nweight(fabs(s - mx), S2, S2p);
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
     const ColParam p = col_param(m, c, true);
     int64_t r0, r1;
     row_range(m, r0, r1);
     acc2 a1, a2;
-    for (int64_t i = r0; i < r1; i++) {
-        const double f = filled(m.reports[i * E + c], p, m.int_dtype);
-        const double s = m.rowv[RV_S * m.n_rows + i];
-        a1.add_prod(nweight(fabs(s + fabs(mn)), S1, S1p), f);
-        a2.add_prod(nweight(fabs(s - mx), S2, S2p), f);
-    }
+    struct V3 {
+        double x, w1, w2;
+    };
+    rows_unrolled<ROW_UNROLL>(
+        r0, r1,
+        [&](int64_t i) {
+            return V3{m.reports[i * E + c], m.rowv[RV_N1 * m.n_rows + i], m.rowv[RV_N2 * m.n_rows + i]};
+        },
+        [&](int64_t, V3 v) {
+            const double f = filled(v.x, p, m.int_dtype);
+            a1.add_prod(v.w1, f);
+            a2.add_prod(v.w2, f);
+        });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, a1.get());
     st_dd(pp + 2, a2.get());
 }
 
 // PCX_M_DECIDE: ranks of old, new1, new2 (scipy rankdata 'average') and the rule (:487-500)
-__global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
-    __shared__ dd lds[16];
-    __shared__ double red[1024];
+// PCX_M_DECIDE (:491-498): new1/new2, then the three average ranks (scipy rankdata),
+// O(E^2) comparisons spread over E/256 blocks; the rank-distance sums are half-integers,
+// so the blocks' partial sums add exactly in any order (atomicAdd).
+__global__ void __launch_bounds__(BT) k_decide_prep(pcx_mat m) {
     const int E = (int)m.n_events;
-    double* old = m.ev + EV_OLD * E;
+    const double* old = m.ev + EV_OLD * E;
     double* n1 = m.ev + EV_D1 * E;   // new1 = normalize(set1) . F + 0.01 * old
     double* n2 = m.ev + EV_D2 * E;   // new2
     double* raw1 = m.pvec + 2 * (m.n_events + 64);  // normalize(set1) . F (continuous rule)
     double* raw2 = pv_y(m);                          // normalize(set2) . F
-    for (int c = threadIdx.x; c < E; c += 1024) {
-        const double a = dd_to_double(cst(m, c, 4));
-        const double b = dd_to_double(cst(m, c, 5));
-        const double t = 0.01 * old[c];
-        n1[c] = a + t;
-        n2[c] = b + t;
-        raw1[c] = a;
-        raw2[c] = b;
-    }
-    __syncthreads();
-    double e1 = 0.0, e2 = 0.0;
-    for (int c = threadIdx.x; c < E; c += 1024) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c == 0) pv_s(m)[8] = 0.0;
+    if (c >= E) return;
+    const double a = dd_to_double(cst(m, c, 4));
+    const double b = dd_to_double(cst(m, c, 5));
+    const double t = 0.01 * old[c];
+    n1[c] = a + t;
+    n2[c] = b + t;
+    raw1[c] = a;
+    raw2[c] = b;
+}
+
+__global__ void __launch_bounds__(BT) k_ranks(pcx_mat m) {
+    __shared__ double red[BT];
+    const int E = (int)m.n_events;
+    const double* old = m.ev + EV_OLD * E;
+    const double* n1 = m.ev + EV_D1 * E;
+    const double* n2 = m.ev + EV_D2 * E;
+    const int c = blockIdx.x * BT + threadIdx.x;
+    double e = 0.0;
+    if (c < E) {
         int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0, lt2 = 0, eq2 = 0;
         const double o = old[c], a = n1[c], b = n2[c];
         for (int k = 0; k < E; k++) {
@@ -901,18 +1053,24 @@ __global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
             eq2 += bk == b;
         }
         const double r0 = lt0 + (eq0 + 1) * 0.5, r1 = lt1 + (eq1 + 1) * 0.5, r2 = lt2 + (eq2 + 1) * 0.5;
-        e1 += fabs(r1 - r0);
-        e2 += fabs(r2 - r0);
+        e = fabs(r1 - r0) - fabs(r2 - r0);
     }
-    // half-integer sums are exact in any order
-    red[threadIdx.x] = e1 - e2;
+    red[threadIdx.x] = e;
     __syncthreads();
-    for (int s = 512; s >= 1; s >>= 1) {
-        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    for (int st = BT / 2; st >= 1; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
         __syncthreads();
     }
-    const double ref = red[0];
-    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&pv_s(m)[8], red[0]);
+}
+
+__global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
+    __shared__ dd lds[16];
+    const int E = (int)m.n_events;
+    const double* old = m.ev + EV_OLD * E;
+    const double* raw1 = m.pvec + 2 * (m.n_events + 64);
+    const double* raw2 = pv_y(m);
+    const double ref = pv_s(m)[8];
     int branch, pick1;
     if (ref == 0) {
         acc2 q1, q2;
@@ -986,23 +1144,38 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
     row_range(m, r0, r1);
     acc2 raw, pc, b1, b15, b2;
     double n1 = 0, n15 = 0, n2 = 0;
-    for (int64_t i = r0; i < r1; i++) {
-        const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
-        const bool ms = missing(x);
-        const double f = ms ? p.guess : x;
-        const double w = m.rowv[RV_SMOOTH * m.n_rows + i];
-        raw.add_prod(w, f);
-        if (ms) pc.add(w);
-        if (f == 1.0) {
-            b1.add(w);
-            n1 += 1;
-        } else if (f == 1.5) {
-            b15.add(w);
-            n15 += 1;
-        } else if (f == 2.0) {
-            b2.add(w);
-            n2 += 1;
+    // explicit unroll (a lambda capturing five accumulators pushed them to scratch)
+    int64_t i = r0;
+    for (; i < r1;) {
+        const int u_n = r1 - i >= ROW_UNROLL ? ROW_UNROLL : (int)(r1 - i);
+        double xv[ROW_UNROLL], wv[ROW_UNROLL];
+#pragma unroll
+        for (int u = 0; u < ROW_UNROLL; u++) {
+            const int64_t ii = u < u_n ? i + u : i;
+            xv[u] = m.reports[ii * E + c];
+            wv[u] = m.rowv[RV_SMOOTH * m.n_rows + ii];
         }
+#pragma unroll
+        for (int u = 0; u < ROW_UNROLL; u++) {
+            if (u >= u_n) break;
+            const double x = rescale(xv[u], p, m.int_dtype);
+            const bool ms = missing(x);
+            const double f = ms ? p.guess : x;
+            const double w = wv[u];
+            raw.add_prod(w, f);
+            if (ms) pc.add(w);
+            if (f == 1.0) {
+                b1.add(w);
+                n1 += 1;
+            } else if (f == 1.5) {
+                b15.add(w);
+                n15 += 1;
+            } else if (f == 2.0) {
+                b2.add(w);
+                n2 += 1;
+            }
+        }
+        i += u_n;
     }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, raw.get());
@@ -1035,6 +1208,23 @@ __global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
 
 // ================================================================== weighted median selection
 // element (value, weight) of scaled event s at local row i; false = not part of the set
+// raw operands of element (s, i) of the selection, loaded ahead of sel_decode
+__device__ __forceinline__ XW sel_load(const pcx_mat& m, int s, int64_t i) {
+    return XW{m.T[(int64_t)s * m.n_rows + i], m.sel_phase == 1 ? m.rep[i] : m.rowv[RV_SMOOTH * m.n_rows + i]};
+}
+
+__device__ __forceinline__ bool sel_decode(const pcx_mat& m, int s, XW v, double& x, double& w) {
+    if (m.sel_phase == 1) {
+        if (__builtin_isnan(v.x)) return false;
+        x = v.x;
+    } else {
+        x = __builtin_isnan(v.x) ? m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]] : v.x;
+        if (__builtin_isnan(x)) return false;
+    }
+    w = v.w;
+    return true;
+}
+
 __device__ __forceinline__ bool sel_elem(const pcx_mat& m, int s, int64_t i, double& x, double& w) {
     const double t = m.T[(int64_t)s * m.n_rows + i];
     if (m.sel_phase == 1) {
@@ -1072,19 +1262,20 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     __syncthreads();
     uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0;
     double wm = -1.0;
-    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
-        double x, w;
-        if (!sel_elem(m, s, i, x, w)) continue;
-        const limbs3 L = to_limbs(w);
-        a += L.l0;
-        b += L.l1;
-        c += L.l2;
-        const uint64_t k = dkey(x);
-        mn = k < mn ? k : mn;
-        mx = k > mx ? k : mx;
-        wm = fmax(wm, w);
-        n++;
-    }
+    rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
+                             [&](int64_t, XW v) {
+                                 double x, w;
+                                 if (!sel_decode(m, s, v, x, w)) return;
+                                 const limbs3 L = to_limbs(w);
+                                 a += L.l0;
+                                 b += L.l1;
+                                 c += L.l2;
+                                 const uint64_t k = dkey(x);
+                                 mn = k < mn ? k : mn;
+                                 mx = k > mx ? k : mx;
+                                 wm = fmax(wm, w);
+                                 n++;
+                             });
     atomicAdd(&la, (unsigned long long)a);
     atomicAdd(&lb, (unsigned long long)b);
     atomicAdd(&lc, (unsigned long long)c);
@@ -1224,11 +1415,12 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     __syncthreads();
     const uint64_t lo = st[1], hi = st[2];
     const int sh = (int)st[3];
-    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
+    rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
+                             [&](int64_t, XW v) {
         double x, w;
-        if (!sel_elem(m, s, i, x, w)) continue;
+        if (!sel_decode(m, s, v, x, w)) return;
         const uint64_t k = dkey(x);
-        if (k < lo || k > hi) continue;
+        if (k < lo || k > hi) return;
         const int b = (int)((k - lo) >> sh);
         const limbs3 L = to_limbs(w);
         atomicAdd(&ha[b], (unsigned long long)L.l0);
@@ -1238,7 +1430,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         atomicMin(&hmin[b], (unsigned long long)k);
         atomicMax(&hmax[b], (unsigned long long)k);
         atomicMin(&hw[b], (unsigned long long)__double_as_longlong(w));
-    }
+    });
     __syncthreads();
     const int64_t o = ((int64_t)m.rank * m.n_scaled + s) * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
@@ -1483,14 +1675,17 @@ __global__ void __launch_bounds__(BT) k_scaled_cert(pcx_mat m) {
     const double adj = m.ev[EV_ADJ * E + c];
     acc2 a;
     double n = 0.0;
-    for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
-        const double t = m.T[(int64_t)s * m.n_rows + i];
-        const double f = __builtin_isnan(t) ? m.ev[EV_GUESS * E + c] : t;
-        if (f == adj) {
-            a.add(m.rowv[RV_SMOOTH * m.n_rows + i]);
-            n += 1.0;
-        }
-    }
+    const double guess = m.ev[EV_GUESS * E + c];
+    rows_strided<ROW_UNROLL>(
+        threadIdx.x, BT, m.n_rows,
+        [&](int64_t i) { return XW{m.T[(int64_t)s * m.n_rows + i], m.rowv[RV_SMOOTH * m.n_rows + i]}; },
+        [&](int64_t, XW v) {
+            const double f = __builtin_isnan(v.x) ? guess : v.x;
+            if (f == adj) {
+                a.add(v.w);
+                n += 1.0;
+            }
+        });
     const dd r = block_sum_dd<BT>(a.get(), lds);
     cnts[threadIdx.x] = n;
     __syncthreads();
@@ -1655,7 +1850,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
             break;
         case PCX_M_COV: {
-            if (!m.wcd || !m.tokp || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
+            if (!m.wcd || !m.tokp || !m.rowpart || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
                 m.wcd_ld < m.n_events) {
                 err = "PCX_M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
                 return hipErrorInvalidValue;
@@ -1685,17 +1880,23 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         }
         case PCX_M_SCORES:
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
-            hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
+            if (m.algorithm == 0 && m.wcd && m.rowpart)  // PCA: wcd and the row counts are ready (PCX_M_COV)
+                hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
+            else
+                hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             break;
         case PCX_M_NCSUMS:
             hipLaunchKernelGGL(k_ncsums, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 4, (int)SC_A1);
             break;
         case PCX_M_GEMV2:
+            hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
             break;
         case PCX_M_DECIDE:
+            hipLaunchKernelGGL(k_decide_prep, dim3(ceb), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), 0, st, m);
             break;
         case PCX_M_REPU:

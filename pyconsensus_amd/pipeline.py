@@ -139,6 +139,7 @@ class MatWorkspace:
         self.cslab = z(self.cov_kslices, E, E)
         self.wcd = t.empty((self.wcd_rows, self.wcd_ld), dtype=f64, device=device)
         self.tokp = t.empty((self.wcd_rows + 64,), dtype=f64, device=device)
+        self.rowpart = t.empty(((self.wcd_ld + 511) // 512, self.wcd_rows, 2), dtype=t.int32, device=device)
         self.C = z(E, E)
         self.Mw = z(2, E, E)
         self.pvec = z(4, E + 64)
@@ -154,7 +155,7 @@ class MatWorkspace:
         self.sel_val = z(world, S, 4)
 
     # buffers every stage writes in full before reading: not re-zeroed on reuse
-    _NO_RESET = ("wcd", "tokp", "T", "cslab", "C", "Mw")
+    _NO_RESET = ("wcd", "tokp", "rowpart", "T", "cslab", "C", "Mw")
 
     def reset(self):
         """Zero the scratch for another consensus of the same shape (reuse across calls)."""
@@ -269,7 +270,7 @@ def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev,
     P = _device.ptr
     m.reports, m.scaled, m.lo, m.hi, m.rep_raw = P(R), P(sc), P(lo_), P(hi_), P(rep)
     m.scaled_cols, m.scaled_index = P(scols), P(sidx)
-    for name in ("wcd", "tokp", "rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
+    for name in ("wcd", "tokp", "rowpart", "rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
                  "Mw", "pvec", "rowv", "rowstat", "skey", "info", "sel_sum", "sel_min", "sel_max", "sel_state",
                  "sel_val"):
         setattr(m, name, P(getattr(ws, name)))
