@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 2
+#define PCX_ABI_VERSION 3
 
 enum pcx_status {
     PCX_OK = 0,
@@ -88,8 +88,20 @@ typedef struct {
     int32_t int_dtype;            /* 1: reports had an integer dtype (truncation, Q3) */
     double  catch_tolerance;      /* Oracle(catch_tolerance=0.1)                 */
     double  alpha;                /* Oracle(alpha=0.1)                           */
-    int32_t algorithm;            /* 0 = "PCA", 1 = "absolute" (nc = 0, Q13)     */
+    int32_t algorithm;            /* enum pcx_algorithm                          */
+    int32_t max_components;       /* "big-five": components summed (Oracle caps it at E, :134-137) */
+    double  variance_threshold;   /* "fixed-variance": cumulative explained-variance stop (:448) */
+    const double* aux_scores;     /* "cokurtosis": [B][N] caller scores, aux["cokurt"] (:455-457) */
 } pcx_batch;
+
+/* Oracle(algorithm=...) values on the GPU path (__init__.py:368-457). */
+enum pcx_algorithm {
+    PCX_ALG_PCA = 0,               /* first principal component + rank rule (:368-371)         */
+    PCX_ALG_ABSOLUTE = 1,          /* unimplemented branch: nc = 0 (:359-362, Q13)             */
+    PCX_ALG_BIG_FIVE = 2,          /* eigenvalue-weighted top max_components scores (:373-390) */
+    PCX_ALG_FIXED_VARIANCE = 3,    /* components up to variance_threshold (:429-451)           */
+    PCX_ALG_COKURTOSIS = 4,        /* caller-supplied scores aux["cokurt"] (:455-457)          */
+};
 
 typedef struct {
     /* [B][N] -- result["agents"] */
@@ -120,6 +132,8 @@ typedef struct {
     /* [B][N][E], optional */
     double* original;             /* result["original"]: rescaled reports        */
     double* filled;               /* result["filled"]                            */
+    /* [B] */
+    int32_t* components;          /* result["components"]: fixed-variance count, else -1 (:449, :610) */
 } pcx_batch_result;
 
 int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_result* out);
@@ -162,6 +176,9 @@ enum pcx_mat_stage_id {
     PCX_M_SEL_STEP = 35,     /*   narrow the range; converged columns get their result */
     PCX_M_SEL_FINISH = 36,   /*   results into guess (phase 1) / outcomes_raw (phase 2) */
     PCX_M_SEL_EXACT = 37,    /* weighted median replayed with the reference's float order (n <= 8192, 1 rank) */
+    PCX_M_EIG = 38,          /* big-five / fixed-variance: eigenpairs of C (svd, :375, :431), the
+                                eigenvalue-weighted component sum (:377-382, :435-449) -> score vector */
+    PCX_M_ZERO_LOADING = 99, /* no wpca ("absolute", "cokurtosis"): first_loading = 0 (:359)          */
 };
 
 typedef struct {
@@ -224,6 +241,11 @@ typedef struct {
     int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
     int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
     uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
+    /* algorithms other than PCA (enum pcx_algorithm) */
+    int32_t max_components;       /* "big-five" component count                                     */
+    int32_t components;           /* out ("fixed-variance"): components used, else -1               */
+    double  variance_threshold;   /* "fixed-variance" stop                                          */
+    const double* aux_scores;     /* "cokurtosis": [n_rows] scores of this rank's rows              */
 } pcx_mat;
 
 /* Run one stage on the context's stream (PCX_M_POWER and the selection steps may

@@ -271,6 +271,137 @@ static int power_iter(const double (*C)[ES], int E, double* v, int* flags) {
     return it + PI_POLISH + sqn;
 }
 
+/* ------------------------------------------------------------------------
+ * "big-five" / "fixed-variance" (__init__.py:373-390, 429-451): the reference
+ * takes U, Sigma = svd(C) (LAPACK gesdd).  SPEC: C is symmetric PSD, so the
+ * singular pairs are the eigenpairs: Sigma = |lambda| in descending order, U's
+ * columns the eigenvectors (each loading is sign-normalised by the reference
+ * itself, loading[0] >= 0).  The eigenpairs come from cyclic two-sided Jacobi
+ * with the round-robin (circle) pair schedule: every step's pairs are disjoint;
+ * all its rotation angles are taken from the matrix at the start of the step,
+ * then the rotations are applied rows first, then columns (and V's columns).
+ * The GPU kernel applies the same steps lane-parallel in the same two phases.
+ * ------------------------------------------------------------------------ */
+#define JAC_MAXSWEEP 30
+#define JAC_TOL 1e-15
+
+static void jac_pair(int i, int r, int n, int* p, int* q) {
+    const int a = i == 0 ? 0 : 1 + (i - 1 + r) % (n - 1);
+    const int b = 1 + (n - 2 - i + r) % (n - 1);
+    *p = a < b ? a : b;
+    *q = a < b ? b : a;
+}
+
+/* one rotation's (c, s) from A[p][p], A[q][q], A[p][q]; s == 0 means "skip" */
+static void jac_angle(double app, double aqq, double apq, double* c, double* s) {
+    *c = 1.0;
+    *s = 0.0;
+    if (apq == 0.0) return;
+    const double tau = (aqq - app) / (2.0 * apq);
+    const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+    *c = 1.0 / sqrt(1.0 + t * t);
+    *s = t * *c;
+}
+
+static void jacobi_eig(double (*A)[ES], double (*V)[ES], int E) {
+    for (int j = 0; j < E; j++)
+        for (int k = 0; k < E; k++) V[j][k] = j == k ? 1.0 : 0.0;
+    if (E < 2) return;
+    const int n = E + (E & 1), npair = n / 2;
+    for (int sweep = 0; sweep < JAC_MAXSWEEP; sweep++) {
+        double off = 0.0, dg = 0.0;  /* max-norms: exact in any order */
+        for (int j = 0; j < E; j++)
+            for (int k = 0; k < E; k++) {
+                const double v = fabs(A[j][k]);
+                if (j == k)
+                    dg = fmax(dg, v);
+                else
+                    off = fmax(off, v);
+            }
+        if (!(off > JAC_TOL * dg)) break;
+        for (int r = 0; r < n - 1; r++) {
+            int pp[EMAX / 2 + 1], qq[EMAX / 2 + 1];
+            double cc[EMAX / 2 + 1], ss[EMAX / 2 + 1];
+            for (int i = 0; i < npair; i++) {
+                jac_pair(i, r, n, &pp[i], &qq[i]);
+                if (qq[i] >= E) {  /* the dummy player of an odd E */
+                    cc[i] = 1.0;
+                    ss[i] = 0.0;
+                } else {
+                    jac_angle(A[pp[i]][pp[i]], A[qq[i]][qq[i]], A[pp[i]][qq[i]], &cc[i], &ss[i]);
+                }
+            }
+            for (int i = 0; i < npair; i++) {  /* rows */
+                if (ss[i] == 0.0) continue;
+                const int p = pp[i], q = qq[i];
+                const double c = cc[i], s = ss[i];
+                for (int k = 0; k < E; k++) {
+                    const double apk = A[p][k], aqk = A[q][k];
+                    A[p][k] = c * apk - s * aqk;
+                    A[q][k] = s * apk + c * aqk;
+                }
+            }
+            for (int i = 0; i < npair; i++) {  /* columns of A and V */
+                if (ss[i] == 0.0) continue;
+                const int p = pp[i], q = qq[i];
+                const double c = cc[i], s = ss[i];
+                for (int j = 0; j < E; j++) {
+                    const double ajp = A[j][p], ajq = A[j][q];
+                    A[j][p] = c * ajp - s * ajq;
+                    A[j][q] = s * ajp + c * ajq;
+                    const double vjp = V[j][p], vjq = V[j][q];
+                    V[j][p] = c * vjp - s * vjq;
+                    V[j][q] = s * vjp + c * vjq;
+                }
+            }
+        }
+    }
+}
+
+/* net_score = sum_c Sigma_c * (wcd . loading_c) over the selected components, the
+ * component loop of :377-382 / :435-448 (score = Sigma * wcd.dot(loading), net +=).
+ * Returns the number of components used (fixed-variance) or -1 (big-five). */
+static int component_scores(int alg, const double (*C)[ES], int E, int N, const double (*F)[ES], const double* mu,
+                            int max_components, double threshold, double* net) {
+    static __thread double A[EMAX][ES], V[EMAX][ES];
+    double diag[EMAX], sig[EMAX];
+    int order[EMAX];
+    for (int j = 0; j < E; j++) {
+        memcpy(A[j], C[j], sizeof(double) * E);
+        diag[j] = C[j][j];
+    }
+    const double trace = pw_sum(diag, E); /* np.trace: add.reduce of the diagonal */
+    jacobi_eig(A, V, E);
+    for (int j = 0; j < E; j++) sig[j] = fabs(A[j][j]);
+    for (int j = 0; j < E; j++) {  /* descending Sigma, ties by index */
+        int rk = 0;
+        for (int k = 0; k < E; k++) rk += (sig[k] > sig[j]) || (sig[k] == sig[j] && k < j);
+        order[rk] = j;
+    }
+    const int kmax = alg == PCX_ALG_BIG_FIVE ? max_components : E;
+    for (int i = 0; i < N; i++) net[i] = 0.0;
+    double ve = 0.0;
+    int used = kmax;
+    for (int c = 0; c < kmax; c++) {
+        const int idx = order[c];
+        const double sg = sig[idx];
+        const double fl = V[0][idx] < 0.0 ? -1.0 : 1.0; /* loading *= -1 if loading[0] < 0 */
+        for (int i = 0; i < N; i++) {
+            double d = 0.0;
+            for (int j = 0; j < E; j++) d = fma(F[i][j] - mu[j], fl * V[j][idx], d);
+            net[i] = net[i] + sg * d;
+        }
+        if (alg == PCX_ALG_FIXED_VARIANCE) { /* cumsum(Sigma / trace) >= threshold -> stop */
+            ve = ve + sg / trace;
+            if (ve >= threshold) {
+                used = c + 1;
+                break;
+            }
+        }
+    }
+    return alg == PCX_ALG_FIXED_VARIANCE ? used : -1;
+}
+
 #define OUT(p, idx, val) do { if (p) (p)[idx] = (val); } while (0)
 
 static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
@@ -353,7 +484,12 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     int flags = 0, iters = 0, branch = PCX_BRANCH_NONE;
     double old[EMAX];
     for (int j = 0; j < E; j++) old[j] = dot2(rep, 1, &F[0][j], ES, N);  /* np.dot(rep, F) */
-    if (in->algorithm == 0) {
+    const int alg = in->algorithm;
+    const int pca_like = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;
+    int comps = -1;
+    for (int j = 0; j < E; j++) loading[j] = 0.0; /* no wpca: first_loading = zeros (:359) */
+    for (int i = 0; i < N; i++) s[i] = nc[i] = 0.0;
+    if (pca_like) {
         /* --- a5: weighted mean (np.ma.average, :317-319) --- */
         double mu[EMAX];
         double den = pw_sum(rep, N);
@@ -384,12 +520,24 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         for (int j = 0; j < E; j++) sq[j] = v[j] * v[j];
         double nv = sqrt(pw_sum(sq, E));
         for (int j = 0; j < E; j++) loading[j] = v[j] / nv;
-        for (int i = 0; i < N; i++) {
-            double acc = 0.0;
-            for (int j = 0; j < E; j++) acc = fma(F[i][j] - mu[j], loading[j], acc);
-            s[i] = acc;
+        if (alg == PCX_ALG_PCA) {
+            for (int i = 0; i < N; i++) {
+                double acc = 0.0;
+                for (int j = 0; j < E; j++) acc = fma(F[i][j] - mu[j], loading[j], acc);
+                s[i] = acc;
+            }
+        } else if (flags & PCX_FLAG_SVD_FAIL) {  /* the reference's second svd raises (:375, :431) */
+            for (int i = 0; i < N; i++) s[i] = NAN;
+        } else {  /* eigenvalue-weighted component scores (:373-390, :429-451) */
+            comps = component_scores(alg, (const double (*)[ES])C, E, N, (const double (*)[ES])F, mu,
+                                     in->max_components, in->variance_threshold, s);
         }
-        /* --- a8/a9: nonconformity_rank (:487-500), tie -> nonconformity (:475-485) --- */
+    } else if (alg == PCX_ALG_COKURTOSIS) {  /* caller-supplied scores (:455-457) */
+        for (int i = 0; i < N; i++) s[i] = in->aux_scores[b * N + i];
+    }
+    if (alg != PCX_ALG_ABSOLUTE) {
+        /* --- a8/a9: nonconformity_rank (:487-500), tie -> nonconformity (:475-485); the
+         * other algorithms call nonconformity directly (:389, :450, :456) --- */
         double mn = s[0], mx = s[0];
         for (int i = 1; i < N; i++) {  /* NaN propagates like np.min / np.max */
             if (isnan(s[i]) || s[i] < mn) mn = isnan(mn) ? mn : s[i];
@@ -412,15 +560,18 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
             new1[j] = a1 + t;
             new2[j] = a2 + t;
         }
-        rank_avg(old, E, r0);
-        rank_avg(new1, E, r1);
-        rank_avg(new2, E, r2);
         double e1[EMAX], e2[EMAX];
-        for (int j = 0; j < E; j++) {
-            e1[j] = fabs(r1[j] - r0[j]);
-            e2[j] = fabs(r2[j] - r0[j]);
+        double ref = 0.0;  /* non-PCA algorithms: straight to the continuous rule */
+        if (alg == PCX_ALG_PCA) {
+            rank_avg(old, E, r0);
+            rank_avg(new1, E, r1);
+            rank_avg(new2, E, r2);
+            for (int j = 0; j < E; j++) {
+                e1[j] = fabs(r1[j] - r0[j]);
+                e2[j] = fabs(r2[j] - r0[j]);
+            }
+            ref = pw_sum(e1, E) - pw_sum(e2, E);
         }
-        double ref = pw_sum(e1, E) - pw_sum(e2, E);
         int pick1;
         if (ref == 0) {
             for (int j = 0; j < E; j++) {
@@ -436,10 +587,7 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
             branch = pick1 ? PCX_BRANCH_SET1 : PCX_BRANCH_SET2;
         }
         for (int i = 0; i < N; i++) nc[i] = pick1 ? set1[i] : set2[i];
-    } else {  /* "absolute": nc = 0, no loading (Q13) */
-        for (int j = 0; j < E; j++) loading[j] = 0.0;
-        for (int i = 0; i < N; i++) s[i] = nc[i] = 0.0;
-    }
+    } /* "absolute": nc = 0 (Q13) */
     /* --- a10: reputation update (:460-472) --- */
     double meanrep = pw_sum(rep, N) / (double)N;
     double u[NMAX], this_[NMAX], smooth[NMAX];
@@ -469,7 +617,10 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         int m = 0;
         for (int i = 0; i < N; i++)
             if (F[i][j] == adj[j]) sel[m++] = smooth[i];
-        cert[j] = m ? pw_sum(sel, m) : NAN;
+        /* an empty match sums to NaN only on the PCA path, where smooth_rep is a
+         * MaskedArray (masked sum, Q11); the other algorithms' smooth_rep is a plain
+         * ndarray and the builtin sum of nothing is 0 (goldens: algos.npz) */
+        cert[j] = m ? pw_sum(sel, m) : (alg == PCX_ALG_PCA ? NAN : 0.0);
     }
     double reward[EMAX];
     normalize_(cert, E, reward);
@@ -542,13 +693,17 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     OUT(out->branch, b, branch);
     OUT(out->flags, b, flags);
     OUT(out->pi_iters, b, iters);
+    OUT(out->components, b, comps);
 }
 
 /* Host-memory restatement of pcx_consensus_batched_f64 (same structs). */
 int pcxo_consensus_batched_f64(const pcx_batch* in, pcx_batch_result* out, int n_threads) {
     if (!in || !out || in->n_reporters < 1 || in->n_reporters > NMAX || in->n_events < 1 ||
-        in->n_events > EMAX || in->n_rounds < 0)
+        in->n_events > EMAX || in->n_rounds < 0 || in->algorithm < 0 || in->algorithm > PCX_ALG_COKURTOSIS)
         return PCX_EINVAL;
+    if (in->algorithm == PCX_ALG_BIG_FIVE && (in->max_components < 1 || in->max_components > in->n_events))
+        return PCX_EINVAL;
+    if (in->algorithm == PCX_ALG_COKURTOSIS && !in->aux_scores) return PCX_EINVAL;
 #pragma omp parallel for schedule(dynamic, 64) num_threads(n_threads > 0 ? n_threads : 1)
     for (int64_t b = 0; b < in->n_rounds; b++) one_round(in, out, b);
     return PCX_OK;

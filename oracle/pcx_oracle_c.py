@@ -38,7 +38,8 @@ def _ptr(a):
 
 
 def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_tolerance=0.1,
-            alpha=0.1, int_dtype=False, algorithm="PCA", threads=1, want=None):
+            alpha=0.1, int_dtype=False, algorithm="PCA", threads=1, want=None, max_components=5,
+            variance_threshold=0.9, aux_scores=None):
     """Run B rounds; returns {name: array} for every output in ``want`` (default: all)."""
     R = np.ascontiguousarray(reports, dtype=np.float64)
     B, N, E = R.shape
@@ -54,8 +55,10 @@ def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_toler
     lo_ = cont(lo, np.float64)
     hi_ = cont(hi, np.float64)
     rp = cont(reputation, np.float64)
+    ax = cont(aux_scores, np.float64)
     inp = Batch(B, N, E, _ptr(R), _ptr(rp), _ptr(sc), _ptr(lo_), _ptr(hi_), int(shared), int(bool(int_dtype)),
-                float(catch_tolerance), float(alpha), ALGORITHMS[algorithm])
+                float(catch_tolerance), float(alpha), ALGORITHMS[algorithm], int(min(max_components, E)),
+                float(variance_threshold), _ptr(ax))
     outs = {}
     res = BatchResult()
     for name, kind, dt in BATCH_OUTPUTS:

@@ -1,12 +1,15 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
 FLAG_ZERO_COV, FLAG_SVD_FAIL, FLAG_PI_MAXIT = 1, 2, 4
-ALGORITHMS = {"PCA": 0, "absolute": 1}
+# enum pcx_algorithm (include/pcx.h); k-means / hierarchical / clusterfeck are not on the GPU path
+ALG_PCA, ALG_ABSOLUTE, ALG_BIG_FIVE, ALG_FIXED_VARIANCE, ALG_COKURTOSIS = 0, 1, 2, 3, 4
+ALGORITHMS = {"PCA": ALG_PCA, "absolute": ALG_ABSOLUTE, "big-five": ALG_BIG_FIVE,
+              "fixed-variance": ALG_FIXED_VARIANCE, "cokurtosis": ALG_COKURTOSIS}
 
 P_D = C.POINTER(C.c_double)
 
@@ -26,6 +29,9 @@ class Batch(C.Structure):
         ("catch_tolerance", C.c_double),
         ("alpha", C.c_double),
         ("algorithm", C.c_int32),
+        ("max_components", C.c_int32),
+        ("variance_threshold", C.c_double),
+        ("aux_scores", C.c_void_p),
     ]
 
 
@@ -41,6 +47,7 @@ BATCH_OUTPUTS = [
     ("participation", "1", "f8"), ("avg_certainty", "1", "f8"),
     ("branch", "1", "i4"), ("flags", "1", "i4"), ("pi_iters", "1", "i4"),
     ("original", "NE", "f8"), ("filled", "NE", "f8"),
+    ("components", "1", "i4"),
 ]
 
 
@@ -58,6 +65,7 @@ M_SCORES, M_NCSUMS, M_GEMV2, M_DECIDE, M_REPU, M_SMOOTH, M_OUTCOMES, M_EVENTS = 
 M_SCALED_CERT, M_FINAL, M_ROWSUMS, M_AGENTS, M_MATRICES = 17, 18, 19, 20, 21
 M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH = 30, 31, 32, 33, 34, 35, 36
 M_SEL_EXACT = 37
+M_EIG = 38
 SEL_EXACT_MAX = 8192
 M_ZERO_LOADING = 99
 
@@ -87,4 +95,6 @@ class Mat(C.Structure):
         ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
     ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),
                                                                    ("filled", _vp)] + [
-        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64), ("rowpart", _vp)]
+        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64), ("rowpart", _vp),
+        ("max_components", C.c_int32), ("components", C.c_int32), ("variance_threshold", C.c_double),
+        ("aux_scores", _vp)]

@@ -992,7 +992,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         const double aj = S.adj[j];
         const bool hit = row && S.F[l * ES + j] == aj;
         const uint64_t hm = ballot(hit);
-        const double c = hm ? wave_pw_sum(smooth_i, hit, S.scr) : __builtin_nan("");
+        const double c = hm ? wave_pw_sum(smooth_i, hit, S.scr) : (a.algorithm == 0 ? __builtin_nan("") : 0.0);
         if (l == j) certj = c;
     }
     // normalize(certainty), mean(certainty)

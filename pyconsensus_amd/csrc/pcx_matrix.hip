@@ -1188,6 +1188,12 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
     st_dd(pp + 14, {n2, 0.0});
 }
 
+// certainty of an event no reporter matched (:542): NaN on the PCA path (smooth_rep is a
+// MaskedArray, Q11), 0.0 for the other algorithms (plain ndarray, builtin sum of nothing)
+__device__ __forceinline__ double empty_certainty(const pcx_mat& m) {
+    return m.algorithm == 0 ? __builtin_nan("") : 0.0;
+}
+
 // PCX_M_EVENTS: binary outcomes (:526-531), certainty of binary events (:540-546)
 __global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
     const int c = blockIdx.x * BT + threadIdx.x;
@@ -1203,7 +1209,7 @@ __global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
     m.ev[EV_RAW * E + c] = raw;
     m.ev[EV_ADJ * E + c] = adj;
     m.ev[EV_FIN * E + c] = adj;
-    m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, slot)) : __builtin_nan("");
+    m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, slot)) : empty_certainty(m);
 }
 
 // ================================================================== weighted median selection
@@ -1705,7 +1711,7 @@ __global__ void __launch_bounds__(1024) k_final(pcx_mat m) {
     for (int c = threadIdx.x; c < E; c += 1024)
         if (m.scaled && m.scaled[c]) {
             const double cnt = dd_to_double(cst(m, c, 15));
-            m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, 14)) : __builtin_nan("");
+            m.ev[EV_CERT * E + c] = cnt > 0 ? dd_to_double(cst(m, c, 14)) : empty_certainty(m);
         }
     __syncthreads();
     acc2 sc, scp, spc, spcp;

@@ -164,6 +164,62 @@ def _median_margin(x, w):
     return float(np.min(np.abs(cum - mid)))
 
 
+def _continuous_decision(s, F, rep, dot):
+    set1 = s + abs(s.min())
+    set2 = s - s.max()
+    old = dot(rep, F)
+    e1 = dot(_normalize(set1), F) - old
+    e2 = dot(_normalize(set2), F) - old
+    if dot is _dot_exact:
+        ref = math.fsum(e1 ** 2) - math.fsum(e2 ** 2)
+    else:
+        ref = np.sum(e1 ** 2) - np.sum(e2 ** 2)
+    return 3 if ref <= 0 else 4
+
+
+def _continuous_neartie(s, F, rep):
+    """nonconformity's decision depends on rounding: it differs under correctly
+    rounded dots, or its margin is within 1e-9 of the two sums' size."""
+    dec = _continuous_decision(s, F, rep, np.dot)
+    if _continuous_decision(s, F, rep, _dot_exact) != dec:
+        return True
+    set1 = s + abs(s.min())
+    set2 = s - s.max()
+    old = _dot_exact(rep, F)
+    a = math.fsum((_dot_exact(_normalize(set1), F) - old) ** 2)
+    b = math.fsum((_dot_exact(_normalize(set2), F) - old) ** 2)
+    return abs(a - b) <= 1e-9 * (a + b) or not np.all(np.isfinite(s))
+
+
+def _eig_neartie(cov, algorithm, o):
+    """big-five / fixed-variance results depend on LAPACK choices: a used component
+    whose singular value is (nearly) repeated has no defined eigenvector; a loading
+    with loading[0] ~ 0 has no defined sign (the reference flips on loading[0] < 0);
+    the fixed-variance count can flip at the threshold."""
+    C = np.asarray(cov, float)
+    if not np.all(np.isfinite(C)):
+        return True
+    U, S, _ = np.linalg.svd(C)
+    E = S.size
+    k = min(o.max_components, E) if algorithm == "big-five" else int(o.num_components)
+    scale = S[0] if S.size and S[0] > 0 else 1.0
+    for i in range(min(k, E)):
+        gaps = []
+        if i > 0:
+            gaps.append(S[i - 1] - S[i])
+        if i + 1 < E:
+            gaps.append(S[i] - S[i + 1])
+        if S[i] > 1e-12 * scale and gaps and min(gaps) <= 1e-6 * scale:
+            return True
+        if S[i] > 1e-12 * scale and abs(U[0, i]) <= 1e-9:
+            return True
+    if algorithm == "fixed-variance":
+        ve = np.cumsum(S / np.trace(C))
+        if np.any(np.abs(ve - o.variance_threshold) <= 1e-9):
+            return True
+    return False
+
+
 # --------------------------------------------------------------------------- runner
 OUT_KEYS_AGENTS = ["old_rep", "this_rep", "smooth_rep", "na_row", "participation_rows",
                    "relative_part", "reporter_bonus", "scores"]
@@ -191,10 +247,22 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
 
     def nc_hook(self, scores, F):
         cap["fallback"] = True
+        if "s" not in cap:  # non-PCA algorithms call nonconformity directly (:389, :450, :456)
+            cap["nc_s"] = np.asarray(scores, float).ravel().copy()
+            cap["nc_F"] = np.asarray(F, float).copy()
+            cap["nc_rep"] = self.reputation.copy()
         return orig_nc(self, scores, F)
+
+    orig_wpca = ref.Oracle.wpca
+
+    def wpca_hook(self, F):
+        r = orig_wpca(self, F)
+        cap["cov"] = np.asarray(r[2], float).copy()
+        return r
 
     ref.Oracle.nonconformity_rank = rank_hook
     ref.Oracle.nonconformity = nc_hook
+    ref.Oracle.wpca = wpca_hook
     try:
         if isinstance(reports, np.ndarray) and not isinstance(reports, np.ma.MaskedArray):
             arg = reports.copy()  # the reference mutates float ndarrays (Q2)
@@ -205,6 +273,7 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
     finally:
         ref.Oracle.nonconformity_rank = orig_rank
         ref.Oracle.nonconformity = orig_nc
+        ref.Oracle.wpca = orig_wpca
     data = np.ma.getdata(reports) if isinstance(reports, np.ma.MaskedArray) else np.asarray(reports)
     d = {
         "in_reports": np.asarray(data, dtype=np.float64),
@@ -242,10 +311,21 @@ def run_case(ref, reports, bounds=None, reputation=None, **kw):
         # the same decision in exact arithmetic (correctly rounded dots)
         d["branch_exact"] = np.array(_decision_full(s, F, rep, _dot_exact))
         d["neartie_rank"] = np.array(bool(_rank_neartie(s, F, rep)))
+    elif "nc_s" in cap:  # continuous rule only: 3 = set1 (ref <= 0), 4 = set2
+        s_, F_, rep_ = cap["nc_s"], cap["nc_F"], cap["nc_rep"]
+        d["branch"] = np.array(_continuous_decision(s_, F_, rep_, np.dot))
+        d["branch_exact"] = np.array(_continuous_decision(s_, F_, rep_, _dot_exact))
+        d["neartie_rank"] = np.array(bool(_continuous_neartie(s_, F_, rep_)))
     else:
         d["branch"] = np.array(5)
         d["branch_exact"] = np.array(5)
         d["neartie_rank"] = np.array(False)
+    d["in_max_components"] = np.array(int(kw.get("max_components", 5)))
+    d["in_variance_threshold"] = np.array(float(kw.get("variance_threshold", 0.9)))
+    if kw.get("aux") is not None:
+        d["in_aux_scores"] = np.asarray(kw["aux"]["cokurt"], dtype=np.float64).ravel()
+    d["neartie_eig"] = np.array(bool("cov" in cap and kw.get("algorithm") in ("big-five", "fixed-variance")
+                                     and _eig_neartie(cap["cov"], kw.get("algorithm"), o)))
     raw = d["events.outcomes_raw"]
     tol = float(kw.get("catch_tolerance", 0.1))
     thr = np.array([1.5 - tol, 1.5 + tol])
@@ -445,6 +525,8 @@ def main():
     np.savez_compressed(os.path.join(HERE, "synth_mixed.npz"), **mixed)
     print("synth_mixed: 120 cases")
 
+    algos_main(ref)
+
     # config C2: 1000 x 100, seed 1
     Rc, sc_, loc, hic, repc = synthetic.matrix(1000, 100, seed=1)
     d = run_case(ref, Rc, synthetic.bounds_list(sc_, loc, hic), repc)
@@ -452,5 +534,66 @@ def main():
     print("c2 done; branch", d["branch"])
 
 
+def algos_main(ref):
+    """algorithm = big-five / fixed-variance / cokurtosis:
+    KAT matrices, seeded 50 x 20 rounds, mixed small shapes, and matrix-path sizes."""
+    from pyconsensus_amd import synthetic
+
+    out = {}
+    algos = ("big-five", "fixed-variance", "cokurtosis")
+
+    def add(name, reports, bounds, rep, alg, seed, **extra):
+        N = np.asarray(reports).shape[0]
+        kw = dict(algorithm=alg, **extra)
+        if alg == "cokurtosis":
+            kw["aux"] = {"cokurt": np.random.default_rng(seed).normal(0.0, 1.0, N)}
+        d = run_case(ref, reports, bounds, rep, **kw)
+        for k, v in d.items():
+            out[name + "/" + k] = v
+
+    kats = kat_cases()
+    for nm in ("readme", "docstring", "t1", "t3", "t5", "t6", "t8", "missing", "scaled_cli", "test_base_shift",
+               "q_float_rep", "q_alpha"):
+        spec = kats[nm]
+        kw = {k: v for k, v in spec.items() if k not in ("reports", "bounds", "reputation")}
+        for a_i, alg in enumerate(algos):
+            add("%s@%s" % (nm, alg), spec["reports"], spec.get("bounds"), spec.get("reputation"), alg,
+                1000 + a_i, **kw)
+    # CLI -x (__init__.py:849-862): the "absolute" branch (no nonconformity, Q13)
+    add("x_example@absolute", kats["t1"]["reports"], None, [2, 10, 4, 2, 7, 1], "absolute", 0)
+    add("missing@absolute", kats["missing"]["reports"], None, kats["missing"]["reputation"], "absolute", 0)
+    for a_i, alg in enumerate(algos):
+        R, sc, lo, hi, rep = synthetic.rounds(120, 50, 20, seed=8 + a_i)
+        for b in range(R.shape[0]):
+            add("s%03d@%s" % (b, alg), R[b], synthetic.bounds_list(sc[b], lo[b], hi[b]), rep[b], alg, 77 * b + a_i)
+        rng = np.random.default_rng(31 + a_i)
+        for k in range(30):
+            n, e = int(rng.integers(3, 65)), int(rng.integers(2, 33))
+            Rm, sm, lom, him, repm = synthetic.rounds(1, n, e, seed=5000 + 100 * a_i + k, reputation=bool(k % 3))
+            extra = {"max_components": int(rng.integers(1, 7))} if alg == "big-five" else {}
+            if alg == "fixed-variance":
+                extra = {"variance_threshold": float(rng.choice([0.5, 0.75, 0.9, 0.99]))}
+            add("m%03d@%s" % (k, alg), Rm[0], synthetic.bounds_list(sm[0], lom[0], him[0]) if k % 4 else None,
+                None if repm is None else repm[0], alg, 9000 + k, **extra)
+        for (n, e) in ((300, 40), (1200, 64)):  # matrix-path sizes
+            Rb, sb, lb, hb, rb = synthetic.matrix(n, e, seed=n + e + a_i)
+            add("big%dx%d@%s" % (n, e, alg), Rb, synthetic.bounds_list(sb, lb, hb), rb, alg, n)
+    np.savez_compressed(os.path.join(HERE, "algos.npz"), **out)
+    cases = split_keys(out)
+    nt = sum(bool(v.get("neartie_rank", False)) or bool(v.get("neartie_eig", False)) for v in cases.values())
+    print("algos: %d cases, %d flagged near-tie" % (len(cases), nt))
+
+
+def split_keys(flat):
+    res = {}
+    for k, v in flat.items():
+        c, kk = k.split("/", 1)
+        res.setdefault(c, {})[kk] = v
+    return res
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "algos":
+        algos_main(load_reference())
+    else:
+        main()

@@ -81,3 +81,17 @@ def flat_result(res):
 
 # keys whose sign follows the eigenvector sign (LAPACK-defined, quirk Q8)
 SIGNED_KEYS = ("agents.scores", "events.adj_first_loadings")
+
+
+def algos():
+    """big-five / fixed-variance / cokurtosis / absolute cases (make_golden.py algos_main)."""
+    return split_cases(load("algos.npz"))
+
+
+def algo_kwargs(case):
+    """Extra constructor kwargs of an algos.npz case."""
+    kw = {"max_components": int(case["in_max_components"]),
+          "variance_threshold": float(case["in_variance_threshold"])}
+    if "in_aux_scores" in case:
+        kw["aux"] = {"cokurt": case["in_aux_scores"]}
+    return kw

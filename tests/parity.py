@@ -52,7 +52,7 @@ def is_neartie(case, path="exact"):
     matrix_large: single-matrix path (exact-arithmetic medians): also fill medians.
     """
     f = lambda k: bool(case.get(k, False))
-    nt = f("neartie_rank") or f("neartie_catch") or f("neartie_median")
+    nt = f("neartie_rank") or f("neartie_catch") or f("neartie_median") or f("neartie_eig")
     if path in ("matrix_small", "matrix_large"):
         nt = nt or f("neartie_catch_fill")
     if path == "matrix_large":
@@ -74,7 +74,9 @@ def compare(case, ours, keys=None):
             continue
         a = np.asarray(ours[ok], float)
         b = np.asarray(case[gk], float)
-        if gk in SIGNED:
+        if gk in SIGNED and (gk != "agents.scores" or str(case.get("in_algorithm", "PCA")) == "PCA"):
+            # only the PCA scores follow the first loading's sign; big-five / fixed-variance
+            # scores are sign-normalised per component (loading[0] >= 0, :379, :437)
             a = a * sign
         if a.shape != b.shape:
             bad.append((gk, "shape", a.shape, b.shape))

@@ -192,7 +192,7 @@ struct Ring {
     static constexpr int LPW = (DIAG ? BK / 4 : BK / 2) + 1;  // glds per wave per stage
 };
 
-template <int BK, int NBUF, bool DIAG>
+template <int BK, int NBUF, bool DIAG, bool PRIO = false>
 __device__ __forceinline__ void glds_tile(const double* W, const double* tok, int Ep, int I, int J, int64_t s0,
                                           int64_t ns, double* lds, d4 (&acc)[4][4]) {
     using R = Ring<BK, DIAG>;
@@ -240,6 +240,7 @@ __device__ __forceinline__ void glds_tile(const double* W, const double* tok, in
         const double* As = buf + R::A_OFF;
         const double* Bs = DIAG ? As : buf + R::B_OFF;
         const double* Ts = buf + R::T_OFF + wv * 32;
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kk = 0; kk < BK / 4; kk++) {
             const int kr = kk * 4 + (lane >> 4);
@@ -255,12 +256,16 @@ __device__ __forceinline__ void glds_tile(const double* W, const double* tok, in
                 for (int b = 0; b < 4; b++)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
         asm volatile("" ::: "memory");
     }
 }
 
-template <int BK, int NBUF>
-__global__ void __launch_bounds__(256) k_syrk_glds(const double* W, const double* tok, int64_t Np, int E, int Ep,
+long long* g_clk = nullptr;  // optional per-block clock stamps (device buffer)
+__device__ long long* d_clk;
+
+template <int BK, int NBUF, bool PRIO = false, int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) k_syrk_glds(const double* W, const double* tok, int64_t Np, int E, int Ep,
                                                    int ntiles, int nks, double* slab) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int item = xcd_remap(blockIdx.x, gridDim.x);
@@ -272,11 +277,133 @@ __global__ void __launch_bounds__(256) k_syrk_glds(const double* W, const double
     const int64_t s0 = ks * per;
     const int64_t s1 = s0 + per < nst ? s0 + per : nst;
     d4 acc[4][4];
+    const long long t0 = __builtin_amdgcn_s_memtime(), q0 = __builtin_amdgcn_s_memrealtime();
     if (I == J)
-        glds_tile<BK, NBUF, true>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+        glds_tile<BK, NBUF, true, PRIO>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
     else
-        glds_tile<BK, NBUF, false>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+        glds_tile<BK, NBUF, false, PRIO>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+    const long long t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+    if (d_clk && threadIdx.x == 0) {
+        d_clk[2 * blockIdx.x] = t1 - t0;
+        d_clk[2 * blockIdx.x + 1] = q1 - q0;
+    }
     store_tile(slab + (int64_t)ks * E * E, E, I, J, acc);
+}
+
+// ---- 8-wave variant: 128x128 tile, waves 2 (rows) x 4 (cols), 64x32 per wave (acc 64
+// VGPRs) so 4 waves fit per SIMD at 2 workgroups per CU
+template <int BK, bool DIAG>
+struct Ring8 {
+    static constexpr int A_OFF = 0;
+    static constexpr int B_OFF = BK * LDP;
+    static constexpr int T_OFF = (DIAG ? 1 : 2) * BK * LDP;
+    static constexpr int STRIDE = T_OFF + 8 * 32;
+    static constexpr int LPW = (DIAG ? BK / 8 : BK / 4) + 1;
+};
+
+template <int BK, int NBUF, bool DIAG>
+__device__ __forceinline__ void glds8_tile(const double* W, const double* tok, int Ep, int I, int J, int64_t s0,
+                                           int64_t ns, double* lds, d4 (&acc)[4][2]) {
+    using R = Ring8<BK, DIAG>;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 2, wc = wv & 3;
+    const double* colA = W + I * CT + 2 * lane;
+    const double* colB = W + J * CT + 2 * lane;
+    auto issue = [&](int64_t s, int b) {
+        double* buf = lds + b * R::STRIDE;
+        const int64_t row0 = (s0 + s) * BK;
+#pragma unroll
+        for (int k = 0; k < BK / 8; k++) {
+            const int r = wv + 8 * k;
+            __builtin_amdgcn_global_load_lds((const void*)(colA + (row0 + r) * Ep), (lds_ptr_t)(buf + R::A_OFF + r * LDP),
+                                             16, 0, 0);
+        }
+        if (!DIAG) {
+#pragma unroll
+            for (int k = 0; k < BK / 8; k++) {
+                const int r = wv + 8 * k;
+                __builtin_amdgcn_global_load_lds((const void*)(colB + (row0 + r) * Ep),
+                                                 (lds_ptr_t)(buf + R::B_OFF + r * LDP), 16, 0, 0);
+            }
+        }
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)(tok + row0) + 4 * lane),
+                                         (lds_ptr_t)(buf + R::T_OFF + wv * 32), 4, 0, 0);
+    };
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 2; b++) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; s++)
+        if (s < ns) issue(s, s);
+    for (int64_t t = 0; t < ns; t++) {
+        if (t + NBUF - 2 < ns)
+            wait_vm<R::LPW * (NBUF - 2)>();
+        else
+            wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + NBUF - 1 < ns) issue(t + NBUF - 1, (int)((t + NBUF - 1) % NBUF));
+        const double* buf = lds + (int)(t % NBUF) * R::STRIDE;
+        const double* As = buf + R::A_OFF;
+        const double* Bs = DIAG ? As : buf + R::B_OFF;
+        const double* Ts = buf + R::T_OFF + wv * 32;
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            const double tk = Ts[kr];
+            double af[4], bf[2];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = As[kr * LDP + wr * 64 + a * 16 + (lane & 15)] * tk;
+#pragma unroll
+            for (int b = 0; b < 2; b++) bf[b] = Bs[kr * LDP + wc * 32 + b * 16 + (lane & 15)];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
+template <int BK, int NBUF, int MINW>
+__global__ void __launch_bounds__(512, MINW) k_syrk_w8(const double* W, const double* tok, int64_t Np, int E, int Ep,
+                                                      int ntiles, int nks, double* slab) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / ntiles, t = item % ntiles;
+    int I, J;
+    tri_index(t, I, J);
+    const int64_t nst = Np / BK;
+    const int64_t per = (nst + nks - 1) / nks;
+    const int64_t s0 = ks * per;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
+    d4 acc[4][2];
+    const long long t0 = __builtin_amdgcn_s_memtime(), q0 = __builtin_amdgcn_s_memrealtime();
+    if (I == J)
+        glds8_tile<BK, NBUF, true>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+    else
+        glds8_tile<BK, NBUF, false>(W, tok, Ep, I, J, s0, s1 - s0, lds, acc);
+    const long long t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+    if (d_clk && threadIdx.x == 0) {
+        d_clk[2 * blockIdx.x] = t1 - t0;
+        d_clk[2 * blockIdx.x + 1] = q1 - q0;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 2, wc = wv & 3;
+    double* out = slab + (int64_t)ks * E * E;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 2; b++)
+            for (int r = 0; r < 4; r++) {
+                const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
+                const int64_t q = (int64_t)J * CT + wc * 32 + b * 16 + (lane & 15);
+                if (p < E && q < E && q <= p) out[p * E + q] = acc[a][b][r];
+            }
+}
+
+template <int BK, int NBUF>
+size_t w8_lds_bytes() {
+    return (size_t)NBUF * Ring8<BK, false>::STRIDE * sizeof(double);
 }
 
 template <int BK, int NBUF>
@@ -308,6 +435,8 @@ static double maxrel(const std::vector<double>& a, const std::vector<double>& b,
     return m / scale;
 }
 
+static double g_last_clock = 0.0;
+
 typedef void (*syrk_fn)(const double*, const double*, int64_t, int, int, int, int, double*);
 
 struct Variant {
@@ -315,6 +444,7 @@ struct Variant {
     syrk_fn fn;
     size_t lds;
     int bk;
+    int threads = 256;
 };
 
 static double run_variant(const Variant& v, const Prob& P, int nks, double* slab, int reps, std::vector<double>* out,
@@ -327,13 +457,13 @@ static double run_variant(const Variant& v, const Prob& P, int nks, double* slab
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipMemset(slab, 0, (size_t)nks * P.E * P.E * sizeof(double)));
-    hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(256), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
+    hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(v.threads), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
     std::vector<float> ms;
     for (int r = 0; r < reps; r++) {
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(256), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
+        hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(v.threads), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float t;
@@ -348,6 +478,24 @@ static double run_variant(const Variant& v, const Prob& P, int nks, double* slab
     }
     double best = 1e30;
     for (float t : ms) best = fmin(best, t);
+    // in-kernel clock of one more launch: median over blocks of d(memtime) / d(realtime) x 100 MHz
+    {
+        long long* clk;
+        CK(hipMalloc(&clk, 2 * (size_t)nwg * sizeof(long long)));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(d_clk), &clk, sizeof(clk)));
+        hipLaunchKernelGGL(v.fn, dim3(nwg), dim3(v.threads), v.lds, 0, P.W, P.tok, P.Np, P.E, P.Ep, ntiles, nks, slab);
+        CK(hipDeviceSynchronize());
+        long long* none = nullptr;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(d_clk), &none, sizeof(none)));
+        std::vector<long long> h(2 * (size_t)nwg);
+        CK(hipMemcpy(h.data(), clk, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        CK(hipFree(clk));
+        std::vector<double> g;
+        for (int b = 0; b < nwg; b++)
+            if (h[2 * b + 1] > 0) g.push_back((double)h[2 * b] / (double)h[2 * b + 1] * 0.1);
+        std::sort(g.begin(), g.end());
+        g_last_clock = g.empty() ? 0.0 : g[g.size() / 2];
+    }
     return best;
 }
 
@@ -406,6 +554,12 @@ int main(int argc, char** argv) {
         {"glds8x3", (syrk_fn)k_syrk_glds<8, 3>, glds_lds_bytes<8, 3>(), 8},
         {"glds32x2", (syrk_fn)k_syrk_glds<32, 2>, glds_lds_bytes<32, 2>(), 32},
         {"glds4x6", (syrk_fn)k_syrk_glds<4, 6>, glds_lds_bytes<4, 6>(), 4},
+        {"glds16x2prio", (syrk_fn)k_syrk_glds<16, 2, true>, glds_lds_bytes<16, 2>(), 16},
+        {"glds8x2w3", (syrk_fn)k_syrk_glds<8, 2, false, 3>, glds_lds_bytes<8, 2>(), 8},
+        {"glds8x3w3", (syrk_fn)k_syrk_glds<8, 3, false, 3>, glds_lds_bytes<8, 3>(), 8},
+        {"w8_16x2", (syrk_fn)k_syrk_w8<16, 2, 4>, w8_lds_bytes<16, 2>(), 16, 512},
+        {"w8_8x2", (syrk_fn)k_syrk_w8<8, 2, 4>, w8_lds_bytes<8, 2>(), 8, 512},
+        {"w8_8x3", (syrk_fn)k_syrk_w8<8, 3, 3>, w8_lds_bytes<8, 3>(), 8, 512},
     };
     for (int pass = 0; pass < 2; pass++) {
         Prob P;
@@ -446,8 +600,8 @@ int main(int argc, char** argv) {
                        err, err < 1e-12 ? "true" : "false");
                 if (!(err < 1e-12)) return 3;
             } else {
-                printf("{\"variant\":\"%s\",\"N\":%lld,\"E\":%d,\"nks\":%d,\"lds\":%zu,\"ms\":%.3f,\"tflops\":%.2f}\n", v.name,
-                       (long long)P.N, P.E, nkv, v.lds, ms, flops / (ms * 1e-3) / 1e12);
+                printf("{\"variant\":\"%s\",\"N\":%lld,\"E\":%d,\"nks\":%d,\"lds\":%zu,\"ms\":%.3f,\"tflops\":%.2f,"
+                       "\"clock_ghz\":%.3f}\n", v.name, (long long)P.N, P.E, nkv, v.lds, ms, flops / (ms * 1e-3) / 1e12, g_last_clock);
             }
             fflush(stdout);
         }
