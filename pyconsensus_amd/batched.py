@@ -18,13 +18,17 @@ MAX_EVENTS = 32
 
 def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
                       catch_tolerance=0.1, alpha=0.1, int_dtype=False, algorithm="PCA",
-                      outputs=None, device=None, filled=False, original=False):
+                      outputs=None, device=None, filled=False, original=False,
+                      max_components=5, variance_threshold=0.9, aux_scores=None):
     """Run B rounds of N x E reports on the GPU.
 
     reports:    (B, N, E) float64, NaN = missing (0.0 is missing too, as in the reference)
     reputation: (B, N) raw weights or None (uniform)
     scaled/lo/hi: event bounds, (B, E) or (E,) shared by every round; None = all binary
     outputs:    iterable of result names to produce (default: all vector/scalar outputs)
+    algorithm:  "PCA" (default), "absolute", "big-five", "fixed-variance", "cokurtosis"
+                (__init__.py:368-457); max_components is capped at E like Oracle (:134-137);
+                aux_scores (B, N) are aux["cokurt"] of each round
 
     Returns a dict of torch tensors on the device, named like the ABI fields
     (``smooth_rep``, ``outcomes_final``, ...).  Asynchronous on torch's current stream.
@@ -55,9 +59,17 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     alg = _abi.ALGORITHMS.get(algorithm)
     if alg is None:
         raise NotImplementedError("algorithm %r is not on the GPU path" % (algorithm,))
+    aux = None
+    if alg == _abi.ALG_COKURTOSIS:
+        if aux_scores is None:
+            raise ValueError("cokurtosis needs aux_scores (aux['cokurt'] of every round)")
+        aux = _device.as_device(aux_scores, t.float64, dev)
+        if tuple(aux.shape) != (B, N):
+            raise ValueError("aux_scores must be (B, N)")
+    mc = int(max_components) if E >= int(max_components) else E  # __init__.py:134-137
     inp = _abi.Batch(B, N, E, _device.ptr(R), _device.ptr(rep), _device.ptr(sc), _device.ptr(lo_),
                      _device.ptr(hi_), shared, int(bool(int_dtype)), float(catch_tolerance),
-                     float(alpha), alg)
+                     float(alpha), alg, mc, float(variance_threshold), _device.ptr(aux))
     res = _abi.BatchResult()
     outs = {}
     for name, kind, dt in _abi.BATCH_OUTPUTS:
@@ -71,5 +83,5 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
         setattr(res, name, x.data_ptr())
     h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev))
     _lib.check(_lib.lib().pcx_consensus_batched_f64(h, C.byref(inp), C.byref(res)))
-    outs["_inputs"] = (R, rep, sc, lo_, hi_)  # keep inputs alive until the caller syncs
+    outs["_inputs"] = (R, rep, sc, lo_, hi_, aux)  # keep inputs alive until the caller syncs
     return outs

@@ -78,7 +78,14 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     if (in->n_events < 1 || in->n_events > 32) return fail(PCX_EINVAL, "batched: n_events must be in [1, 32]");
     if (!in->reports) return fail(PCX_EINVAL, "batched: reports is NULL");
     if (in->scaled && (!in->lo || !in->hi)) return fail(PCX_EINVAL, "batched: scaled given without lo/hi");
-    if (in->algorithm != 0 && in->algorithm != 1) return fail(PCX_EINVAL, "batched: algorithm must be 0 (PCA) or 1");
+    if (in->algorithm < PCX_ALG_PCA || in->algorithm > PCX_ALG_COKURTOSIS)
+        return fail(PCX_EINVAL, "batched: algorithm must be an enum pcx_algorithm value (0..4)");
+    if (in->algorithm == PCX_ALG_BIG_FIVE && (in->max_components < 1 || in->max_components > in->n_events))
+        return fail(PCX_EINVAL, "batched: big-five needs 1 <= max_components <= n_events");
+    if (in->algorithm == PCX_ALG_FIXED_VARIANCE && !std::isfinite(in->variance_threshold))
+        return fail(PCX_EINVAL, "batched: variance_threshold must be finite");
+    if (in->algorithm == PCX_ALG_COKURTOSIS && !in->aux_scores)
+        return fail(PCX_EINVAL, "batched: cokurtosis needs aux_scores (aux[\"cokurt\"])");
     if (!std::isfinite(in->catch_tolerance) || !std::isfinite(in->alpha))
         return fail(PCX_EINVAL, "batched: catch_tolerance/alpha must be finite");
     hipError_t e = hipSetDevice(ctx->device);
@@ -96,6 +103,9 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     a.bounds_shared = in->bounds_shared;
     a.int_dtype = in->int_dtype;
     a.algorithm = in->algorithm;
+    a.max_components = in->max_components;
+    a.variance_threshold = in->variance_threshold;
+    a.aux_scores = in->aux_scores;
     a.catch_tol = in->catch_tolerance;
     a.alpha = in->alpha;
     a.old_rep = out->old_rep;
@@ -120,6 +130,7 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     a.branch = out->branch;
     a.flags = out->flags;
     a.pi_iters = out->pi_iters;
+    a.components = out->components;
     a.original = out->original;
     a.filled = out->filled;
     const char* st_env = getenv("PCX_STAMPS");

@@ -527,6 +527,94 @@ __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
     wsync();
 }
 
+// ---- "big-five" / "fixed-variance" eigenpairs: SPEC jacobi_eig of
+// oracle/pcx_oracle_batched.c (cyclic two-sided Jacobi, round-robin pairs; each
+// step's angles from the matrix at the step's start, rows then columns), one lane
+// per (pair, row/column) element -- the same arithmetic, so bit-identical.
+constexpr int JAC_MAXSWEEP = 30;
+constexpr double JAC_TOL = 1e-15;
+
+__device__ __forceinline__ void jac_pair(int i, int r, int n, int& p, int& q) {
+    const int a = i == 0 ? 0 : 1 + (i - 1 + r) % (n - 1);
+    const int b = 1 + (n - 2 - i + r) % (n - 1);
+    p = a < b ? a : b;
+    q = a < b ? b : a;
+}
+
+// A (E x E, row stride ES) -> eigenvalues on its diagonal; V -> eigenvectors (columns).
+// prm: 64 doubles of LDS (rotation cosines at [0, 32), sines at [32, 64)).
+__device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm) {
+    const int l = lane_id();
+    for (int o = l; o < E * E; o += W) {
+        const int j = o / E, k = o - j * E;
+        V[j * ES + k] = j == k ? 1.0 : 0.0;
+    }
+    wsync();
+    if (E < 2) return;
+    const int n = E + (E & 1), npair = n / 2;
+    for (int sweep = 0; sweep < JAC_MAXSWEEP; sweep++) {
+        double off = 0.0, dg = 0.0;  // max-norms: exact in any order
+        for (int o = l; o < E * E; o += W) {
+            const int j = o / E, k = o - j * E;
+            const double v = fabs(A[j * ES + k]);
+            if (j == k)
+                dg = fmax(dg, v);
+            else
+                off = fmax(off, v);
+        }
+        off = wave_max(off);
+        dg = wave_max(dg);
+        if (!(off > JAC_TOL * dg)) break;
+        for (int r = 0; r < n - 1; r++) {
+            if (l < npair) {
+                int p, q;
+                jac_pair(l, r, n, p, q);
+                double c = 1.0, s = 0.0;
+                if (q < E) {
+                    const double apq = A[p * ES + q];
+                    if (apq != 0.0) {
+                        const double app = A[p * ES + p], aqq = A[q * ES + q];
+                        const double tau = (aqq - app) / (2.0 * apq);
+                        const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        s = t * c;
+                    }
+                }
+                prm[l] = c;
+                prm[32 + l] = s;
+            }
+            wsync();
+            for (int o = l; o < npair * E; o += W) {  // rows p, q
+                const int i = o / E, k = o - i * E;
+                const double s = prm[32 + i];
+                if (s == 0.0) continue;
+                int p, q;
+                jac_pair(i, r, n, p, q);
+                const double c = prm[i];
+                const double apk = A[p * ES + k], aqk = A[q * ES + k];
+                A[p * ES + k] = c * apk - s * aqk;
+                A[q * ES + k] = s * apk + c * aqk;
+            }
+            wsync();
+            for (int o = l; o < npair * E; o += W) {  // columns p, q of A and V
+                const int i = o / E, j = o - i * E;
+                const double s = prm[32 + i];
+                if (s == 0.0) continue;
+                int p, q;
+                jac_pair(i, r, n, p, q);
+                const double c = prm[i];
+                const double ajp = A[j * ES + p], ajq = A[j * ES + q];
+                A[j * ES + p] = c * ajp - s * ajq;
+                A[j * ES + q] = s * ajp + c * ajq;
+                const double vjp = V[j * ES + p], vjq = V[j * ES + q];
+                V[j * ES + p] = c * vjp - s * vjq;
+                V[j * ES + q] = s * vjp + c * vjq;
+            }
+            wsync();
+        }
+    }
+}
+
 }  // namespace
 
 // NT/ET > 0: the round shape is a compile-time constant (the Monte Carlo shapes the
@@ -726,8 +814,9 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
     if (col) S.old[l] = oldj;
 
     double sc_i = 0.0, nc_i = 0.0, ld_j = 0.0;
-    int branch = 5, flags = 0, iters = 0;
-    if (a.algorithm == 0) {
+    int branch = 5, flags = 0, iters = 0, comps = -1;
+    const int alg = a.algorithm;
+    if (alg == 0 || alg == 2 || alg == 3) {  // wpca (:315-339): PCA, big-five, fixed-variance
         // ---- a5: weighted mean, np.ma.average (:317-319) -------------------
         const double den = wave_pw_sum(rep, row, S.scr);
         double muj = 0.0;
@@ -857,14 +946,66 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         wsync();
         if (col) S.ld[l] = ld_j;
         wsync();
-        // scores s = wcd . loading (:337), row phase
-        if (row) {
-            double acc = 0.0;
-            for (int j = 0; j < E; j++) acc = fma(S.F[l * ES + j] - S.mu[j], S.ld[j], acc);
-            sc_i = acc;
+        if (alg == 0) {
+            // scores s = wcd . loading (:337), row phase
+            if (row) {
+                double acc = 0.0;
+                for (int j = 0; j < E; j++) acc = fma(S.F[l * ES + j] - S.mu[j], S.ld[j], acc);
+                sc_i = acc;
+            }
+        } else if (flags & 2) {
+            sc_i = __builtin_nan("");  // the reference's second svd raises (:375, :431)
+        } else {
+            // ---- big-five (:373-390) / fixed-variance (:429-451): net score =
+            // sum_c Sigma_c * (wcd . loading_c); Sigma, loadings from Jacobi (SPEC)
+            const double trace = wave_pw_sum(col ? S.C[l * ES + l] : 0.0, col, S.scr);  // np.trace
+            wsync();
+            for (int o = l; o < E * E; o += W) {
+                const int j = o / E, k = o - j * E;
+                S.M[j * ES + k] = S.C[j * ES + k];
+            }
+            wsync();
+            jacobi_eig_wave(S.M, S.C, ES, E, S.scr);  // A in M; V overwrites C
+            const double sig = col ? fabs(S.M[l * ES + l]) : 0.0;
+            if (col) S.nv1[l] = sig;
+            wsync();
+            if (col) {  // order: descending Sigma, ties by index
+                int rk = 0;
+                for (int k = 0; k < E; k++) rk += (S.nv1[k] > sig) | ((S.nv1[k] == sig) & (k < l));
+                S.nv2[rk] = (double)l;
+            }
+            wsync();
+            const int kmax = alg == 2 ? a.max_components : E;
+            double net = 0.0, ve = 0.0;
+            int used = kmax;
+            for (int c = 0; c < kmax; c++) {
+                const int idx = (int)S.nv2[c];
+                const double sg = S.nv1[idx];
+                const double fl = S.C[idx] < 0.0 ? -1.0 : 1.0;  // loading *= -1 if loading[0] < 0
+                if (row) {
+                    double d = 0.0;
+                    for (int j = 0; j < E; j++) d = fma(S.F[l * ES + j] - S.mu[j], fl * S.C[j * ES + idx], d);
+                    net = net + sg * d;
+                }
+                if (alg == 3) {  // cumsum(Sigma / trace) >= threshold -> stop (:432, :448)
+                    ve = ve + sg / trace;
+                    if (ve >= a.variance_threshold) {
+                        used = c + 1;
+                        break;
+                    }
+                }
+            }
+            comps = alg == 3 ? used : -1;
+            sc_i = net;
+            wsync();
         }
-        STAMP(6);
-        // ---- a8/a9: nonconformity_rank (:487-500) / nonconformity (:475-485)
+    } else if (alg == 4) {  // cokurtosis: caller-supplied scores (:455-457)
+        sc_i = row ? a.aux_scores[b * N + l] : 0.0;
+    }
+    STAMP(6);
+    if (alg != 1) {
+        // ---- a8/a9: nonconformity_rank (:487-500) / nonconformity (:475-485); the
+        // non-PCA algorithms call nonconformity directly (:389, :450, :456)
         const bool any_nan = ballot(row && __builtin_isnan(sc_i)) != 0;
         double mn = wave_max(row ? -sc_i : -__builtin_inf());
         mn = -mn;
@@ -901,11 +1042,14 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
             S.nv2[l] = d2 + t;
         }
         wsync();
-        const double r0 = rank_avg(S.old, E);
-        const double r1 = rank_avg(S.nv1, E);
-        const double r2 = rank_avg(S.nv2, E);
-        const double e1 = fabs(r1 - r0), e2 = fabs(r2 - r0);
-        const double ref = wave_pw_sum(e1, col, S.scr) - wave_pw_sum(e2, col, S.scr);
+        double ref = 0.0;  // non-PCA: straight to the continuous rule
+        if (alg == 0) {
+            const double r0 = rank_avg(S.old, E);
+            const double r1 = rank_avg(S.nv1, E);
+            const double r2 = rank_avg(S.nv2, E);
+            const double e1 = fabs(r1 - r0), e2 = fabs(r2 - r0);
+            ref = wave_pw_sum(e1, col, S.scr) - wave_pw_sum(e2, col, S.scr);
+        }
         bool pick1;
         if (ref == 0) {
             const double q1 = d1 - oldj, q2 = d2 - oldj;
@@ -1084,6 +1228,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         if (a.branch) a.branch[b] = branch;
         if (a.flags) a.flags[b] = flags;
         if (a.pi_iters) a.pi_iters[b] = iters;
+        if (a.components) a.components[b] = comps;
     }
     STAMP(12);
     if (a.stamps && threadIdx.x == 0) {

@@ -22,6 +22,9 @@ struct BatchArgs {
     int bounds_shared;
     int int_dtype;
     int algorithm;
+    int max_components;       // big-five
+    double variance_threshold;  // fixed-variance
+    const double* aux_scores;   // cokurtosis [B][N]
     double catch_tol;
     double alpha;
     double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
@@ -29,7 +32,7 @@ struct BatchArgs {
     double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
         *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
     double *participation, *avg_certainty;
-    int32_t *branch, *flags, *pi_iters;
+    int32_t *branch, *flags, *pi_iters, *components;
     double *original, *filled;
     long long* stamps;  // diagnostic phase clocks [B][16] (PCX_STAMPS), normally NULL
 };

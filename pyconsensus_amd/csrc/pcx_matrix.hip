@@ -24,7 +24,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
 #include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <numeric>
+#include <vector>
 
 #include "../../include/pcx.h"
 #include "pcx_device.h"
@@ -844,7 +852,9 @@ __global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
     const int lane = threadIdx.x % WAVE;
     const int64_t ld = m.wcd_ld;
     const int ncb = (int)((ld + WCD_COLS - 1) / WCD_COLS);
-    const double* LD = m.ev + EV_LD * m.n_events;  // zero padded to ld below
+    // PCA: the first loading; big-five / fixed-variance: the eigenvalue-weighted sum of the
+    // sign-normalised loadings (PCX_M_EIG), i.e. net_score = wcd . g (:377-382, :435-440)
+    const double* LD = m.ev + (m.algorithm == 0 ? EV_LD : EV_SPARE) * m.n_events;
     const int64_t row0 = blockIdx.x * (int64_t)(BT / WAVE) + threadIdx.x / WAVE;
     uint64_t kmin = ~0ull, kmax = 0;
     bool anynan = false;
@@ -897,6 +907,7 @@ __global__ void __launch_bounds__(BT) k_scores(pcx_mat m) {
             if (m.algorithm == 0) acc = fma(f - p.mu, m.ev[EV_LD * E + c], acc);
         }
         acc = wave_sum_d(acc);
+        if (m.algorithm == 4) acc = m.aux_scores[i];  // cokurtosis: caller scores (:455-457)
         for (int s = 32; s >= 1; s >>= 1) {
             nn += __shfl_xor(nn, s, WAVE);
             nz += __shfl_xor(nz, s, WAVE);
@@ -1070,7 +1081,7 @@ __global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
     const double* old = m.ev + EV_OLD * E;
     const double* raw1 = m.pvec + 2 * (m.n_events + 64);
     const double* raw2 = pv_y(m);
-    const double ref = pv_s(m)[8];
+    const double ref = m.algorithm == 0 ? pv_s(m)[8] : 0.0;  // non-PCA: nonconformity directly
     int branch, pick1;
     if (ref == 0) {
         acc2 q1, q2;
@@ -1107,7 +1118,7 @@ __global__ void __launch_bounds__(BT) k_repu(pcx_mat m) {
     acc2 a, ap;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         double nc = 0.0;
-        if (m.algorithm == 0) {
+        if (m.algorithm != 1) {  // "absolute": nc = 0 (Q13)
             const double s = m.rowv[RV_S * m.n_rows + i];
             nc = pick1 ? s + fabs(mn) : s - mx;
         }
@@ -1797,7 +1808,7 @@ __global__ void __launch_bounds__(BT) k_agents(pcx_mat m) {
         if (m.old_rep) m.old_rep[i] = m.rep[i];
         if (m.this_rep) m.this_rep[i] = m.rowv[RV_THIS * m.n_rows + i];
         if (m.smooth_rep) m.smooth_rep[i] = sm;
-        if (m.scores) m.scores[i] = m.algorithm == 0 ? m.rowv[RV_S * m.n_rows + i] : 0.0;
+        if (m.scores) m.scores[i] = m.algorithm != 1 ? m.rowv[RV_S * m.n_rows + i] : 0.0;
         if (m.na_row) m.na_row[i] = narow;
         if (m.participation_rows) m.participation_rows[i] = pr;
         if (m.relative_part) m.relative_part[i] = rel;
@@ -1822,6 +1833,135 @@ __global__ void k_info_clear(pcx_mat m, int slot) { m.info[slot] = 0; }
 
 __global__ void k_zero_loading(pcx_mat m) {
     for (int j = threadIdx.x; j < m.n_events; j += blockDim.x) m.ev[EV_LD * m.n_events + j] = 0.0;
+}
+
+// ---------------------------------------------------------------- PCX_M_EIG helpers
+// gather diag(C) and the first component of every eigenvector (row k of the
+// row-major view of rocSOLVER's column-major eigenvector matrix)
+__global__ void __launch_bounds__(BT) k_eig_gather(const double* C, const double* U, int E, double* out) {
+    for (int j = blockIdx.x * BT + threadIdx.x; j < E; j += gridDim.x * BT) {
+        out[j] = C[(int64_t)j * E + j];
+        out[E + j] = U[(int64_t)j * E];
+    }
+}
+
+// g_j = sum_c coef_c * u_{idx_c, j} (components in order; coef = Sigma * sign)
+__global__ void __launch_bounds__(BT) k_eig_combine(const double* U, int E, const double* coef, const int* idx,
+                                                    int k, double* g) {
+    for (int j = blockIdx.x * BT + threadIdx.x; j < E; j += gridDim.x * BT) {
+        double acc = 0.0;
+        for (int c = 0; c < k; c++) acc = fma(coef[c], U[(int64_t)idx[c] * E + j], acc);
+        g[j] = acc;
+    }
+}
+
+// numpy pairwise add.reduce (np.trace of the diagonal)
+double np_pairwise(const double* a, int64_t n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; i++) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int k = 0; k < 8; k++) r[k] = a[k];
+        int64_t i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int k = 0; k < 8; k++) r[k] += a[i + k];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+rocblas_handle blas_handle(int device) {
+    static std::mutex mu;
+    static std::map<int, rocblas_handle> handles;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = handles.find(device);
+    if (it != handles.end()) return it->second;
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    handles[device] = h;
+    return h;
+}
+
+// big-five / fixed-variance (:375-382, :431-449): eigenpairs of C by rocSOLVER dsyevd
+// (the reference calls LAPACK gesdd on the same symmetric PSD matrix: Sigma = |lambda|,
+// U = eigenvectors), component selection on the host (E numbers), and the score
+// vector g = sum_c Sigma_c * sign_c * u_c into ev[EV_SPARE] (PCX_M_SCORES: wcd . g).
+hipError_t eig_stage(pcx_mat& m, hipStream_t st, std::string& err) {
+    const int E = (int)m.n_events;
+    const int64_t nn = (int64_t)E * E;
+    double* U = m.Mw;                 // eigenvectors (in place of the copy of C)
+    double* D = m.Mw + nn;            // eigenvalues, ascending
+    double* work = D + E;             // tridiagonal off-diagonal
+    double* tmp = work + E;           // [2E] diag(C), u_k[0]
+    double* coef = tmp + 2 * E;       // [E]
+    int* idx = (int*)(coef + E);      // [E]
+    rocblas_int* info = (rocblas_int*)(idx + E + 2);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    rocblas_handle h = blas_handle(dev);
+    if (!h) {
+        err = "PCX_M_EIG: rocblas_create_handle failed";
+        return hipErrorInvalidValue;
+    }
+    if ((e = hipMemcpyAsync(U, m.C, nn * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+    rocblas_set_stream(h, st);
+    if (rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_lower, E, U, E, D, work, info) !=
+        rocblas_status_success) {
+        err = "PCX_M_EIG: rocsolver_dsyevd failed";
+        return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k_eig_gather, dim3((E + BT - 1) / BT), dim3(BT), 0, st, (const double*)m.C, (const double*)U,
+                       E, tmp);
+    std::vector<double> lam(E), dg(E), u0(E);
+    rocblas_int hinfo = 0;
+    if ((e = hipMemcpyAsync(lam.data(), D, E * sizeof(double), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(dg.data(), tmp, E * sizeof(double), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(u0.data(), tmp + E, E * sizeof(double), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return e;
+    if ((e = hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (hinfo != 0) {
+        err = "PCX_M_EIG: dsyevd did not converge (info " + std::to_string(hinfo) + ")";
+        return hipErrorInvalidValue;
+    }
+    std::vector<double> sig(E);
+    std::vector<int> order(E);
+    for (int j = 0; j < E; j++) sig[j] = std::fabs(lam[j]);
+    std::iota(order.begin(), order.end(), 0);
+    // singular values descending; equal ones keep the eigen-solver's (ascending) order reversed
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return sig[x] > sig[y]; });
+    const double trace = np_pairwise(dg.data(), E);
+    int k = m.algorithm == 2 ? std::min(std::max(m.max_components, 1), E) : E;
+    if (m.algorithm == 3) {
+        double ve = 0.0;
+        for (int c = 0; c < E; c++) {
+            ve = ve + sig[order[c]] / trace;
+            if (ve >= m.variance_threshold) {
+                k = c + 1;
+                break;
+            }
+        }
+    }
+    std::vector<double> hc(k);
+    std::vector<int> hi(k);
+    for (int c = 0; c < k; c++) {
+        hi[c] = order[c];
+        hc[c] = sig[order[c]] * (u0[order[c]] < 0.0 ? -1.0 : 1.0);  // loading *= -1 if loading[0] < 0
+    }
+    if ((e = hipMemcpyAsync(coef, hc.data(), k * sizeof(double), hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(idx, hi.data(), k * sizeof(int), hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_eig_combine, dim3((E + BT - 1) / BT), dim3(BT), 0, st, (const double*)U, E,
+                       (const double*)coef, (const int*)idx, k, m.ev + EV_SPARE * E);
+    m.components = m.algorithm == 3 ? k : -1;
+    return hipStreamSynchronize(st);
 }
 
 int grid_rows(int64_t n, int per_block) {
@@ -1886,7 +2026,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         }
         case PCX_M_SCORES:
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
-            if (m.algorithm == 0 && m.wcd && m.rowpart)  // PCA: wcd and the row counts are ready (PCX_M_COV)
+            if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && m.wcd && m.rowpart)  // wcd ready (PCX_M_COV)
                 hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             else
                 hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
@@ -1902,7 +2042,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case PCX_M_DECIDE:
             hipLaunchKernelGGL(k_decide_prep, dim3(ceb), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
+            if (m.algorithm == 0) hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), 0, st, m);
             break;
         case PCX_M_REPU:
@@ -2050,6 +2190,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (m.original || m.filled)
                 hipLaunchKernelGGL(k_matrices, dim3(grid_rows(m.n_rows * m.n_events, BT)), dim3(BT), 0, st, m);
             break;
+        case PCX_M_EIG:
+            if (m.algorithm != 2 && m.algorithm != 3) break;
+            return eig_stage(m, st, err);
         case 99:  // "absolute": no loading
             hipLaunchKernelGGL(k_zero_loading, dim3(1), dim3(256), 0, st, m);
             break;

@@ -26,9 +26,11 @@ NO, YES, BAD, NA = 1.0, 2.0, 1.5, 0.0  # __init__.py:65-68
 class Oracle(object):
     """``Oracle(reports, event_bounds, reputation, ...).consensus()`` on the GPU.
 
-    Supported ``algorithm`` values: ``"PCA"`` (default, the hot path) and
+    Supported ``algorithm`` values: ``"PCA"`` (default, the hot path), ``"big-five"``
+    and ``"fixed-variance"`` (eigenvalue-weighted component scores, :373-390,
+    :429-451), ``"cokurtosis"`` (``aux["cokurt"]`` scores, :455-457) and
     ``"absolute"`` (the reference's unimplemented branch: uniform this_rep,
-    __init__.py:359-362).  The other reference algorithms raise
+    :359-362).  ``"k-means"``, ``"hierarchical"`` and ``"clusterfeck"`` raise
     NotImplementedError (scope).
     """
 
@@ -100,33 +102,45 @@ class Oracle(object):
 
     def consensus(self):
         if self.algorithm not in _abi.ALGORITHMS:
-            raise NotImplementedError("algorithm %r: only 'PCA' (and 'absolute') run on the GPU path"
-                                      % (self.algorithm,))
+            raise NotImplementedError("algorithm %r is not on the GPU path (supported: %s)"
+                                      % (self.algorithm, ", ".join(sorted(_abi.ALGORITHMS))))
         sc, lo, hi = self._bounds_arrays()
         N, E = self.num_reports, self.num_events
+        aux = None
+        if self.algorithm == "cokurtosis":
+            aux = np.asarray(self.aux["cokurt"], dtype=np.float64).ravel()  # :456
+            if aux.size != N:
+                raise ValueError("aux['cokurt'] must hold one score per reporter")
+        kw = dict(catch_tolerance=self.catch_tolerance, alpha=self.alpha, int_dtype=self._int_dtype,
+                  algorithm=self.algorithm, device=self.device, max_components=self.max_components,
+                  variance_threshold=self.variance_threshold)
         if N <= MAX_REPORTERS and E <= MAX_EVENTS:
             out = consensus_batched(self._data[None], None if self._rep_raw is None else self._rep_raw[None],
-                                    sc, lo, hi, catch_tolerance=self.catch_tolerance, alpha=self.alpha,
-                                    int_dtype=self._int_dtype, algorithm=self.algorithm,
-                                    device=self.device, filled=True, original=True)
+                                    sc, lo, hi, filled=True, original=True,
+                                    aux_scores=None if aux is None else aux[None], **kw)
             g = {k: v[0].cpu().numpy() for k, v in out.items() if not k.startswith("_")}
             participation = float(g["participation"])
             avg_certainty = float(g["avg_certainty"])
+            comps = int(g["components"])
             self.last_info = {"branch": int(g["branch"]), "flags": int(g["flags"]),
                               "pi_iters": int(g["pi_iters"]), "path": "batched"}
         else:
             from .pipeline import consensus_matrix
 
-            ev, ag, meta = consensus_matrix(self._data, self._rep_raw, sc, lo, hi,
-                                            catch_tolerance=self.catch_tolerance, alpha=self.alpha,
-                                            int_dtype=self._int_dtype, algorithm=self.algorithm,
-                                            device=self.device, matrices=True, n_total=N, row_offset=0)
+            ev, ag, meta = consensus_matrix(self._data, self._rep_raw, sc, lo, hi, matrices=True, n_total=N,
+                                            row_offset=0, aux_scores=aux, **kw)
             g = {k: v.cpu().numpy() for k, v in list(ev.items()) + list(ag.items())}
             participation = float(meta["participation"])
             avg_certainty = float(meta["avg_certainty"])
+            comps = int(meta["components"])
             self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
                               "path": "matrix"}
-        self.convergence = self.algorithm == "PCA"  # :483, :499
+        if self.algorithm in ("big-five", "fixed-variance") and self.last_info["flags"] & _abi.FLAG_SVD_FAIL:
+            # the reference's second svd (:375, :431) is outside the try of :329-333
+            raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")
+        if self.algorithm == "fixed-variance":
+            self.num_components = comps  # :449
+        self.convergence = self.algorithm != "absolute"  # nonconformity(_rank) set it (:483, :499)
         return self._result(g, participation, avg_certainty)
 
     def _result(self, g, participation, avg_certainty):
@@ -140,7 +154,12 @@ class Oracle(object):
         self.reports = np.ma.masked_array(original, self.reports.mask)
         ints = self._int_dtype
         cnt = (lambda a: [int(x) for x in a]) if ints else (lambda a: [float(x) for x in a])
-        ma = np.ma.masked_array
+        # PCA's reputation vectors and scores are MaskedArrays (the masked first loading
+        # propagates, :336-337); the other algorithms produce plain ndarrays
+        ma = np.ma.masked_array if self.algorithm == "PCA" else np.asarray
+        scores = g["scores"]
+        if self.algorithm == "cokurtosis":
+            scores = self.aux["cokurt"]  # returned as given (:457)
         outcomes_adj = [float(x) for x in g["outcomes_adjusted"]]
         return {
             "original": original,
@@ -153,7 +172,7 @@ class Oracle(object):
                 "participation_rows": [float(x) for x in g["participation_rows"]],
                 "relative_part": [float(x) for x in g["relative_part"]],
                 "reporter_bonus": [float(x) for x in g["reporter_bonus"]],
-                "scores": ma(g["scores"]),
+                "scores": ma(scores) if self.algorithm != "cokurtosis" else scores,
             },
             "events": {
                 "adj_first_loadings": [float(x) for x in g["adj_first_loadings"]],

@@ -141,7 +141,7 @@ class MatWorkspace:
         self.tokp = t.empty((self.wcd_rows + 64,), dtype=f64, device=device)
         self.rowpart = t.empty(((self.wcd_ld + 511) // 512, self.wcd_rows, 2), dtype=t.int32, device=device)
         self.C = z(E, E)
-        self.Mw = z(2, E, E)
+        self.Mw = z(2 * E * E + 8 * E + 64)  # power-iteration matrices; PCX_M_EIG scratch
         self.pvec = z(4, E + 64)
         self.rowv = z(6, n_rows)
         self.rowstat = z(n_rows, 2, dt=t.int32)
@@ -205,7 +205,8 @@ def clear_workspace_cache():
 
 def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, catch_tolerance=0.1,
                      alpha=0.1, int_dtype=False, algorithm="PCA", comm=None, n_total=None,
-                     row_offset=None, device=None, matrices=False, profile=None):
+                     row_offset=None, device=None, matrices=False, profile=None, max_components=5,
+                     variance_threshold=0.9, aux_scores=None):
     """Consensus of one report matrix on the GPU(s).
 
     reports:    this rank's rows, (n_rows, E) float64 (torch tensor on the GPU, or numpy)
@@ -215,6 +216,8 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     matrices:   also return this rank's rescaled ("original") and filled reports
     profile:    optional dict; receives per-stage device milliseconds (HIP events on the
                 launching stream) under the stage names of include/pcx.h
+    algorithm:  "PCA", "absolute", "big-five" (max_components, capped at E), "fixed-variance"
+                (variance_threshold), "cokurtosis" (aux_scores: this rank's rows of aux["cokurt"])
 
     Returns (events, agents, info): event-level tensors (identical on every rank),
     this rank's per-reporter tensors, and a dict of scalars/diagnostics.
@@ -246,18 +249,27 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     alg = _abi.ALGORITHMS.get(algorithm)
     if alg is None:
         raise NotImplementedError("algorithm %r is not on the GPU path" % (algorithm,))
+    aux = None
+    if alg == _abi.ALG_COKURTOSIS:
+        if aux_scores is None:
+            raise ValueError("cokurtosis needs aux_scores (this rank's rows of aux['cokurt'])")
+        aux = _device.as_device(aux_scores, t.float64, dev).reshape(-1)
+        if aux.numel() != n_rows:
+            raise ValueError("aux_scores must hold this rank's %d rows" % n_rows)
+    algo = (alg, int(max_components) if E >= int(max_components) else E, float(variance_threshold), aux)
 
     ws = _workspace(n_rows, E, n_scaled, comm.world, comm.rank, dev)
     try:
-        return _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev, catch_tolerance,
+        return _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, algo, comm, dev, catch_tolerance,
                     alpha, int_dtype, matrices, profile)
     finally:
         ws._busy = False
 
 
-def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev, catch_tolerance, alpha,
+def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, algo, comm, dev, catch_tolerance, alpha,
          int_dtype, matrices, profile):
     t = _device.torch()
+    alg, max_components, variance_threshold, aux = algo
     n_rows, E = R.shape
     out, scalars = ws.new_outputs()
     m = _abi.Mat()
@@ -267,6 +279,8 @@ def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev,
     m.n_scaled, m.sel_phase, m.col_blocks = n_scaled, 1, ws.col_blocks
     m.cov_tiles, m.cov_kslices = ws.cov_tiles, ws.cov_kslices
     m.wcd_rows, m.wcd_ld = ws.wcd_rows, ws.wcd_ld
+    m.max_components, m.components, m.variance_threshold = max_components, -1, variance_threshold
+    m.aux_scores = _device.ptr(aux)
     P = _device.ptr
     m.reports, m.scaled, m.lo, m.hi, m.rep_raw = P(R), P(sc), P(lo_), P(hi_), P(rep)
     m.scaled_cols, m.scaled_index = P(scols), P(sidx)
@@ -313,21 +327,24 @@ def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev,
     stage(_abi.M_GUESS)
     _select(stage, m, ws, comm, phase=1)                 # scaled fills: weighted median (:300-303)
     stage(_abi.M_MEAN)
-    pca = alg == 0
-    if pca:
+    pca = alg == _abi.ALG_PCA
+    wpca = alg in (_abi.ALG_PCA, _abi.ALG_BIG_FIVE, _abi.ALG_FIXED_VARIANCE)
+    if wpca:
         # a6: covariance on fp64 MFMA (:326), a7: power iteration (:330-336)
         stage(_abi.M_COV)
         stage(_abi.M_COV_REDUCE)
         comm.all_reduce_sum(ws.C)
         stage(_abi.M_COV_FINISH)
         stage(_abi.M_POWER)
+        if not pca:  # big-five / fixed-variance components (:373-390, :429-451)
+            stage(_abi.M_EIG)
     else:
         stage(_abi.M_ZERO_LOADING)
     comm.clear_slots(ws.skey)
     stage(_abi.M_SCORES)
     comm.reduce_slots(ws.skey)
-    if pca:
-        # a8/a9: sign-choice rule (:487-500)
+    if alg != _abi.ALG_ABSOLUTE:
+        # a8/a9: sign-choice rule (:487-500; the other algorithms: nonconformity, :475-485)
         comm.clear_slots(ws.scal, (S(2, 6),))
         stage(_abi.M_NCSUMS)
         comm.reduce_slots(ws.scal, (S(2, 6),))
@@ -367,8 +384,9 @@ def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, alg, comm, dev,
     agents = {k: out[k] for k in _abi.MAT_OUTPUT_AGENTS}
     agents.update(mats)
     meta = {"participation": scal[0], "avg_certainty": scal[1],
-            "branch": int(info[_abi.INFO_BRANCH]) if pca else _abi.BRANCH_NONE,
-            "pi_iters": int(info[_abi.INFO_PI_ITERS]), "flags": int(info[_abi.INFO_FLAGS]) if pca else 0,
+            "branch": int(info[_abi.INFO_BRANCH]) if alg != _abi.ALG_ABSOLUTE else _abi.BRANCH_NONE,
+            "pi_iters": int(info[_abi.INFO_PI_ITERS]), "flags": int(info[_abi.INFO_FLAGS]) if wpca else 0,
+            "components": int(m.components),
             "filled_guess": ws.ev[0].clone(), "workspace": ws, "inputs": (R, rep, sc, lo_, hi_)}
     return events, agents, meta
 

@@ -29,7 +29,8 @@ def test_library_exports_every_declared_symbol():
     h = _lib.lib()
     missing = [n for n in declared_functions() if not hasattr(h, n)]
     assert not missing, missing
-    assert h.pcx_abi_version() == 1
+    from pyconsensus_amd import _abi
+    assert h.pcx_abi_version() == _abi.ABI_VERSION
 
 
 def test_struct_layout_matches_header():

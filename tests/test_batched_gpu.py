@@ -97,13 +97,15 @@ def test_bitexact_vs_c_oracle_c3(gpu_lib):
 
 
 @pytest.mark.parametrize("variant", ["uniform_rep", "shared_bounds", "no_bounds", "int_dtype",
-                                     "absolute", "E1", "N1", "N64_E32"])
+                                     "absolute", "E1", "N1", "N64_E32", "big-five", "fixed-variance",
+                                     "cokurtosis", "big-five_E7", "fixed-variance_N64_E32"])
 def test_variants_bitexact_vs_c_oracle(gpu_lib, variant):
     from oracle import pcx_oracle_c as OC
     from pyconsensus_amd import synthetic
     from pyconsensus_amd.batched import consensus_batched
 
-    N, E = {"E1": (30, 1), "N1": (1, 6), "N64_E32": (64, 32)}.get(variant, (50, 20))
+    N, E = {"E1": (30, 1), "N1": (1, 6), "N64_E32": (64, 32), "big-five_E7": (40, 7),
+            "fixed-variance_N64_E32": (64, 32)}.get(variant, (50, 20))
     R, sc, lo, hi, rep = synthetic.rounds(512, N, E, seed=5)
     kw = dict(reputation=rep, scaled=sc, lo=lo, hi=hi)
     if variant == "uniform_rep":
@@ -117,6 +119,13 @@ def test_variants_bitexact_vs_c_oracle(gpu_lib, variant):
         kw["int_dtype"] = True
     if variant == "absolute":
         kw["algorithm"] = "absolute"
+    alg = variant.split("_")[0]
+    if alg in ("big-five", "fixed-variance", "cokurtosis"):
+        kw["algorithm"] = alg
+        kw["max_components"] = 5
+        kw["variance_threshold"] = 0.75
+    if alg == "cokurtosis":
+        kw["aux_scores"] = np.random.default_rng(9).normal(size=(R.shape[0], N))
     g = _np(consensus_batched(R, filled=True, original=True, **kw))
     c = OC.batched(R, **kw, threads=8)
     for k, v in g.items():
