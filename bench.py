@@ -112,19 +112,20 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
             "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
             "branch": meta["branch"], "pi_iters": meta["pi_iters"], "flags": meta["flags"],
             "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
-            "roofline_cov": {"bound": "mfma", "kernel": "k_cov", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
+            "roofline_cov": {"bound": "mfma", "kernel": "k_syrk", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
                              "unit": "TFLOP/s", "frac": (tfs / FP64_MFMA_PEAK_TFS) if tfs else None,
-                             "flops_per_launch": cov_flops_rank},
+                             "flops_per_launch": cov_flops_rank, "traffic": load_traffic("k_syrk")},
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}
 
 
-def load_traffic():
-    """Per-launch HBM bytes from the committed rocprofv3 PMC pass (profiles/), or None."""
+def load_traffic(kernel="batched_round_kernel"):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, tools/gpu_profile.sh), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        return d.get("batched_round_kernel", {}).get("bytes_per_launch")
+        return d.get(kernel, {}).get("bytes_per_launch")
     except Exception:
         return None
 

@@ -151,7 +151,7 @@ enum pcx_mat_stage_id {
     PCX_M_COLSTATS = 2,      /* rescale + NA + present sums per event (:266-299)     */
     PCX_M_GUESS = 3,         /* binary fills (:304-309), median setup (:300-303)     */
     PCX_M_MEAN = 4,          /* weighted mean mu, old = rep . F (:317-319, 490)     */
-    PCX_M_COV = 5,           /* token-weighted covariance partial tiles, fp64 MFMA (:326) */
+    PCX_M_COV = 5,           /* token-weighted covariance partial tiles, fp64 MFMA (:326); needs PCX_M_WCD */
     PCX_M_COV_REDUCE = 6,    /* sum split-K slabs into this rank's partial C         */
     PCX_M_COV_FINISH = 7,    /* C = partial / (sum tokens - 1), symmetric            */
     PCX_M_POWER = 8,         /* leading eigenvector by power iteration (:330-336)    */
@@ -176,6 +176,7 @@ enum pcx_mat_stage_id {
     PCX_M_SEL_STEP = 35,     /*   narrow the range; converged columns get their result */
     PCX_M_SEL_FINISH = 36,   /*   results into guess (phase 1) / outcomes_raw (phase 2) */
     PCX_M_SEL_EXACT = 37,    /* weighted median replayed with the reference's float order (n <= 8192, 1 rank) */
+    PCX_M_WCD = 39,          /* wcd = F - mu materialised once (:317-322), row NaN/zero counts */
     PCX_M_EIG = 38,          /* big-five / fixed-variance: eigenpairs of C (svd, :375, :431), the
                                 eigenvalue-weighted component sum (:377-382, :435-449) -> score vector */
     PCX_M_ZERO_LOADING = 99, /* no wpca ("absolute", "cokurtosis"): first_loading = 0 (:359)          */

@@ -66,6 +66,7 @@ M_SCALED_CERT, M_FINAL, M_ROWSUMS, M_AGENTS, M_MATRICES = 17, 18, 19, 20, 21
 M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH = 30, 31, 32, 33, 34, 35, 36
 M_SEL_EXACT = 37
 M_EIG = 38
+M_WCD = 39
 SEL_EXACT_MAX = 8192
 M_ZERO_LOADING = 99
 

@@ -18,6 +18,7 @@
 //   entry phase  lane o = matrix entry o  (covariance, matrix squaring)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "pcx_internal.h"
 
@@ -1244,7 +1245,13 @@ size_t batched_lds_bytes(int N, int E) {
 }
 
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
-    const size_t lds = batched_lds_bytes(a.N, a.E);
+    // PCX_BATCHED_LDS_PAD (diagnostic): extra dynamic LDS bytes per round, to measure
+    // throughput against resident rounds per CU (tools/occupancy_batched.py)
+    static const size_t pad = [] {
+        const char* e = getenv("PCX_BATCHED_LDS_PAD");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+    }();
+    const size_t lds = batched_lds_bytes(a.N, a.E) + pad;
     if (a.B <= 0) return hipSuccess;
     if (a.N == 50 && a.E == 20 && a.ES == 21)
         hipLaunchKernelGGL((batched_round_kernel<50, 20>), dim3((unsigned)a.B), dim3(64), lds, stream, a);

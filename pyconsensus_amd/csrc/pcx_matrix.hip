@@ -498,12 +498,13 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
 // PCX_M_COV step 2: partial C = wcd^T diag(tok) wcd (:326) over one row slice, one
 // 128x128 lower-triangle tile per workgroup on fp64 MFMA.  Rows arrive by
 // global_load_lds_dwordx4 (one 1 KB tile row per wave instruction) into a two-stage
-// LDS ring of 16-row stages; one raw barrier per stage, counted vmcnt (the only
-// vector-memory ops in the loop are these DMAs).  75 KB LDS + 208 VGPRs = 2
-// workgroups (2 waves per SIMD) per CU: one wave alone issues an f64 MFMA only every
-// ~128 cycles, two interleave to the 64-cycle rate (tools/covbench, profiles/).
+// LDS ring of 8-row stages; one raw barrier per stage, counted vmcnt (the only
+// vector-memory ops in the loop are these DMAs).  39 KB LDS and <= 168 VGPRs
+// (launch bounds) = 3 workgroups (3 waves per SIMD) per CU: one wave alone issues an
+// f64 MFMA only every ~128 cycles, several interleave to the 64-cycle rate.  Variant
+// sweep (BK, ring depth, waves per SIMD, 8-wave tiles): tools/covbench, profiles/r1.
 // The A operand is rounded as tok*w before the MFMA (np.ma.multiply(wcd.T, tokens)).
-constexpr int SY_BK = 16;                       // rows per stage
+constexpr int SY_BK = 8;                        // rows per stage
 constexpr int SY_NBUF = 2;                      // LDS ring depth
 constexpr int SY_LDP = CT + 16;                 // padded LDS row: conflict-free b64 fragment reads
 
@@ -599,7 +600,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 }
 
 // one work item = (lower-triangle tile (I,J), row slice ks) -> cslab[ks] (lower part)
-__global__ void __launch_bounds__(256) k_syrk(pcx_mat m) {
+__global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
     extern __shared__ __attribute__((aligned(16))) double sy_lds[];
     const int E = (int)m.n_events;
     const int ntiles = m.cov_tiles, nks = m.cov_kslices;
@@ -1995,15 +1996,20 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case PCX_M_MEAN:
             hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
             break;
+        case PCX_M_WCD:
         case PCX_M_COV: {
             if (!m.wcd || !m.tokp || !m.rowpart || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
                 m.wcd_ld < m.n_events) {
                 err = "PCX_M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
                 return hipErrorInvalidValue;
             }
-            const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
-            hipLaunchKernelGGL(k_wcd, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(m.wcd_rows, 4096 / ncb)), ncb),
-                               dim3(BT), 0, st, m);
+            if (stage == PCX_M_WCD) {
+                const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
+                hipLaunchKernelGGL(k_wcd,
+                                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(m.wcd_rows, 4096 / ncb)), ncb),
+                                   dim3(BT), 0, st, m);
+                break;
+            }
             static bool lds_set = false;
             if (!lds_set) {
                 hipError_t e = hipFuncSetAttribute((const void*)k_syrk, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -121,9 +121,9 @@ class MatWorkspace:
         # covariance operand wcd, materialised [wcd_rows][wcd_ld] (16-row stages, 128-col tiles)
         self.wcd_rows = (n_rows + COV_STAGE - 1) // COV_STAGE * COV_STAGE
         self.wcd_ld = nb * COV_TILE
-        # row slices: >= ~16 workgroups per CU slot (2 per CU), each slice >= 8 stages
+        # row slices: >= ~16 workgroups per CU slot (3 per CU), each slice >= 8 stages
         stages = self.wcd_rows // COV_STAGE
-        ks = -(-16 * 2 * 256 // self.cov_tiles)
+        ks = -(-16 * 3 * 256 // self.cov_tiles)
         self.cov_kslices = max(1, min(32, ks, stages // 8 if stages >= 8 else 1))
         z = lambda *shape, dt=f64: t.zeros(shape, dtype=dt, device=device)
         self.rep = z(n_rows)
@@ -330,7 +330,8 @@ def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, algo, comm, dev
     pca = alg == _abi.ALG_PCA
     wpca = alg in (_abi.ALG_PCA, _abi.ALG_BIG_FIVE, _abi.ALG_FIXED_VARIANCE)
     if wpca:
-        # a6: covariance on fp64 MFMA (:326), a7: power iteration (:330-336)
+        # a5: wcd materialised (:322); a6: covariance on fp64 MFMA (:326); a7: power iteration (:330-336)
+        stage(_abi.M_WCD)
         stage(_abi.M_COV)
         stage(_abi.M_COV_REDUCE)
         comm.all_reduce_sum(ws.C)

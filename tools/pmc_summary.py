@@ -14,12 +14,23 @@ import json
 import statistics
 
 
+def kname(full):
+    """Short kernel name: drop namespaces, template arguments and the parameter list."""
+    s = full.replace("(anonymous namespace)::", "")
+    return s.split("(")[0].split("<")[0].split("::")[-1].split(" ")[-1]
+
+
+def ours(full):
+    """Only libpcx kernels (torch's own fill/copy kernels of the bench setup are left out)."""
+    return "pcx::" in full
+
+
 def per_kernel(path, counter):
     out = {}
     for r in csv.DictReader(open(path)):
-        if r.get("Counter_Name") != counter:
+        if r.get("Counter_Name") != counter or not ours(r["Kernel_Name"]):
             continue
-        name = r["Kernel_Name"].split("(")[0].split("::")[-1]
+        name = kname(r["Kernel_Name"])
         out.setdefault(name, []).append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in out.items()}
 
@@ -42,7 +53,9 @@ def main():
                   "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide reads)"}
     if a.stats:
         for r in csv.DictReader(open(a.stats)):
-            k = r["Name"].split("(")[0].split("::")[-1]
+            if not ours(r["Name"]):
+                continue
+            k = kname(r["Name"])
             res.setdefault(k, {})["avg_ns"] = float(r["AverageNs"])
             res[k]["calls"] = int(r["Calls"])
     if a.note:
