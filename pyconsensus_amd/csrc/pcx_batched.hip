@@ -413,54 +413,77 @@ __device__ __forceinline__ double rank_avg(const double* v, int E) {
 
 struct Smem {
     double* F;      // [N][ES] rescaled, then filled reports
-    double* C;      // [E][ES] covariance
-    double* M;      // [E][ES] power-iteration working matrix
-    double* rep;    // [64]
-    double* tok;    // [64]
-    double* s;      // [64] scores
-    double* n1;     // [64] normalize(set1)
-    double* n2;     // [64] normalize(set2)
-    double* smooth; // [64]
-    double* sx;     // [64] scratch
-    double* sw;     // [64] scratch
-    double* scr;    // [64] scratch
-    double* mu;     // [32]
-    double* guess;  // [32]
-    double* x;      // [32] power-iteration vector
-    double* ld;     // [32] loading
-    double* old;    // [32]
-    double* nv1;    // [32]
-    double* nv2;    // [32]
-    double* adj;    // [32]
-    uint64_t* nanm; // [32] bit i = report (i, j) is NaN
-    uint64_t* zerm; // [32] bit i = report (i, j) == 0.0
+    double* C;      // [E][ES] covariance (phase aliases: see carve)
+    double* M;      // [max(E*ES, 128)] power-iteration / Jacobi working matrix
+    double* rep;    // [N]
+    double* tok;    // [N]
+    double* n1;     // [N] normalize(set1) (aliases C)
+    double* n2;     // [N] normalize(set2) (aliases C)
+    double* smooth; // [N] (aliases C)
+    double* sx;     // [64] median scratch (aliases M)
+    double* sw;     // [64] median scratch (aliases M + 64)
+    double* scr;    // [48] Jacobi rotation parameters (aliases tok)
+    double* mu;     // [E]
+    double* guess;  // [E] (aliases C)
+    double* x;      // [E] power-iteration vector
+    double* ld;     // [E] loading
+    double* old;    // [E]
+    double* nv1;    // [E]
+    double* nv2;    // [E]
+    double* adj;    // [E] (aliases C)
+    uint64_t* nanm; // [E] bit i = report (i, j) is NaN
+    uint64_t* zerm; // [E] bit i = report (i, j) == 0.0
 };
 
+// LDS per round, by phase.  The kernel is latency bound: throughput scales with the
+// rounds resident per CU (tools/occupancy_batched.py), and LDS is what bounds them, so
+// vectors whose lifetimes do not overlap the matrices' share their space:
+//   C  (covariance, Jacobi V) is live from the covariance to the scores only; before
+//      it holds guess (interpolation), after it n1 | n2 | smooth | adj;
+//   M  (squared matrix, Jacobi A) is dead in both median phases: sx | sw live there;
+//   tok is dead after the covariance: the Jacobi rotation parameters (scr) reuse it.
+// Per-row vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20:
+// 17.2 KB, nine rounds per CU.
+__host__ __device__ inline int smem_rows(int N) { return (N + 1) & ~1; }
+__host__ __device__ inline int smem_evs(int E) { return (E + 1) & ~1; }
+__host__ __device__ inline int smem_c_size(int N, int E, int ES) {
+    const int need = 3 * smem_rows(N) + smem_evs(E);
+    return E * ES > need ? E * ES : need;
+}
+__host__ __device__ inline int smem_m_size(int E, int ES) { return E * ES > 128 ? E * ES : 128; }
+__host__ __device__ inline int smem_tok_size(int N) { return smem_rows(N) > 48 ? smem_rows(N) : 48; }
+
+__host__ __device__ inline size_t smem_doubles(int N, int E, int ES) {
+    return (size_t)N * ES + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + smem_tok_size(N) +
+           8 * (size_t)smem_evs(E);
+}
+
 __device__ Smem carve(double* base, int N, int E, int ES) {
+    const int nr = smem_rows(N), ne = smem_evs(E);
     Smem s;
     double* p = base;
     s.F = p; p += N * ES;
-    s.C = p; p += E * ES;
-    s.M = p; p += E * ES;
-    s.rep = p; p += 64;
-    s.tok = p; p += 64;
-    s.s = p; p += 64;
-    s.n1 = p; p += 64;
-    s.n2 = p; p += 64;
-    s.smooth = p; p += 64;
-    s.sx = p; p += 64;
-    s.sw = p; p += 64;
-    s.scr = p; p += 64;
-    s.mu = p; p += 32;
-    s.guess = p; p += 32;
-    s.x = p; p += 32;
-    s.ld = p; p += 32;
-    s.old = p; p += 32;
-    s.nv1 = p; p += 32;
-    s.nv2 = p; p += 32;
-    s.adj = p; p += 32;
-    s.nanm = reinterpret_cast<uint64_t*>(p); p += 32;
-    s.zerm = reinterpret_cast<uint64_t*>(p); p += 32;
+    s.C = p; p += smem_c_size(N, E, ES);
+    s.M = p; p += smem_m_size(E, ES);
+    s.rep = p; p += nr;
+    s.tok = p; p += smem_tok_size(N);
+    s.mu = p; p += ne;
+    s.x = p; p += ne;
+    s.ld = p; p += ne;
+    s.old = p; p += ne;
+    s.nv1 = p; p += ne;
+    s.nv2 = p; p += ne;
+    s.nanm = reinterpret_cast<uint64_t*>(p); p += ne;
+    s.zerm = reinterpret_cast<uint64_t*>(p); p += ne;
+    // phase aliases (see above)
+    s.guess = s.C;
+    s.n1 = s.C;
+    s.n2 = s.C + nr;
+    s.smooth = s.C + 2 * nr;
+    s.adj = s.C + 3 * nr;
+    s.sx = s.M;
+    s.sw = s.M + 64;
+    s.scr = s.tok;
     return s;
 }
 
@@ -543,7 +566,7 @@ __device__ __forceinline__ void jac_pair(int i, int r, int n, int& p, int& q) {
 }
 
 // A (E x E, row stride ES) -> eigenvalues on its diagonal; V -> eigenvectors (columns).
-// prm: 64 doubles of LDS (rotation cosines at [0, 32), sines at [32, 64)).
+// prm: 48 doubles of LDS (rotation cosines at [0, npair), sines at [32, 32 + npair), npair <= 16).
 __device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm) {
     const int l = lane_id();
     for (int o = l; o < E * E; o += W) {
@@ -623,7 +646,7 @@ __device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm
 // the sequential column/row loops unroll and their LDS reads issue ahead of the
 // dependent adds.  NT = ET = 0: any N <= 64, E <= 32 at run time.  Same arithmetic.
 template <int NT, int ET>
-__global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
+__global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? (ET | 1) : a.ES;
     const int l = lane_id();
@@ -1031,7 +1054,6 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
         if (row) {
             S.n1[l] = a1 / S1;
             S.n2[l] = a2 / S2;
-            S.s[l] = sc_i;
         }
         wsync();
         double d1 = 0.0, d2 = 0.0;
@@ -1240,8 +1262,7 @@ __global__ void __launch_bounds__(64) batched_round_kernel(BatchArgs a) {
 
 size_t batched_lds_bytes(int N, int E) {
     const int ES = E | 1;
-    const size_t doubles = (size_t)N * ES + 2 * (size_t)E * ES + 9 * 64 + 8 * 32 + 2 * 32;
-    return doubles * sizeof(double);
+    return smem_doubles(N, E, ES) * sizeof(double);
 }
 
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
