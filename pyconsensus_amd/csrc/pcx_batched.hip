@@ -251,21 +251,29 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
     return bcast(res, 0);
 }
 
-// The same weighted median as wave_wmedian, without LDS scratch or a serial lane:
-//  * rank: every selected lane counts the selected pairs before it in the total order
-//    (x, w, lane) -- exactly the stable (x, w) rank -- against wave-uniform broadcasts
-//    (readlane), one pass over the rows;
-//  * ds_permute moves each pair to lane = rank (unselected lanes fill the tail);
-//  * the left-to-right cumulative weight runs as a DPP wave_shr chain: after t steps
-//    lanes 0..t hold the sequential sums cum_1..cum_{t+1} (already-final lanes recompute
-//    the same value), so it is the SPEC's sequential sum bit for bit;
-//  * the crossing is the first lane with cum > mid; `before` is the same subtraction.
+// The same weighted median as wave_wmedian, with the sort and the walk spread over
+// the wave:
+//  * rank: every selected lane counts the selected pairs strictly below its own in
+//    the (x, w) order, one LDS-broadcast pass over the rows (unselected rows hold
+//    (+inf, +inf), which no selected pair exceeds, so they need no mask);
+//  * compare-equal pairs share that count; an LDS atomic on a per-rank counter
+//    spreads them over [r, r + d).  Equal pairs are bitwise equal here (x and w are
+//    never +-0 with equal partners: zero reports are missing), so their order cannot
+//    change the walk;
+//  * each pair is scattered to its rank (ox, ow), and the cumulative weight runs
+//    left to right, four broadcast loads per step group, stopping at the first
+//    cum > mid: the SPEC's sequential sums bit for bit; `before` is the same subtraction.
 // NaN keys have no total order: rounds with a NaN among the selected pairs take
 // wave_wmedian.  NR = compile-time row count bound (64 when the shape is dynamic).
+// scr: MED_SCR doubles of LDS (sx | sw | ox | ow | 64 int counters).
+constexpr int MED_SCR = 288;
+
 template <int NR>
-__device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* sx, double* sw,
-                                    long long* prof = nullptr) {
+__device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
+                                                    long long* prof = nullptr) {
     const int l = lane_id();
+    double *sx = scr, *sw = scr + 64, *ox = scr + 128, *ow = scr + 192;
+    int* cnt = reinterpret_cast<int*>(scr + 256);
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
     const double mid = 0.5 * Wtot;
     const uint64_t dom = ballot(sel && w > mid);
@@ -276,123 +284,69 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     }
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
     if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
-    const uint64_t selm = ballot(sel);
-    const int n = popc(selm);
-    // every lane publishes its pair; the comparisons read them back as LDS broadcasts
+    const int n = popc(ballot(sel));
     wsync();
     sx[l] = sel ? x : __builtin_inf();
     sw[l] = sel ? w : __builtin_inf();
+    cnt[l] = 0;
     wsync();
     int r = 0;
-    // straight-line body (no per-row branch, non-short-circuit logic) so the broadcast
-    // reads issue ahead of the compares; unselected rows are masked by selm
 #pragma unroll
     for (int m = 0; m < NR; m++) {
+        if (NR == 64 && m >= N) break;
         const double xm = sx[m], wm = sw[m];
-        const bool lt = (xm < x) | ((xm == x) & ((wm < w) | ((wm == w) & (m < l))));
-        r += (lt & (bool)((selm >> m) & 1)) ? 1 : 0;
+        r += ((xm < x) | ((xm == x) & (wm < w))) ? 1 : 0;
     }
-    const uint64_t unsel = ~selm;
-    const int upos = __builtin_amdgcn_mbcnt_hi((uint32_t)(unsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)unsel, 0));
-    const int dst = sel ? r : n + upos;
-    const double kx = permute_d(dst, x);
-    const double kw = permute_d(dst, w);
+    if (sel) {
+        const int slot = r + atomicAdd(&cnt[r], 1);
+        ox[slot] = x;
+        ow[slot] = w;
+    }
+    wsync();
     if (prof) {
         const long long t1 = (long long)__builtin_amdgcn_s_memtime();
         prof[0] += t1 - t0;
         prof[2] = t1;
     }
-    double cum = l == 0 ? 0.0 + kw : 0.0;
-    for (int t = 1; t < n; t++) cum = shr1_d(cum) + kw;  // after step t lanes 0..t are final
-    const uint64_t over = ballot(l < n && cum > mid);
+    // wave-uniform walk: cum_k = (((0 + w_0) + w_1) + ... + w_{k-1}), eight sorted
+    // weights per step group as LDS broadcasts, the next group's loads issued before
+    // the current group's dependent adds
+    double cum = 0.0, before = 0.0;
+    int k = 0;
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = ow[q];
+    for (int t = 0; t < n; t += 8) {
+        double nv[8], c[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) nv[q] = ow[(t + 8 + q) & 63];
+        c[0] = cum + v[0];
+#pragma unroll
+        for (int q = 1; q < 8; q++) c[q] = c[q - 1] + v[q];
+        int hit = 8;
+#pragma unroll
+        for (int q = 7; q >= 0; q--)
+            if (t + q < n && c[q] > mid) hit = q;
+        if (hit < 8) {
+            k = t + hit + 1;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (q == hit) before = c[q] - v[q];
+            break;
+        }
+        cum = c[7];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = nv[q];
+    }
     if (prof) prof[1] += (long long)__builtin_amdgcn_s_memtime() - prof[2];
-    if (!over) return __builtin_nan("");
-    const int k = __builtin_ctzll(over) + 1;  // items summed when the walk stops
-    const double before = readlane_d(cum, k - 1) - readlane_d(kw, k - 1);
+    if (!k) return __builtin_nan("");
     if (fabs(before - mid) < DBL_EPS) {
-        if (k >= 2) return (readlane_d(kx, k - 2) + readlane_d(kx, k - 1)) / 2.0;
-        return n == 1 ? readlane_d(kx, 0) / 1.0 : __builtin_nan("");
+        if (k >= 2) return (ox[k - 2] + ox[k - 1]) / 2.0;
+        return n == 1 ? ox[0] / 1.0 : __builtin_nan("");
     }
-    return readlane_d(kx, k - 1);
+    return ox[k - 1];
 }
 
-// K independent weighted medians at once (same steps as wave_wmedian_rank, the K
-// instruction streams interleaved so their dependent latencies overlap).  Only for
-// "regular" medians -- no dominant weight, some positive weight, no NaN -- which the
-// caller checks with wmedian_regular().  scr: K x 128 doubles of LDS scratch.
-__device__ __forceinline__ bool wmedian_regular(double x, double w, bool sel, double Wtot) {
-    const double mid = 0.5 * Wtot;
-    return !ballot(sel && w > mid) && ballot(sel && w > 0.0) &&
-           !ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)));
-}
-
-template <int NR, int K>
-__device__ __forceinline__ void wave_wmedian_rank_k(const double (&x)[K], const double (&w)[K], const bool (&sel)[K],
-                                                    const double (&Wtot)[K], double* scr, double (&out)[K],
-                                                    long long* prof = nullptr) {
-    const int l = lane_id();
-    const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    uint64_t selm[K];
-    int n[K], r[K];
-    wsync();
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        selm[k] = ballot(sel[k]);
-        n[k] = popc(selm[k]);
-        r[k] = 0;
-        scr[k * 128 + l] = sel[k] ? x[k] : __builtin_inf();
-        scr[k * 128 + 64 + l] = sel[k] ? w[k] : __builtin_inf();
-    }
-    wsync();
-#pragma unroll 10
-    for (int m = 0; m < NR; m++) {
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const double xm = scr[k * 128 + m], wm = scr[k * 128 + 64 + m];
-            const bool lt = (xm < x[k]) | ((xm == x[k]) & ((wm < w[k]) | ((wm == w[k]) & (m < l))));
-            r[k] += (lt & (bool)((selm[k] >> m) & 1)) ? 1 : 0;
-        }
-    }
-    double kx[K], kw[K], cum[K];
-    int nmax = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int dst = sel[k] ? r[k] : n[k] + mbcnt64(~selm[k]);
-        kx[k] = permute_d(dst, x[k]);
-        kw[k] = permute_d(dst, w[k]);
-        cum[k] = l == 0 ? 0.0 + kw[k] : 0.0;
-        nmax = n[k] > nmax ? n[k] : nmax;
-    }
-    if (prof) {
-        const long long t1 = (long long)__builtin_amdgcn_s_memtime();
-        prof[0] += t1 - t0;
-        prof[2] = t1;
-    }
-    for (int t = 1; t < nmax; t++) {
-#pragma unroll
-        for (int k = 0; k < K; k++) cum[k] = shr1_d(cum[k]) + kw[k];
-    }
-    if (prof) prof[1] += (long long)__builtin_amdgcn_s_memtime() - prof[2];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const double mid = 0.5 * Wtot[k];
-        const uint64_t over = ballot(l < n[k] && cum[k] > mid);
-        if (!over) {
-            out[k] = __builtin_nan("");
-            continue;
-        }
-        const int c = __builtin_ctzll(over) + 1;
-        const double before = readlane_d(cum[k], c - 1) - readlane_d(kw[k], c - 1);
-        if (fabs(before - mid) < DBL_EPS) {
-            if (c >= 2)
-                out[k] = (readlane_d(kx[k], c - 2) + readlane_d(kx[k], c - 1)) / 2.0;
-            else
-                out[k] = n[k] == 1 ? readlane_d(kx[k], 0) / 1.0 : __builtin_nan("");
-        } else {
-            out[k] = readlane_d(kx[k], c - 1);
-        }
-    }
-}
 
 // scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
 __device__ __forceinline__ double rank_avg(const double* v, int E) {
@@ -420,8 +374,6 @@ struct Smem {
     double* n1;     // [N] normalize(set1) (aliases C)
     double* n2;     // [N] normalize(set2) (aliases C)
     double* smooth; // [N] (aliases C)
-    double* sx;     // [64] median scratch (aliases M)
-    double* sw;     // [64] median scratch (aliases M + 64)
     double* scr;    // [48] Jacobi rotation parameters (aliases tok)
     double* mu;     // [E]
     double* guess;  // [E] (aliases C)
@@ -440,7 +392,8 @@ struct Smem {
 // vectors whose lifetimes do not overlap the matrices' share their space:
 //   C  (covariance, Jacobi V) is live from the covariance to the scores only; before
 //      it holds guess (interpolation), after it n1 | n2 | smooth | adj;
-//   M  (squared matrix, Jacobi A) is dead in both median phases: sx | sw live there;
+//   M  (squared matrix, Jacobi A) is dead in both median phases: the median scratch
+//      (MED_SCR doubles) lives there;
 //   tok is dead after the covariance: the Jacobi rotation parameters (scr) reuse it.
 // Per-row vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20:
 // 17.2 KB, nine rounds per CU.
@@ -450,7 +403,7 @@ __host__ __device__ inline int smem_c_size(int N, int E, int ES) {
     const int need = 3 * smem_rows(N) + smem_evs(E);
     return E * ES > need ? E * ES : need;
 }
-__host__ __device__ inline int smem_m_size(int E, int ES) { return E * ES > 128 ? E * ES : 128; }
+__host__ __device__ inline int smem_m_size(int E, int ES) { return E * ES > MED_SCR ? E * ES : MED_SCR; }
 __host__ __device__ inline int smem_tok_size(int N) { return smem_rows(N) > 48 ? smem_rows(N) : 48; }
 
 __host__ __device__ inline size_t smem_doubles(int N, int E, int ES) {
@@ -481,8 +434,6 @@ __device__ Smem carve(double* base, int N, int E, int ES) {
     s.n2 = s.C + nr;
     s.smooth = s.C + 2 * nr;
     s.adj = s.C + 3 * nr;
-    s.sx = s.M;
-    s.sw = s.M + 64;
     s.scr = s.tok;
     return s;
 }
@@ -788,34 +739,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             if (a.int_dtype) g = trunc(g);
             if (l == 0) S.guess[j] = g;
         };
-        // two medians at a time while the C/M tiles (dead until the covariance) hold
-        // their scratch; a non-regular median takes the single path
-        // (pairing two medians through wave_wmedian_rank_k measured no faster at 50 x 20:
-        // the rank pass is VALU-throughput bound and the pair raised register pressure)
-        const bool pair_ok = false;
+        // one median at a time: the scratch lives in M, dead until the covariance
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             double x0, w0, W0;
             bool p0;
             pair_of(j, x0, w0, p0, W0);
-            if (pair_ok && todo && wmedian_regular(x0, w0, p0, W0)) {
-                const int j2 = __builtin_ctzll(todo);
-                double x1, w1, W1;
-                bool p1;
-                pair_of(j2, x1, w1, p1, W1);
-                if (wmedian_regular(x1, w1, p1, W1)) {
-                    todo &= todo - 1;
-                    double xs[2] = {x0, x1}, ws[2] = {w0, w1}, Ws[2] = {W0, W1}, g[2];
-                    bool ps[2] = {p0, p1};
-                    wave_wmedian_rank_k<(NT > 0 ? NT : 64), 2>(xs, ws, ps, Ws, S.C, g, a.stamps ? mprof : nullptr);
-                    finish(j, g[0]);
-                    finish(j2, g[1]);
-                    wsync();
-                    continue;
-                }
-            }
-            finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.sx, S.sw, a.stamps ? mprof : nullptr));
+            finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.M, a.stamps ? mprof : nullptr));
             wsync();
         }
     }
@@ -1113,26 +1044,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             return bcast(w, 0);
         }();
         uint64_t todo = scaled_mask;
-        const bool pair_ok = false;  // see phase a3
-        while (todo) {
+        while (todo) {  // scratch in M, dead after the scores
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const double x0 = row ? S.F[l * ES + j] : 0.0;
-            if (pair_ok && todo && wmedian_regular(x0, smooth_i, row, Wsm)) {
-                const int j2 = __builtin_ctzll(todo);
-                const double x1 = row ? S.F[l * ES + j2] : 0.0;
-                if (wmedian_regular(x1, smooth_i, row, Wsm)) {
-                    todo &= todo - 1;
-                    double xs[2] = {x0, x1}, ws[2] = {smooth_i, smooth_i}, Ws[2] = {Wsm, Wsm}, g[2];
-                    bool ps[2] = {row, row};
-                    wave_wmedian_rank_k<(NT > 0 ? NT : 64), 2>(xs, ws, ps, Ws, S.C, g, a.stamps ? mprof : nullptr);
-                    if (l == j) rawj = g[0];
-                    if (l == j2) rawj = g[1];
-                    wsync();
-                    continue;
-                }
-            }
-            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, smooth_i, row, Wsm, N, S.sx, S.sw, a.stamps ? mprof : nullptr);
+            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, smooth_i, row, Wsm, N, S.M, a.stamps ? mprof : nullptr);
             if (l == j) rawj = m;
             wsync();
         }
