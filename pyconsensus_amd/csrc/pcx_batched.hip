@@ -28,7 +28,8 @@ namespace {
 
 constexpr int W = 64;        // wavefront
 constexpr int NMAX = 64;  // reporters per round (one lane each)
-constexpr int EMAX = 32;
+constexpr int EMAX = 32;  // events per round (MFMA tiles 2 x 16; pcx_api.cpp validates)
+static_assert(EMAX <= 2 * 16, "2 x 2 grid of 16 x 16 MFMA tiles");
 static_assert(NMAX == W, "one reporter per lane");
 
 // power iteration constants (SPEC; equal to oracle/pcx_oracle_batched.c)
@@ -136,7 +137,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 // runs as a DPP wave_shr chain (each step recomputes final lanes identically); the
 // accumulators, the fixed tree and the tail are then read back wave-uniformly.
 // Same additions in the same order as numpy (and the C oracle's pw_sum).
-__device__ __forceinline__ double wave_pw_sum(double v, bool sel, double* /*scr*/) {
+__device__ __forceinline__ double wave_pw_sum(double v, bool sel) {
     const int l = lane_id();
     const uint64_t m = ballot(sel);
     const int n = popc(m);
@@ -368,20 +369,18 @@ __device__ __forceinline__ double rank_avg(const double* v, int E) {
 struct Smem {
     double* F;      // [N][ES] rescaled, then filled reports
     double* C;      // [E][ES] covariance (phase aliases: see carve)
-    double* M;      // [max(E*ES, 128)] power-iteration / Jacobi working matrix
+    double* M;      // [max(E*ES, MED_SCR)] power-iteration / Jacobi working matrix
     double* rep;    // [N]
-    double* tok;    // [N]
     double* n1;     // [N] normalize(set1) (aliases C)
     double* n2;     // [N] normalize(set2) (aliases C)
     double* smooth; // [N] (aliases C)
-    double* scr;    // [48] Jacobi rotation parameters (aliases tok)
     double* mu;     // [E]
     double* guess;  // [E] (aliases C)
     double* x;      // [E] power-iteration vector
     double* ld;     // [E] loading
-    double* old;    // [E]
-    double* nv1;    // [E]
-    double* nv2;    // [E]
+    double* old;    // [E] (aliases C)
+    double* nv1;    // [E] (aliases M)
+    double* nv2;    // [E] (aliases M)
     double* adj;    // [E] (aliases C)
     uint64_t* nanm; // [E] bit i = report (i, j) is NaN
     uint64_t* zerm; // [E] bit i = report (i, j) == 0.0
@@ -391,24 +390,26 @@ struct Smem {
 // rounds resident per CU (tools/occupancy_batched.py), and LDS is what bounds them, so
 // vectors whose lifetimes do not overlap the matrices' share their space:
 //   C  (covariance, Jacobi V) is live from the covariance to the scores only; before
-//      it holds guess (interpolation), after it n1 | n2 | smooth | adj;
-//   M  (squared matrix, Jacobi A) is dead in both median phases: the median scratch
-//      (MED_SCR doubles) lives there;
-//   tok is dead after the covariance: the Jacobi rotation parameters (scr) reuse it.
-// Per-row vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20:
-// 17.2 KB, nine rounds per CU.
+//      it holds guess (interpolation), after it n1 | n2 | smooth | adj | old;
+//   M  (squared matrix, Jacobi A) is dead in both median phases, where the median
+//      scratch (MED_SCR doubles) lives, and after the eigenpairs, where nv1 | nv2 live;
+//   x | ld (power iteration, loading) are dead in the Jacobi sweeps: rotation cos | sin.
+// The integer tokens are recomputed from rep where the covariance needs them.  Per-row
+// vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20: 16.3 KB,
+// ten rounds per CU.
 __host__ __device__ inline int smem_rows(int N) { return (N + 1) & ~1; }
 __host__ __device__ inline int smem_evs(int E) { return (E + 1) & ~1; }
 __host__ __device__ inline int smem_c_size(int N, int E, int ES) {
-    const int need = 3 * smem_rows(N) + smem_evs(E);
+    const int need = 3 * smem_rows(N) + 2 * smem_evs(E);
     return E * ES > need ? E * ES : need;
 }
-__host__ __device__ inline int smem_m_size(int E, int ES) { return E * ES > MED_SCR ? E * ES : MED_SCR; }
-__host__ __device__ inline int smem_tok_size(int N) { return smem_rows(N) > 48 ? smem_rows(N) : 48; }
+__host__ __device__ inline int smem_m_size(int E, int ES) {
+    const int need = MED_SCR > 2 * smem_evs(E) ? MED_SCR : 2 * smem_evs(E);
+    return E * ES > need ? E * ES : need;
+}
 
 __host__ __device__ inline size_t smem_doubles(int N, int E, int ES) {
-    return (size_t)N * ES + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + smem_tok_size(N) +
-           8 * (size_t)smem_evs(E);
+    return (size_t)N * ES + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + 5 * (size_t)smem_evs(E);
 }
 
 __device__ Smem carve(double* base, int N, int E, int ES) {
@@ -419,13 +420,9 @@ __device__ Smem carve(double* base, int N, int E, int ES) {
     s.C = p; p += smem_c_size(N, E, ES);
     s.M = p; p += smem_m_size(E, ES);
     s.rep = p; p += nr;
-    s.tok = p; p += smem_tok_size(N);
     s.mu = p; p += ne;
     s.x = p; p += ne;
     s.ld = p; p += ne;
-    s.old = p; p += ne;
-    s.nv1 = p; p += ne;
-    s.nv2 = p; p += ne;
     s.nanm = reinterpret_cast<uint64_t*>(p); p += ne;
     s.zerm = reinterpret_cast<uint64_t*>(p); p += ne;
     // phase aliases (see above)
@@ -434,7 +431,9 @@ __device__ Smem carve(double* base, int N, int E, int ES) {
     s.n2 = s.C + nr;
     s.smooth = s.C + 2 * nr;
     s.adj = s.C + 3 * nr;
-    s.scr = s.tok;
+    s.old = s.C + 3 * nr + ne;
+    s.nv1 = s.M;
+    s.nv2 = s.M + ne;
     return s;
 }
 
@@ -517,8 +516,8 @@ __device__ __forceinline__ void jac_pair(int i, int r, int n, int& p, int& q) {
 }
 
 // A (E x E, row stride ES) -> eigenvalues on its diagonal; V -> eigenvectors (columns).
-// prm: 48 doubles of LDS (rotation cosines at [0, npair), sines at [32, 32 + npair), npair <= 16).
-__device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm) {
+// pc, ps: rotation cosines and sines, npair <= 16 doubles of LDS each.
+__device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* pc, double* ps) {
     const int l = lane_id();
     for (int o = l; o < E * E; o += W) {
         const int j = o / E, k = o - j * E;
@@ -555,17 +554,17 @@ __device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm
                         s = t * c;
                     }
                 }
-                prm[l] = c;
-                prm[32 + l] = s;
+                pc[l] = c;
+                ps[l] = s;
             }
             wsync();
             for (int o = l; o < npair * E; o += W) {  // rows p, q
                 const int i = o / E, k = o - i * E;
-                const double s = prm[32 + i];
+                const double s = ps[i];
                 if (s == 0.0) continue;
                 int p, q;
                 jac_pair(i, r, n, p, q);
-                const double c = prm[i];
+                const double c = pc[i];
                 const double apk = A[p * ES + k], aqk = A[q * ES + k];
                 A[p * ES + k] = c * apk - s * aqk;
                 A[q * ES + k] = s * apk + c * aqk;
@@ -573,11 +572,11 @@ __device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* prm
             wsync();
             for (int o = l; o < npair * E; o += W) {  // columns p, q of A and V
                 const int i = o / E, j = o - i * E;
-                const double s = prm[32 + i];
+                const double s = ps[i];
                 if (s == 0.0) continue;
                 int p, q;
                 jac_pair(i, r, n, p, q);
-                const double c = prm[i];
+                const double c = pc[i];
                 const double ajp = A[j * ES + p], ajq = A[j * ES + q];
                 A[j * ES + p] = c * ajp - s * ajq;
                 A[j * ES + q] = s * ajp + c * ajq;
@@ -647,16 +646,13 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     // ---- a1: reputation (__init__.py:138-146) -----------------------------
     double rep;
     if (a.reputation) {
-        const double tot = wave_pw_sum(raw, row, S.scr);
+        const double tot = wave_pw_sum(raw, row);
         rep = raw / tot;
     } else {
         rep = 1.0 / (double)N;
     }
     const double tok = trunc(rep * 1e6);
-    if (row) {
-        S.rep[l] = rep;
-        S.tok[l] = tok;
-    }
+    if (row) S.rep[l] = rep;
     const double denom = tree_sum(row ? tok : 0.0) - 1.0;  // exact integer sum
     wsync();
 
@@ -766,18 +762,17 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(3);
     // ---- old = rep . F (np.dot) -------------------------------------------
     double oldj = col ? dot2(S.rep, S.F + l, ES, N) : 0.0;
-    if (col) S.old[l] = oldj;
 
     double sc_i = 0.0, nc_i = 0.0, ld_j = 0.0;
     int branch = 5, flags = 0, iters = 0, comps = -1;
     const int alg = a.algorithm;
     if (alg == 0 || alg == 2 || alg == 3) {  // wpca (:315-339): PCA, big-five, fixed-variance
         // ---- a5: weighted mean, np.ma.average (:317-319) -------------------
-        const double den = wave_pw_sum(rep, row, S.scr);
+        const double den = wave_pw_sum(rep, row);
         double muj = 0.0;
         if (E == 1) {
             const double p = row ? S.F[l * ES] * rep : 0.0;
-            const double acc = wave_pw_sum(p, row, S.scr);
+            const double acc = wave_pw_sum(p, row);
             muj = acc / den;
         } else if (col) {
             double acc = S.F[l] * S.rep[0];
@@ -805,7 +800,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                 if (i0 < N) {
                     const int i = i0 + kq;
                     const bool ok = i < N;
-                    const double tk = ok ? S.tok[i] : 0.0;
+                    const double tk = ok ? trunc(S.rep[i] * 1e6) : 0.0;  // the integer tokens (a1)
                     const bool v0 = ok && ml < E, v1 = ok && 16 + ml < E;
                     const double d0 = v0 ? S.F[i * ES + ml] - mu0 : 0.0;
                     const double d1 = v1 ? S.F[i * ES + 16 + ml] - mu1 : 0.0;
@@ -896,7 +891,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             iters = it + PI_POLISH + sqn;
         }
         // loading = v / sqrt(sum(v**2)) with numpy's pairwise sum (:336)
-        const double nv = sqrt(wave_pw_sum(xv * xv, col, S.scr));
+        const double nv = sqrt(wave_pw_sum(xv * xv, col));
         ld_j = col ? xv / nv : 0.0;
         wsync();
         if (col) S.ld[l] = ld_j;
@@ -913,14 +908,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         } else {
             // ---- big-five (:373-390) / fixed-variance (:429-451): net score =
             // sum_c Sigma_c * (wcd . loading_c); Sigma, loadings from Jacobi (SPEC)
-            const double trace = wave_pw_sum(col ? S.C[l * ES + l] : 0.0, col, S.scr);  // np.trace
+            const double trace = wave_pw_sum(col ? S.C[l * ES + l] : 0.0, col);  // np.trace
             wsync();
             for (int o = l; o < E * E; o += W) {
                 const int j = o / E, k = o - j * E;
                 S.M[j * ES + k] = S.C[j * ES + k];
             }
             wsync();
-            jacobi_eig_wave(S.M, S.C, ES, E, S.scr);  // A in M; V overwrites C
+            jacobi_eig_wave(S.M, S.C, ES, E, S.x, S.ld);  // A in M; V overwrites C; x, ld are dead
             const double sig = col ? fabs(S.M[l * ES + l]) : 0.0;
             if (col) S.nv1[l] = sig;
             wsync();
@@ -972,20 +967,21 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         const double set1 = sc_i + fabs(mn);
         const double set2 = sc_i - mx;
         double a1 = fabs(set1), a2 = fabs(set2);
-        double S1 = wave_pw_sum(a1, row, S.scr);
+        double S1 = wave_pw_sum(a1, row);
         if (S1 == 0) {
             a1 += 1.0;
-            S1 = wave_pw_sum(a1, row, S.scr);
+            S1 = wave_pw_sum(a1, row);
         }
-        double S2 = wave_pw_sum(a2, row, S.scr);
+        double S2 = wave_pw_sum(a2, row);
         if (S2 == 0) {
             a2 += 1.0;
-            S2 = wave_pw_sum(a2, row, S.scr);
+            S2 = wave_pw_sum(a2, row);
         }
         if (row) {
             S.n1[l] = a1 / S1;
             S.n2[l] = a2 / S2;
         }
+        if (col) S.old[l] = oldj;
         wsync();
         double d1 = 0.0, d2 = 0.0;
         if (col) {
@@ -1002,12 +998,12 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             const double r1 = rank_avg(S.nv1, E);
             const double r2 = rank_avg(S.nv2, E);
             const double e1 = fabs(r1 - r0), e2 = fabs(r2 - r0);
-            ref = wave_pw_sum(e1, col, S.scr) - wave_pw_sum(e2, col, S.scr);
+            ref = wave_pw_sum(e1, col) - wave_pw_sum(e2, col);
         }
         bool pick1;
         if (ref == 0) {
             const double q1 = d1 - oldj, q2 = d2 - oldj;
-            const double ref2 = wave_pw_sum(q1 * q1, col, S.scr) - wave_pw_sum(q2 * q2, col, S.scr);
+            const double ref2 = wave_pw_sum(q1 * q1, col) - wave_pw_sum(q2 * q2, col);
             pick1 = ref2 <= 0;
             branch = pick1 ? 3 : 4;
         } else {
@@ -1019,12 +1015,12 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
 
     STAMP(7);
     // ---- a10: reputation update (:460-472) --------------------------------
-    const double meanrep = wave_pw_sum(rep, row, S.scr) / (double)N;
+    const double meanrep = wave_pw_sum(rep, row) / (double)N;
     double u = fabs(nc_i * (rep / meanrep));
-    double Su = wave_pw_sum(u, row, S.scr);
+    double Su = wave_pw_sum(u, row);
     if (Su == 0) {
         u += 1.0;
-        Su = wave_pw_sum(u, row, S.scr);
+        Su = wave_pw_sum(u, row);
     }
     const double this_i = u / Su;
     const double smooth_i = a.alpha * this_i + (1.0 - a.alpha) * rep;
@@ -1075,18 +1071,18 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         const double aj = S.adj[j];
         const bool hit = row && S.F[l * ES + j] == aj;
         const uint64_t hm = ballot(hit);
-        const double c = hm ? wave_pw_sum(smooth_i, hit, S.scr) : (a.algorithm == 0 ? __builtin_nan("") : 0.0);
+        const double c = hm ? wave_pw_sum(smooth_i, hit) : (a.algorithm == 0 ? __builtin_nan("") : 0.0);
         if (l == j) certj = c;
     }
     // normalize(certainty), mean(certainty)
     double ac = fabs(certj);
-    double Sc = wave_pw_sum(ac, col, S.scr);
+    double Sc = wave_pw_sum(ac, col);
     if (Sc == 0) {
         ac += 1.0;
-        Sc = wave_pw_sum(ac, col, S.scr);
+        Sc = wave_pw_sum(ac, col);
     }
     const double reward = ac / Sc;
-    const double avg_cert = wave_pw_sum(certj, col, S.scr) / (double)E;
+    const double avg_cert = wave_pw_sum(certj, col) / (double)E;
 
     STAMP(10);
     // ---- a15: participation and bonuses (:549-581) -------------------------
@@ -1120,19 +1116,19 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     }
     const bool rowmasked = row && nnan == E;
     const double pr = 1.0 - narow / (double)E;
-    const double pna = 1.0 - wave_pw_sum(pcj, col, S.scr) / (double)E;
+    const double pna = 1.0 - wave_pw_sum(pcj, col) / (double)E;
     double ar = rowmasked ? 0.0 : fabs(pr);
-    double Sr = wave_pw_sum(ar, row, S.scr);
+    double Sr = wave_pw_sum(ar, row);
     if (Sr == 0) {
         ar = rowmasked ? 0.0 : fabs(pr) + 1.0;
-        Sr = wave_pw_sum(ar, row, S.scr);
+        Sr = wave_pw_sum(ar, row);
     }
     const double rel = rowmasked ? fabs(pr) : ar / Sr;
     double apc = fabs(pcj);
-    double Spc = wave_pw_sum(apc, col, S.scr);
+    double Spc = wave_pw_sum(apc, col);
     if (Spc == 0) {
         apc += 1.0;
-        Spc = wave_pw_sum(apc, col, S.scr);
+        Spc = wave_pw_sum(apc, col);
     }
     const double relc = apc / Spc;
 

@@ -1,7 +1,7 @@
 """Throughput of batched_round_kernel against resident rounds per CU (diagnostic).
 
 Pads the kernel's dynamic LDS (PCX_BATCHED_LDS_PAD, read once per process) so that
-at most k rounds fit one CU's 160 KiB, for k = 9 (unpadded) down to 4, and times the
+at most k rounds fit one CU's 160 KiB, for k = 10 (unpadded) down to 6, and times the
 C3 launch (65,536 50x20 rounds) with HIP events.  If time scales like 1/k the kernel is
 latency bound and more resident rounds (less LDS / fewer VGPRs per round) pay off.
 
@@ -43,8 +43,8 @@ def child():
 
 def main():
     ES = 21  # batched_lds_bytes(50, 20): smem_doubles() in pcx_batched.hip
-    base = 8 * (50 * ES + 2 * 20 * ES + 2 * 50 + 8 * 20)
-    for k in (9, 8, 7, 6, 4):
+    base = 8 * (50 * ES + 2 * 20 * ES + 50 + 5 * 20)
+    for k in (10, 9, 8, 6):
         pad = max(0, LDS_CU // k - base - 256) if k < LDS_CU // base else 0
         env = dict(os.environ, PCX_BATCHED_LDS_PAD=str(pad))
         r = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
