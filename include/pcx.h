@@ -1,6 +1,7 @@
 /*
  * pcx.h -- C ABI of libpcx, the MI355X (gfx950) implementation of
- * pyconsensus's Oracle.consensus() hot path (algorithm="PCA").
+ * pyconsensus's Oracle.consensus() hot path (algorithm "PCA", plus "absolute",
+ * "big-five", "fixed-variance" and "cokurtosis" on the same kernels).
  *
  * The reference (IanMadlenya/pyconsensus) is pure Python with no FFI: its whole
  * public surface is `Oracle(reports, event_bounds, reputation, ...).consensus()`
