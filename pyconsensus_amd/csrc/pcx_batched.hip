@@ -262,7 +262,7 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
 //    never +-0 with equal partners: zero reports are missing), so their order cannot
 //    change the walk;
 //  * each pair is scattered to its rank (ox, ow), and the cumulative weight runs
-//    left to right, four broadcast loads per step group, stopping at the first
+//    left to right, eight broadcast loads per step group, stopping at the first
 //    cum > mid: the SPEC's sequential sums bit for bit; `before` is the same subtraction.
 // NaN keys have no total order: rounds with a NaN among the selected pairs take
 // wave_wmedian.  NR = compile-time row count bound (64 when the shape is dynamic).
@@ -277,11 +277,9 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     int* cnt = reinterpret_cast<int*>(scr + 256);
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
     const double mid = 0.5 * Wtot;
-    const uint64_t dom = ballot(sel && w > mid);
-    if (dom) {
+    if (ballot(sel && w > mid)) {  // weightedstats: a weight above half the total wins outright
         const double mx = wave_max(sel ? w : -__builtin_inf());
-        const uint64_t at = ballot(sel && w == mx);
-        return bcast(x, __builtin_ctzll(at));
+        return bcast(x, __builtin_ctzll(ballot(sel && w == mx)));  // first maximal weight
     }
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
     if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
@@ -398,6 +396,10 @@ struct Smem {
 // vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20: 16.3 KB,
 // ten rounds per CU.
 __host__ __device__ inline int smem_rows(int N) { return (N + 1) & ~1; }
+// F also holds the certainty phase's compacted hit lists, [E][N | 1]
+__host__ __device__ inline int smem_f_size(int N, int E, int ES) {
+    return N * ES > E * (N | 1) ? N * ES : E * (N | 1);
+}
 __host__ __device__ inline int smem_evs(int E) { return (E + 1) & ~1; }
 __host__ __device__ inline int smem_c_size(int N, int E, int ES) {
     const int need = 3 * smem_rows(N) + 2 * smem_evs(E);
@@ -409,14 +411,14 @@ __host__ __device__ inline int smem_m_size(int E, int ES) {
 }
 
 __host__ __device__ inline size_t smem_doubles(int N, int E, int ES) {
-    return (size_t)N * ES + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + 5 * (size_t)smem_evs(E);
+    return (size_t)smem_f_size(N, E, ES) + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + 5 * (size_t)smem_evs(E);
 }
 
 __device__ Smem carve(double* base, int N, int E, int ES) {
     const int nr = smem_rows(N), ne = smem_evs(E);
     Smem s;
     double* p = base;
-    s.F = p; p += N * ES;
+    s.F = p; p += smem_f_size(N, E, ES);
     s.C = p; p += smem_c_size(N, E, ES);
     s.M = p; p += smem_m_size(E, ES);
     s.rep = p; p += nr;
@@ -683,53 +685,73 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(2);
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
     uint64_t miss_j = 0;
-    double Wj = 0.0;
     if (col) miss_j = S.nanm[l] | S.zerm[l];
     {
-        // branch-free sequential sums over the present rows (a skipped row keeps the
-        // accumulator as is: the same left-to-right sums as the SPEC loops)
+        // tot: the SPEC's sequential sum of the present reputations (a missing row adds
+        // +0.0, which leaves a sum that starts at +0.0 unchanged).  A binary column's
+        // guess only matters through catch(): the sum of (rep/tot)*F is formed cheaply as
+        // (sum rep*F)/tot, and the SPEC's exact sequential sum is replayed only for a
+        // column whose cheap value lies within 1e-12 * sum|rep*F|/tot of a catch threshold
+        // (the two differ by at most ~2*(N+2) ulp of that magnitude), so the caught value
+        // is the SPEC's bit for bit.  Scaled columns only need tot here (the median).
         constexpr int NR = NT > 0 ? NT : 64;
-        double tot = 0.0;
-#pragma unroll
+        double tot = 0.0, sp = 0.0, sa = 0.0;
+#pragma unroll 10
         for (int i = 0; i < NR; i++) {
             if (i < N) {
-                const double r = S.rep[i];
-                tot = ((miss_j >> i) & 1) ? tot : tot + r;
+                const bool miss = (miss_j >> i) & 1;
+                const double re = miss ? 0.0 : S.rep[i];
+                const double f = miss ? 0.0 : S.F[i * ES + (col ? l : 0)];
+                tot = tot + re;
+                sp = fma(re, f, sp);
+                sa = fma(fabs(re), fabs(f), sa);
             }
         }
-        double acc = 0.0;  // scaled: sum of rep/tot (weightedstats total); binary: sum of (rep/tot)*F
+        const double t_lo = 1.5 - a.catch_tol, t_hi = 1.5 + a.catch_tol;  // catch_() thresholds
+        const double accf = sp / tot, margin = 1e-12 * (sa / tot);
+        const bool binary_fill = col && miss_j && !scj;
+        const bool fast = tot > 0.0 && __builtin_isfinite(accf) && __builtin_isfinite(margin) &&
+                          fabs(accf - t_lo) > margin && fabs(accf - t_hi) > margin;
+        double acc = accf;
+        if (ballot(binary_fill && !fast)) {
+            double ex = 0.0;  // SPEC: sum of (rep/tot)*F over the present rows, in row order
 #pragma unroll
-        for (int i = 0; i < NR; i++) {
-            if (i < N) {
-                const double q = S.rep[i] / tot;
-                const double t = scj ? q : q * S.F[i * ES + (col ? l : 0)];
-                acc = ((miss_j >> i) & 1) ? acc : acc + t;
+            for (int i = 0; i < NR; i++) {
+                if (i < N) {
+                    const double t = (S.rep[i] / tot) * S.F[i * ES + (col ? l : 0)];
+                    ex = ((miss_j >> i) & 1) ? ex : ex + t;
+                }
             }
+            if (!fast) acc = ex;
         }
-        if (col && miss_j) {
-            if (scj) {
-                Wj = acc;
-            } else {
-                double g = catch_(acc, a.catch_tol);
-                if (a.int_dtype) g = trunc(g);
-                S.guess[l] = g;
-            }
-            S.mu[l] = tot;  // stash the present-reputation total for the median phase
+        if (binary_fill) {
+            double g = catch_(acc, a.catch_tol);
+            if (a.int_dtype) g = trunc(g);
+            S.guess[l] = g;
         }
+        if (col && miss_j) S.mu[l] = tot;  // the present-reputation total, for the median phase
     }
     wsync();
     STAMP(13);
     // scaled columns with missing reports: weighted median of the present values
     {
         uint64_t todo = ballot(col && scj && miss_j != 0);
-        // the (x, w) pairs of interpolation median j: present reports, rep / tot (:292-303)
+        // the (x, w) pairs of interpolation median j: present reports, rep / tot (:292-303);
+        // Wsum = weightedstats' sum(weights), sequential in row order (absent rows add +0.0,
+        // which leaves a sum from +0.0 unchanged)
         auto pair_of = [&](int j, double& x, double& w, bool& present, double& Wsum) {
             const uint64_t mj = S.nanm[j] | S.zerm[j];
             present = row && !((mj >> l) & 1);
             const double tot = S.mu[j];
             x = row ? S.F[l * ES + j] : 0.0;
             w = present ? S.rep[l] / tot : 0.0;
-            Wsum = bcast(Wj, j);
+            double* ws = S.M;  // median scratch, dead until the covariance
+            wsync();
+            ws[l] = w;
+            wsync();
+            Wsum = 0.0;
+#pragma unroll 8
+            for (int i = 0; i < N; i++) Wsum = Wsum + ws[i];
         };
         auto finish = [&](int j, double g) {
             if (a.int_dtype) g = trunc(g);
@@ -1066,13 +1088,47 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
 
     STAMP(9);
     // ---- a14: certainty (:540-546): pairwise sum of the matching smooth_rep --
+    // every column at once, one lane per column: the hit masks first (F is read for the
+    // last time), then each row lane scatters its smooth_rep into the compacted hit list of
+    // every column it matches (into F, dead from here on), then lane j runs numpy's pairwise
+    // add.reduce (n <= 128: eight strided accumulators, fixed tree, sequential tail) on
+    // its column's list
     double certj = 0.0;
-    for (int j = 0; j < E; j++) {
-        const double aj = S.adj[j];
-        const bool hit = row && S.F[l * ES + j] == aj;
-        const uint64_t hm = ballot(hit);
-        const double c = hm ? wave_pw_sum(smooth_i, hit) : (a.algorithm == 0 ? __builtin_nan("") : 0.0);
-        if (l == j) certj = c;
+    {
+        uint64_t* hitm = reinterpret_cast<uint64_t*>(S.M);  // [E]; M is dead after the medians
+        for (int j = 0; j < E; j++) {
+            const uint64_t hm = ballot(row && S.F[l * ES + j] == S.adj[j]);
+            if (l == 0) hitm[j] = hm;
+        }
+        wsync();
+        const int NS = N | 1;  // odd stride: lane-per-column reads spread over the banks
+        double* comp = S.F;    // [E][NS]
+        for (int j = 0; j < E; j++) {
+            const uint64_t hm = hitm[j];
+            if ((hm >> l) & 1) comp[j * NS + mbcnt64(hm)] = smooth_i;
+        }
+        wsync();
+        if (col) {
+            constexpr int TMAX = (NT > 0 ? NT : 64) / 8;
+            const uint64_t hm = hitm[l];
+            const int n = popc(hm), T = n >> 3;
+            const double* c = comp + l * NS;
+            double res = 0.0;
+            if (T) {
+                double r[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) r[k] = c[k];
+#pragma unroll
+                for (int t = 1; t < TMAX; t++)
+                    if (t < T) {
+#pragma unroll
+                        for (int k = 0; k < 8; k++) r[k] = r[k] + c[8 * t + k];
+                    }
+                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            }
+            for (int q = 8 * T; q < n; q++) res = res + c[q];  // the tail (everything when n < 8)
+            certj = n ? res : (a.algorithm == 0 ? __builtin_nan("") : 0.0);
+        }
     }
     // normalize(certainty), mean(certainty)
     double ac = fabs(certj);
