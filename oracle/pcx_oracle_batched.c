@@ -179,8 +179,12 @@ static void square_scaled(double (*M)[ES], int E) {
             double a = fabs(acc);
             if (a > mx) mx = a;
         }
+    /* scale by the power of two that brings max|MM| into [1, 2): exact, so only the
+     * products round (a zero / subnormal / non-finite maximum divides as before) */
+    const int pow2 = mx >= DBL_MIN && isfinite(mx);
+    const double sc = pow2 ? ldexp(1.0, -ilogb(mx)) : 1.0;
     for (int j = 0; j < E; j++)
-        for (int k = 0; k < E; k++) M[j][k] = mx > 0.0 ? T[j][k] / mx : T[j][k];
+        for (int k = 0; k < E; k++) M[j][k] = pow2 ? T[j][k] * sc : (mx > 0.0 ? T[j][k] / mx : T[j][k]);
 }
 
 static void matvec_unit(const double (*M)[ES], int E, const double* x, double* y) {

@@ -39,6 +39,7 @@ constexpr int PI_PRESQUARE = 3;
 constexpr int PI_SQUARE_EVERY = 32;
 constexpr int PI_MAX_SQUARINGS = 8;
 constexpr int PI_POLISH = 4;
+constexpr double DBL_MIN_ = 2.2250738585072014e-308;
 constexpr double DBL_EPS = 2.220446049250313080847e-16;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
@@ -491,14 +492,19 @@ __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
         if (j1 < E && k1 < E) mx = fmax(mx, fabs(t11[r]));
     }
     mx = wave_max(mx);
+    // SPEC: scale by the power of two that brings max|MM| into [1, 2) (exact); a zero,
+    // subnormal or non-finite maximum divides instead
+    const bool pow2 = mx >= DBL_MIN_ && __builtin_isfinite(mx);
+    const double sc = pow2 ? ldexp(1.0, -ilogb(mx)) : 1.0;
+    auto scaled = [&](double t) { return pow2 ? t * sc : (mx > 0.0 ? t / mx : t); };
     wsync();
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
-        if (j0 < E && k0 < E) M[j0 * ES + k0] = mx > 0.0 ? t00[r] / mx : t00[r];
-        if (j0 < E && k1 < E) M[j0 * ES + k1] = mx > 0.0 ? t01[r] / mx : t01[r];
-        if (j1 < E && k0 < E) M[j1 * ES + k0] = mx > 0.0 ? t10[r] / mx : t10[r];
-        if (j1 < E && k1 < E) M[j1 * ES + k1] = mx > 0.0 ? t11[r] / mx : t11[r];
+        if (j0 < E && k0 < E) M[j0 * ES + k0] = scaled(t00[r]);
+        if (j0 < E && k1 < E) M[j0 * ES + k1] = scaled(t01[r]);
+        if (j1 < E && k0 < E) M[j1 * ES + k0] = scaled(t10[r]);
+        if (j1 < E && k1 < E) M[j1 * ES + k1] = scaled(t11[r]);
     }
     wsync();
 }
@@ -865,10 +871,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             xv = l == 0 ? 1.0 : 0.0;
             flags |= 1;
         } else {
-            // start: the column with the largest diagonal entry (first max)
-            int kd = 0;
-            for (int j = 1; j < E; j++)
-                if (S.C[j * ES + j] > S.C[kd * ES + kd]) kd = j;
+            // start: the column with the largest diagonal entry (first max; C is finite here)
+            const double dg = col ? S.C[l * ES + l] : -__builtin_inf();
+            const int kd = __builtin_ctzll(ballot(col && dg == wave_max(dg)));
             double x0 = col ? S.C[l * ES + kd] : 0.0;
             const double n0 = sqrt(tree_sum(x0 * x0));
             xv = col ? x0 / n0 : 0.0;
