@@ -145,11 +145,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; PCX_DIST_BACKEND=gloo (ranks may then share a GPU) rehearses the
+    # multi-rank path on a one-GPU box -- the driver's N-GPU runs use RCCL ("nccl")
+    backend = os.environ.get("PCX_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
