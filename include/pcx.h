@@ -1,7 +1,9 @@
 /*
  * pcx.h -- C ABI of libpcx, the MI355X (gfx950) implementation of
  * pyconsensus's Oracle.consensus() hot path (algorithm "PCA", plus "absolute",
- * "big-five", "fixed-variance" and "cokurtosis" on the same kernels).
+ * "big-five", "fixed-variance" and "cokurtosis" on the same kernels, and the
+ * clustering algorithms "k-means", "hierarchical" and "clusterfeck" in the
+ * batched regime).
  *
  * The reference (IanMadlenya/pyconsensus) is pure Python with no FFI: its whole
  * public surface is `Oracle(reports, event_bounds, reputation, ...).consensus()`
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 3
+#define PCX_ABI_VERSION 4
 
 enum pcx_status {
     PCX_OK = 0,
@@ -93,6 +95,15 @@ typedef struct {
     int32_t max_components;       /* "big-five": components summed (Oracle caps it at E, :134-137) */
     double  variance_threshold;   /* "fixed-variance": cumulative explained-variance stop (:448) */
     const double* aux_scores;     /* "cokurtosis": [B][N] caller scores, aux["cokurt"] (:455-457) */
+    /* clustering algorithms (ABI >= 4; __init__.py:392-428) */
+    double  hierarchy_threshold;  /* "hierarchical": fcluster distance cut, Oracle(hierarchy_threshold=0.5) (:406) */
+    double  cluster_threshold;    /* "clusterfeck": leader-clustering cut after the reference's default rule
+                                     log10(E)/1.77 (0.3 when that is 0) (:210-213); <= 0: computed on the device */
+    int32_t kmeans_k;             /* "k-means": code-book size, int(ceil(sqrt(N))) in the reference (:396)     */
+    int32_t kmeans_restarts;      /* "k-means": scipy.cluster.vq.kmeans iter= (20)                              */
+    const int32_t* kmeans_init;   /* "k-means": [B][restarts][k] rows of the initial code books -- the draws of
+                                     scipy's _kpoints, rng.choice(N, k, replace=False) on numpy's global
+                                     RandomState, made by the host so the device replays the same restarts */
 } pcx_batch;
 
 /* Oracle(algorithm=...) values on the GPU path (__init__.py:368-457). */
@@ -102,6 +113,9 @@ enum pcx_algorithm {
     PCX_ALG_BIG_FIVE = 2,          /* eigenvalue-weighted top max_components scores (:373-390) */
     PCX_ALG_FIXED_VARIANCE = 3,    /* components up to variance_threshold (:429-451)           */
     PCX_ALG_COKURTOSIS = 4,        /* caller-supplied scores aux["cokurt"] (:455-457)          */
+    PCX_ALG_KMEANS = 5,            /* cluster sizes of scipy kmeans on whitened wcd (:392-405); batched only */
+    PCX_ALG_HIERARCHICAL = 6,      /* cluster sizes of single-linkage fclusterdata(wcd) (:407-419); batched only */
+    PCX_ALG_CLUSTERFECK = 7,       /* leader clustering of the filled reports (:148-242, :421-424); batched only */
 };
 
 typedef struct {

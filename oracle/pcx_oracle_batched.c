@@ -406,6 +406,318 @@ static int component_scores(int alg, const double (*C)[ES], int E, int N, const 
     return alg == PCX_ALG_FIXED_VARIANCE ? used : -1;
 }
 
+/* ------------------------------------------------------------------------
+ * Clustering algorithms: k-means (:392-405), hierarchical
+ * (:407-419), clusterfeck (:148-242, :421-424).  Each turns the filled reports into
+ * a nonconformity vector nc; the rest of the round is the common tail.
+ * ------------------------------------------------------------------------ */
+
+/* nc from cluster sizes (:398-405, :412-419): (size - min size) / sum, the sum of
+ * integers exact; every cluster the same size gives 0/0 = NaN, as numpy does. */
+static void nc_from_sizes(const int* size, int N, double* nc) {
+    int mn = size[0];
+    for (int i = 1; i < N; i++) mn = size[i] < mn ? size[i] : mn;
+    long long tot = 0;
+    for (int i = 0; i < N; i++) tot += size[i] - mn;
+    for (int i = 0; i < N; i++) nc[i] = (double)(size[i] - mn) / (double)tot;
+}
+
+/* hierarchical: scipy fclusterdata(wcd, t, criterion='distance'), single linkage on
+ * euclidean pdist.  SPEC: d_ij = sqrt(sum_k (wcd_ik - wcd_jk)^2), sequential, no fma
+ * (scipy's pdist order, checked bit for bit); flat clusters = connected components of
+ * {d_ij <= t} (single-linkage cophenetic distance <= t). */
+static void hier_nc(const double (*F)[ES], const double* mu, int N, int E, double t, double* nc) {
+    int parent[NMAX], size[NMAX];
+    for (int i = 0; i < N; i++) parent[i] = i;
+    for (int i = 0; i < N; i++)
+        for (int j = i + 1; j < N; j++) {
+            double d2 = 0.0;
+            for (int k = 0; k < E; k++) {
+                const double df = (F[i][k] - mu[k]) - (F[j][k] - mu[k]);
+                d2 = d2 + df * df;
+            }
+            if (sqrt(d2) <= t) {
+                int a = i, b = j;
+                while (parent[a] != a) a = parent[a];
+                while (parent[b] != b) b = parent[b];
+                if (a != b) parent[a > b ? a : b] = a < b ? a : b;
+            }
+        }
+    int root[NMAX], cnt[NMAX] = {0};
+    for (int i = 0; i < N; i++) {
+        int a = i;
+        while (parent[a] != a) a = parent[a];
+        root[i] = a;
+        cnt[a]++;
+    }
+    for (int i = 0; i < N; i++) size[i] = cnt[root[i]];
+    nc_from_sizes(size, N, nc);
+}
+
+/* k-means distance^2 of scipy's _vq.vq as built here: E < 5 the naive loop
+ * sum (x-c)^2; otherwise -2 x.c (OpenBLAS dgemm: one fma chain per entry for
+ * K < 32, eight interleaved chains summed as a tree for K = 32) + |x|^2 + |c|^2,
+ * the squares sequential.  Measured against scipy 1.15 / scipy-openblas in the
+ * build container (the goldens' origin). */
+static double vq_d2(const double* x, const double* c, int E, double xs, double cs) {
+    if (E < 5) {
+        double s = 0.0;
+        for (int k = 0; k < E; k++) {
+            const double d = x[k] - c[k];
+            s = s + d * d;
+        }
+        return s;
+    }
+    double dot;
+    if (E < 32) {
+        dot = 0.0;
+        for (int k = 0; k < E; k++) dot = fma(x[k], c[k], dot);
+    } else {
+        double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < E; k++) a[k & 7] = fma(x[k], c[k], a[k & 7]);
+        dot = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    }
+    return (-2.0 * dot + xs) + cs;
+}
+
+static double sqsum(const double* x, int E) {
+    double s = 0.0;
+    for (int k = 0; k < E; k++) s = s + x[k] * x[k];
+    return s;
+}
+
+/* vq: labels and distortions of every observation against ncodes codes */
+static void vq_(const double (*obs)[ES], int N, int E, const double (*book)[ES], int ncodes, int* lab,
+                double* dist) {
+    double cs[NMAX];
+    for (int c = 0; c < ncodes; c++) cs[c] = sqsum(book[c], E);
+    for (int i = 0; i < N; i++) {
+        const double xs = sqsum(obs[i], E);
+        double low = INFINITY;
+        int l = 0;
+        for (int c = 0; c < ncodes; c++) {
+            const double d = vq_d2(obs[i], book[c], E, xs, cs[c]);
+            if (d < low) {
+                low = d;
+                l = c;
+            }
+        }
+        lab[i] = l;
+        dist[i] = low > 0 ? sqrt(low) : 0.0;
+    }
+}
+
+/* scipy.cluster.vq._kmeans: Lloyd steps until |avg_prev - avg| <= 1e-5; returns the
+ * code count, *avg = the last mean distortion (np.mean: pairwise sum / N) */
+static int kmeans_run(const double (*obs)[ES], int N, int E, double (*book)[ES], int ncodes, double* avg) {
+    double prev0 = INFINITY, prev1 = INFINITY;
+    int first = 1;
+    for (;;) {
+        int lab[NMAX];
+        double dist[NMAX];
+        vq_(obs, N, E, (const double (*)[ES])book, ncodes, lab, dist);
+        const double a = pw_sum(dist, N) / (double)N;
+        if (first) {
+            prev1 = a;
+            first = 0;
+        } else {
+            prev0 = prev1;
+            prev1 = a;
+        }
+        /* update_cluster_means: member sums in row order, then / count; empty codes dropped */
+        double sum[NMAX][ES];
+        int cnt[NMAX] = {0};
+        for (int c = 0; c < ncodes; c++)
+            for (int k = 0; k < E; k++) sum[c][k] = 0.0;
+        for (int i = 0; i < N; i++) {
+            cnt[lab[i]]++;
+            for (int k = 0; k < E; k++) sum[lab[i]][k] = sum[lab[i]][k] + obs[i][k];
+        }
+        int m = 0;
+        for (int c = 0; c < ncodes; c++)
+            if (cnt[c] > 0) {
+                for (int k = 0; k < E; k++) book[m][k] = sum[c][k] / (double)cnt[c];
+                m++;
+            }
+        ncodes = m;
+        const double diff = fabs(prev0 - prev1);
+        if (!(diff > 1e-5)) break;
+    }
+    *avg = prev1;
+    return ncodes;
+}
+
+static void kmeans_nc(const double (*F)[ES], const double* mu, int N, int E, int k, int restarts,
+                      const int32_t* init, double* nc) {
+    /* whiten(wcd): per-column population std (np.std axis 0: sequential column sums,
+     * pairwise when E == 1), zero std -> 1 */
+    static __thread double obs[NMAX][ES];
+    double sd[EMAX];
+    for (int j = 0; j < E; j++) {
+        double col[NMAX], sq[NMAX];
+        for (int i = 0; i < N; i++) col[i] = F[i][j] - mu[j];
+        double s = 0.0;
+        if (E == 1) s = pw_sum(col, N);
+        else for (int i = 0; i < N; i++) s = s + col[i];
+        const double m = s / (double)N;
+        for (int i = 0; i < N; i++) sq[i] = (col[i] - m) * (col[i] - m);
+        double v = 0.0;
+        if (E == 1) v = pw_sum(sq, N);
+        else for (int i = 0; i < N; i++) v = v + sq[i];
+        sd[j] = sqrt(v / (double)N);
+        if (sd[j] == 0.0) sd[j] = 1.0;
+    }
+    for (int i = 0; i < N; i++)
+        for (int j = 0; j < E; j++) obs[i][j] = (F[i][j] - mu[j]) / sd[j];
+    static __thread double book[NMAX][ES], best[NMAX][ES];
+    double best_d = INFINITY;
+    int best_n = 0;
+    for (int r = 0; r < restarts; r++) {
+        for (int c = 0; c < k; c++) memcpy(book[c], obs[init[r * k + c]], sizeof(double) * E);
+        double d;
+        const int n = kmeans_run((const double (*)[ES])obs, N, E, book, k, &d);
+        if (d < best_d) {
+            best_d = d;
+            best_n = n;
+            for (int c = 0; c < n; c++) memcpy(best[c], book[c], sizeof(double) * E);
+        }
+    }
+    if (best_n == 0) {  /* no restart with a finite distortion: the reference raises */
+        for (int i = 0; i < N; i++) nc[i] = NAN;
+        return;
+    }
+    int lab[NMAX], cnt[NMAX] = {0}, size[NMAX];
+    double dist[NMAX];
+    vq_((const double (*)[ES])obs, N, E, (const double (*)[ES])best, best_n, lab, dist);
+    for (int i = 0; i < N; i++) cnt[lab[i]]++;
+    for (int i = 0; i < N; i++) size[i] = cnt[lab[i]];
+    nc_from_sizes(size, N, nc);
+}
+
+/* clusterfeck L2dist (:148-149): sqrt(np.sum((v1 - v2)**2)), numpy pairwise sum */
+static double l2dist(const double* a, const double* b, int E) {
+    double sq[EMAX];
+    for (int k = 0; k < E; k++) sq[k] = (a[k] - b[k]) * (a[k] - b[k]);
+    return sqrt(pw_sum(sq, E));
+}
+
+typedef struct {
+    int n;                 /* clusters */
+    int first[NMAX];       /* first member (its row is a singleton's meanVec) */
+    int count[NMAX];
+    double rep[NMAX];      /* cmax.rep: running sum of member weights */
+    double sum[NMAX][ES];  /* sum(vec * repVec, axis=0): running, in member order */
+    int of[NMAX];          /* cluster of each row, -1 = none */
+} feck_t;
+
+static void feck_mean(const feck_t* c, const double (*F)[ES], int x, int E, double* m) {
+    for (int k = 0; k < E; k++) m[k] = c->count[x] == 1 ? F[c->first[x]][k] : c->sum[x][k] / c->rep[x];
+}
+
+/* Oracle.cluster (:194-230): rows in order join the nearest cluster (first minimum)
+ * when its mean is closer than thr, else found a new cluster (rows with NaN never do);
+ * returns the mode (first cluster of largest weight, :162-165) */
+static int feck_pass(feck_t* c, const double (*F)[ES], const double* w, int N, int E, double thr) {
+    c->n = 0;
+    for (int i = 0; i < N; i++) {
+        c->of[i] = -1;
+        double sd = 0x1p255;  /* 2**255 */
+        int bx = -1;
+        for (int x = 0; x < c->n; x++) {
+            double m[EMAX];
+            feck_mean(c, F, x, E, m);
+            const double d = l2dist(F[i], m, E);
+            if (d < sd) {
+                sd = d;
+                bx = x;
+            }
+        }
+        if (bx >= 0 && sd < thr) {
+            for (int k = 0; k < E; k++) c->sum[bx][k] = c->sum[bx][k] + F[i][k] * w[i];
+            c->rep[bx] = c->rep[bx] + w[i];
+            c->count[bx]++;
+            c->of[i] = bx;
+        } else {
+            int hasnan = 0;
+            for (int k = 0; k < E; k++) hasnan |= isnan(F[i][k]);
+            if (!hasnan) {
+                const int x = c->n++;
+                c->first[x] = i;
+                c->count[x] = 1;
+                c->rep[x] = w[i];
+                for (int k = 0; k < E; k++) c->sum[x][k] = F[i][k] * w[i];
+                c->of[i] = x;
+            }
+        }
+    }
+    int mode = -1;
+    double top = 0.0;
+    for (int x = 0; x < c->n; x++)
+        if (c->rep[x] > top) {
+            top = c->rep[x];
+            mode = x;
+        }
+    return mode;
+}
+
+/* per-row distance of its cluster's mean to the best mode's mean (:177-183) */
+static void feck_rowdist(const feck_t* c, const double (*F)[ES], int mode, int N, int E, double* dm) {
+    double mm[EMAX], dx[NMAX];
+    feck_mean(c, F, mode, E, mm);
+    for (int x = 0; x < c->n; x++) {
+        double m[EMAX];
+        feck_mean(c, F, x, E, m);
+        dx[x] = l2dist(mm, m, E);
+    }
+    for (int i = 0; i < N; i++) dm[i] = c->of[i] >= 0 ? dx[c->of[i]] : 0.0;
+}
+
+/* clusterfeck: outsideCluster(reports_filled, reptokens) (:185-196, :150-183) */
+static void feck_nc(const double (*F)[ES], const double* tok, int N, int E, double thr, double* nc) {
+    double w[NMAX];
+    for (int i = 0; i < N; i++) w[i] = tok[i] == 0.0 ? 0.00001 : tok[i];  /* :202-204, in the caller's list */
+    if (!(thr > 0.0)) {
+        thr = log10((double)E) / 1.77;
+        if (thr == 0.0) thr = 0.3;
+    }
+    /* outcomes = np.ma.average(features, axis=0, weights=rep) (:167) */
+    double outc[EMAX];
+    {
+        const double scl = pw_sum(w, N);
+        for (int k = 0; k < E; k++) {
+            double num;
+            if (E == 1) {
+                double p[NMAX];
+                for (int i = 0; i < N; i++) p[i] = F[i][k] * w[i];
+                num = pw_sum(p, N);
+            } else {
+                num = F[0][k] * w[0];
+                for (int i = 1; i < N; i++) num = num + F[i][k] * w[i];
+            }
+            outc[k] = num / scl;
+        }
+    }
+    static __thread feck_t c1, c2;
+    double dm[NMAX], m[EMAX];
+    const int mode1 = feck_pass(&c1, F, w, N, E, thr);
+    feck_mean(&c1, F, mode1, E, m);
+    const double d1 = l2dist(m, outc, E);
+    /* best = mode1 (bestDist starts at 2**255); a far mode re-clusters once with 3 x thr */
+    feck_rowdist(&c1, F, mode1, N, E, dm);
+    if (d1 > 1.07) {
+        const int mode2 = feck_pass(&c2, F, w, N, E, thr * 3);
+        feck_mean(&c2, F, mode2, E, m);
+        const double d2 = l2dist(m, outc, E);
+        if (d2 < d1) feck_rowdist(&c2, F, mode2, N, E, dm);
+    }
+    double mx = dm[0];  /* np.amax: NaN propagates */
+    for (int i = 1; i < N; i++)
+        if (isnan(dm[i]) || dm[i] > mx) mx = isnan(mx) ? mx : dm[i];
+    double rv[NMAX];
+    for (int i = 0; i < N; i++) rv[i] = 1.0 - dm[i] / (mx + 0.00000001);
+    normalize_(rv, N, nc);
+}
+
 #define OUT(p, idx, val) do { if (p) (p)[idx] = (val); } while (0)
 
 static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
@@ -493,9 +805,9 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     int comps = -1;
     for (int j = 0; j < E; j++) loading[j] = 0.0; /* no wpca: first_loading = zeros (:359) */
     for (int i = 0; i < N; i++) s[i] = nc[i] = 0.0;
-    if (pca_like) {
+    double mu[EMAX];
+    if (pca_like || alg >= PCX_ALG_KMEANS) {  /* the clustering algorithms call wpca too (:393, :408, :422) */
         /* --- a5: weighted mean (np.ma.average, :317-319) --- */
-        double mu[EMAX];
         double den = pw_sum(rep, N);
         for (int j = 0; j < E; j++) {
             double acc;
@@ -524,7 +836,9 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         for (int j = 0; j < E; j++) sq[j] = v[j] * v[j];
         double nv = sqrt(pw_sum(sq, E));
         for (int j = 0; j < E; j++) loading[j] = v[j] / nv;
-        if (alg == PCX_ALG_PCA) {
+        if (alg >= PCX_ALG_KMEANS) {
+            /* loading only: scores stay zeros */
+        } else if (alg == PCX_ALG_PCA) {
             for (int i = 0; i < N; i++) {
                 double acc = 0.0;
                 for (int j = 0; j < E; j++) acc = fma(F[i][j] - mu[j], loading[j], acc);
@@ -539,7 +853,16 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     } else if (alg == PCX_ALG_COKURTOSIS) {  /* caller-supplied scores (:455-457) */
         for (int i = 0; i < N; i++) s[i] = in->aux_scores[b * N + i];
     }
-    if (alg != PCX_ALG_ABSOLUTE) {
+    const int clustering = alg >= PCX_ALG_KMEANS;
+    if (clustering) {  /* scores stay zeros (:357); nc from the clusters */
+        if (alg == PCX_ALG_HIERARCHICAL)
+            hier_nc((const double (*)[ES])F, mu, N, E, in->hierarchy_threshold, nc);
+        else if (alg == PCX_ALG_KMEANS)
+            kmeans_nc((const double (*)[ES])F, mu, N, E, in->kmeans_k, in->kmeans_restarts,
+                      in->kmeans_init + b * in->kmeans_restarts * in->kmeans_k, nc);
+        else
+            feck_nc((const double (*)[ES])F, tok, N, E, in->cluster_threshold, nc);
+    } else if (alg != PCX_ALG_ABSOLUTE) {
         /* --- a8/a9: nonconformity_rank (:487-500), tie -> nonconformity (:475-485); the
          * other algorithms call nonconformity directly (:389, :450, :456) --- */
         double mn = s[0], mx = s[0];
@@ -703,7 +1026,10 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
 /* Host-memory restatement of pcx_consensus_batched_f64 (same structs). */
 int pcxo_consensus_batched_f64(const pcx_batch* in, pcx_batch_result* out, int n_threads) {
     if (!in || !out || in->n_reporters < 1 || in->n_reporters > NMAX || in->n_events < 1 ||
-        in->n_events > EMAX || in->n_rounds < 0 || in->algorithm < 0 || in->algorithm > PCX_ALG_COKURTOSIS)
+        in->n_events > EMAX || in->n_rounds < 0 || in->algorithm < 0 || in->algorithm > PCX_ALG_CLUSTERFECK)
+        return PCX_EINVAL;
+    if (in->algorithm == PCX_ALG_KMEANS &&
+        (!in->kmeans_init || in->kmeans_k < 1 || in->kmeans_k > in->n_reporters || in->kmeans_restarts < 1))
         return PCX_EINVAL;
     if (in->algorithm == PCX_ALG_BIG_FIVE && (in->max_components < 1 || in->max_components > in->n_events))
         return PCX_EINVAL;

@@ -12,6 +12,7 @@ import subprocess
 import numpy as np
 
 from pyconsensus_amd._abi import BATCH_OUTPUTS, Batch, BatchResult, out_shape, ALGORITHMS
+from pyconsensus_amd.batched import clusterfeck_threshold
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "lib", "libpcx_oracle.so")
@@ -39,7 +40,8 @@ def _ptr(a):
 
 def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_tolerance=0.1,
             alpha=0.1, int_dtype=False, algorithm="PCA", threads=1, want=None, max_components=5,
-            variance_threshold=0.9, aux_scores=None):
+            variance_threshold=0.9, aux_scores=None, hierarchy_threshold=0.5, kmeans_init=None,
+            cluster_threshold=None):
     """Run B rounds; returns {name: array} for every output in ``want`` (default: all)."""
     R = np.ascontiguousarray(reports, dtype=np.float64)
     B, N, E = R.shape
@@ -56,9 +58,14 @@ def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_toler
     hi_ = cont(hi, np.float64)
     rp = cont(reputation, np.float64)
     ax = cont(aux_scores, np.float64)
+    ki = cont(kmeans_init, np.int32)
+    k = restarts = 0
+    if ki is not None:
+        restarts, k = ki.shape[1], ki.shape[2]
+    cthr = clusterfeck_threshold(E) if cluster_threshold is None else float(cluster_threshold)
     inp = Batch(B, N, E, _ptr(R), _ptr(rp), _ptr(sc), _ptr(lo_), _ptr(hi_), int(shared), int(bool(int_dtype)),
                 float(catch_tolerance), float(alpha), ALGORITHMS[algorithm], int(min(max_components, E)),
-                float(variance_threshold), _ptr(ax))
+                float(variance_threshold), _ptr(ax), float(hierarchy_threshold), cthr, k, restarts, _ptr(ki))
     outs = {}
     res = BatchResult()
     for name, kind, dt in BATCH_OUTPUTS:

@@ -1,15 +1,19 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
 FLAG_ZERO_COV, FLAG_SVD_FAIL, FLAG_PI_MAXIT = 1, 2, 4
-# enum pcx_algorithm (include/pcx.h); k-means / hierarchical / clusterfeck are not on the GPU path
+# enum pcx_algorithm (include/pcx.h); the clustering algorithms run in the batched regime only
 ALG_PCA, ALG_ABSOLUTE, ALG_BIG_FIVE, ALG_FIXED_VARIANCE, ALG_COKURTOSIS = 0, 1, 2, 3, 4
+ALG_KMEANS, ALG_HIERARCHICAL, ALG_CLUSTERFECK = 5, 6, 7
 ALGORITHMS = {"PCA": ALG_PCA, "absolute": ALG_ABSOLUTE, "big-five": ALG_BIG_FIVE,
-              "fixed-variance": ALG_FIXED_VARIANCE, "cokurtosis": ALG_COKURTOSIS}
+              "fixed-variance": ALG_FIXED_VARIANCE, "cokurtosis": ALG_COKURTOSIS,
+              "k-means": ALG_KMEANS, "hierarchical": ALG_HIERARCHICAL, "clusterfeck": ALG_CLUSTERFECK}
+CLUSTER_ALGORITHMS = ("k-means", "hierarchical", "clusterfeck")
+KMEANS_RESTARTS = 20  # scipy.cluster.vq.kmeans(iter=20)
 
 P_D = C.POINTER(C.c_double)
 
@@ -32,6 +36,11 @@ class Batch(C.Structure):
         ("max_components", C.c_int32),
         ("variance_threshold", C.c_double),
         ("aux_scores", C.c_void_p),
+        ("hierarchy_threshold", C.c_double),
+        ("cluster_threshold", C.c_double),
+        ("kmeans_k", C.c_int32),
+        ("kmeans_restarts", C.c_int32),
+        ("kmeans_init", C.c_void_p),
     ]
 
 

@@ -10,16 +10,46 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
+
 from . import _abi, _device, _lib
 
 MAX_REPORTERS = 64
 MAX_EVENTS = 32
 
 
+def kmeans_k(N):
+    """Code-book size of the reference's k-means, int(ceil(sqrt(N))) (__init__.py:396)."""
+    return int(np.ceil(np.sqrt(N)))
+
+
+def kmeans_draws(B, N, restarts=_abi.KMEANS_RESTARTS, random_state=None):
+    """Initial code-book rows of B k-means rounds, [B][restarts][k] int32.
+
+    scipy.cluster.vq.kmeans(obs, k) (seed=None, __init__.py:397) draws each restart's
+    code book as ``rng.choice(N, size=k, replace=False)`` on numpy's global RandomState;
+    these are the same draws in the same order (round after round), so a batch consumes
+    the global stream exactly as B sequential reference consensus() calls would."""
+    rs = np.random.mtrand._rand if random_state is None else random_state
+    k = kmeans_k(N)
+    out = np.empty((B, restarts, k), dtype=np.int32)
+    for b in range(B):
+        for r in range(restarts):
+            out[b, r] = rs.choice(N, size=k, replace=False)
+    return out
+
+
+def clusterfeck_threshold(E):
+    """The reference's default leader-clustering cut (__init__.py:187-190, 210-213)."""
+    t = np.log10(E) / 1.77
+    return 0.3 if t == 0 else float(t)
+
+
 def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
                       catch_tolerance=0.1, alpha=0.1, int_dtype=False, algorithm="PCA",
                       outputs=None, device=None, filled=False, original=False,
-                      max_components=5, variance_threshold=0.9, aux_scores=None):
+                      max_components=5, variance_threshold=0.9, aux_scores=None,
+                      hierarchy_threshold=0.5, kmeans_init=None, cluster_threshold=None):
     """Run B rounds of N x E reports on the GPU.
 
     reports:    (B, N, E) float64, NaN = missing (0.0 is missing too, as in the reference)
@@ -27,8 +57,12 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     scaled/lo/hi: event bounds, (B, E) or (E,) shared by every round; None = all binary
     outputs:    iterable of result names to produce (default: all vector/scalar outputs)
     algorithm:  "PCA" (default), "absolute", "big-five", "fixed-variance", "cokurtosis"
-                (__init__.py:368-457); max_components is capped at E like Oracle (:134-137);
-                aux_scores (B, N) are aux["cokurt"] of each round
+                (__init__.py:368-457), "k-means", "hierarchical", "clusterfeck" (:392-428);
+                max_components is capped at E like Oracle (:134-137); aux_scores (B, N)
+                are aux["cokurt"] of each round
+    kmeans_init: (B, restarts, k) initial code-book rows (default: :func:`kmeans_draws`
+                on numpy's global RandomState, as the reference's scipy call draws them)
+    cluster_threshold: clusterfeck's cut (default: the reference's log10(E)/1.77 rule)
 
     Returns a dict of torch tensors on the device, named like the ABI fields
     (``smooth_rep``, ``outcomes_final``, ...).  Asynchronous on torch's current stream.
@@ -66,10 +100,23 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
         aux = _device.as_device(aux_scores, t.float64, dev)
         if tuple(aux.shape) != (B, N):
             raise ValueError("aux_scores must be (B, N)")
+    kinit = None
+    k = restarts = 0
+    if alg == _abi.ALG_KMEANS:
+        if kmeans_init is None:
+            kmeans_init = kmeans_draws(B, N)
+        kinit = _device.as_device(kmeans_init, t.int32, dev)
+        if kinit.dim() != 3 or kinit.shape[0] != B:
+            raise ValueError("kmeans_init must be (B, restarts, k)")
+        restarts, k = int(kinit.shape[1]), int(kinit.shape[2])
+        if not (1 <= k <= N) or restarts < 1 or int(kinit.min()) < 0 or int(kinit.max()) >= N:
+            raise ValueError("kmeans_init rows must lie in [0, N) with 1 <= k <= N")
+    cthr = clusterfeck_threshold(E) if cluster_threshold is None else float(cluster_threshold)
     mc = int(max_components) if E >= int(max_components) else E  # __init__.py:134-137
     inp = _abi.Batch(B, N, E, _device.ptr(R), _device.ptr(rep), _device.ptr(sc), _device.ptr(lo_),
                      _device.ptr(hi_), shared, int(bool(int_dtype)), float(catch_tolerance),
-                     float(alpha), alg, mc, float(variance_threshold), _device.ptr(aux))
+                     float(alpha), alg, mc, float(variance_threshold), _device.ptr(aux),
+                     float(hierarchy_threshold), cthr, k, restarts, _device.ptr(kinit))
     res = _abi.BatchResult()
     outs = {}
     for name, kind, dt in _abi.BATCH_OUTPUTS:
@@ -83,5 +130,5 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
         setattr(res, name, x.data_ptr())
     h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev))
     _lib.check(_lib.lib().pcx_consensus_batched_f64(h, C.byref(inp), C.byref(res)))
-    outs["_inputs"] = (R, rep, sc, lo_, hi_, aux)  # keep inputs alive until the caller syncs
+    outs["_inputs"] = (R, rep, sc, lo_, hi_, aux, kinit)  # keep inputs alive until the caller syncs
     return outs

@@ -584,6 +584,57 @@ def algos_main(ref):
     print("algos: %d cases, %d flagged near-tie" % (len(cases), nt))
 
 
+def clusters_main(ref):
+    """algorithm = k-means / hierarchical / clusterfeck (__init__.py:392-428):
+    KAT matrices, seeded 50 x 20 rounds and mixed small shapes (the batched regime).  k-means
+    draws its initial code books from numpy's global RandomState (scipy.cluster.vq.kmeans,
+    seed=None): every case seeds it first and records the seed (in_np_seed)."""
+    from pyconsensus_amd import synthetic
+
+    out = {}
+    algos = ("k-means", "hierarchical", "clusterfeck")
+
+    def add(name, reports, bounds, rep, alg, seed, **extra):
+        kw = dict(algorithm=alg, **extra)
+        np.random.seed(seed)
+        d = run_case(ref, reports, bounds, rep, **kw)
+        d["in_np_seed"] = np.array(seed)
+        d["in_hierarchy_threshold"] = np.array(float(extra.get("hierarchy_threshold", 0.5)))
+        for k, v in d.items():
+            out[name + "/" + k] = v
+
+    kats = kat_cases()
+    for nm in ("readme", "docstring", "t1", "t2", "t3", "t4", "t5", "t6", "t8", "t10", "missing", "scaled_cli",
+               "test_base_shift", "q_float_rep", "q_alpha"):
+        if nm not in kats:
+            continue
+        spec = kats[nm]
+        kw = {k: v for k, v in spec.items() if k not in ("reports", "bounds", "reputation")}
+        for a_i, alg in enumerate(algos):
+            extra = dict(kw)
+            if alg == "hierarchical":
+                extra["hierarchy_threshold"] = 1.5
+            add("%s@%s" % (nm, alg), spec["reports"], spec.get("bounds"), spec.get("reputation"), alg,
+                2000 + a_i, **extra)
+    thr = (0.5, 1.5, 2.5, 3.5)
+    for a_i, alg in enumerate(algos):
+        R, sc, lo, hi, rep = synthetic.rounds(120, 50, 20, seed=40 + a_i)
+        for b in range(R.shape[0]):
+            extra = {"hierarchy_threshold": thr[b % 4]} if alg == "hierarchical" else {}
+            add("s%03d@%s" % (b, alg), R[b], synthetic.bounds_list(sc[b], lo[b], hi[b]), rep[b], alg,
+                100 * b + a_i, **extra)
+        rng = np.random.default_rng(61 + a_i)
+        for k in range(40):
+            n, e = int(rng.integers(2, 65)), int(rng.integers(1, 33))
+            Rm, sm, lom, him, repm = synthetic.rounds(1, n, e, seed=7000 + 100 * a_i + k, reputation=bool(k % 3))
+            extra = {"hierarchy_threshold": float(rng.choice(thr))} if alg == "hierarchical" else {}
+            add("m%03d@%s" % (k, alg), Rm[0], synthetic.bounds_list(sm[0], lom[0], him[0]) if k % 4 else None,
+                None if repm is None else repm[0], alg, 9100 + k, **extra)
+    np.savez_compressed(os.path.join(HERE, "clusters.npz"), **out)
+    cases = split_keys(out)
+    print("clusters: %d cases" % len(cases))
+
+
 def split_keys(flat):
     res = {}
     for k, v in flat.items():
@@ -595,5 +646,7 @@ def split_keys(flat):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "algos":
         algos_main(load_reference())
+    elif len(sys.argv) > 1 and sys.argv[1] == "clusters":
+        clusters_main(load_reference())
     else:
         main()

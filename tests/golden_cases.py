@@ -95,3 +95,14 @@ def algo_kwargs(case):
     if "in_aux_scores" in case:
         kw["aux"] = {"cokurt": case["in_aux_scores"]}
     return kw
+
+
+def clusters():
+    """k-means / hierarchical / clusterfeck cases (make_golden.py clusters_main)."""
+    return split_cases(load("clusters.npz"))
+
+
+def cluster_kwargs(case):
+    """Extra constructor kwargs of a clusters.npz case (k-means also needs numpy's global
+    RandomState seeded with case['in_np_seed'] before the call)."""
+    return {"hierarchy_threshold": float(case["in_hierarchy_threshold"])}
