@@ -512,7 +512,7 @@ static void vq_(const double (*obs)[ES], int N, int E, const double (*book)[ES],
 static int kmeans_run(const double (*obs)[ES], int N, int E, double (*book)[ES], int ncodes, double* avg) {
     double prev0 = INFINITY, prev1 = INFINITY;
     int first = 1;
-    for (;;) {
+    for (int it = 0;; it++) {
         int lab[NMAX];
         double dist[NMAX];
         vq_(obs, N, E, (const double (*)[ES])book, ncodes, lab, dist);
@@ -541,7 +541,7 @@ static int kmeans_run(const double (*obs)[ES], int N, int E, double (*book)[ES],
             }
         ncodes = m;
         const double diff = fabs(prev0 - prev1);
-        if (!(diff > 1e-5)) break;
+        if (!(diff > 1e-5) || it + 1 >= 4096) break;  /* 4096: the device's guard (KMEANS_MAXIT) */
     }
     *avg = prev1;
     return ncodes;

@@ -78,8 +78,14 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     if (in->n_events < 1 || in->n_events > 32) return fail(PCX_EINVAL, "batched: n_events must be in [1, 32]");
     if (!in->reports) return fail(PCX_EINVAL, "batched: reports is NULL");
     if (in->scaled && (!in->lo || !in->hi)) return fail(PCX_EINVAL, "batched: scaled given without lo/hi");
-    if (in->algorithm < PCX_ALG_PCA || in->algorithm > PCX_ALG_COKURTOSIS)
-        return fail(PCX_EINVAL, "batched: algorithm must be an enum pcx_algorithm value (0..4)");
+    if (in->algorithm < PCX_ALG_PCA || in->algorithm > PCX_ALG_CLUSTERFECK)
+        return fail(PCX_EINVAL, "batched: algorithm must be an enum pcx_algorithm value (0..7)");
+    if (in->algorithm == PCX_ALG_KMEANS &&
+        (!in->kmeans_init || in->kmeans_k < 1 || in->kmeans_k > 8 || in->kmeans_k > in->n_reporters ||
+         in->kmeans_restarts < 1))
+        return fail(PCX_EINVAL, "batched: k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 8), restarts >= 1");
+    if (in->algorithm == PCX_ALG_HIERARCHICAL && std::isnan(in->hierarchy_threshold))
+        return fail(PCX_EINVAL, "batched: hierarchy_threshold is NaN");
     if (in->algorithm == PCX_ALG_BIG_FIVE && (in->max_components < 1 || in->max_components > in->n_events))
         return fail(PCX_EINVAL, "batched: big-five needs 1 <= max_components <= n_events");
     if (in->algorithm == PCX_ALG_FIXED_VARIANCE && !std::isfinite(in->variance_threshold))
@@ -106,6 +112,11 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     a.max_components = in->max_components;
     a.variance_threshold = in->variance_threshold;
     a.aux_scores = in->aux_scores;
+    a.hierarchy_threshold = in->hierarchy_threshold;
+    a.cluster_threshold = in->cluster_threshold;
+    a.kmeans_k = in->kmeans_k;
+    a.kmeans_restarts = in->kmeans_restarts;
+    a.kmeans_init = in->kmeans_init;
     a.catch_tol = in->catch_tolerance;
     a.alpha = in->alpha;
     a.old_rep = out->old_rep;

@@ -597,13 +597,397 @@ __device__ void jacobi_eig_wave(double* A, double* V, int ES, int E, double* pc,
     }
 }
 
+// ---- clustering algorithms (SPEC: oracle/pcx_oracle_batched.c) ------
+// k-means (:392-405), hierarchical (:407-419) and clusterfeck (:148-242, :421-424) each
+// turn the filled reports into the nonconformity vector; they run in their own kernel
+// instantiation (CLUS = true) with an extra LDS region X, so the PCA kernel is untouched.
+constexpr int KMAX = 8;  // k-means code books: ceil(sqrt(64))
+constexpr int KMEANS_MAXIT = 4096;  // Lloyd steps per restart (a guard; scipy has none)
+
+__host__ __device__ inline int cluster_lds_doubles(int N, int E, int ES) {
+    const int nr = smem_rows(N), ne = smem_evs(E);
+    const int feck = N * ES + 6 * nr + 2 * ne;                          // sums, 6 row vectors, outcomes
+    const int km = N * ES + 2 * KMAX * ES + ne + 2 * nr + 2 * KMAX;     // obs, books, sd, labels, counts
+    return feck > km ? feck : km;
+}
+
+// numpy pairwise add.reduce of get(0..n-1) on ONE lane (n <= 128: eight accumulators)
+template <class G>
+__device__ __forceinline__ double lane_pw_sum(G get, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; i++) r += get(i);
+        return r;
+    }
+    double r0 = get(0), r1 = get(1), r2 = get(2), r3 = get(3), r4 = get(4), r5 = get(5), r6 = get(6), r7 = get(7);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+        r0 += get(i); r1 += get(i + 1); r2 += get(i + 2); r3 += get(i + 3);
+        r4 += get(i + 4); r5 += get(i + 5); r6 += get(i + 6); r7 += get(i + 7);
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) res += get(i);
+    return res;
+}
+
+// (size - min size) / sum over the row lanes (:398-405); the integer sum is exact, and
+// equal sizes give 0/0 = NaN as numpy does
+__device__ __forceinline__ double nc_from_sizes(double size, bool row) {
+    const double mn = -wave_max(row ? -size : -__builtin_inf());
+    const double tot = tree_sum(row ? size - mn : 0.0);
+    return row ? (size - mn) / tot : 0.0;
+}
+
+// hierarchical: single-linkage flat clusters at cophenetic distance <= t = connected
+// components of {d_ij <= t}, d_ij = sqrt(sequential sum of squared wcd differences)
+// (scipy pdist order).  Lane i owns row i's adjacency mask; masks are closed under
+// "OR the masks of my members" until no lane changes.
+__device__ __noinline__ double hier_nc(const double* F, const double* mu, int ES, int N, int E, double t,
+                                       uint64_t* comp) {
+    const int l = lane_id();
+    const bool row = l < N;
+    uint64_t adj = 0;
+    if (row) {
+        adj = 1ull << l;
+        for (int j = 0; j < N; j++) {
+            double d2 = 0.0;
+            for (int k = 0; k < E; k++) {
+                const double df = (F[l * ES + k] - mu[k]) - (F[j * ES + k] - mu[k]);
+                d2 = d2 + df * df;
+            }
+            if (sqrt(d2) <= t) adj |= 1ull << j;
+        }
+        comp[l] = adj;
+    }
+    wsync();
+    for (;;) {
+        uint64_t nw = adj;
+        if (row) {
+            uint64_t m = adj;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                nw |= comp[j];
+            }
+        }
+        const bool changed = nw != adj;
+        wsync();
+        if (row) comp[l] = nw;
+        adj = nw;
+        wsync();
+        if (!ballot(changed)) break;
+    }
+    return nc_from_sizes(row ? (double)popc(adj) : 0.0, row);
+}
+
+// scipy _vq.vq distance^2 as built in the goldens' container: naive for E < 5, else
+// -2 x.c (OpenBLAS: one fma chain for K < 32, eight chains + tree at K = 32) + |x|^2 + |c|^2
+__device__ __forceinline__ double vq_d2(const double* x, const double* c, int E, double xs, double cs) {
+    if (E < 5) {
+        double s = 0.0;
+        for (int k = 0; k < E; k++) {
+            const double d = x[k] - c[k];
+            s = s + d * d;
+        }
+        return s;
+    }
+    double dot;
+    if (E < 32) {
+        dot = 0.0;
+        for (int k = 0; k < E; k++) dot = fma(x[k], c[k], dot);
+    } else {
+        double q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < E; k += 8)
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k + u < E) q[u] = fma(x[k + u], c[k + u], q[u]);
+        dot = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+    }
+    return (-2.0 * dot + xs) + cs;
+}
+
+__device__ __forceinline__ double sqsum(const double* x, int E) {
+    double s = 0.0;
+    for (int k = 0; k < E; k++) s = s + x[k] * x[k];
+    return s;
+}
+
+// k-means: whiten(wcd), scipy kmeans(obs, k) over the host-drawn restarts (best mean
+// distortion, strict <), vq labels, cluster sizes.  Lane i = observation i in vq;
+// lanes take (code, feature) pairs in the mean update.
+__device__ __noinline__ double kmeans_nc(const BatchArgs& a, int64_t b, const double* F, const double* mu, int ES,
+                                         int N, int E, double* X) {
+    const int l = lane_id();
+    const bool row = l < N, col = l < E;
+    const int nr = smem_rows(N), ne = smem_evs(E);
+    double* obs = X;                       // [N][ES]
+    double* book = obs + N * ES;           // [KMAX][ES]
+    double* best = book + KMAX * ES;       // [KMAX][ES]
+    double* sd = best + KMAX * ES;         // [E]
+    int* lab = reinterpret_cast<int*>(sd + ne);  // [N]
+    double* csq = sd + ne + 2 * nr;        // [KMAX]
+    int* cntv = reinterpret_cast<int*>(csq + KMAX);  // [KMAX]
+    // np.std(wcd, axis=0): sequential column sums (pairwise when E == 1); 0 -> 1
+    double sdj = 0.0;
+    if (E == 1) {
+        const double w = row ? F[l * ES] - mu[0] : 0.0;
+        const double m = wave_pw_sum(w, row) / (double)N;
+        const double q = row ? (w - m) * (w - m) : 0.0;
+        sdj = sqrt(wave_pw_sum(q, row) / (double)N);
+    } else if (col) {
+        double s = 0.0;
+        for (int i = 0; i < N; i++) s = s + (F[i * ES + l] - mu[l]);
+        const double m = s / (double)N;
+        double v = 0.0;
+        for (int i = 0; i < N; i++) {
+            const double d = (F[i * ES + l] - mu[l]) - m;
+            v = v + d * d;
+        }
+        sdj = sqrt(v / (double)N);
+    }
+    if (sdj == 0.0) sdj = 1.0;
+    if (col) sd[l] = sdj;
+    wsync();
+    for (int o = l; o < N * E; o += W) {
+        const int i = o / E, k = o - i * E;
+        obs[i * ES + k] = (F[i * ES + k] - mu[k]) / sd[k];
+    }
+    wsync();
+    const double xs = row ? sqsum(obs + l * ES, E) : 0.0;
+    const int K = a.kmeans_k, RS = a.kmeans_restarts;
+    const int32_t* init = a.kmeans_init + b * (int64_t)RS * K;
+    double best_d = __builtin_inf();
+    int best_n = 0;
+    for (int r = 0; r < RS; r++) {
+        for (int o = l; o < K * E; o += W) {
+            const int c = o / E, k = o - c * E;
+            const int row0 = init[r * K + c];
+            book[c * ES + k] = obs[(row0 < 0 ? 0 : row0 >= N ? N - 1 : row0) * ES + k];
+        }
+        int nc = K;
+        double prev0 = __builtin_inf(), prev1 = __builtin_inf();
+        for (int it = 0;; it++) {
+            wsync();
+            if (l < nc) csq[l] = sqsum(book + l * ES, E);
+            wsync();
+            int li = 0;
+            double low = __builtin_inf();
+            if (row)
+                for (int c = 0; c < nc; c++) {
+                    const double d = vq_d2(obs + l * ES, book + c * ES, E, xs, csq[c]);
+                    if (d < low) {
+                        low = d;
+                        li = c;
+                    }
+                }
+            const double dist = row ? (low > 0 ? sqrt(low) : 0.0) : 0.0;
+            prev0 = prev1;
+            prev1 = wave_pw_sum(dist, row) / (double)N;
+            if (row) lab[l] = li;
+            wsync();
+            // update_cluster_means: member sums in row order, / count; empty codes dropped
+            int cnt = 0;
+            if (l < nc)
+                for (int i = 0; i < N; i++) cnt += lab[i] == l;
+            const uint64_t nonempty = ballot(l < nc && cnt > 0);
+            double nv[4];
+            int nk[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int p = l + W * q;
+                nk[q] = -1;
+                if (p < nc * E) {
+                    const int c = p / E, k = p - c * E;
+                    double sm = 0.0;
+                    int n = 0;
+                    for (int i = 0; i < N; i++)
+                        if (lab[i] == c) {
+                            sm = sm + obs[i * ES + k];
+                            n++;
+                        }
+                    if (n > 0) {
+                        nv[q] = sm / (double)n;
+                        nk[q] = popc(nonempty & ((1ull << c) - 1)) * ES + k;
+                    }
+                }
+            }
+            wsync();
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (nk[q] >= 0) book[nk[q]] = nv[q];
+            nc = popc(nonempty);
+            if (!(fabs(prev0 - prev1) > 1e-5) || it + 1 >= KMEANS_MAXIT) break;
+        }
+        wsync();
+        if (prev1 < best_d) {
+            best_d = prev1;
+            best_n = nc;
+            for (int o = l; o < nc * ES; o += W) best[o] = book[o];
+        }
+    }
+    wsync();
+    if (best_n == 0) return row ? __builtin_nan("") : 0.0;  // no finite distortion: the reference raises
+    if (l < best_n) csq[l] = sqsum(best + l * ES, E);
+    wsync();
+    int li = 0;
+    double low = __builtin_inf();
+    if (row)
+        for (int c = 0; c < best_n; c++) {
+            const double d = vq_d2(obs + l * ES, best + c * ES, E, xs, csq[c]);
+            if (d < low) {
+                low = d;
+                li = c;
+            }
+        }
+    if (row) lab[l] = li;
+    wsync();
+    if (l < best_n) {
+        int n = 0;
+        for (int i = 0; i < N; i++) n += lab[i] == l;
+        cntv[l] = n;
+    }
+    wsync();
+    return nc_from_sizes(row ? (double)cntv[li] : 0.0, row);
+}
+
+// clusterfeck: leader clustering of the filled reports with the token weights (0 -> 1e-5),
+// mode = heaviest cluster; a mode farther than 1.07 from the weighted outcomes re-clusters
+// once at 3x the cut and the closer mode wins; nc = normalize(1 - dist(own cluster, mode) /
+// (max + 1e-8)).  Rows are visited in order (wave-uniform); lane x = cluster x.
+struct Feck {
+    double* sum;   // [N][ES] sum(vec * repVec, axis=0), running in member order
+    double* crep;  // [N] running member weight
+    int* first;    // [N] founding row (a singleton's meanVec)
+    int* count;    // [N]
+    int* of;       // [N] cluster of each row, -1 = none
+    double* dx;    // [N] per-cluster distance to the mode
+    const double* F;
+    int ES, E;
+    __device__ double mean(int x, int k) const {
+        return count[x] == 1 ? F[first[x] * ES + k] : sum[x * ES + k] / crep[x];
+    }
+};
+
+// one cluster() pass (:194-230); returns the mode (:162-165) and, through dm, the row
+// distances of process() (:177-183) for that mode, and the mode's distance to outc
+__device__ __noinline__ void feck_pass(Feck& f, const double* wv, int N, double thr, const double* outc, double& dmode,
+                                       double& dm) {
+    const int l = lane_id(), E = f.E, ES = f.ES;
+    const bool col = l < E;
+    int ncl = 0;
+    for (int i = 0; i < N; i++) {
+        const double* Fi = f.F + i * ES;
+        const bool valid = l < ncl;
+        double d = 0.0;
+        if (valid)
+            d = sqrt(lane_pw_sum([&](int k) { const double t = Fi[k] - f.mean(l, k); return t * t; }, E));
+        const bool cand = valid && d < 0x1p255;
+        const double dmin = -wave_max(cand ? -d : -__builtin_inf());
+        const uint64_t at = ballot(cand && d == dmin);
+        const double wi = wv[i];
+        if (at && dmin < thr) {
+            const int bx = __builtin_ctzll(at);
+            if (col) f.sum[bx * ES + l] = f.sum[bx * ES + l] + Fi[l] * wi;
+            wsync();
+            if (l == 0) {
+                f.crep[bx] = f.crep[bx] + wi;
+                f.count[bx] += 1;
+                f.of[i] = bx;
+            }
+        } else if (!ballot(col && __builtin_isnan(Fi[l]))) {
+            const int x = ncl++;
+            if (col) f.sum[x * ES + l] = Fi[l] * wi;
+            if (l == 0) {
+                f.first[x] = i;
+                f.count[x] = 1;
+                f.crep[x] = wi;
+                f.of[i] = x;
+            }
+        } else if (l == 0) {
+            f.of[i] = -1;
+        }
+        wsync();
+    }
+    const bool valid = l < ncl;
+    const double r = valid ? f.crep[l] : 0.0;
+    const double top = wave_max(valid ? r : -__builtin_inf());
+    const uint64_t tm = ballot(valid && r == top && r > 0.0);
+    const int mode = tm ? __builtin_ctzll(tm) : 0;
+    dmode = sqrt(lane_pw_sum([&](int k) { const double t = f.mean(mode, k) - outc[k]; return t * t; }, E));
+    if (valid) f.dx[l] = sqrt(lane_pw_sum([&](int k) { const double t = f.mean(mode, k) - f.mean(l, k); return t * t; }, E));
+    wsync();
+    dm = 0.0;
+    if (l < N) {
+        const int o = f.of[l];
+        dm = o >= 0 ? f.dx[o] : 0.0;
+    }
+    wsync();
+}
+
+__device__ __noinline__ double feck_nc(const BatchArgs& a, const double* F, int ES, int N, int E, double rep,
+                                       double* X) {
+    const int l = lane_id();
+    const bool row = l < N, col = l < E;
+    const int nr = smem_rows(N), ne = smem_evs(E);
+    Feck f;
+    f.F = F;
+    f.ES = ES;
+    f.E = E;
+    f.sum = X;
+    f.crep = X + N * ES;
+    f.first = reinterpret_cast<int*>(f.crep + nr);
+    f.count = reinterpret_cast<int*>(f.crep + 2 * nr);
+    f.of = reinterpret_cast<int*>(f.crep + 3 * nr);
+    f.dx = f.crep + 4 * nr;
+    double* wv = f.crep + 5 * nr;
+    double* outc = wv + nr;  // [E]
+    const double tok = trunc(rep * 1e6);
+    const double w = row ? (tok == 0.0 ? 0.00001 : tok) : 0.0;  // :202-204
+    if (row) wv[l] = w;
+    double thr = a.cluster_threshold;
+    if (!(thr > 0.0)) {
+        thr = log10((double)E) / 1.77;
+        if (thr == 0.0) thr = 0.3;
+    }
+    // outcomes = np.ma.average(features, axis=0, weights=rep) (:167)
+    const double scl = wave_pw_sum(w, row);
+    if (E == 1) {
+        const double num = wave_pw_sum(row ? F[l * ES] * w : 0.0, row);
+        if (l == 0) outc[0] = num / scl;
+    }
+    wsync();
+    if (E > 1 && col) {
+        double num = F[l] * wv[0];
+        for (int i = 1; i < N; i++) num = num + F[i * ES + l] * wv[i];
+        outc[l] = num / scl;
+    }
+    wsync();
+    (void)ne;
+    double d1, dm;
+    feck_pass(f, wv, N, thr, outc, d1, dm);
+    if (d1 > 1.07) {  // :174-176
+        double d2, dm2;
+        feck_pass(f, wv, N, thr * 3, outc, d2, dm2);
+        if (d2 < d1) dm = dm2;
+    }
+    const double mx = wave_max(row ? dm : -__builtin_inf());
+    const double rv = 1.0 - dm / (mx + 0.00000001);
+    double u = row ? fabs(rv) : 0.0;
+    double Su = wave_pw_sum(u, row);
+    if (Su == 0) {
+        u += 1.0;
+        Su = wave_pw_sum(u, row);
+    }
+    return row ? u / Su : 0.0;
+}
+
 }  // namespace
 
 // NT/ET > 0: the round shape is a compile-time constant (the Monte Carlo shapes the
 // launcher specialises, e.g. the 50 x 20 of config C3): every loop bound is known, so
 // the sequential column/row loops unroll and their LDS reads issue ahead of the
 // dependent adds.  NT = ET = 0: any N <= 64, E <= 32 at run time.  Same arithmetic.
-template <int NT, int ET>
+template <int NT, int ET, bool CLUS>
 __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? (ET | 1) : a.ES;
@@ -794,7 +1178,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     double sc_i = 0.0, nc_i = 0.0, ld_j = 0.0;
     int branch = 5, flags = 0, iters = 0, comps = -1;
     const int alg = a.algorithm;
-    if (alg == 0 || alg == 2 || alg == 3) {  // wpca (:315-339): PCA, big-five, fixed-variance
+    const bool clus = CLUS && alg >= 5;  // k-means / hierarchical / clusterfeck call wpca too (:393, :408, :422)
+    if (alg == 0 || alg == 2 || alg == 3 || clus) {  // wpca (:315-339): PCA, big-five, fixed-variance
         // ---- a5: weighted mean, np.ma.average (:317-319) -------------------
         const double den = wave_pw_sum(rep, row);
         double muj = 0.0;
@@ -923,7 +1308,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         wsync();
         if (col) S.ld[l] = ld_j;
         wsync();
-        if (alg == 0) {
+        if (clus) {
+            // the loading only: scores stay zeros (:357)
+        } else if (alg == 0) {
             // scores s = wcd . loading (:337), row phase
             if (row) {
                 double acc = 0.0;
@@ -980,7 +1367,19 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         sc_i = row ? a.aux_scores[b * N + l] : 0.0;
     }
     STAMP(6);
-    if (alg != 1) {
+    if constexpr (CLUS) {
+        if (clus) {
+            double* X = smem + smem_doubles(N, E, ES);
+            if (alg == 6)
+                nc_i = hier_nc(S.F, S.mu, ES, N, E, a.hierarchy_threshold, reinterpret_cast<uint64_t*>(X));
+            else if (alg == 5)
+                nc_i = kmeans_nc(a, b, S.F, S.mu, ES, N, E, X);
+            else
+                nc_i = feck_nc(a, S.F, ES, N, E, rep, X);
+            wsync();
+        }
+    }
+    if (alg != 1 && !clus) {
         // ---- a8/a9: nonconformity_rank (:487-500) / nonconformity (:475-485); the
         // non-PCA algorithms call nonconformity directly (:389, :450, :456)
         const bool any_nan = ballot(row && __builtin_isnan(sc_i)) != 0;
@@ -1245,12 +1644,20 @@ hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
         const char* e = getenv("PCX_BATCHED_LDS_PAD");
         return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
     }();
-    const size_t lds = batched_lds_bytes(a.N, a.E) + pad;
+    size_t lds = batched_lds_bytes(a.N, a.E) + pad;
     if (a.B <= 0) return hipSuccess;
-    if (a.N == 50 && a.E == 20 && a.ES == 21)
-        hipLaunchKernelGGL((batched_round_kernel<50, 20>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    if (a.algorithm >= 5) {  // clustering algorithms: their own instantiation and LDS region
+        lds = batched_lds_bytes(a.N, a.E) + sizeof(double) * (size_t)cluster_lds_doubles(a.N, a.E, a.ES);
+        static bool attr = [] {
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(&batched_round_kernel<0, 0, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+        }();
+        (void)attr;
+        hipLaunchKernelGGL((batched_round_kernel<0, 0, true>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+    } else if (a.N == 50 && a.E == 20 && a.ES == 21)
+        hipLaunchKernelGGL((batched_round_kernel<50, 20, false>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     else
-        hipLaunchKernelGGL((batched_round_kernel<0, 0>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((batched_round_kernel<0, 0, false>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 

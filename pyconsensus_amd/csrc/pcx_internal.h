@@ -25,6 +25,10 @@ struct BatchArgs {
     int max_components;       // big-five
     double variance_threshold;  // fixed-variance
     const double* aux_scores;   // cokurtosis [B][N]
+    double hierarchy_threshold;  // hierarchical
+    double cluster_threshold;    // clusterfeck (<= 0: log10(E)/1.77 rule)
+    int kmeans_k, kmeans_restarts;
+    const int32_t* kmeans_init;  // k-means [B][restarts][k]
     double catch_tol;
     double alpha;
     double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,

@@ -30,8 +30,11 @@ class Oracle(object):
     and ``"fixed-variance"`` (eigenvalue-weighted component scores, :373-390,
     :429-451), ``"cokurtosis"`` (``aux["cokurt"]`` scores, :455-457) and
     ``"absolute"`` (the reference's unimplemented branch: uniform this_rep,
-    :359-362).  ``"k-means"``, ``"hierarchical"`` and ``"clusterfeck"`` raise
-    NotImplementedError (scope).
+    :359-362), and the clustering algorithms ``"k-means"`` (:392-405; its restarts draw
+    from numpy's global RandomState exactly as the reference's scipy call does),
+    ``"hierarchical"`` (:407-419) and ``"clusterfeck"`` (:148-242, :421-424) for rounds
+    of at most 64 reporters x 32 events (the batched kernel); larger clustering
+    problems raise NotImplementedError (DESIGN.md, scope).
     """
 
     def __init__(self, reports=None, event_bounds=None, reputation=None,
@@ -114,10 +117,15 @@ class Oracle(object):
         kw = dict(catch_tolerance=self.catch_tolerance, alpha=self.alpha, int_dtype=self._int_dtype,
                   algorithm=self.algorithm, device=self.device, max_components=self.max_components,
                   variance_threshold=self.variance_threshold)
-        if N <= MAX_REPORTERS and E <= MAX_EVENTS:
+        small = N <= MAX_REPORTERS and E <= MAX_EVENTS
+        if self.algorithm in _abi.CLUSTER_ALGORITHMS and not small:
+            raise NotImplementedError("algorithm %r runs in the batched regime only (N <= %d, E <= %d; got %d x %d)"
+                                      % (self.algorithm, MAX_REPORTERS, MAX_EVENTS, N, E))
+        if small:
             out = consensus_batched(self._data[None], None if self._rep_raw is None else self._rep_raw[None],
                                     sc, lo, hi, filled=True, original=True,
-                                    aux_scores=None if aux is None else aux[None], **kw)
+                                    aux_scores=None if aux is None else aux[None],
+                                    hierarchy_threshold=self.hierarchy_threshold, **kw)
             g = {k: v[0].cpu().numpy() for k, v in out.items() if not k.startswith("_")}
             participation = float(g["participation"])
             avg_certainty = float(g["avg_certainty"])
@@ -140,7 +148,9 @@ class Oracle(object):
             raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")
         if self.algorithm == "fixed-variance":
             self.num_components = comps  # :449
-        self.convergence = self.algorithm != "absolute"  # nonconformity(_rank) set it (:483, :499)
+        self.convergence = self.algorithm != "absolute"  # nonconformity(_rank) / the clusterings set it
+        if self.algorithm == "clusterfeck":  # cluster() rewrites zero tokens in the caller's list (:202-204)
+            self.reptokens = [0.00001 if t == 0 else t for t in self.reptokens]
         return self._result(g, participation, avg_certainty)
 
     def _result(self, g, participation, avg_certainty):

@@ -247,8 +247,8 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
         scols = cols.to(dev)
         sidx = idx.to(dev)
     alg = _abi.ALGORITHMS.get(algorithm)
-    if alg is None:
-        raise NotImplementedError("algorithm %r is not on the GPU path" % (algorithm,))
+    if alg is None or algorithm in _abi.CLUSTER_ALGORITHMS:
+        raise NotImplementedError("algorithm %r is not on the single-matrix path" % (algorithm,))
     aux = None
     if alg == _abi.ALG_COKURTOSIS:
         if aux_scores is None:
