@@ -183,9 +183,13 @@ __global__ void __launch_bounds__(64) k_spart_finish(pcx_mat m, int nblk, int k,
 
 // ================================================================== column passes
 // grid (ceil(E/BT), G): thread = one event column, loop over a chunk of rows.
-__device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t& r1) {
-    const int64_t per = (m.n_rows + gridDim.y - 1) / gridDim.y;
+// align > 1 rounds the chunk up to a multiple of align rows (whole 128-byte lines for
+// the column-major T writes of k_colstats); trailing blocks may get an empty range.
+__device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t& r1, int64_t align = 1) {
+    int64_t per = (m.n_rows + gridDim.y - 1) / gridDim.y;
+    per = (per + align - 1) / align * align;
     r0 = (int64_t)blockIdx.y * per;
+    r0 = r0 < m.n_rows ? r0 : m.n_rows;
     r1 = r0 + per < m.n_rows ? r0 + per : m.n_rows;
 }
 
@@ -235,10 +239,12 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     const int si = m.scaled_index ? m.scaled_index[c] : -1;
     double* Tc = si >= 0 ? m.T + (int64_t)si * m.n_rows : nullptr;
     int64_t r0, r1;
-    row_range(m, r0, r1);
+    // 16 rows per step: each lane writes whole 128-byte lines of its T column (with 8,
+    // half-line partial writes doubled the write traffic: 14 GB for 8 GB of T at C5)
+    row_range(m, r0, r1, 16);
     acc2 sr, srx;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
-    rows_unrolled<ROW_UNROLL>(
+    rows_unrolled<16>(
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
         [&](int64_t i, XW v) {
             const double x = rescale(v.x, p, m.int_dtype);
