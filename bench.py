@@ -230,7 +230,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "batched_round_kernel", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": bpl},
+                         "algorithmic_bytes_per_launch": bpl,
+                         "limiter": ("latency / VALU issue, not HBM: one wave64 per LDS-resident round, "
+                                     "10 rounds per CU, SQ VALU busy ~55% "
+                                     "(profiles/r1/sq_counters_batched_pass*.csv, DESIGN.md 5)")},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
