@@ -81,8 +81,11 @@ def test_matrix_golden_c2(gpu_lib):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("shape", [(3000, 150), (20000, 400)])
+@pytest.mark.parametrize("shape", [(3000, 150), (20000, 400),
+                                   pytest.param((100_000, 1000), id="C4_100k_x_1k")])
 def test_matrix_vs_numpy_oracle(gpu_lib, shape):
+    """Against the numpy restatement run on the box; (100_000, 1000) is BASELINE config C4
+    at full size (the oracle takes ~35 s there)."""
     from oracle.pcx_oracle import OracleCPU
     from pyconsensus_amd import Oracle, synthetic
 
