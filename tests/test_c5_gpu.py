@@ -6,9 +6,9 @@ generated on the GPU shard by shard):
 
 * reputation vectors are distributions (non-negative, sum to 1);
 * binary outcomes are catch values {1, 1.5, 2}; scaled outcomes lie inside their bounds;
-* row-shard invariance: two virtual ranks (ThreadComm, each generating its own 4 of the
-  8 row shards, exactly what rank r of `bench.py --gpus 2` builds) reproduce the 1-rank
-  result -- the multi-GPU C5 configuration rehearsed at full size on one device.
+* row-shard invariance: 2, 4 and 8 virtual ranks (ThreadComm, each generating its own
+  8/N of the 8 row shards, exactly what rank r of `bench.py --gpus N` builds) reproduce
+  the 1-rank result -- the multi-GPU C5 configurations rehearsed at full size on one device.
 """
 import threading
 
@@ -28,8 +28,7 @@ def test_c5_full_size_properties_and_shard_invariance(gpu_lib):
     import torch
 
     from pyconsensus_amd import synthetic
-    from pyconsensus_amd.pipeline import (ThreadComm, ThreadGroup, clear_workspace_cache, consensus_matrix,
-                                          shard_rows)
+    from pyconsensus_amd.pipeline import clear_workspace_cache, consensus_matrix
 
     dev = torch.device("cuda:0")
     R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, device=dev)
@@ -53,7 +52,16 @@ def test_c5_full_size_properties_and_shard_invariance(gpu_lib):
     assert np.all((fin[scaled] >= lo_[scaled]) & (fin[scaled] <= hi_[scaled]))
     assert branch in (1, 2, 3, 4)
 
-    world = 2
+    for world in (2, 4, 8):  # the N of the driver's scaling runs
+        _check_world(world, dev, ref_ev, ref_ag, branch)
+
+
+def _check_world(world, dev, ref_ev, ref_ag, branch):
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.pipeline import ThreadComm, ThreadGroup, clear_workspace_cache, consensus_matrix, shard_rows
+
     grp = ThreadGroup(world)
     res = [None] * world
     errs = []
