@@ -81,7 +81,7 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     if shards is None or cnt * world != N:
         raise ValueError("C5 needs a GPU count dividing 8")
     R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, shards=shards, device=dev)
-    comm = Comm(world, rank)
+    comm = Comm.from_env(dev.index)  # RCCL inside libpcx for the nccl backend
 
     def run(profile=None):
         return consensus_matrix(R, None, sc, lo, hi, comm=comm, n_total=N, row_offset=off, device=dev,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 4
+#define PCX_ABI_VERSION 5
 
 enum pcx_status {
     PCX_OK = 0,
@@ -155,118 +155,131 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
 
 /* ------------------------------------------------------------------------ */
 /* Single-matrix regime: one N x E report matrix, optionally sharded by        */
-/* reporter rows over several GPUs (one process per GPU).  The consensus is a   */
-/* fixed sequence of stages (pcx_mat_stage); between some stages the host       */
-/* combines per-rank partial buffers across ranks (pyconsensus_amd/pipeline.py, */
-/* torch.distributed over RCCL).  Every buffer is caller-allocated device memory */
-/* sized as documented in pipeline.py (MatWorkspace).                           */
+/* contiguous reporter rows over several GPUs (one process -- or one thread --  */
+/* per rank).  One call runs the whole Oracle(...).consensus() of              */
+/* __init__.py:502-611; stage sequencing, scratch memory and the cross-rank    */
+/* exchange (RCCL over xGMI, or the backends below) are owned by the library.   */
 /* ------------------------------------------------------------------------ */
-enum pcx_mat_stage_id {
-    PCX_M_REPUTATION = 1,    /* rep, tokens (__init__.py:138-146)                    */
-    PCX_M_COLSTATS = 2,      /* rescale + NA + present sums per event (:266-299)     */
-    PCX_M_GUESS = 3,         /* binary fills (:304-309), median setup (:300-303)     */
-    PCX_M_MEAN = 4,          /* weighted mean mu, old = rep . F (:317-319, 490)     */
-    PCX_M_COV = 5,           /* token-weighted covariance partial tiles, fp64 MFMA (:326); needs PCX_M_WCD */
-    PCX_M_COV_REDUCE = 6,    /* sum split-K slabs into this rank's partial C         */
-    PCX_M_COV_FINISH = 7,    /* C = partial / (sum tokens - 1), symmetric            */
-    PCX_M_POWER = 8,         /* leading eigenvector by power iteration (:330-336)    */
-    PCX_M_SCORES = 9,        /* scores = wcd . loading (:337), row NA counts         */
-    PCX_M_NCSUMS = 10,       /* sums of |set1|, |set2| (:488-489, normalize)         */
-    PCX_M_GEMV2 = 11,        /* normalize(set1/2) . F (:492-493)                     */
-    PCX_M_DECIDE = 12,       /* rank rule / continuous fallback (:491-498, 475-485)  */
-    PCX_M_REPU = 13,         /* nc * rep / mean(rep) and its sum (:460-462)          */
-    PCX_M_SMOOTH = 14,       /* this_rep, smooth_rep (:460-472)                      */
-    PCX_M_OUTCOMES = 15,     /* smooth . F, participation, certainty bins (:510, 559, 542) */
-    PCX_M_EVENTS = 16,       /* catch/unscale binary events (:526-538)               */
-    PCX_M_SCALED_CERT = 17,  /* certainty of scaled events (:540-546)                */
-    PCX_M_FINAL = 18,        /* reward, author bonus, participation (:545-581)      */
-    PCX_M_ROWSUMS = 19,      /* participation_rows normalisation sums (:567-576)     */
-    PCX_M_AGENTS = 20,       /* per-reporter outputs (:576-577, 586-595)             */
-    PCX_M_MATRICES = 21,     /* result["original"] / result["filled"] (:584-585)     */
-    PCX_M_SEL_INIT = 30,     /* weighted median (:303, :520): totals, key range, max weight */
-    PCX_M_SEL_START = 31,    /*   dominance test, first histogram range              */
-    PCX_M_SEL_ARGMAX = 32,   /*   first row with the dominant weight                 */
-    PCX_M_SEL_VALUE = 33,    /*   value at that row                                  */
-    PCX_M_SEL_HIST = 34,     /*   exact weight histogram over the current key range  */
-    PCX_M_SEL_STEP = 35,     /*   narrow the range; converged columns get their result */
-    PCX_M_SEL_FINISH = 36,   /*   results into guess (phase 1) / outcomes_raw (phase 2) */
-    PCX_M_SEL_EXACT = 37,    /* weighted median replayed with the reference's float order (n <= 8192, 1 rank) */
-    PCX_M_WCD = 39,          /* wcd = F - mu materialised once (:317-322), row NaN/zero counts */
-    PCX_M_EIG = 38,          /* big-five / fixed-variance: eigenpairs of C (svd, :375, :431), the
-                                eigenvalue-weighted component sum (:377-382, :435-449) -> score vector */
-    PCX_M_ZERO_LOADING = 99, /* no wpca ("absolute", "cokurtosis"): first_loading = 0 (:359)          */
+
+/* Multi-rank contexts.  pcx_create() above is a one-rank context.  For RCCL,
+ * rank 0 calls pcx_comm_unique_id(), the caller broadcasts the 128 bytes over any
+ * channel (e.g. torch.distributed), and every rank calls pcx_create_rank()
+ * (ncclCommInitRank, collective over the ranks).  Replaces nothing in the
+ * reference (it has no distribution). */
+typedef struct { char internal[128]; } pcx_comm_id;
+int      pcx_comm_unique_id(pcx_comm_id* out);
+pcx_ctx* pcx_create_rank(int device_id, int world, int rank, const pcx_comm_id* id);
+
+/* In-process virtual ranks: `world` threads, each with its own context on any
+ * device, exchanging through host memory.  Used to rehearse the sharded path on
+ * one GPU (tests, 1-GPU boxes).  The group must outlive its contexts. */
+typedef struct pcx_group pcx_group;
+pcx_group* pcx_group_create(int world);
+void       pcx_group_destroy(pcx_group* g);
+pcx_ctx*   pcx_create_grouped(int device_id, pcx_group* g, int rank);
+
+/* Caller-supplied exchange (MPI, gloo, ...).  The library passes HOST buffers
+ * (it stages device data through pinned memory); return 0 on success.
+ *   allreduce: in place, `count` elements of enum pcx_dtype, enum pcx_redop.
+ *   allgather: recv[world][bytes] <- every rank's `bytes` of send, rank order. */
+enum pcx_dtype { PCX_F64 = 0, PCX_U64 = 1 };
+enum pcx_redop { PCX_SUM = 0, PCX_MIN = 1, PCX_MAX = 2 };
+typedef struct {
+    void* user;
+    int (*allreduce)(void* user, void* buf, int64_t count, int32_t dtype, int32_t op);
+    int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);
+} pcx_comm_ops;
+pcx_ctx* pcx_create_custom(int device_id, int world, int rank, const pcx_comm_ops* ops);
+
+int pcx_ctx_world(const pcx_ctx* ctx);
+int pcx_ctx_rank(const pcx_ctx* ctx);
+/* Drop the cached scratch of the single-matrix path (it is kept between calls of
+ * the same shape: a C5 consensus needs ~50 GB of it). */
+int pcx_release_workspace(pcx_ctx* ctx);
+
+enum pcx_mem_kind {
+    PCX_MEM_DEVICE = 0,  /* every pointer of pcx_problem / pcx_result is device memory of ctx's device */
+    PCX_MEM_HOST = 1,    /* every pointer is host memory; the library copies in and out (timed apart) */
 };
 
 typedef struct {
-    /* shape and parameters */
-    int64_t n_rows;               /* rows held by this rank                       */
-    int64_t n_events;             /* E                                            */
-    int64_t n_total;              /* N over all ranks                             */
-    int64_t row_offset;           /* global index of this rank's first row        */
-    int32_t world, rank;
-    int32_t int_dtype, algorithm;
-    double  catch_tolerance, alpha;
-    int32_t n_scaled;             /* number of scaled events                      */
-    int32_t sel_phase;            /* 1: interpolation medians, 2: outcome medians */
-    int32_t col_blocks;           /* row chunks of the column passes (G)          */
-    int32_t cov_tiles, cov_kslices;
-    /* inputs */
-    const double*  reports;       /* [n_rows][E]                                  */
-    const uint8_t* scaled;        /* [E] or NULL (event_bounds None)              */
-    const double*  lo;            /* [E]                                          */
-    const double*  hi;            /* [E]                                          */
-    const double*  rep_raw;       /* [n_total] raw reputation, or NULL = uniform   */
-    const int32_t* scaled_cols;   /* [n_scaled] event index of each scaled event   */
-    const int32_t* scaled_index;  /* [E] position of event j among scaled events, -1 if binary */
-    /* workspace */
-    double*   rep;                /* [n_rows]                                     */
-    double*   tok;                /* [n_rows]                                     */
-    double*   T;                  /* [n_scaled][n_rows] rescaled scaled events, NaN = missing */
-    double*   part;               /* [col_blocks][E][8][2] column-pass block partials */
-    double*   mpart;              /* [col_blocks][E][4] block max/min partials     */
-    double*   cstat;              /* [world][E][16][2] per-rank column sums (dd)   */
-    double*   cmax;               /* [world][E][4] per-rank max rep / argmax / min / max */
-    double*   scal;               /* [world][16][2] per-rank scalar sums (dd)      */
-    double*   spart;              /* [4096][4][2] row-pass block partials          */
-    double*   ev;                 /* [16][E] event vectors (guess, mu, old, ...)   */
-    double*   cslab;              /* [cov_kslices][E][E] covariance partial tiles  */
-    double*   C;                  /* [E][E] covariance                             */
-    double*   Mw;                 /* [2][E][E] power-iteration working matrices    */
-    double*   pvec;               /* [4][E + 64] power-iteration scratch           */
-    double*   rowv;               /* [6][n_rows] scores, this, smooth, u, ...       */
-    uint32_t* rowstat;            /* [n_rows][2] NaN / zero counts per row         */
-    uint64_t* skey;               /* [world][4] score min/max keys, flags          */
-    int64_t*  info;               /* [16] host-visible status (branch, iterations, active columns) */
-    /* weighted-median selection state (per scaled event) */
-    uint64_t* sel_sum;            /* [world][n_scaled][256][4] limb sums + counts  */
-    uint64_t* sel_min;            /* [world][n_scaled][256][2] min key, min weight bits */
-    uint64_t* sel_max;            /* [world][n_scaled][256] max key                */
-    uint64_t* sel_state;          /* [n_scaled][16] range, sums, flags             */
-    double*   sel_val;            /* [world][n_scaled][4] max weight, value, result */
-    /* outputs ([E] events, [n_rows] agents of this rank) */
+    int64_t n_rows;               /* reporters held by this rank                         */
+    int64_t n_events;             /* E                                                   */
+    int64_t n_total;              /* N over all ranks (== n_rows on one rank)            */
+    int64_t row_offset;           /* global index of this rank's first reporter          */
+    const double*  reports;       /* [n_rows][E] row-major, NaN = missing (0.0 too, :278) */
+    const double*  reputation;    /* [n_total] raw weights (every rank passes all N), or NULL = None (:138-141) */
+    const uint8_t* scaled;        /* [E] event_bounds[j]["scaled"], or NULL = event_bounds None (Q12) */
+    const double*  lo;            /* [E] event_bounds[j]["min"]                          */
+    const double*  hi;            /* [E] event_bounds[j]["max"]                          */
+    double  catch_tolerance;      /* Oracle(catch_tolerance=0.1)                         */
+    double  alpha;                /* Oracle(alpha=0.1)                                   */
+    int32_t int_dtype;            /* 1: reports had an integer dtype (truncation, Q3)    */
+    int32_t algorithm;            /* enum pcx_algorithm: PCA, absolute, big-five, fixed-variance, cokurtosis */
+    int32_t max_components;       /* big-five (Oracle caps it at E, :134-137)            */
+    int32_t mem_kind;             /* enum pcx_mem_kind                                   */
+    double  variance_threshold;   /* fixed-variance (:448)                               */
+    const double* aux_scores;     /* cokurtosis: [n_rows] this rank's aux["cokurt"] (:455-457) */
+} pcx_problem;
+
+typedef struct {
+    /* [n_rows] -- result["agents"], this rank's reporters; NULL = not written */
     double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
         *reporter_bonus;
+    /* [E] -- result["events"] (identical on every rank) */
     double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
         *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
-    double* scalars;              /* [4]: participation, avg_certainty, branch, flags */
-    double* original;             /* [n_rows][E] rescaled reports (PCX_M_MATRICES), optional */
-    double* filled;               /* [n_rows][E] filled reports (PCX_M_MATRICES), optional   */
-    /* covariance operands (PCX_M_COV): the centred, filled matrix materialised once */
-    double* wcd;                  /* [wcd_rows][wcd_ld] wcd = F - mu (:322), zero padded          */
-    double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
-    int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
-    int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
-    uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
-    /* algorithms other than PCA (enum pcx_algorithm) */
-    int32_t max_components;       /* "big-five" component count                                     */
-    int32_t components;           /* out ("fixed-variance"): components used, else -1               */
-    double  variance_threshold;   /* "fixed-variance" stop                                          */
-    const double* aux_scores;     /* "cokurtosis": [n_rows] scores of this rank's rows              */
-} pcx_mat;
+    /* [n_rows][E], optional: result["original"] (rescaled reports), result["filled"] */
+    double *original, *filled;
+    /* wpca intermediates (:317-326), optional: [E] weighted_mean, [E][E] covariance_matrix */
+    double *weighted_mean, *covariance;
+    /* scalars, always written (host memory inside this struct) */
+    double  participation;        /* result["participation"]                             */
+    double  avg_certainty;        /* result["avg_certainty"]                             */
+    int32_t branch;               /* enum pcx_branch                                     */
+    int32_t flags;                /* enum pcx_flag bits                                  */
+    int32_t pi_iters;             /* power-iteration steps (incl. Gram squarings)        */
+    int32_t components;           /* result["components"]: fixed-variance count, else -1 (:449, :610) */
+    int32_t n_hard;               /* weighted medians / binary fills replayed in sequential float order */
+    int32_t sel_passes;           /* weighted-selection histogram passes                 */
+} pcx_result;
 
-/* Run one stage on the context's stream (PCX_M_POWER and the selection steps may
- * synchronise the stream to read convergence state). */
-int pcx_mat_stage(pcx_ctx* ctx, pcx_mat* m, int stage);
+/* The whole consensus (__init__.py:502-611) on this rank's rows; collective over
+ * the context's ranks.  Synchronous: returns after every output is written. */
+int pcx_consensus_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r);
+
+/* The reference's stage methods on the same kernels (Oracle.interpolate / wpca /
+ * lie_detector / nonconformity(_rank), __init__.py:260-500).
+ *   pcx_interpolate_f64: p->reports raw; writes original / filled (:260-313).
+ *   pcx_wpca_f64:        p->reports is a FILLED matrix (no NA handling); writes
+ *                        weighted_mean, covariance, adj_first_loadings (first
+ *                        loading) and scores (first score) (:315-339).
+ *   pcx_lie_detector_f64: p->reports FILLED; wpca + nonconformity_rank (PCA) or
+ *                        the algorithm's branch, then this_rep / smooth_rep
+ *                        (:341-473); writes scores, adj_first_loadings, old_rep,
+ *                        this_rep, smooth_rep, branch.
+ *   pcx_nonconformity_f64: p->reports FILLED, scores [n_rows] given; rank_rule 1 =
+ *                        nonconformity_rank (:487-500), 0 = nonconformity (:475-485);
+ *                        writes nc [n_rows] and r->branch. */
+int pcx_interpolate_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r);
+int pcx_wpca_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r);
+int pcx_lie_detector_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r);
+int pcx_nonconformity_f64(pcx_ctx* ctx, const pcx_problem* p, const double* scores, int rank_rule, double* nc,
+                          pcx_result* r);
+
+/* Per-stage device time of the last single-matrix call (HIP events on the
+ * context's stream) when enabled; names by pcx_stage_name(k), k < PCX_NSTAGES. */
+#define PCX_NSTAGES 48
+int         pcx_profile_enable(pcx_ctx* ctx, int on);
+int         pcx_profile_read(pcx_ctx* ctx, double* ms /* [PCX_NSTAGES] */);
+const char* pcx_stage_name(int k);
+
+/* Sequential float sums of a constant (weightedstats' builtin-sum walk over equal
+ * weights, __init__.py:287-303, :519-523): S(k) = 0 + c + c + ... (k terms, each
+ * addition rounded to nearest-even), in O(log k) by binade stepping; and the least
+ * k >= 1 with S(k) > t (kmax + 1 if none up to kmax).  Exported for the CPU tests. */
+double  pcx_seqsum_const(double c, int64_t k);
+int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
@@ -68,19 +68,11 @@ def out_shape(kind, B, N, E):
     return {"N": (B, N), "E": (B, E), "1": (B,), "NE": (B, N, E)}[kind]
 
 
-# ---------------------------------------------------------------- single-matrix stages
-M_REPUTATION, M_COLSTATS, M_GUESS, M_MEAN, M_COV, M_COV_REDUCE, M_COV_FINISH, M_POWER = 1, 2, 3, 4, 5, 6, 7, 8
-M_SCORES, M_NCSUMS, M_GEMV2, M_DECIDE, M_REPU, M_SMOOTH, M_OUTCOMES, M_EVENTS = 9, 10, 11, 12, 13, 14, 15, 16
-M_SCALED_CERT, M_FINAL, M_ROWSUMS, M_AGENTS, M_MATRICES = 17, 18, 19, 20, 21
-M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH = 30, 31, 32, 33, 34, 35, 36
-M_SEL_EXACT = 37
-M_EIG = 38
-M_WCD = 39
-SEL_EXACT_MAX = 8192
-M_ZERO_LOADING = 99
-
-# info[] slots (pcx_matrix.hip info_slot)
-INFO_BRANCH, INFO_PI_ITERS, INFO_FLAGS, INFO_SEL_ACTIVE, INFO_SEL_ARGMAX, INFO_PICK1 = 0, 1, 2, 3, 4, 5
+# ---------------------------------------------------------------- single-matrix regime
+MEM_DEVICE, MEM_HOST = 0, 1
+F64, U64 = 0, 1                  # enum pcx_dtype
+RED_SUM, RED_MIN, RED_MAX = 0, 1, 2  # enum pcx_redop
+NSTAGES = 48                     # PCX_NSTAGES
 
 MAT_OUTPUT_AGENTS = ["old_rep", "this_rep", "smooth_rep", "scores", "na_row", "participation_rows",
                      "relative_part", "reporter_bonus"]
@@ -90,21 +82,32 @@ MAT_OUTPUT_EVENTS = ["adj_first_loadings", "outcomes_raw", "outcomes_adjusted", 
 _vp = C.c_void_p
 
 
-class Mat(C.Structure):
+class CommId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
+ALLREDUCE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32)
+ALLGATHER_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
+
+class CommOps(C.Structure):
+    _fields_ = [("user", _vp), ("allreduce", ALLREDUCE_CB), ("allgather", ALLGATHER_CB)]
+
+
+class Problem(C.Structure):
     _fields_ = [
         ("n_rows", C.c_int64), ("n_events", C.c_int64), ("n_total", C.c_int64), ("row_offset", C.c_int64),
-        ("world", C.c_int32), ("rank", C.c_int32), ("int_dtype", C.c_int32), ("algorithm", C.c_int32),
+        ("reports", _vp), ("reputation", _vp), ("scaled", _vp), ("lo", _vp), ("hi", _vp),
         ("catch_tolerance", C.c_double), ("alpha", C.c_double),
-        ("n_scaled", C.c_int32), ("sel_phase", C.c_int32), ("col_blocks", C.c_int32),
-        ("cov_tiles", C.c_int32), ("cov_kslices", C.c_int32),
-        ("reports", _vp), ("scaled", _vp), ("lo", _vp), ("hi", _vp), ("rep_raw", _vp),
-        ("scaled_cols", _vp), ("scaled_index", _vp),
-        ("rep", _vp), ("tok", _vp), ("T", _vp), ("part", _vp), ("mpart", _vp), ("cstat", _vp),
-        ("cmax", _vp), ("scal", _vp), ("spart", _vp), ("ev", _vp), ("cslab", _vp), ("C", _vp), ("Mw", _vp),
-        ("pvec", _vp), ("rowv", _vp), ("rowstat", _vp), ("skey", _vp), ("info", _vp),
-        ("sel_sum", _vp), ("sel_min", _vp), ("sel_max", _vp), ("sel_state", _vp), ("sel_val", _vp),
-    ] + [(n, _vp) for n in MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS] + [("scalars", _vp), ("original", _vp),
-                                                                   ("filled", _vp)] + [
-        ("wcd", _vp), ("tokp", _vp), ("wcd_rows", C.c_int64), ("wcd_ld", C.c_int64), ("rowpart", _vp),
-        ("max_components", C.c_int32), ("components", C.c_int32), ("variance_threshold", C.c_double),
-        ("aux_scores", _vp)]
+        ("int_dtype", C.c_int32), ("algorithm", C.c_int32), ("max_components", C.c_int32), ("mem_kind", C.c_int32),
+        ("variance_threshold", C.c_double), ("aux_scores", _vp)]
+
+
+RESULT_VECTORS = MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS + ["original", "filled", "weighted_mean", "covariance"]
+
+
+class Result(C.Structure):
+    _fields_ = [(n, _vp) for n in RESULT_VECTORS] + [
+        ("participation", C.c_double), ("avg_certainty", C.c_double),
+        ("branch", C.c_int32), ("flags", C.c_int32), ("pi_iters", C.c_int32), ("components", C.c_int32),
+        ("n_hard", C.c_int32), ("sel_passes", C.c_int32)]

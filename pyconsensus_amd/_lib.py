@@ -36,8 +36,31 @@ def _declare(lib):
     lib.pcx_synchronize.restype = C.c_int
     lib.pcx_consensus_batched_f64.argtypes = [C.c_void_p, C.POINTER(_abi.Batch), C.POINTER(_abi.BatchResult)]
     lib.pcx_consensus_batched_f64.restype = C.c_int
-    lib.pcx_mat_stage.argtypes = [C.c_void_p, C.POINTER(_abi.Mat), C.c_int]
-    lib.pcx_mat_stage.restype = C.c_int
+    vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+    for name, res, args in [
+        ("pcx_comm_unique_id", i32, [C.POINTER(_abi.CommId)]),
+        ("pcx_create_rank", vp, [i32, i32, i32, C.POINTER(_abi.CommId)]),
+        ("pcx_group_create", vp, [i32]),
+        ("pcx_group_destroy", None, [vp]),
+        ("pcx_create_grouped", vp, [i32, vp, i32]),
+        ("pcx_create_custom", vp, [i32, i32, i32, C.POINTER(_abi.CommOps)]),
+        ("pcx_ctx_world", i32, [vp]),
+        ("pcx_ctx_rank", i32, [vp]),
+        ("pcx_release_workspace", i32, [vp]),
+        ("pcx_consensus_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
+        ("pcx_interpolate_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
+        ("pcx_wpca_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
+        ("pcx_lie_detector_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
+        ("pcx_nonconformity_f64", i32, [vp, C.POINTER(_abi.Problem), vp, i32, vp, C.POINTER(_abi.Result)]),
+        ("pcx_profile_enable", i32, [vp, i32]),
+        ("pcx_profile_read", i32, [vp, C.POINTER(C.c_double)]),
+        ("pcx_stage_name", C.c_char_p, [i32]),
+        ("pcx_seqsum_const", C.c_double, [C.c_double, i64]),
+        ("pcx_seqsum_first_above", i64, [C.c_double, C.c_double, i64]),
+    ]:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
 
 
 def lib():
@@ -77,7 +100,14 @@ def context(device_index):
     return h
 
 
-def bind_stream(device_index, stream_handle):
-    h = context(device_index)
+def bind_stream(device_index, stream_handle, ctx=None):
+    h = context(device_index) if ctx is None else ctx
     check(lib().pcx_set_stream(h, C.c_void_p(stream_handle)))
     return h
+
+
+def new_context(ptr, what):
+    """Check a pcx_create* result (NULL = error with pcx_last_error())."""
+    if not ptr:
+        raise PcxError("%s failed: %s" % (what, lib().pcx_last_error().decode(errors="replace")))
+    return ptr

@@ -13,11 +13,7 @@
 
 #include "../../include/pcx.h"
 #include "pcx_internal.h"
-
-struct pcx_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-};
+#include "pcx_seqsum.h"
 
 namespace {
 thread_local std::string g_err;
@@ -38,23 +34,95 @@ int pcx_abi_version(void) { return PCX_ABI_VERSION; }
 
 const char* pcx_last_error(void) { return g_err.c_str(); }
 
-pcx_ctx* pcx_create(int device_id) {
+namespace {
+pcx_ctx* new_ctx(int device_id, const char* who) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || device_id < 0 || device_id >= n) {
-        g_err = "pcx_create: no HIP device " + std::to_string(device_id);
+        g_err = std::string(who) + ": no HIP device " + std::to_string(device_id);
         return nullptr;
     }
     pcx_ctx* c = new (std::nothrow) pcx_ctx;
     if (!c) {
-        g_err = "pcx_create: out of host memory";
+        g_err = std::string(who) + ": out of host memory";
         return nullptr;
     }
     c->device = device_id;
     return c;
 }
 
-void pcx_destroy(pcx_ctx* ctx) { delete ctx; }
+pcx_ctx* with_comm(pcx_ctx* c, pcx::Comm* comm, const std::string& err) {
+    if (!c) return nullptr;
+    if (!comm) {
+        g_err = err.empty() ? "communicator setup failed" : err;
+        delete c;
+        return nullptr;
+    }
+    c->comm = comm;
+    return c;
+}
+}  // namespace
+
+pcx_ctx* pcx_create(int device_id) { return new_ctx(device_id, "pcx_create"); }
+
+int pcx_comm_unique_id(pcx_comm_id* out) {
+    if (!out) return fail(PCX_EINVAL, "pcx_comm_unique_id: null argument");
+    std::string err;
+    const int rc = pcx::comm_rccl_unique_id(out, err);
+    return rc ? fail(rc, err) : PCX_OK;
+}
+
+pcx_ctx* pcx_create_rank(int device_id, int world, int rank, const pcx_comm_id* id) {
+    if (!id || world < 1 || rank < 0 || rank >= world) {
+        g_err = "pcx_create_rank: bad id / world / rank";
+        return nullptr;
+    }
+    pcx_ctx* c = new_ctx(device_id, "pcx_create_rank");
+    if (!c) return nullptr;
+    if (world == 1) return c;
+    std::string err;
+    return with_comm(c, pcx::comm_rccl(device_id, world, rank, id, err), err);
+}
+
+pcx_group* pcx_group_create(int world) {
+    pcx_group* g = pcx::group_create(world);
+    if (!g) g_err = "pcx_group_create: world must be >= 1";
+    return g;
+}
+
+void pcx_group_destroy(pcx_group* g) { pcx::group_destroy(g); }
+
+pcx_ctx* pcx_create_grouped(int device_id, pcx_group* g, int rank) {
+    pcx_ctx* c = new_ctx(device_id, "pcx_create_grouped");
+    if (!c) return nullptr;
+    std::string err;
+    return with_comm(c, pcx::comm_group(g, rank, err), err);
+}
+
+pcx_ctx* pcx_create_custom(int device_id, int world, int rank, const pcx_comm_ops* ops) {
+    pcx_ctx* c = new_ctx(device_id, "pcx_create_custom");
+    if (!c) return nullptr;
+    std::string err;
+    return with_comm(c, pcx::comm_custom(world, rank, ops, err), err);
+}
+
+int pcx_ctx_world(const pcx_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->world : 1; }
+int pcx_ctx_rank(const pcx_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }
+
+int pcx_release_workspace(pcx_ctx* ctx) {
+    if (!ctx) return fail(PCX_EINVAL, "pcx_release_workspace: null context");
+    (void)hipSetDevice(ctx->device);
+    pcx::workspace_free(ctx);
+    return PCX_OK;
+}
+
+void pcx_destroy(pcx_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    pcx::workspace_free(ctx);
+    delete ctx->comm;
+    delete ctx;
+}
 
 int pcx_set_stream(pcx_ctx* ctx, void* s) {
     if (!ctx) return fail(PCX_EINVAL, "pcx_set_stream: null context");
@@ -179,19 +247,54 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     return e == hipSuccess ? PCX_OK : hip_fail(e, "batched_round_kernel launch");
 }
 
-int pcx_mat_stage(pcx_ctx* ctx, pcx_mat* m, int stage) {
-    if (!ctx || !m) return fail(PCX_EINVAL, "pcx_mat_stage: null argument");
-    if (m->n_rows < 1 || m->n_events < 1 || m->n_total < m->n_rows || !m->reports)
-        return fail(PCX_EINVAL, "pcx_mat_stage: bad shape or missing reports");
-    if (m->n_events > 65536) return fail(PCX_EINVAL, "pcx_mat_stage: n_events > 65536");
-    if (m->n_rows > 0x7fffffffll) return fail(PCX_EINVAL, "pcx_mat_stage: n_rows >= 2^31 per rank");
-    if (m->rank < 0 || m->rank >= m->world) return fail(PCX_EINVAL, "pcx_mat_stage: bad rank/world");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+namespace {
+int run(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, const double* scores, int rank_rule, double* nc,
+        const char* who) {
+    if (!ctx || !p || !r) return fail(PCX_EINVAL, std::string(who) + ": null argument");
     std::string err;
-    e = pcx::mat_stage(*m, stage, ctx->stream, err);
-    if (!err.empty()) return fail(PCX_EINVAL, err);
-    return e == hipSuccess ? PCX_OK : hip_fail(e, "pcx_mat_stage");
+    const int rc = pcx::run_matrix(ctx, p, r, entry, scores, rank_rule, nc, err);
+    return rc ? fail(rc, std::string(who) + ": " + err) : PCX_OK;
 }
+}  // namespace
+
+int pcx_consensus_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r) {
+    return run(ctx, p, r, 0, nullptr, 0, nullptr, "pcx_consensus_f64");
+}
+
+int pcx_interpolate_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r) {
+    return run(ctx, p, r, 1, nullptr, 0, nullptr, "pcx_interpolate_f64");
+}
+
+int pcx_wpca_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r) {
+    return run(ctx, p, r, 2, nullptr, 0, nullptr, "pcx_wpca_f64");
+}
+
+int pcx_lie_detector_f64(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r) {
+    return run(ctx, p, r, 3, nullptr, 0, nullptr, "pcx_lie_detector_f64");
+}
+
+int pcx_nonconformity_f64(pcx_ctx* ctx, const pcx_problem* p, const double* scores, int rank_rule, double* nc,
+                          pcx_result* r) {
+    if (!scores || !nc) return fail(PCX_EINVAL, "pcx_nonconformity_f64: scores and nc are required");
+    return run(ctx, p, r, 4, scores, rank_rule, nc, "pcx_nonconformity_f64");
+}
+
+int pcx_profile_enable(pcx_ctx* ctx, int on) {
+    if (!ctx) return fail(PCX_EINVAL, "pcx_profile_enable: null context");
+    ctx->profile = on ? 1 : 0;
+    return PCX_OK;
+}
+
+int pcx_profile_read(pcx_ctx* ctx, double* ms) {
+    if (!ctx || !ms) return fail(PCX_EINVAL, "pcx_profile_read: null argument");
+    for (int k = 0; k < PCX_NSTAGES; k++) ms[k] = ctx->stage_ms[k];
+    return PCX_OK;
+}
+
+const char* pcx_stage_name(int k) { return pcx::stage_name(k); }
+
+double pcx_seqsum_const(double c, int64_t k) { return pcx::seqsum_const(c, k); }
+
+int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax) { return pcx::seqsum_first_above(c, t, kmax); }
 
 }  // extern "C"

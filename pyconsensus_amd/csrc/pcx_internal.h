@@ -8,6 +8,87 @@
 
 #include "../../include/pcx.h"
 
+// Kernel-side view of one single-matrix consensus on one rank: problem, scratch and
+// outputs as device pointers (built by pcx_runner.cpp, passed by value to every
+// kernel of pcx_matrix.hip).  Internal: the public boundary is pcx_problem /
+// pcx_result (include/pcx.h).
+typedef struct {
+    /* shape and parameters */
+    int64_t n_rows;               /* rows held by this rank                       */
+    int64_t n_events;             /* E                                            */
+    int64_t n_total;              /* N over all ranks                             */
+    int64_t row_offset;           /* global index of this rank's first row        */
+    int32_t world, rank;
+    int32_t int_dtype, algorithm;
+    double  catch_tolerance, alpha;
+    int32_t n_scaled;             /* number of scaled events                      */
+    int32_t sel_phase;            /* 1: interpolation medians, 2: outcome medians */
+    int32_t col_blocks;           /* row chunks of the column passes (G)          */
+    int32_t cov_tiles, cov_kslices;
+    int32_t no_fill;              /* reports are already filled (stage entries): no NA fill */
+    int32_t rank_rule;            /* sign choice by nonconformity_rank (:487-500), else nonconformity */
+    int32_t scores_given;         /* scores come from aux_scores (nonconformity entries, cokurtosis) */
+    /* inputs */
+    const double*  reports;       /* [n_rows][E]                                  */
+    const uint8_t* scaled;        /* [E] or NULL (event_bounds None)              */
+    const double*  lo;            /* [E]                                          */
+    const double*  hi;            /* [E]                                          */
+    const double*  rep_raw;       /* [n_total] raw reputation, or NULL = uniform   */
+    const int32_t* scaled_cols;   /* [n_scaled] event index of each scaled event   */
+    const int32_t* scaled_index;  /* [E] position of event j among scaled events, -1 if binary */
+    /* workspace */
+    double*   rep;                /* [n_rows]                                     */
+    double*   tok;                /* [n_rows]                                     */
+    double*   T;                  /* [n_scaled][n_rows] rescaled scaled events, NaN = missing */
+    double*   part;               /* [col_blocks][E][8][2] column-pass block partials */
+    double*   mpart;              /* [col_blocks][E][4] block max/min partials     */
+    double*   cstat;              /* [world][E][16][2] per-rank column sums (dd)   */
+    double*   cmax;               /* [world][E][4] per-rank max rep / argmax / min / max */
+    double*   scal;               /* [world][16][2] per-rank scalar sums (dd)      */
+    double*   spart;              /* [4096][4][2] row-pass block partials          */
+    double*   ev;                 /* [16][E] event vectors (guess, mu, old, ...)   */
+    double*   cslab;              /* [cov_kslices][E][E] covariance partial tiles  */
+    double*   C;                  /* [E][E] covariance                             */
+    double*   Mw;                 /* [2][E][E] power-iteration working matrices    */
+    double*   pvec;               /* [4][E + 64] power-iteration scratch           */
+    double*   rowv;               /* [6][n_rows] scores, this, smooth, u, ...       */
+    uint32_t* rowstat;            /* [n_rows][2] NaN / zero counts per row         */
+    uint64_t* skey;               /* [world][4] score min/max keys, flags          */
+    int64_t*  info;               /* [16] host-visible status (branch, iterations, counts) */
+    /* weighted-median selection: per scaled event (reduced over ranks by SUM / MIN / MAX) */
+    uint64_t* sel_state;          /* [n_scaled][SELS] range, sums, mode, result    */
+    uint64_t* sel_isum;           /* [n_scaled][4] total weight limbs, count       (SUM) */
+    uint64_t* sel_imin;           /* [n_scaled][2] min key, min weight bits        (MIN) */
+    uint64_t* sel_imax;           /* [n_scaled][2] max key, max weight bits        (MAX) */
+    uint64_t* hist_sum;           /* [n_active][256][4] bucket weight limbs, count (SUM) */
+    uint64_t* hist_min;           /* [n_active][256][2] bucket min key, min weight (MIN) */
+    uint64_t* hist_max;           /* [n_active][256] bucket max key                (MAX) */
+    uint64_t* sel_arg;            /* [2][n_scaled] first dominant row (MIN), its value key (MAX) */
+    int32_t*  sel_act;            /* [n_scaled] active scaled events, compacted in event order */
+    int32_t*  hard;               /* [E] 0 / hard-replay mode per event (binary fill mean, median) */
+    /* outputs ([E] events, [n_rows] agents of this rank) */
+    double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
+        *reporter_bonus;
+    double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
+        *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
+    double* scalars;              /* [4]: participation, avg_certainty            */
+    double* original;             /* [n_rows][E] rescaled reports (M_MATRICES), optional */
+    double* filled;               /* [n_rows][E] filled reports (M_MATRICES), optional   */
+    double* weighted_mean;        /* [E] optional (wpca entry)                     */
+    double* nc_out;               /* [n_rows] optional (nonconformity entry)       */
+    /* covariance operands (M_COV): the centred, filled matrix materialised once */
+    double* wcd;                  /* [wcd_rows][wcd_ld] wcd = F - mu (:322), zero padded          */
+    double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
+    int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
+    int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
+    uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
+    /* algorithms other than PCA (enum pcx_algorithm) */
+    int32_t max_components;       /* "big-five" component count                                     */
+    int32_t components;           /* out ("fixed-variance"): components used, else -1               */
+    double  variance_threshold;   /* "fixed-variance" stop                                          */
+    const double* aux_scores;     /* [n_rows] cokurtosis scores / given scores                      */
+} pcx_mat;
+
 namespace pcx {
 
 // Kernel arguments of the batched round kernel (by value).
@@ -44,7 +125,89 @@ struct BatchArgs {
 size_t batched_lds_bytes(int N, int E);
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream);
 
-// single-matrix path: launch one stage (pcx_matrix.hip)
+// ---------------------------------------------------------------- single-matrix stages
+// Internal stage ids (pcx_stage_name); the runner (pcx_runner.cpp) sequences them.
+enum mat_stage_id {
+    M_REPUTATION = 1, M_COLSTATS, M_GUESS, M_MEAN, M_COV, M_COV_REDUCE, M_COV_FINISH, M_POWER, M_SCORES,
+    M_NCSUMS, M_GEMV2, M_DECIDE, M_REPU, M_SMOOTH, M_OUTCOMES, M_EVENTS, M_SCALED_CERT, M_FINAL, M_ROWSUMS,
+    M_AGENTS, M_MATRICES, M_WCD, M_EIG, M_ZERO_LOADING, M_NC_OUT, M_WMEAN_OUT,
+    M_SEL_EXACT, M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_VALUE_FINISH, M_SEL_COMPACT,
+    M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH, M_HARD_LIST, M_HARD_GATHER, M_HARD_PREP, M_HARD_SORT, M_HARD_WALK,
+    M_EXCHANGE, M_H2D, M_D2H, M_NSTAGE
+};
+static_assert(M_NSTAGE <= PCX_NSTAGES, "stage table");
+const char* stage_name(int k);
+
+constexpr int SEL_NB = 256;         // selection buckets per pass
+constexpr int SEL_EXACT_MAX = 8192; // one-block exact replay of weightedstats (one rank)
+
+// launch one stage (pcx_matrix.hip)
 hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t stream, std::string& err);
 
+// hard replay of weightedstats / the interpolation mean in the reference's sequential float
+// order, for events whose exact-arithmetic decision lies within rounding of a threshold
+struct HardArgs {
+    int32_t n_hard;          // events in this batch
+    const int32_t* cols;     // [n_hard] event index
+    const int32_t* modes;    // [n_hard] HARD_MEAN (binary fill) / HARD_MEDIAN
+    int64_t cap;             // max elements of one event on one rank (= n_rows)
+    double* send;            // [n_hard][cap][2] (x, w) of this rank, row order
+    int64_t* send_cnt;       // [n_hard]
+    double* recv;            // [world][n_hard][cap][2]
+    int64_t* recv_cnt;       // [world][n_hard]
+    int64_t P;               // sort segment length (power of two >= max total count)
+    uint64_t* keys;          // [n_hard][P][2] sort keys (value key, weight key)
+    double* W;               // [n_hard][N] weights in row order (scratch)
+    double* X;               // [n_hard][N] values in row order (scratch)
+    double* hs;              // [n_hard][4] per event: mid, count, status, result
+};
+enum hard_mode { HARD_NONE = 0, HARD_MEAN = 1, HARD_MEDIAN = 2 };
+hipError_t hard_stage(pcx_mat& m, const HardArgs& h, int stage, hipStream_t st, std::string& err);
+
+hipError_t hard_list(pcx_mat& m, int32_t* cols, int32_t* modes, hipStream_t st);
+hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st);
+hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
+// info[] slots read by the runner
+enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
+                     INFO_PICK1 = 5, INFO_HARD = 6 };
+
+// pack / unpack of strided dd slot ranges for the slot exchange (runner)
+hipError_t copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch, int64_t width, int64_t rows,
+                  hipStream_t st);
+
+// ---------------------------------------------------------------- cross-rank exchange
+struct Comm {
+    int world = 1, rank = 0;
+    virtual ~Comm() {}
+    // in place over `count` elements on the device, stream-ordered; 0 = ok
+    virtual int allreduce(void* buf, int64_t count, int dtype, int op, hipStream_t st, std::string& err) = 0;
+    // recv[world][bytes] <- send of every rank; send may alias recv + rank*bytes
+    virtual int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) = 0;
+    virtual const char* kind() const = 0;
+};
+Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err);
+int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);
+Comm* comm_group(pcx_group* g, int rank, std::string& err);
+Comm* comm_custom(int world, int rank, const pcx_comm_ops* ops, std::string& err);
+pcx_group* group_create(int world);
+void group_destroy(pcx_group* g);
+
+}  // namespace pcx
+
+// the context (pcx_api.cpp / pcx_runner.cpp)
+struct pcx_workspace;
+struct pcx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    pcx::Comm* comm = nullptr;     // NULL = one rank
+    pcx_workspace* ws = nullptr;   // single-matrix scratch, cached between calls
+    int profile = 0;
+    double stage_ms[PCX_NSTAGES] = {0};
+};
+
+namespace pcx {
+void workspace_free(pcx_ctx* c);
+// entry: 0 consensus, 1 interpolate, 2 wpca, 3 lie_detector, 4 nonconformity
+int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const double* scores_in, int rank_rule,
+               double* nc_out, std::string& err);
 }  // namespace pcx

@@ -37,21 +37,22 @@
 #include "../../include/pcx.h"
 #include "pcx_device.h"
 #include "pcx_internal.h"
+#include "pcx_seqsum.h"
 
 namespace pcx {
 namespace {
 
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
-constexpr int NB = 256;          // selection buckets
-constexpr int SELS = 16;         // sel_state words per scaled event
+constexpr int NB = SEL_NB;       // selection buckets
+constexpr int SELS = 24;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
                EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP };
-enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1 };
+enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -333,12 +334,21 @@ __global__ void __launch_bounds__(BT) k_guess(pcx_mat m) {
     m.ev[EV_NZERO * E + c] = dd_to_double(cst(m, c, 3));
     const bool sc = m.scaled && m.scaled[c];
     double g = 0.0;
-    if (!sc) {
+    m.hard[c] = HARD_NONE;
+    if (!sc && !m.no_fill) {
         // sequential weighted mean of the present reports, then catch (:304-309)
-        g = present > 0 ? catch_value(dd_div(S_rx, S_r), m.catch_tolerance) : catch_value(0.0, m.catch_tolerance);
+        const double mean = present > 0 ? dd_div(S_rx, S_r) : 0.0;
+        g = catch_value(mean, m.catch_tolerance);
         if (m.int_dtype) g = trunc(g);
+        // within the sequential sum's rounding of a catch threshold: replay the reference's
+        // order (k_hard_*); the bound is (n terms of |w x|, plus the w / total roundings)
+        if (miss > 0 && present > 0) {
+            const double B = (4.0 * present + 64.0) * 0x1p-53 * (fabs(mean) + 1.0);
+            if (fabs(mean - (1.5 - m.catch_tolerance)) <= B || fabs(mean - (1.5 + m.catch_tolerance)) <= B)
+                m.hard[c] = HARD_MEAN;
+        }
     }
-    m.ev[EV_GUESS * E + c] = g;  // scaled events: phase-1 median (PCX_M_SEL_*)
+    m.ev[EV_GUESS * E + c] = g;  // scaled events: phase-1 median (selection)
 }
 
 // PCX_M_MEAN: mu = rep . F / sum(rep) (np.ma.average, :317-319); old = rep . F (:490)
@@ -914,7 +924,7 @@ __global__ void __launch_bounds__(BT) k_scores(pcx_mat m) {
             if (m.algorithm == 0) acc = fma(f - p.mu, m.ev[EV_LD * E + c], acc);
         }
         acc = wave_sum_d(acc);
-        if (m.algorithm == 4) acc = m.aux_scores[i];  // cokurtosis: caller scores (:455-457)
+        if (m.scores_given) acc = m.aux_scores[i];  // cokurtosis (:455-457) / given scores
         for (int s = 32; s >= 1; s >>= 1) {
             nn += __shfl_xor(nn, s, WAVE);
             nz += __shfl_xor(nz, s, WAVE);
@@ -1088,7 +1098,7 @@ __global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
     const double* old = m.ev + EV_OLD * E;
     const double* raw1 = m.pvec + 2 * (m.n_events + 64);
     const double* raw2 = pv_y(m);
-    const double ref = m.algorithm == 0 ? pv_s(m)[8] : 0.0;  // non-PCA: nonconformity directly
+    const double ref = m.rank_rule ? pv_s(m)[8] : 0.0;  // no rank rule: nonconformity directly
     int branch, pick1;
     if (ref == 0) {
         acc2 q1, q2;
@@ -1231,8 +1241,79 @@ __global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
 }
 
 // ================================================================== weighted median selection
-// element (value, weight) of scaled event s at local row i; false = not part of the set
-// raw operands of element (s, i) of the selection, loaded ahead of sel_decode
+// weightedstats.weighted_median (:303 over the present reports of a scaled event with
+// weights rep/sum(rep); :520-523 over the filled column with smooth_rep) in three tiers:
+//
+//  1. exact selection: an order-preserving u64 key per value, weights as exact fixed-point
+//     limbs; 8-bit histogram passes narrow the key range to the run of equal values where
+//     the exact prefix crosses half the total.  Every per-rank partial reduces with a plain
+//     SUM / MIN / MAX, so the result does not depend on the sharding.
+//  2. equal weights (reputation=None: every weight of the column is one double): the
+//     reference's float walk depends on the count alone, and pcx_seqsum.h replays it in
+//     O(log n) -- crossing index k* and the DBL_EPSILON half test -- after which an exact
+//     count selection fetches the k*-th value (and its predecessor for an exact half).
+//  3. the exact crossing is decisive unless the prefix at either end of the run lies
+//     within the sequential-sum error bound of half the total; such events (and dominant
+//     weights at the bound) are "hard" and are replayed in the reference's own float order
+//     (k_hard_*: gather in row order, sequential totals, (value, weight) sort, walk).
+enum sel_word {
+    SW_STATUS = 0,   // 0 done, 1 histogram pass pending, 2 dominant weight (first argmax row), 3 hard
+    SW_LO, SW_HI, SW_SHIFT,           // current key range and bucket shift
+    SW_BELOW0, SW_BELOW1, SW_BELOW2,  // exact weight before the range
+    SW_TOT0, SW_TOT1, SW_TOT2,        // exact total weight
+    SW_BELOW_MAX, SW_HAS_BELOW,       // largest key before the range
+    SW_RESULT,                        // result bits (status 0)
+    SW_WMAX,                          // max weight bits
+    SW_MODE,                          // 0 weight walk, 1 count rank (equal weights)
+    SW_NEED,                          // phase 1: the event has missing reports
+    SW_COUNT,                         // elements
+    SW_TARGET,                        // count mode: 0-based rank of the crossing element
+    SW_CNT_BELOW,                     // count mode: elements before the range
+    SW_HALF,                          // count mode: 1 exact half (mean with predecessor), 2 half at k*=1
+    SW_NWORDS
+};
+static_assert(SW_NWORDS <= SELS, "sel_state words");
+
+__device__ __forceinline__ L3 ld_l3(const uint64_t* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ void st_l3(uint64_t* p, L3 v) {
+    p[0] = v.a;
+    p[1] = v.b;
+    p[2] = v.c;
+}
+// x - y for x >= y (both normalised)
+__device__ __forceinline__ L3 l3_sub(L3 x, L3 y) {
+    const uint64_t M = (1ull << 43);
+    uint64_t c = x.c, b = x.b, a = x.a;
+    if (c < y.c) {
+        c += M;
+        if (b == 0) {
+            b += M;
+            a -= 1;
+        }
+        b -= 1;
+    }
+    c -= y.c;
+    if (b < y.b) {
+        b += M;
+        a -= 1;
+    }
+    b -= y.b;
+    a -= y.a;
+    return l3_norm({a, b, c});
+}
+__device__ __forceinline__ L3 l3_absdiff(L3 x, L3 y) { return l3_cmp(x, y) >= 0 ? l3_sub(x, y) : l3_sub(y, x); }
+
+// |2 P - T| within the sequential-sum error bound of T?  The reference's cumulative
+// weights and midpoint are float sums of n terms (each <= (n-1) u sum|w|, weights >= 0;
+// phase 1 also divides every weight by a float total): both sides move by < (2n + 2) u T.
+// The bound doubles that and adds the weightedstats DBL_EPSILON test (weights sum to ~1).
+__device__ __forceinline__ bool near_half(L3 P, L3 T, uint64_t n) {
+    const double d = l3_to_double(l3_absdiff(l3_twice(P), T));
+    const double t = l3_to_double(T);
+    const double bound = t * ((4.0 * (double)n + 64.0) * 0x1p-53) + 16.0 * 0x1p-52;
+    return d <= bound;
+}
+
 __device__ __forceinline__ XW sel_load(const pcx_mat& m, int s, int64_t i) {
     return XW{m.T[(int64_t)s * m.n_rows + i], m.sel_phase == 1 ? m.rep[i] : m.rowv[RV_SMOOTH * m.n_rows + i]};
 }
@@ -1250,42 +1331,42 @@ __device__ __forceinline__ bool sel_decode(const pcx_mat& m, int s, XW v, double
 }
 
 __device__ __forceinline__ bool sel_elem(const pcx_mat& m, int s, int64_t i, double& x, double& w) {
-    const double t = m.T[(int64_t)s * m.n_rows + i];
-    if (m.sel_phase == 1) {
-        if (__builtin_isnan(t)) return false;
-        x = t;
-        w = m.rep[i];
-    } else {
-        const int c = m.scaled_cols[s];
-        x = __builtin_isnan(t) ? m.ev[EV_GUESS * m.n_events + c] : t;
-        if (__builtin_isnan(x)) return false;
-        w = m.rowv[RV_SMOOTH * m.n_rows + i];
-    }
-    return true;
+    return sel_decode(m, s, sel_load(m, s, i), x, w);
 }
 
-__device__ __forceinline__ L3 ld_l3(const uint64_t* p) { return {p[0], p[1], p[2]}; }
-__device__ __forceinline__ void st_l3(uint64_t* p, L3 v) {
-    p[0] = v.a;
-    p[1] = v.b;
-    p[2] = v.c;
+__device__ __forceinline__ void sel_done(uint64_t* st, double r) {
+    st[SW_RESULT] = __double_as_longlong(r);
+    st[SW_STATUS] = 0;
 }
 
-// PCX_M_SEL_INIT: per active scaled event: exact total weight, key range, max weight
+// phase setup: which scaled events run a selection (phase 1: those with missing reports)
+__global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    const int c = m.scaled_cols[s];
+    const bool need = m.sel_phase == 1 ? m.ev[EV_MISS * m.n_events + c] > 0 : true;
+    for (int k = 0; k < SELS; k++) st[k] = 0;
+    st[SW_STATUS] = need ? 1 : 0;
+    st[SW_NEED] = need ? 1 : 0;
+    if (m.sel_phase == 2 || need) m.hard[c] = HARD_NONE;
+}
+
+// PCX selection init: this rank's exact total weight (limbs), count, key range, min / max weight
 __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     const int s = blockIdx.x;
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] == 0) return;
-    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wmaxb;
+    if (st[SW_STATUS] != 1) return;
+    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wminb, wmaxb;
     if (threadIdx.x == 0) {
         la = lb = lc = cnt = 0;
         kmin = ~0ull;
         kmax = 0;
-        wmaxb = 0;  // bits of +0.0; weights are >= 0 and order like their bit patterns
+        wminb = ~0ull;
+        wmaxb = 0;  // weights are >= 0 and order like their bit patterns
     }
     __syncthreads();
-    uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0;
-    double wm = -1.0;
+    uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0, wlo = ~0ull, whi = 0;
     rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
                              [&](int64_t, XW v) {
                                  double x, w;
@@ -1297,7 +1378,9 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
                                  const uint64_t k = dkey(x);
                                  mn = k < mn ? k : mn;
                                  mx = k > mx ? k : mx;
-                                 wm = fmax(wm, w);
+                                 const uint64_t wb = (uint64_t)__double_as_longlong(w);
+                                 wlo = wb < wlo ? wb : wlo;
+                                 whi = wb > whi ? wb : whi;
                                  n++;
                              });
     atomicAdd(&la, (unsigned long long)a);
@@ -1306,19 +1389,19 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     atomicAdd(&cnt, (unsigned long long)n);
     atomicMin(&kmin, (unsigned long long)mn);
     atomicMax(&kmax, (unsigned long long)mx);
-    wm = wave_max_d(wm);
-    if ((threadIdx.x & 63) == 0) atomicMax(&wmaxb, (unsigned long long)__double_as_longlong(wm < 0 ? 0.0 : wm));
+    atomicMin(&wminb, (unsigned long long)wlo);
+    atomicMax(&wmaxb, (unsigned long long)whi);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int64_t o = ((int64_t)m.rank * m.n_scaled + s) * NB;
-        L3 t = l3_norm({la, lb, lc});
-        m.sel_sum[o * 4 + 0] = t.a;
-        m.sel_sum[o * 4 + 1] = t.b;
-        m.sel_sum[o * 4 + 2] = t.c;
-        m.sel_sum[o * 4 + 3] = cnt;
-        m.sel_min[o * 2 + 0] = kmin;
-        m.sel_max[o] = kmax;
-        m.sel_val[((int64_t)m.rank * m.n_scaled + s) * 4 + 0] = cnt ? __longlong_as_double(wmaxb) : -1.0;
+        // limbs stay unnormalised here (carries are exact under the cross-rank SUM)
+        m.sel_isum[s * 4 + 0] = la;
+        m.sel_isum[s * 4 + 1] = lb;
+        m.sel_isum[s * 4 + 2] = lc;
+        m.sel_isum[s * 4 + 3] = cnt;
+        m.sel_imin[s * 2 + 0] = kmin;
+        m.sel_imin[s * 2 + 1] = wminb;
+        m.sel_imax[s * 2 + 0] = kmax;
+        m.sel_imax[s * 2 + 1] = wmaxb;
     }
 }
 
@@ -1329,106 +1412,166 @@ __device__ __forceinline__ int shift_for(uint64_t lo, uint64_t hi) {
     return bits > 8 ? bits - 8 : 0;
 }
 
-// PCX_M_SEL_START: combine ranks; dominance (any w > mid); first range
+__device__ __forceinline__ void mark_hard(const pcx_mat& m, int s, uint64_t* st) {
+    st[SW_STATUS] = 3;
+    m.hard[m.scaled_cols[s]] = HARD_MEDIAN;
+}
+
+// start: totals of all ranks (already reduced); empty / no positive weight -> None (NaN);
+// equal weights -> the reference's walk by pcx_seqsum.h, then a count selection; else the
+// dominant-weight test (:any(w > midpoint)) and the exact weight selection
 __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
     if (s >= m.n_scaled) return;
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] == 0) return;
-    L3 tot{0, 0, 0};
-    uint64_t kmin = ~0ull, kmax = 0, cnt = 0;
-    double wmax = -1.0;
-    for (int w = 0; w < m.world; w++) {
-        const int64_t o = ((int64_t)w * m.n_scaled + s) * NB;
-        tot = l3_add(tot, {m.sel_sum[o * 4], m.sel_sum[o * 4 + 1], m.sel_sum[o * 4 + 2]});
-        cnt += m.sel_sum[o * 4 + 3];
-        kmin = m.sel_min[o * 2] < kmin ? m.sel_min[o * 2] : kmin;
-        kmax = m.sel_max[o] > kmax ? m.sel_max[o] : kmax;
-        wmax = fmax(wmax, m.sel_val[((int64_t)w * m.n_scaled + s) * 4]);
-    }
-    st_l3(st + 7, tot);
-    st_l3(st + 4, {0, 0, 0});
-    st[10] = 0;  // max key below the range (valid if st[11])
-    st[11] = 0;
-    st[13] = __double_as_longlong(wmax);
-    const bool positive = tot.a | tot.b | tot.c;
-    if (cnt == 0 || !positive) {  // weighted_median returns None -> NaN
-        st[0] = 0;
-        st[12] = __double_as_longlong(__builtin_nan(""));
+    if (st[SW_STATUS] != 1) return;
+    const L3 tot = l3_norm({m.sel_isum[s * 4], m.sel_isum[s * 4 + 1], m.sel_isum[s * 4 + 2]});
+    const uint64_t n = m.sel_isum[s * 4 + 3];
+    const uint64_t kmin = m.sel_imin[s * 2], kmax = m.sel_imax[s * 2];
+    const uint64_t wminb = m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
+    st_l3(st + SW_TOT0, tot);
+    st_l3(st + SW_BELOW0, {0, 0, 0});
+    st[SW_BELOW_MAX] = 0;
+    st[SW_HAS_BELOW] = 0;
+    st[SW_CNT_BELOW] = 0;
+    st[SW_WMAX] = wmaxb;
+    st[SW_COUNT] = n;
+    st[SW_LO] = kmin;
+    st[SW_HI] = kmax;
+    st[SW_SHIFT] = shift_for(kmin, kmax);
+    if (n == 0 || !(tot.a | tot.b | tot.c)) {  // weighted_median returns None -> NaN
+        sel_done(st, __builtin_nan(""));
         return;
     }
-    // any(w > mid): 2*wmax > total
-    if (l3_cmp(l3_twice(l3_of(wmax)), tot) > 0) {
-        st[0] = 2;  // needs the first row holding wmax
-        atomicAdd((unsigned long long*)&m.info[IN_SEL_ARGMAX], 1ull);
-        return;
+    if (wminb == wmaxb) {
+        // equal weights: W0 = w (phase 1: w / sequential total, :294-302); mid = 0.5 * sum
+        const double w = __longlong_as_double(wmaxb);
+        const double W0 = m.sel_phase == 1 ? w / seqsum_const(w, (int64_t)n) : w;
+        const double mid = 0.5 * seqsum_const(W0, (int64_t)n);
+        if (W0 > mid) {  // dominant weight: data[first argmax] = the first element
+            st[SW_STATUS] = 2;
+            atomicAdd((unsigned long long*)&m.info[IN_SEL_ARGMAX], 1ull);
+            return;
+        }
+        if (!(W0 > 0.0)) {
+            sel_done(st, __builtin_nan(""));
+            return;
+        }
+        const int64_t ks = seqsum_first_above(W0, mid, (int64_t)n);
+        const double before = seqsum_const(W0, ks) - W0;
+        const bool half = fabs(before - mid) < 2.220446049250313080847e-16;
+        st[SW_MODE] = 1;
+        st[SW_TARGET] = (uint64_t)(ks - 1);
+        st[SW_HALF] = half ? (ks >= 2 ? 1 : (n == 1 ? 0 : 2)) : 0;
+    } else {
+        const L3 wmax = l3_of(__longlong_as_double(wmaxb));
+        if (near_half(wmax, tot, n)) {
+            mark_hard(m, s, st);
+            return;
+        }
+        if (l3_cmp(l3_twice(wmax), tot) > 0) {  // any(w > mid)
+            st[SW_STATUS] = 2;
+            atomicAdd((unsigned long long*)&m.info[IN_SEL_ARGMAX], 1ull);
+            return;
+        }
+        st[SW_MODE] = 0;
     }
-    st[1] = kmin;
-    st[2] = kmax;
-    st[3] = shift_for(kmin, kmax);
-    if (kmin == kmax) {  // one distinct value: it is the crossing value
-        st[0] = 0;
-        st[12] = __double_as_longlong(dkey_inv(kmin));
+    if (kmin == kmax) {  // one distinct value: every crossing returns it
+        sel_done(st, st[SW_HALF] == 2 ? __builtin_nan("") : dkey_inv(kmin));
     }
 }
 
-// PCX_M_SEL_ARGMAX: first local row whose weight equals the dominant weight
+// dominant weight: first global row (data order) holding the max weight -> sel_arg[s][0] (MIN)
 __global__ void __launch_bounds__(BT) k_sel_argmax(pcx_mat m) {
     const int s = blockIdx.x;
     const uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] != 2) return;
-    const double wmax = __longlong_as_double(st[13]);
+    if (st[SW_STATUS] != 2) return;
+    const uint64_t wmaxb = st[SW_WMAX];
     __shared__ unsigned long long best;
     if (threadIdx.x == 0) best = ~0ull;
     __syncthreads();
     for (int64_t i = threadIdx.x; i < m.n_rows; i += BT) {
         double x, w;
-        if (sel_elem(m, s, i, x, w) && w == wmax) {
+        if (sel_elem(m, s, i, x, w) && (uint64_t)__double_as_longlong(w) == wmaxb) {
             atomicMin(&best, (unsigned long long)(m.row_offset + i));
             break;
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) m.sel_val[((int64_t)m.rank * m.n_scaled + s) * 4 + 1] = best == ~0ull ? -1.0 : (double)best;
+    if (threadIdx.x == 0) {
+        m.sel_arg[s] = best;
+        m.sel_arg[m.n_scaled + s] = 0;
+    }
 }
 
-// PCX_M_SEL_VALUE: the rank owning the first dominant row publishes its value
+// the rank owning that row publishes its value key -> sel_arg[s][1] (MAX)
 __global__ void __launch_bounds__(BT) k_sel_value(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
     if (s >= m.n_scaled) return;
-    uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] != 2) return;
-    double first = -1.0;
-    for (int w = 0; w < m.world; w++) {
-        const double v = m.sel_val[((int64_t)w * m.n_scaled + s) * 4 + 1];
-        if (v >= 0 && (first < 0 || v < first)) first = v;
-    }
-    const int64_t gi = (int64_t)first;
-    double* out = m.sel_val + ((int64_t)m.rank * m.n_scaled + s) * 4 + 2;
-    *out = 0.0;
-    if (gi >= m.row_offset && gi < m.row_offset + m.n_rows) {
+    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[SW_STATUS] != 2) return;
+    const uint64_t gi = m.sel_arg[s];
+    uint64_t key = 0;
+    if (gi != ~0ull && (int64_t)gi >= m.row_offset && (int64_t)gi < m.row_offset + m.n_rows) {
         double x, w;
-        sel_elem(m, s, gi - m.row_offset, x, w);
-        *out = x;
+        sel_elem(m, s, (int64_t)gi - m.row_offset, x, w);
+        key = dkey(x);
     }
+    m.sel_arg[m.n_scaled + s] = key;
 }
 
 __global__ void __launch_bounds__(BT) k_sel_value_finish(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
     if (s >= m.n_scaled) return;
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] != 2) return;
-    double x = 0.0;
-    for (int w = 0; w < m.world; w++) x += m.sel_val[((int64_t)w * m.n_scaled + s) * 4 + 2];
-    st[12] = __double_as_longlong(x);
-    st[0] = 0;
+    if (st[SW_STATUS] != 2) return;
+    const uint64_t key = m.sel_arg[m.n_scaled + s];
+    sel_done(st, key ? dkey_inv(key) : __builtin_nan(""));
 }
 
-// PCX_M_SEL_HIST: exact weight histogram of the keys inside [lo, hi] (NB buckets)
+// ordered compaction of [0, n) by pred into out[] (block-wide, order preserving); returns count
+template <class PRED, class EMIT>
+__device__ int64_t block_compact(int64_t n, PRED pred, EMIT emit) {
+    __shared__ int wsum[16];
+    __shared__ int64_t base_s;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    if (tid == 0) base_s = 0;
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < n; c0 += blockDim.x) {
+        const int64_t i = c0 + tid;
+        const bool p = i < n && pred(i);
+        const uint64_t bal = __ballot(p);
+        const int before_lane = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wv] = __popcll(bal);
+        __syncthreads();
+        int off = 0;
+        for (int k = 0; k < wv; k++) off += wsum[k];
+        const int64_t base = base_s;
+        if (p) emit(i, base + off + before_lane);
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int k = 0; k < nw; k++) t += wsum[k];
+            base_s = base + t;
+        }
+        __syncthreads();
+    }
+    return base_s;
+}
+
+// active events (status 1) in event order -> sel_act, count -> info[IN_SEL_ACTIVE]
+__global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
+    const int64_t cnt = block_compact(
+        m.n_scaled, [&](int64_t s) { return m.sel_state[s * SELS + SW_STATUS] == 1; },
+        [&](int64_t s, int64_t pos) { m.sel_act[pos] = (int32_t)s; });
+    if (threadIdx.x == 0) m.info[IN_SEL_ACTIVE] = cnt;
+}
+
+// exact weight / count histogram of the keys inside [lo, hi] (NB buckets) of active event a
 __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
-    const int s = blockIdx.x;
+    const int a = blockIdx.x;
+    const int s = m.sel_act[a];
     const uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] != 1) return;
     __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB], hw[NB];
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
@@ -1437,8 +1580,9 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         hw[b] = ~0ull;
     }
     __syncthreads();
-    const uint64_t lo = st[1], hi = st[2];
-    const int sh = (int)st[3];
+    const uint64_t lo = st[SW_LO], hi = st[SW_HI];
+    const int sh = (int)st[SW_SHIFT];
+    const bool wmode = st[SW_MODE] == 0;
     rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
                              [&](int64_t, XW v) {
         double x, w;
@@ -1446,94 +1590,102 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         const uint64_t k = dkey(x);
         if (k < lo || k > hi) return;
         const int b = (int)((k - lo) >> sh);
-        const limbs3 L = to_limbs(w);
-        atomicAdd(&ha[b], (unsigned long long)L.l0);
-        atomicAdd(&hb[b], (unsigned long long)L.l1);
-        atomicAdd(&hc[b], (unsigned long long)L.l2);
+        if (wmode) {
+            const limbs3 L = to_limbs(w);
+            atomicAdd(&ha[b], (unsigned long long)L.l0);
+            atomicAdd(&hb[b], (unsigned long long)L.l1);
+            atomicAdd(&hc[b], (unsigned long long)L.l2);
+            atomicMin(&hw[b], (unsigned long long)__double_as_longlong(w));
+        }
         atomicAdd(&hn[b], 1ull);
         atomicMin(&hmin[b], (unsigned long long)k);
         atomicMax(&hmax[b], (unsigned long long)k);
-        atomicMin(&hw[b], (unsigned long long)__double_as_longlong(w));
     });
     __syncthreads();
-    const int64_t o = ((int64_t)m.rank * m.n_scaled + s) * NB;
+    const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
-        L3 t = l3_norm({ha[b], hb[b], hc[b]});
-        m.sel_sum[(o + b) * 4 + 0] = t.a;
-        m.sel_sum[(o + b) * 4 + 1] = t.b;
-        m.sel_sum[(o + b) * 4 + 2] = t.c;
-        m.sel_sum[(o + b) * 4 + 3] = hn[b];
-        m.sel_min[(o + b) * 2 + 0] = hmin[b];
-        m.sel_min[(o + b) * 2 + 1] = hw[b];
-        m.sel_max[o + b] = hmax[b];
+        m.hist_sum[(o + b) * 4 + 0] = ha[b];
+        m.hist_sum[(o + b) * 4 + 1] = hb[b];
+        m.hist_sum[(o + b) * 4 + 2] = hc[b];
+        m.hist_sum[(o + b) * 4 + 3] = hn[b];
+        m.hist_min[(o + b) * 2 + 0] = hmin[b];
+        m.hist_min[(o + b) * 2 + 1] = hw[b];
+        m.hist_max[o + b] = hmax[b];
     }
 }
 
-// PCX_M_SEL_STEP: walk the buckets (all ranks), keep the one where the prefix crosses
-// half the total; a single-key range is the crossing value (weightedstats semantics)
-__global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m) {
-    const int s = blockIdx.x * BT + threadIdx.x;
-    if (s >= m.n_scaled) return;
+// walk the buckets (reduced over ranks): weight mode keeps the bucket where the exact
+// prefix crosses half the total, count mode the one holding rank `target`; a single-key
+// bucket resolves (weight mode: unless the crossing is near a rounding-decided half)
+__global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
+    const int a = blockIdx.x * BT + threadIdx.x;
+    if (a >= n_active) return;
+    const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] != 1) return;
-    const L3 tot = ld_l3(st + 7);
-    L3 below = ld_l3(st + 4);
-    uint64_t below_max = st[10];
-    bool has_below = st[11] != 0;
+    const bool wmode = st[SW_MODE] == 0;
+    const L3 tot = ld_l3(st + SW_TOT0);
+    const uint64_t n_all = st[SW_COUNT], target = st[SW_TARGET];
+    L3 below = ld_l3(st + SW_BELOW0);
+    uint64_t cbelow = st[SW_CNT_BELOW];
+    uint64_t below_max = st[SW_BELOW_MAX];
+    bool has_below = st[SW_HAS_BELOW] != 0;
+    const int64_t o = (int64_t)a * NB;
     for (int b = 0; b < NB; b++) {
-        L3 hs{0, 0, 0};
-        uint64_t n = 0, kmin = ~0ull, kmax = 0, wmin = ~0ull;
-        for (int w = 0; w < m.world; w++) {
-            const int64_t o = ((int64_t)w * m.n_scaled + s) * NB + b;
-            hs = l3_add(hs, {m.sel_sum[o * 4], m.sel_sum[o * 4 + 1], m.sel_sum[o * 4 + 2]});
-            n += m.sel_sum[o * 4 + 3];
-            kmin = m.sel_min[o * 2] < kmin ? m.sel_min[o * 2] : kmin;
-            wmin = m.sel_min[o * 2 + 1] < wmin ? m.sel_min[o * 2 + 1] : wmin;
-            kmax = m.sel_max[o] > kmax ? m.sel_max[o] : kmax;
-        }
+        const uint64_t* hs = m.hist_sum + (o + b) * 4;
+        const uint64_t n = hs[3];
         if (n == 0) continue;
-        const L3 upto = l3_add(below, hs);
-        if (l3_cmp(l3_twice(upto), tot) > 0) {
-            // crossing bucket
+        const L3 hw = l3_norm({hs[0], hs[1], hs[2]});
+        const uint64_t kmin = m.hist_min[(o + b) * 2], kmax = m.hist_max[o + b];
+        const L3 upto = l3_add(below, hw);
+        const bool cross = wmode ? l3_cmp(l3_twice(upto), tot) > 0 : cbelow + n > target;
+        if (cross) {
             if (kmin == kmax) {
                 const double xs = dkey_inv(kmin);
-                const L3 first = l3_add(below, l3_of(__longlong_as_double(wmin)));
-                const bool at_start = l3_cmp(l3_twice(first), tot) > 0;
-                double res = xs;
-                if (at_start && has_below && l3_cmp(l3_twice(below), tot) == 0)
-                    res = (dkey_inv(below_max) + xs) / 2.0;  // exact half: mean of the pair
-                st[12] = __double_as_longlong(res);
-                st[0] = 0;
+                if (wmode) {
+                    if (near_half(below, tot, n_all) || near_half(upto, tot, n_all)) {
+                        mark_hard(m, s, st);
+                        return;
+                    }
+                    sel_done(st, xs);
+                } else {
+                    double r = xs;
+                    if (st[SW_HALF] == 2) {
+                        r = __builtin_nan("");
+                    } else if (st[SW_HALF] == 1) {
+                        const double pred = target >= cbelow + 1 ? xs : dkey_inv(below_max);
+                        r = (pred + xs) / 2.0;  // sum(bounds) / float(len(bounds))
+                    }
+                    sel_done(st, r);
+                }
             } else {
-                st[1] = kmin;
-                st[2] = kmax;
-                st[3] = shift_for(kmin, kmax);
-                st_l3(st + 4, below);
-                st[10] = below_max;
-                st[11] = has_below ? 1 : 0;
-                atomicAdd((unsigned long long*)&m.info[IN_SEL_ACTIVE], 1ull);
+                st[SW_LO] = kmin;
+                st[SW_HI] = kmax;
+                st[SW_SHIFT] = shift_for(kmin, kmax);
+                st_l3(st + SW_BELOW0, below);
+                st[SW_CNT_BELOW] = cbelow;
+                st[SW_BELOW_MAX] = below_max;
+                st[SW_HAS_BELOW] = has_below ? 1 : 0;
             }
             return;
         }
         below = upto;
+        cbelow += n;
         below_max = kmax;
         has_below = true;
     }
-    // no crossing (cannot happen with exact sums): give up with NaN
-    st[12] = __double_as_longlong(__builtin_nan(""));
-    st[0] = 0;
+    sel_done(st, __builtin_nan(""));  // no crossing (cannot happen with exact sums)
 }
 
-// PCX_M_SEL_FINISH: phase 1 -> guess (int dtype truncates, :312); phase 2 -> outcomes
+// results into guess (phase 1; int dtype truncates, :312) / outcomes (phase 2, :537-538)
 __global__ void __launch_bounds__(BT) k_sel_finish(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
     if (s >= m.n_scaled) return;
     const int E = (int)m.n_events;
     const int c = m.scaled_cols[s];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    const double r = __longlong_as_double(st[12]);
+    const double r = __longlong_as_double(st[SW_RESULT]);
     if (m.sel_phase == 1) {
-        if (st[15]) m.ev[EV_GUESS * E + c] = m.int_dtype ? trunc(r) : r;
+        if (st[SW_NEED]) m.ev[EV_GUESS * E + c] = m.int_dtype ? trunc(r) : r;
     } else {
         m.ev[EV_RAW * E + c] = r;
         m.ev[EV_ADJ * E + c] = r;
@@ -1549,12 +1701,10 @@ __global__ void __launch_bounds__(BT) k_sel_finish(pcx_mat m) {
 // present reports in row order.  Phase 2 (:520-523): weights smooth_rep over all rows.
 // mid = 0.5 * builtin sum (row order); dominant weight -> first argmax; else bitonic sort
 // by (value, weight) and the sequential walk with the DBL_EPSILON exact-half test.
-constexpr int SEL_EXACT_MAX = 8192;
-
 __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
     const int s = blockIdx.x;
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[0] == 0) return;
+    if (st[SW_STATUS] == 0) return;
     __shared__ double xs[SEL_EXACT_MAX];
     __shared__ double ws[SEL_EXACT_MAX];
     __shared__ int cnt;
@@ -1608,17 +1758,11 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
     }
     __syncthreads();
     if (first_s >= 0) {
-        if (tid == 0) {
-            st[12] = __double_as_longlong(xs[first_s]);
-            st[0] = 0;
-        }
+        if (tid == 0) sel_done(st, xs[first_s]);
         return;
     }
     if (wmax_s == 0.0) {  // no positive weight: None
-        if (tid == 0) {
-            st[12] = __double_as_longlong(__builtin_nan(""));
-            st[0] = 0;
-        }
+        if (tid == 0) sel_done(st, __builtin_nan(""));
         return;
     }
     // bitonic sort of (x, w) pairs, padded to a power of two with +inf
@@ -1672,21 +1816,283 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
                 res = xs[k - 1];
             }
         }
-        st[12] = __double_as_longlong(res);
-        st[0] = 0;
+        sel_done(st, res);
     }
 }
 
-// phase setup: which scaled events run a selection (phase 1: those with missing reports)
-__global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
-    const int s = blockIdx.x * BT + threadIdx.x;
-    if (s >= m.n_scaled) return;
+// ------------------------------------------------------------------ hard replay
+// Events whose decision sits within rounding of a threshold are replayed in the
+// reference's own order.  Phase 1 (interpolate, :287-309): the present reports of the
+// event in row order with weights rep_j / (sequential total); binary events: the
+// sequential weighted mean then catch; scaled events: weightedstats on those pairs.
+// Phase 2 (:519-523): weightedstats over the filled column with smooth_rep.
+
+// this rank's elements of hard event j in row order -> send[j][0 .. cnt)
+__global__ void __launch_bounds__(1024) k_hard_gather(pcx_mat m, HardArgs h) {
+    const int j = blockIdx.x;
+    const int c = h.cols[j];
+    const ColParam p = col_param(m, c, true);
+    double* out = h.send + (int64_t)j * h.cap * 2;
+    const double* wsrc = m.sel_phase == 1 ? m.rep : m.rowv + RV_SMOOTH * m.n_rows;
+    const int64_t E = m.n_events;
+    const int64_t n = block_compact(
+        m.n_rows,
+        [&](int64_t i) {
+            const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
+            if (m.sel_phase == 1) return !missing(x);
+            return !__builtin_isnan(missing(x) ? p.guess : x);
+        },
+        [&](int64_t i, int64_t pos) {
+            const double x = rescale(m.reports[i * E + c], p, m.int_dtype);
+            out[pos * 2 + 0] = missing(x) ? p.guess : x;
+            out[pos * 2 + 1] = wsrc[i];
+        });
+    if (threadIdx.x == 0) h.send_cnt[j] = n;
+}
+
+// sequential left-to-right fp64 sum of f(k), k in [0, n), by thread 0, fed through LDS
+// tiles loaded by the whole block (the add chain is the limit: ~10 cycles per element)
+template <class F>
+__device__ double block_serial_sum(int64_t n, F f, double* tile, int TILE) {
+    __shared__ double acc_s;
+    double acc = 0.0;
+    for (int64_t t0 = 0; t0 < n; t0 += TILE) {
+        const int len = (int)(n - t0 < TILE ? n - t0 : TILE);
+        for (int k = threadIdx.x; k < len; k += blockDim.x) tile[k] = f(t0 + k);
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int k = 0; k < len; k++) acc = acc + tile[k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) acc_s = acc;
+    __syncthreads();
+    return acc_s;
+}
+
+constexpr int HARD_TILE = 4096;
+
+__global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
+    __shared__ double tile[HARD_TILE];
+    __shared__ double wmax_s;
+    __shared__ unsigned long long first_s;
+    __shared__ int pos_s;
+    const int j = blockIdx.x;
+    const int c = h.cols[j];
+    const int mode = h.modes[j];
+    const int64_t N = m.n_total;
+    double* X = h.X + (int64_t)j * N;
+    double* W = h.W + (int64_t)j * N;
+    double* hs = h.hs + (int64_t)j * 4;
+    // concatenate the ranks' rows (rank order = row order)
+    int64_t n = 0;
+    for (int w = 0; w < m.world; w++) {
+        const int64_t cw = h.recv_cnt[(int64_t)w * h.n_hard + j];
+        const double* src = h.recv + ((int64_t)w * h.n_hard + j) * h.cap * 2;
+        for (int64_t k = threadIdx.x; k < cw; k += blockDim.x) {
+            X[n + k] = src[2 * k];
+            W[n + k] = src[2 * k + 1];
+        }
+        n += cw;
+    }
+    __syncthreads();
+    if (m.sel_phase == 1) {  // weights rep_j / sequential total of the present rep (:294-302)
+        const double tot = block_serial_sum(n, [&](int64_t k) { return W[k]; }, tile, HARD_TILE);
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x) W[k] = W[k] / tot;
+        __syncthreads();
+    }
+    const int s = m.scaled_index ? m.scaled_index[c] : -1;
+    if (mode == HARD_MEAN) {  // guess = sum_seq(w * x) then catch (:304-309)
+        const double g = block_serial_sum(n, [&](int64_t k) { return W[k] * X[k]; }, tile, HARD_TILE);
+        if (threadIdx.x == 0) {
+            double v = n > 0 ? catch_value(g, m.catch_tolerance) : catch_value(0.0, m.catch_tolerance);
+            if (m.int_dtype) v = trunc(v);
+            m.ev[EV_GUESS * m.n_events + c] = v;
+            hs[2] = 0.0;
+        }
+        return;
+    }
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    const int c = m.scaled_cols[s];
-    const bool need = m.sel_phase == 1 ? m.ev[EV_MISS * m.n_events + c] > 0 : true;
-    for (int k = 0; k < SELS; k++) st[k] = 0;
-    st[0] = need ? 1 : 0;
-    st[15] = need ? 1 : 0;
+    const double mid = 0.5 * block_serial_sum(n, [&](int64_t k) { return W[k]; }, tile, HARD_TILE);
+    // dominance: any(w > mid) -> data[first index of max(w)]; no positive weight -> None
+    if (threadIdx.x == 0) {
+        wmax_s = 0.0;  // weights are >= 0: max over their bit patterns
+        first_s = ~0ull;
+        pos_s = 0;
+    }
+    __syncthreads();
+    double wl = -__builtin_inf();
+    int posl = 0;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+        wl = fmax(wl, W[k]);
+        posl |= W[k] > 0.0;
+    }
+    wl = wave_max_d(wl);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax((unsigned long long*)&wmax_s, (unsigned long long)__double_as_longlong(wl < 0 ? 0.0 : wl));
+    }
+    if (posl) pos_s = 1;
+    __syncthreads();
+    const double wmax = wmax_s;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x)
+        if (W[k] == wmax) {
+            atomicMin(&first_s, (unsigned long long)k);
+            break;
+        }
+    __syncthreads();
+    if (wmax > mid) {
+        if (threadIdx.x == 0) {
+            sel_done(st, X[first_s]);
+            hs[2] = 0.0;
+        }
+        return;
+    }
+    if (!pos_s) {
+        if (threadIdx.x == 0) {
+            sel_done(st, __builtin_nan(""));
+            hs[2] = 0.0;
+        }
+        return;
+    }
+    uint64_t* keys = h.keys + (int64_t)j * h.P * 2;
+    for (int64_t k = threadIdx.x; k < h.P; k += blockDim.x) {
+        keys[2 * k + 0] = k < n ? dkey(X[k]) : ~0ull;
+        keys[2 * k + 1] = k < n ? dkey(W[k]) : ~0ull;
+    }
+    if (threadIdx.x == 0) {
+        hs[0] = mid;
+        hs[1] = (double)n;
+        hs[2] = 1.0;  // sort + walk pending
+    }
+}
+
+// bitonic sort of every segment keys[j][0 .. P) by (value key, weight key)
+__device__ __forceinline__ bool key_gt(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    return ah > bh || (ah == bh && al > bl);
+}
+
+constexpr int BS_TILE = 4096;  // elements sorted in LDS per block (64 KB)
+
+// stages size <= min(P, BS_TILE) of the network (init) or strides < BS_TILE of one size (merge)
+__global__ void __launch_bounds__(1024) k_bsort_lds(uint64_t* keys, int64_t P, int64_t size_only) {
+    __shared__ uint64_t kh[BS_TILE], kl[BS_TILE];
+    const int64_t tile = P < BS_TILE ? P : BS_TILE;
+    const int64_t base = (int64_t)blockIdx.x * tile;  // global element index (segments are contiguous)
+    for (int k = threadIdx.x; k < tile; k += 1024) {
+        kh[k] = keys[2 * (base + k)];
+        kl[k] = keys[2 * (base + k) + 1];
+    }
+    __syncthreads();
+    const int64_t s0 = size_only ? size_only : 2;
+    const int64_t s1 = size_only ? size_only : tile;
+    for (int64_t size = s0; size <= s1; size <<= 1) {
+        for (int64_t stride = (size_only ? tile : size) >> 1; stride > 0; stride >>= 1) {
+            if (stride >= size) continue;
+            for (int t = threadIdx.x; t < tile / 2; t += 1024) {
+                const int lo = (int)(2 * stride * (t / stride) + (t % stride));
+                const int hi = lo + (int)stride;
+                const int64_t g = (base + lo) % P;  // index within the segment: direction
+                const bool up = (g & size) == 0;
+                const bool gt = key_gt(kh[lo], kl[lo], kh[hi], kl[hi]);
+                if (gt == up) {
+                    const uint64_t a = kh[lo], b = kl[lo];
+                    kh[lo] = kh[hi];
+                    kl[lo] = kl[hi];
+                    kh[hi] = a;
+                    kl[hi] = b;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int k = threadIdx.x; k < tile; k += 1024) {
+        keys[2 * (base + k)] = kh[k];
+        keys[2 * (base + k) + 1] = kl[k];
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_bsort_global(uint64_t* keys, int64_t P, int64_t total, int64_t size,
+                                                     int64_t stride) {
+    for (int64_t t = blockIdx.x * (int64_t)BT + threadIdx.x; t < total / 2; t += (int64_t)gridDim.x * BT) {
+        const int64_t lo = 2 * stride * (t / stride) + (t % stride);
+        const int64_t hi = lo + stride;
+        const bool up = ((lo % P) & size) == 0;
+        const uint64_t ah = keys[2 * lo], al = keys[2 * lo + 1], bh = keys[2 * hi], bl = keys[2 * hi + 1];
+        if (key_gt(ah, al, bh, bl) == up) {
+            keys[2 * lo] = bh;
+            keys[2 * lo + 1] = bl;
+            keys[2 * hi] = ah;
+            keys[2 * hi + 1] = al;
+        }
+    }
+}
+
+// the walk (:weighted_median while loop) over the sorted pairs of each pending event
+__global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
+    __shared__ double tw[HARD_TILE];
+    __shared__ int done_s;
+    __shared__ int64_t k_s;
+    __shared__ double cum_s;
+    const int j = blockIdx.x;
+    double* hs = h.hs + (int64_t)j * 4;
+    if (h.modes[j] != HARD_MEDIAN || hs[2] != 1.0) return;
+    const int c = h.cols[j];
+    uint64_t* st = m.sel_state + (int64_t)m.scaled_index[c] * SELS;
+    const uint64_t* keys = h.keys + (int64_t)j * h.P * 2;
+    const double mid = hs[0];
+    const int64_t n = (int64_t)hs[1];
+    if (threadIdx.x == 0) {
+        done_s = 0;
+        k_s = 0;
+        cum_s = 0.0;
+    }
+    __syncthreads();
+    // cum += w while cum <= mid, tile by tile
+    for (int64_t t0 = 0; t0 < n && !done_s; t0 += HARD_TILE) {
+        const int len = (int)(n - t0 < HARD_TILE ? n - t0 : HARD_TILE);
+        for (int k = threadIdx.x; k < len; k += 1024) tw[k] = dkey_inv(keys[2 * (t0 + k) + 1]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double cum = cum_s;
+            int k = 0;
+            while (cum <= mid && k < len) cum += tw[k++];
+            cum_s = cum;
+            k_s = t0 + k;
+            if (cum > mid) done_s = 1;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        double res;
+        const int64_t k = k_s;
+        if (!done_s) {
+            res = __builtin_nan("");  // the walk ran off the end (the reference raises IndexError)
+        } else {
+            const double wk = dkey_inv(keys[2 * (k - 1) + 1]);
+            const double before = cum_s - wk;
+            const double xk = dkey_inv(keys[2 * (k - 1)]);
+            if (fabs(before - mid) < 2.220446049250313080847e-16) {
+                if (k >= 2)
+                    res = (dkey_inv(keys[2 * (k - 2)]) + xk) / 2.0;
+                else
+                    res = n == 1 ? xk / 1.0 : __builtin_nan("");
+            } else {
+                res = xk;
+            }
+        }
+        sel_done(st, res);
+        hs[2] = 0.0;
+    }
+}
+
+// events marked hard (m.hard[c] != 0) in event order -> cols / modes, count -> info[IN_HARD]
+__global__ void __launch_bounds__(1024) k_hard_list(pcx_mat m, int32_t* cols, int32_t* modes) {
+    const int64_t cnt = block_compact(
+        m.n_events, [&](int64_t c) { return m.hard[c] != HARD_NONE; },
+        [&](int64_t c, int64_t pos) {
+            cols[pos] = (int32_t)c;
+            modes[pos] = m.hard[c];
+        });
+    if (threadIdx.x == 0) m.info[IN_HARD] = cnt;
 }
 
 // PCX_M_SCALED_CERT: sum of smooth_rep over rows whose filled value equals the outcome
@@ -1838,6 +2244,34 @@ __global__ void __launch_bounds__(BT) k_matrices(pcx_mat m) {
 
 __global__ void k_info_clear(pcx_mat m, int slot) { m.info[slot] = 0; }
 
+// nonconformity entry: nc = set1 or set2 (:494-498, :482-484)
+__global__ void __launch_bounds__(BT) k_nc_out(pcx_mat m) {
+    double mn, mx;
+    score_minmax(m, mn, mx);
+    const int pick1 = (int)m.info[IN_PICK1];
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double s = m.rowv[RV_S * m.n_rows + i];
+        m.nc_out[i] = pick1 ? s + fabs(mn) : s - mx;
+    }
+}
+
+// wpca entry: weighted_mean (:317-319)
+__global__ void __launch_bounds__(BT) k_wmean_out(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c < m.n_events) m.weighted_mean[c] = m.ev[EV_MU * m.n_events + c];
+}
+
+// strided 2-D copy (slot exchange pack / unpack)
+__global__ void __launch_bounds__(BT) k_copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch,
+                                               int64_t width, int64_t rows) {
+    const int64_t n = width * rows;
+    for (int64_t t = blockIdx.x * (int64_t)BT + threadIdx.x; t < n; t += (int64_t)gridDim.x * BT) {
+        const int64_t r = t / width, c = t % width;
+        dst[r * dpitch + c] = src[r * spitch + c];
+    }
+}
+
+
 __global__ void k_zero_loading(pcx_mat m) {
     for (int j = threadIdx.x; j < m.n_events; j += blockDim.x) m.ev[EV_LD * m.n_events + j] = 0.0;
 }
@@ -1884,22 +2318,24 @@ double np_pairwise(const double* a, int64_t n) {
     return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
 }
 
+// one rocBLAS handle per (host thread, device): rocblas_set_stream + dsyevd on a handle
+// shared between the threads of virtual ranks would race (handles are not thread-safe)
 rocblas_handle blas_handle(int device) {
-    static std::mutex mu;
-    static std::map<int, rocblas_handle> handles;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = handles.find(device);
-    if (it != handles.end()) return it->second;
+    struct Handles {
+        std::map<int, rocblas_handle> h;
+        ~Handles() {
+            for (auto& kv : h) rocblas_destroy_handle(kv.second);
+        }
+    };
+    static thread_local Handles handles;
+    auto it = handles.h.find(device);
+    if (it != handles.h.end()) return it->second;
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-    handles[device] = h;
+    handles.h[device] = h;
     return h;
 }
 
-// big-five / fixed-variance (:375-382, :431-449): eigenpairs of C by rocSOLVER dsyevd
-// (the reference calls LAPACK gesdd on the same symmetric PSD matrix: Sigma = |lambda|,
-// U = eigenvectors), component selection on the host (E numbers), and the score
-// vector g = sum_c Sigma_c * sign_c * u_c into ev[EV_SPARE] (PCX_M_SCORES: wcd . g).
 hipError_t eig_stage(pcx_mat& m, hipStream_t st, std::string& err) {
     const int E = (int)m.n_events;
     const int64_t nn = (int64_t)E * E;
@@ -1981,151 +2417,207 @@ int grid_rows(int64_t n, int per_block) {
 }  // namespace
 
 // ------------------------------------------------------------------ stage dispatcher
+const char* stage_name(int k) {
+    static const char* names[M_NSTAGE] = {
+        "none", "REPUTATION", "COLSTATS", "GUESS", "MEAN", "COV", "COV_REDUCE", "COV_FINISH", "POWER",
+        "SCORES", "NCSUMS", "GEMV2", "DECIDE", "REPU", "SMOOTH", "OUTCOMES", "EVENTS", "SCALED_CERT", "FINAL",
+        "ROWSUMS", "AGENTS", "MATRICES", "WCD", "EIG", "ZERO_LOADING", "NC_OUT", "WMEAN_OUT", "SEL_EXACT",
+        "SEL_INIT", "SEL_START", "SEL_ARGMAX", "SEL_VALUE", "SEL_VALUE_FINISH", "SEL_COMPACT", "SEL_HIST",
+        "SEL_STEP", "SEL_FINISH", "HARD_LIST", "HARD_GATHER", "HARD_PREP", "HARD_SORT", "HARD_WALK", "EXCHANGE",
+        "H2D", "D2H"};
+    return (k >= 0 && k < M_NSTAGE) ? names[k] : "";
+}
+
+hipError_t copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch, int64_t width, int64_t rows,
+                  hipStream_t st) {
+    if (width <= 0 || rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_copy2d, dim3(grid_rows(width * rows, BT)), dim3(BT), 0, st, dst, dpitch, src, spitch, width,
+                       rows);
+    return hipGetLastError();
+}
+
+hipError_t hard_stage(pcx_mat& m, const HardArgs& h, int stage, hipStream_t st, std::string& err) {
+    if (h.n_hard <= 0) return hipSuccess;
+    switch (stage) {
+        case M_HARD_GATHER:
+            hipLaunchKernelGGL(k_hard_gather, dim3(h.n_hard), dim3(1024), 0, st, m, h);
+            break;
+        case M_HARD_PREP:
+            hipLaunchKernelGGL(k_hard_prep, dim3(h.n_hard), dim3(1024), 0, st, m, h);
+            break;
+        case M_HARD_SORT: {
+            // bitonic network over n_hard contiguous segments of P (a power of two)
+            const int64_t P = h.P, total = P * h.n_hard;
+            const int64_t tile = P < BS_TILE ? P : BS_TILE;
+            const unsigned nblk = (unsigned)(total / tile);
+            hipLaunchKernelGGL(k_bsort_lds, dim3(nblk), dim3(1024), 0, st, h.keys, P, (int64_t)0);
+            for (int64_t size = tile * 2; size <= P; size <<= 1) {
+                for (int64_t stride = size >> 1; stride >= tile; stride >>= 1)
+                    hipLaunchKernelGGL(k_bsort_global, dim3(grid_rows(total / 2, BT)), dim3(BT), 0, st, h.keys, P,
+                                       total, size, stride);
+                hipLaunchKernelGGL(k_bsort_lds, dim3(nblk), dim3(1024), 0, st, h.keys, P, size);
+            }
+            break;
+        }
+        case M_HARD_WALK:
+            hipLaunchKernelGGL(k_hard_walk, dim3(h.n_hard), dim3(1024), 0, st, m, h);
+            break;
+        default:
+            err = "hard_stage: unknown stage";
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
     const int E = (int)m.n_events;
     const int ceb = (E + BT - 1) / BT;
     const dim3 colgrid(ceb, m.col_blocks);
     const int rg = grid_rows(m.n_rows, BT);
+    const int sg = (m.n_scaled + BT - 1) / BT;
     switch (stage) {
-        case PCX_M_REPUTATION:
+        case M_REPUTATION:
             if (m.rep_raw) hipLaunchKernelGGL(k_rep_total, dim3(1), dim3(1024), 0, st, m);
             hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_TOK);
             break;
-        case PCX_M_COLSTATS:
+        case M_COLSTATS:
             hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
             break;
-        case PCX_M_GUESS:
+        case M_GUESS:
             hipLaunchKernelGGL(k_guess, dim3(ceb), dim3(BT), 0, st, m);
             break;
-        case PCX_M_MEAN:
+        case M_MEAN:
             hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
             break;
-        case PCX_M_WCD:
-        case PCX_M_COV: {
+        case M_WCD:
+        case M_COV: {
             if (!m.wcd || !m.tokp || !m.rowpart || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
                 m.wcd_ld < m.n_events) {
-                err = "PCX_M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
+                err = "M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
                 return hipErrorInvalidValue;
             }
-            if (stage == PCX_M_WCD) {
+            if (stage == M_WCD) {
                 const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
                 hipLaunchKernelGGL(k_wcd,
                                    dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(m.wcd_rows, 4096 / ncb)), ncb),
                                    dim3(BT), 0, st, m);
                 break;
             }
-            static bool lds_set = false;
-            if (!lds_set) {
-                hipError_t e = hipFuncSetAttribute((const void*)k_syrk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   (int)SY_LDS_BYTES);
-                if (e != hipSuccess) return e;
-                lds_set = true;
-            }
+            static std::once_flag lds_once;
+            static hipError_t lds_err = hipSuccess;
+            std::call_once(lds_once, [] {
+                lds_err = hipFuncSetAttribute((const void*)k_syrk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)SY_LDS_BYTES);
+            });
+            if (lds_err != hipSuccess) return lds_err;
             hipLaunchKernelGGL(k_syrk, dim3(m.cov_tiles * m.cov_kslices), dim3(256), SY_LDS_BYTES, st, m);
             break;
         }
-        case PCX_M_COV_REDUCE: {
+        case M_COV_REDUCE: {
             const int64_t n = (int64_t)E * E;
             hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);
             break;
         }
-        case PCX_M_COV_FINISH: {
+        case M_COV_FINISH: {
             const int64_t n = (int64_t)E * E;
             hipLaunchKernelGGL(k_cov_finish, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);
             break;
         }
-        case PCX_M_SCORES:
+        case M_SCORES:
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
-            if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && m.wcd && m.rowpart)  // wcd ready (PCX_M_COV)
+            if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart)
                 hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             else
                 hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             break;
-        case PCX_M_NCSUMS:
+        case M_NCSUMS:
             hipLaunchKernelGGL(k_ncsums, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 4, (int)SC_A1);
             break;
-        case PCX_M_GEMV2:
+        case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
             break;
-        case PCX_M_DECIDE:
+        case M_DECIDE:
             hipLaunchKernelGGL(k_decide_prep, dim3(ceb), dim3(BT), 0, st, m);
-            if (m.algorithm == 0) hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
+            if (m.rank_rule) hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), 0, st, m);
             break;
-        case PCX_M_REPU:
+        case M_REPU:
             hipLaunchKernelGGL(k_repu, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_U);
             break;
-        case PCX_M_SMOOTH:
+        case M_SMOOTH:
             hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_OUTCOMES:
+        case M_OUTCOMES:
             hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
             break;
-        case PCX_M_EVENTS:
+        case M_EVENTS:
             hipLaunchKernelGGL(k_events, dim3(ceb), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SCALED_CERT:
+        case M_SCALED_CERT:
             if (m.n_scaled > 0) hipLaunchKernelGGL(k_scaled_cert, dim3(m.n_scaled), dim3(BT), 0, st, m);
             break;
-        case PCX_M_FINAL:
+        case M_FINAL:
             hipLaunchKernelGGL(k_final, dim3(1), dim3(1024), 0, st, m);
             break;
-        case PCX_M_ROWSUMS:
+        case M_ROWSUMS:
             hipLaunchKernelGGL(k_rowsums, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_AR);
             break;
-        case PCX_M_AGENTS:
+        case M_AGENTS:
             hipLaunchKernelGGL(k_agents, dim3(rg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_INIT:
+        case M_NC_OUT:
+            hipLaunchKernelGGL(k_nc_out, dim3(rg), dim3(BT), 0, st, m);
+            break;
+        case M_WMEAN_OUT:
+            hipLaunchKernelGGL(k_wmean_out, dim3(ceb), dim3(BT), 0, st, m);
+            break;
+        case M_SEL_INIT:
             if (m.n_scaled == 0) break;
-            hipLaunchKernelGGL(k_sel_setup, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_setup, dim3(sg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_init, dim3(m.n_scaled), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_EXACT:
+        case M_SEL_EXACT:
             if (m.n_scaled == 0) break;
             if (m.world != 1 || m.n_rows > SEL_EXACT_MAX) {
-                err = "PCX_M_SEL_EXACT needs one rank and n_rows <= 8192";
+                err = "M_SEL_EXACT needs one rank and n_rows <= 8192";
                 return hipErrorInvalidValue;
             }
-            hipLaunchKernelGGL(k_sel_setup, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_setup, dim3(sg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_exact, dim3(m.n_scaled), dim3(1024), 0, st, m);
             break;
-        case PCX_M_SEL_START:
+        case M_SEL_START:
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_SEL_ARGMAX);
-            hipLaunchKernelGGL(k_sel_start, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_start, dim3(sg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_ARGMAX:
+        case M_SEL_ARGMAX:
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_sel_argmax, dim3(m.n_scaled), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_VALUE:
+        case M_SEL_VALUE:
             if (m.n_scaled == 0) break;
-            hipLaunchKernelGGL(k_sel_value, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_value, dim3(sg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_HIST:
+        case M_SEL_VALUE_FINISH:
             if (m.n_scaled == 0) break;
-            hipLaunchKernelGGL(k_sel_hist, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_value_finish, dim3(sg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_STEP:
+        case M_SEL_COMPACT:
+            hipLaunchKernelGGL(k_sel_compact, dim3(1), dim3(1024), 0, st, m);
+            break;
+        case M_SEL_FINISH:
             if (m.n_scaled == 0) break;
-            hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_SEL_ACTIVE);
-            hipLaunchKernelGGL(k_sel_step, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_finish, dim3(sg), dim3(BT), 0, st, m);
             break;
-        case PCX_M_SEL_FINISH:
-            if (m.n_scaled == 0) break;
-            hipLaunchKernelGGL(k_sel_value_finish, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_sel_finish, dim3((m.n_scaled + BT - 1) / BT), dim3(BT), 0, st, m);
-            break;
-        case PCX_M_POWER: {
+        case M_POWER: {
             // replicated on every rank (C is identical everywhere); host loop with polling
             hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_FLAGS);
             const int64_t nn = (int64_t)E * E;
@@ -2198,20 +2690,38 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (e != hipSuccess) return e;
             break;
         }
-        case PCX_M_MATRICES:
+        case M_MATRICES:
             if (m.original || m.filled)
                 hipLaunchKernelGGL(k_matrices, dim3(grid_rows(m.n_rows * m.n_events, BT)), dim3(BT), 0, st, m);
             break;
-        case PCX_M_EIG:
+        case M_EIG:
             if (m.algorithm != 2 && m.algorithm != 3) break;
             return eig_stage(m, st, err);
-        case 99:  // "absolute": no loading
+        case M_ZERO_LOADING:  // "absolute" / "cokurtosis": no wpca loading
             hipLaunchKernelGGL(k_zero_loading, dim3(1), dim3(256), 0, st, m);
             break;
         default:
-            err = "pcx_mat_stage: unknown stage " + std::to_string(stage);
+            err = "mat_stage: unknown stage " + std::to_string(stage);
             return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// hard-list compaction (events with m.hard[c] != 0) into cols / modes, count -> info[IN_HARD]
+hipError_t hard_list(pcx_mat& m, int32_t* cols, int32_t* modes, hipStream_t st) {
+    hipLaunchKernelGGL(k_hard_list, dim3(1), dim3(1024), 0, st, m, cols, modes);
+    return hipGetLastError();
+}
+
+hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st) {
+    if (n_active <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sel_hist, dim3(n_active), dim3(BT), 0, st, m);
+    return hipGetLastError();
+}
+
+hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st) {
+    if (n_active <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sel_step, dim3((n_active + BT - 1) / BT), dim3(BT), 0, st, m, n_active);
     return hipGetLastError();
 }
 

@@ -1,0 +1,750 @@
+// pcx_runner.cpp -- the single-matrix consensus as ONE library call.
+//
+// Sequences the stages of pcx_matrix.hip for Oracle.consensus() (__init__.py:502-611)
+// and for the reference's stage methods (interpolate / wpca / lie_detector /
+// nonconformity(_rank), :260-500); owns the scratch (cached per context) and the
+// cross-rank exchange between stages (pcx_comm.cpp: RCCL, in-process group, callbacks).
+//
+// Exchange discipline:
+//   * per-rank double-double partial sums live in slot [rank] of [world][...] buffers and
+//     are ALL-GATHERED; kernels then combine the ranks in rank order, so every rank gets
+//     bit-identical event vectors whatever the collective's internal order;
+//   * exact integer selection state (weight limbs, counts) is all-reduced with SUM, key
+//     ranges and minimum weights with MIN / MAX -- order-independent by construction;
+//   * the covariance partial (E x E) is the one floating-point SUM all-reduce.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "pcx_internal.h"
+
+namespace {
+constexpr int BT = 256;
+constexpr int CS = 16;  // dd slots per column in cstat
+constexpr int SS = 16;  // dd slots in scal
+constexpr int COV_TILE = 128;
+constexpr int COV_STAGE = 16;
+constexpr int SELS = 24;
+constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
+
+template <class T>
+T* at(void* base, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(base) + off);
+}
+}  // namespace
+
+// one rank's scratch for an (n_rows x E) shard with n_scaled scaled events
+struct pcx_workspace {
+    int64_t n_rows = -1, E = -1, n_total = -1;
+    int n_scaled = -1, world = -1;
+    int64_t col_blocks = 0, cov_tiles = 0, cov_kslices = 0, wcd_rows = 0, wcd_ld = 0;
+    std::vector<void*> blocks;
+    size_t bytes = 0;
+    // zeroed before every call
+    void* zero_base = nullptr;
+    size_t zero_bytes = 0;
+    // buffers
+    double *rep, *tok, *T, *part, *mpart, *cstat, *cmax, *scal, *spart, *ev, *cslab, *C, *Mw, *pvec, *rowv;
+    uint32_t* rowstat;
+    uint64_t* skey;
+    int64_t* info;
+    uint64_t *sel_state, *sel_isum, *sel_imin, *sel_imax, *hist_sum, *hist_min, *hist_max, *sel_arg;
+    int32_t *sel_act, *hard, *hard_cols, *hard_modes, *scols, *sidx;
+    double *wcd, *tokp, *scalars, *xsend, *xrecv;
+    uint32_t* rowpart;
+    int64_t xcap = 0;  // doubles per rank in xsend
+
+    ~pcx_workspace() {
+        for (void* p : blocks) (void)hipFree(p);
+    }
+};
+
+namespace pcx {
+namespace {
+
+struct Fail {
+    int code;
+};
+
+struct Run {
+    pcx_ctx* c;
+    hipStream_t st;
+    std::string& err;
+    Comm* comm;
+    int world, rank;
+    std::vector<hipEvent_t> evs;
+    std::vector<int> ev_stage;
+
+    void hip(hipError_t e, const char* what) {
+        if (e != hipSuccess) {
+            err = std::string(what) + ": " + hipGetErrorString(e);
+            throw Fail{PCX_EHIP};
+        }
+    }
+    void check_err(hipError_t e, const char* what) {
+        if (!err.empty()) throw Fail{PCX_EINVAL};
+        hip(e, what);
+    }
+    void comm_rc(int rc) {
+        if (rc) throw Fail{rc};
+    }
+    // profiling marks (HIP events on the context's stream)
+    void mark(int stage) {
+        if (!c->profile) return;
+        hipEvent_t e;
+        hip(hipEventCreate(&e), "hipEventCreate");
+        hip(hipEventRecord(e, st), "hipEventRecord");
+        evs.push_back(e);
+        ev_stage.push_back(stage);
+    }
+    void stage(pcx_mat& m, int s) {
+        mark(s);
+        check_err(mat_stage(m, s, st, err), stage_name(s));
+        mark(-1);
+    }
+    void sync() { hip(hipStreamSynchronize(st), "hipStreamSynchronize"); }
+    template <class T>
+    T read(const T* dev) {
+        T v;
+        hip(hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, st), "D2H");
+        sync();
+        return v;
+    }
+
+    // ---- exchanges
+    void allreduce(void* buf, int64_t count, int dtype, int op) {
+        if (world == 1 || count <= 0) return;
+        mark(M_EXCHANGE);
+        comm_rc(comm->allreduce(buf, count, dtype, op, st, err));
+        mark(-1);
+    }
+    // dd slots [s0, s1) of every column of a [world][rows][pitch/2] dd buffer
+    void gather_slots(double* buf, int64_t rows, int64_t pitch, int s0, int s1, pcx_workspace* w) {
+        if (world == 1) return;
+        mark(M_EXCHANGE);
+        const int64_t width = (int64_t)(s1 - s0) * 2, blk = rows * pitch;
+        if (width * rows > w->xcap) {
+            err = "exchange buffer too small";
+            throw Fail{PCX_EINVAL};
+        }
+        hip(copy2d(w->xsend, width, buf + (int64_t)rank * blk + 2 * s0, pitch, width, rows, st), "pack");
+        comm_rc(comm->allgather(w->xsend, w->xrecv, width * rows * 8, st, err));
+        for (int r = 0; r < world; r++)
+            if (r != rank)
+                hip(copy2d(buf + (int64_t)r * blk + 2 * s0, pitch, w->xrecv + (int64_t)r * width * rows, width, width,
+                           rows, st),
+                    "unpack");
+        mark(-1);
+    }
+    // whole per-rank blocks of a [world][bytes] buffer (in place)
+    void gather_block(void* buf, int64_t bytes) {
+        if (world == 1) return;
+        mark(M_EXCHANGE);
+        comm_rc(comm->allgather(static_cast<char*>(buf) + (int64_t)rank * bytes, buf, bytes, st, err));
+        mark(-1);
+    }
+};
+
+// ------------------------------------------------------------------ workspace
+pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total, int n_scaled, int world,
+                         std::string& err, int& rc) {
+    pcx_workspace* w = c->ws;
+    if (w && w->n_rows == n_rows && w->E == E && w->n_scaled == n_scaled && w->world == world &&
+        w->n_total == n_total)
+        return w;
+    delete c->ws;  // one cached workspace per context (a C5 shard's is ~50 GB)
+    c->ws = nullptr;
+    w = new (std::nothrow) pcx_workspace;
+    if (!w) {
+        rc = PCX_ENOMEM;
+        err = "workspace: out of host memory";
+        return nullptr;
+    }
+    w->n_rows = n_rows;
+    w->E = E;
+    w->n_total = n_total;
+    w->n_scaled = n_scaled;
+    w->world = world;
+    const int64_t S = std::max(1, n_scaled);
+    const int64_t ceb = (E + BT - 1) / BT;
+    // enough row chunks to give ~2048 column-pass blocks, at least 32 rows each
+    w->col_blocks = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(1, 2048 / ceb),
+                                                                             (n_rows + 31) / 32),
+                                                           4096));
+    const int64_t nb = (E + COV_TILE - 1) / COV_TILE;
+    w->cov_tiles = nb * (nb + 1) / 2;
+    w->wcd_rows = (n_rows + COV_STAGE - 1) / COV_STAGE * COV_STAGE;
+    w->wcd_ld = nb * COV_TILE;
+    const int64_t stages = w->wcd_rows / COV_STAGE;
+    const int64_t ks = (16 * 3 * 256 + w->cov_tiles - 1) / w->cov_tiles;
+    w->cov_kslices = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(32, ks), stages >= 8 ? stages / 8 : 1));
+    w->xcap = E * CS * 2;
+
+    // small buffers (zeroed per call) in one block, the big ones in their own
+    struct Item {
+        void** dst;
+        size_t bytes;
+        bool zero;
+    };
+    std::vector<Item> items = {
+        {(void**)&w->rep, (size_t)n_rows * 8, true},
+        {(void**)&w->tok, (size_t)n_rows * 8, true},
+        {(void**)&w->part, (size_t)(w->col_blocks * E * 16) * 8, true},
+        {(void**)&w->mpart, (size_t)(w->col_blocks * E * 4) * 8, true},
+        {(void**)&w->cstat, (size_t)(world * E * CS * 2) * 8, true},
+        {(void**)&w->cmax, (size_t)(world * E * 4) * 8, true},
+        {(void**)&w->scal, (size_t)(world * SS * 2) * 8, true},
+        {(void**)&w->spart, (size_t)(4096 * 8) * 8, true},
+        {(void**)&w->ev, (size_t)(16 * E) * 8, true},
+        {(void**)&w->pvec, (size_t)(4 * (E + 64)) * 8, true},
+        {(void**)&w->rowv, (size_t)(6 * n_rows) * 8, true},
+        {(void**)&w->rowstat, (size_t)(2 * n_rows) * 4, true},
+        {(void**)&w->skey, (size_t)(world * 4) * 8, true},
+        {(void**)&w->info, (size_t)16 * 8, true},
+        {(void**)&w->sel_state, (size_t)(S * SELS) * 8, true},
+        {(void**)&w->sel_isum, (size_t)(S * 4) * 8, true},
+        {(void**)&w->sel_imin, (size_t)(S * 2) * 8, true},
+        {(void**)&w->sel_imax, (size_t)(S * 2) * 8, true},
+        {(void**)&w->sel_arg, (size_t)(S * 2) * 8, true},
+        {(void**)&w->sel_act, (size_t)S * 4, true},
+        {(void**)&w->hard, (size_t)E * 4, true},
+        {(void**)&w->hard_cols, (size_t)E * 4, true},
+        {(void**)&w->hard_modes, (size_t)E * 4, true},
+        {(void**)&w->scols, (size_t)S * 4, false},
+        {(void**)&w->sidx, (size_t)E * 4, false},
+        {(void**)&w->scalars, (size_t)4 * 8, true},
+        {(void**)&w->hist_sum, (size_t)(S * SEL_NB * 4) * 8, false},
+        {(void**)&w->hist_min, (size_t)(S * SEL_NB * 2) * 8, false},
+        {(void**)&w->hist_max, (size_t)(S * SEL_NB) * 8, false},
+        {(void**)&w->xsend, (size_t)w->xcap * 8, false},
+        {(void**)&w->xrecv, (size_t)(w->xcap * world) * 8, false},
+        {(void**)&w->T, (size_t)(S * n_rows) * 8, false},
+        {(void**)&w->cslab, (size_t)(w->cov_kslices * E * E) * 8, false},
+        {(void**)&w->C, (size_t)(E * E) * 8, false},
+        {(void**)&w->Mw, (size_t)(2 * E * E + 8 * E + 64) * 8, false},
+        {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
+        {(void**)&w->tokp, (size_t)(w->wcd_rows + 64) * 8, false},
+        {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
+    };
+    auto align = [](size_t b) { return (b + 255) / 256 * 256; };
+    size_t zb = 0;
+    for (auto& it : items)
+        if (it.zero) zb += align(it.bytes);
+    void* zbase = nullptr;
+    hipError_t e = hipMalloc(&zbase, zb);
+    if (e != hipSuccess) {
+        delete w;
+        rc = PCX_ENOMEM;
+        err = "workspace: hipMalloc of " + std::to_string(zb) + " bytes failed";
+        return nullptr;
+    }
+    w->blocks.push_back(zbase);
+    w->zero_base = zbase;
+    w->zero_bytes = zb;
+    size_t off = 0;
+    w->bytes = zb;
+    for (auto& it : items) {
+        if (it.zero) {
+            *it.dst = at<void>(zbase, off);
+            off += align(it.bytes);
+        } else {
+            void* p = nullptr;
+            e = hipMalloc(&p, std::max<size_t>(it.bytes, 256));
+            if (e != hipSuccess) {
+                const size_t want = it.bytes;
+                delete w;
+                rc = PCX_ENOMEM;
+                err = "workspace: hipMalloc of " + std::to_string(want) + " bytes failed";
+                return nullptr;
+            }
+            w->blocks.push_back(p);
+            w->bytes += it.bytes;
+            *it.dst = p;
+        }
+    }
+    c->ws = w;
+    return w;
+}
+
+// ------------------------------------------------------------------ host <-> device staging
+struct Io {
+    std::vector<void*> owned;
+    ~Io() {
+        for (void* p : owned) (void)hipFree(p);
+    }
+    template <class T>
+    T* dev(Run& R, const T* host, int64_t n) {  // device copy of a host input (NULL stays NULL)
+        if (!host || n <= 0) return nullptr;
+        void* p = nullptr;
+        R.hip(hipMalloc(&p, n * sizeof(T)), "hipMalloc(input)");
+        owned.push_back(p);
+        R.hip(hipMemcpyAsync(p, host, n * sizeof(T), hipMemcpyHostToDevice, R.st), "H2D");
+        return (T*)p;
+    }
+    double* out(Run& R, double* host, int64_t n) {  // device buffer for a host output
+        if (!host || n <= 0) return nullptr;
+        void* p = nullptr;
+        R.hip(hipMalloc(&p, n * 8), "hipMalloc(output)");
+        owned.push_back(p);
+        return (double*)p;
+    }
+};
+
+int64_t pow2_at_least(int64_t n) {
+    int64_t p = 2;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// events whose decision is rounding-decided: replay the reference's own float order
+void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
+    R.mark(M_HARD_LIST);
+    R.hip(hard_list(m, w->hard_cols, w->hard_modes, R.st), "k_hard_list");
+    R.mark(-1);
+    const int64_t H = R.read(m.info + INFO_HARD);
+    if (H <= 0) return;
+    res->n_hard += (int32_t)H;
+    const int64_t N = m.n_total, cap = std::max<int64_t>(1, m.n_rows);
+    const int64_t P_max = pow2_at_least(N);
+    // batch size: keep the batch's scratch near 2 GB
+    const int64_t per = cap * 16 * (1 + R.world) + P_max * 16 + N * 16 + 64;
+    const int64_t Hb = std::max<int64_t>(1, std::min<int64_t>(H, (int64_t)(2ll << 30) / per));
+    void* scratch = nullptr;
+    const size_t bytes = (size_t)(Hb * per + 4096);
+    R.hip(hipMalloc(&scratch, bytes), "hipMalloc(hard replay scratch)");
+    struct Free {
+        void* p;
+        ~Free() { (void)hipFree(p); }
+    } fr{scratch};
+    size_t off = 0;
+    auto carve = [&](size_t b) {
+        void* p = at<void>(scratch, off);
+        off += (b + 255) / 256 * 256;
+        return p;
+    };
+    HardArgs h{};
+    h.cap = cap;
+    h.send = (double*)carve(Hb * cap * 16);
+    h.recv = R.world == 1 ? h.send : (double*)carve(R.world * Hb * cap * 16);
+    h.keys = (uint64_t*)carve(Hb * P_max * 16);
+    h.X = (double*)carve(Hb * N * 8);
+    h.W = (double*)carve(Hb * N * 8);
+    h.hs = (double*)carve(Hb * 4 * 8);
+    h.send_cnt = (int64_t*)carve(Hb * 8);
+    h.recv_cnt = R.world == 1 ? h.send_cnt : (int64_t*)carve(R.world * Hb * 8);
+    for (int64_t b0 = 0; b0 < H; b0 += Hb) {
+        h.n_hard = (int32_t)std::min<int64_t>(Hb, H - b0);
+        h.cols = w->hard_cols + b0;
+        h.modes = w->hard_modes + b0;
+        R.mark(M_HARD_GATHER);
+        R.check_err(hard_stage(m, h, M_HARD_GATHER, R.st, R.err), "hard gather");
+        R.mark(-1);
+        if (R.world > 1) {
+            // compact the send rows of the batch: [n_hard][cap] pairs, counts
+            R.mark(M_EXCHANGE);
+            R.comm_rc(R.comm->allgather(h.send, h.recv, (int64_t)h.n_hard * cap * 16, R.st, R.err));
+            R.comm_rc(R.comm->allgather(h.send_cnt, h.recv_cnt, (int64_t)h.n_hard * 8, R.st, R.err));
+            R.mark(-1);
+        }
+        // segment length: the largest gathered count, rounded up to a power of two
+        std::vector<int64_t> cnt((size_t)R.world * h.n_hard);
+        R.hip(hipMemcpyAsync(cnt.data(), h.recv_cnt, cnt.size() * 8, hipMemcpyDeviceToHost, R.st), "D2H counts");
+        R.sync();
+        int64_t nmax = 1;
+        for (int j = 0; j < h.n_hard; j++) {
+            int64_t t = 0;
+            for (int r = 0; r < R.world; r++) t += cnt[(size_t)r * h.n_hard + j];
+            nmax = std::max(nmax, t);
+        }
+        h.P = pow2_at_least(nmax);
+        R.mark(M_HARD_PREP);
+        R.check_err(hard_stage(m, h, M_HARD_PREP, R.st, R.err), "hard prep");
+        R.mark(-1);
+        R.mark(M_HARD_SORT);
+        R.check_err(hard_stage(m, h, M_HARD_SORT, R.st, R.err), "hard sort");
+        R.mark(-1);
+        R.mark(M_HARD_WALK);
+        R.check_err(hard_stage(m, h, M_HARD_WALK, R.st, R.err), "hard walk");
+        R.mark(-1);
+        R.sync();  // the scratch is reused by the next batch / freed
+    }
+}
+
+// weighted medians of the scaled events (phase 1: interpolation fills, phase 2: outcomes),
+// plus the replay of rounding-decided binary fills (phase 1)
+void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
+    m.sel_phase = phase;
+    const int S = m.n_scaled;
+    if (R.world == 1 && m.n_rows <= SEL_EXACT_MAX) {
+        // small matrices: replay the reference's float walk directly
+        if (S) R.stage(m, M_SEL_EXACT);
+    } else if (S) {
+        R.stage(m, M_SEL_INIT);
+        R.allreduce(w->sel_isum, (int64_t)S * 4, PCX_U64, PCX_SUM);
+        R.allreduce(w->sel_imin, (int64_t)S * 2, PCX_U64, PCX_MIN);
+        R.allreduce(w->sel_imax, (int64_t)S * 2, PCX_U64, PCX_MAX);
+        R.stage(m, M_SEL_START);
+        R.stage(m, M_SEL_COMPACT);
+        int64_t inf2[2];
+        R.hip(hipMemcpyAsync(inf2, m.info + INFO_SEL_ACTIVE, 16, hipMemcpyDeviceToHost, R.st), "D2H");
+        R.sync();
+        int64_t active = inf2[0];
+        if (inf2[1] > 0) {  // dominant weights: the first row holding the max weight (all ranks)
+            R.stage(m, M_SEL_ARGMAX);
+            R.allreduce(w->sel_arg, S, PCX_U64, PCX_MIN);
+            R.stage(m, M_SEL_VALUE);
+            R.allreduce(w->sel_arg + S, S, PCX_U64, PCX_MAX);
+            R.stage(m, M_SEL_VALUE_FINISH);
+        }
+        int passes = 0;
+        while (active > 0) {
+            if (passes == MAX_SEL_PASSES) {
+                R.err = "weighted selection did not converge";
+                throw Fail{PCX_EINVAL};
+            }
+            R.mark(M_SEL_HIST);
+            R.check_err(sel_hist(m, (int)active, R.st), "k_sel_hist");
+            R.mark(-1);
+            R.allreduce(w->hist_sum, active * SEL_NB * 4, PCX_U64, PCX_SUM);
+            R.allreduce(w->hist_min, active * SEL_NB * 2, PCX_U64, PCX_MIN);
+            R.allreduce(w->hist_max, active * SEL_NB, PCX_U64, PCX_MAX);
+            R.mark(M_SEL_STEP);
+            R.check_err(sel_step(m, (int)active, R.st), "k_sel_step");
+            R.mark(-1);
+            R.stage(m, M_SEL_COMPACT);
+            active = R.read(m.info + INFO_SEL_ACTIVE);
+            passes++;
+        }
+        res->sel_passes += passes;
+    }
+    hard_replay(R, m, w, res);
+    if (S) R.stage(m, M_SEL_FINISH);
+}
+
+}  // namespace
+
+void workspace_free(pcx_ctx* c) {
+    delete c->ws;
+    c->ws = nullptr;
+}
+
+int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const double* scores_in, int rank_rule,
+               double* nc_out, std::string& err) {
+    if (!p || !r) {
+        err = "null problem / result";
+        return PCX_EINVAL;
+    }
+    const int world = c->comm ? c->comm->world : 1, rank = c->comm ? c->comm->rank : 0;
+    const int64_t n_rows = p->n_rows, E = p->n_events, N = p->n_total;
+    if (n_rows < 1 || E < 1 || N < n_rows || !p->reports) {
+        err = "bad shape or missing reports";
+        return PCX_EINVAL;
+    }
+    if (E > 65536 || n_rows > 0x7fffffffll) {
+        err = "n_events > 65536 or n_rows >= 2^31 per rank";
+        return PCX_EINVAL;
+    }
+    if (p->row_offset < 0 || p->row_offset + n_rows > N || (world == 1 && (N != n_rows || p->row_offset != 0))) {
+        err = "row_offset / n_total inconsistent with n_rows and the context's world";
+        return PCX_EINVAL;
+    }
+    if (p->scaled && (!p->lo || !p->hi)) {
+        err = "scaled given without lo / hi";
+        return PCX_EINVAL;
+    }
+    const int alg = p->algorithm;
+    if (alg < PCX_ALG_PCA || alg > PCX_ALG_COKURTOSIS) {
+        err = "algorithm must be PCA, absolute, big-five, fixed-variance or cokurtosis on the single-matrix path";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_COKURTOSIS && !p->aux_scores && entry != 4) {
+        err = "cokurtosis needs aux_scores";
+        return PCX_EINVAL;
+    }
+    if (!std::isfinite(p->catch_tolerance) || !std::isfinite(p->alpha)) {
+        err = "catch_tolerance / alpha must be finite";
+        return PCX_EINVAL;
+    }
+    if (p->mem_kind != PCX_MEM_DEVICE && p->mem_kind != PCX_MEM_HOST) {
+        err = "mem_kind must be PCX_MEM_DEVICE or PCX_MEM_HOST";
+        return PCX_EINVAL;
+    }
+    hipError_t he = hipSetDevice(c->device);
+    if (he != hipSuccess) {
+        err = std::string("hipSetDevice: ") + hipGetErrorString(he);
+        return PCX_EHIP;
+    }
+    Run R{c, c->stream, err, c->comm, world, rank, {}, {}};
+    const bool host = p->mem_kind == PCX_MEM_HOST;
+    const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
+    try {
+        Io io;
+        // ---- scaled events (host view)
+        std::vector<uint8_t> sc_h;
+        const uint8_t* sc_in = filled_input ? nullptr : p->scaled;
+        if (sc_in) {
+            sc_h.resize(E);
+            if (host)
+                memcpy(sc_h.data(), sc_in, E);
+            else {
+                R.hip(hipMemcpyAsync(sc_h.data(), sc_in, E, hipMemcpyDeviceToHost, R.st), "D2H scaled");
+                R.sync();
+            }
+        }
+        std::vector<int32_t> scols, sidx(E, -1);
+        for (int64_t j = 0; j < (int64_t)sc_h.size(); j++)
+            if (sc_h[j]) {
+                sidx[j] = (int32_t)scols.size();
+                scols.push_back((int32_t)j);
+            }
+        const int n_scaled = (int)scols.size();
+        int rc = 0;
+        pcx_workspace* w = workspace(c, n_rows, E, N, n_scaled, world, err, rc);
+        if (!w) return rc;
+        R.hip(hipMemsetAsync(w->zero_base, 0, w->zero_bytes, R.st), "hipMemset(workspace)");
+        if (n_scaled) R.hip(hipMemcpyAsync(w->scols, scols.data(), n_scaled * 4, hipMemcpyHostToDevice, R.st), "H2D");
+        R.hip(hipMemcpyAsync(w->sidx, sidx.data(), E * 4, hipMemcpyHostToDevice, R.st), "H2D");
+
+        // ---- inputs / outputs on the device
+        pcx_mat m{};
+        R.mark(M_H2D);
+        const double* reports = host ? io.dev(R, p->reports, n_rows * E) : p->reports;
+        const double* rep_raw = host ? io.dev(R, p->reputation, N) : p->reputation;
+        const uint8_t* scaled = host ? io.dev(R, sc_in, E) : sc_in;
+        const double* lo = sc_in ? (host ? io.dev(R, p->lo, E) : p->lo) : nullptr;
+        const double* hi = sc_in ? (host ? io.dev(R, p->hi, E) : p->hi) : nullptr;
+        const double* aux_src = entry == 4 ? scores_in : p->aux_scores;
+        const double* aux = aux_src ? (host ? io.dev(R, aux_src, n_rows) : aux_src) : nullptr;
+        R.mark(-1);
+        struct OutMap {
+            double* user;
+            double* dev;
+            int64_t n;
+        };
+        std::vector<OutMap> outs;
+        auto out = [&](double* user, int64_t n) -> double* {
+            if (!user) return nullptr;
+            if (!host) return user;
+            double* d = io.out(R, user, n);
+            outs.push_back({user, d, n});
+            return d;
+        };
+        const bool cons = entry == 0, lie = entry == 3;
+        m.old_rep = (cons || lie) ? out(r->old_rep, n_rows) : nullptr;
+        m.this_rep = (cons || lie) ? out(r->this_rep, n_rows) : nullptr;
+        m.smooth_rep = (cons || lie) ? out(r->smooth_rep, n_rows) : nullptr;
+        m.scores = (cons || lie) ? out(r->scores, n_rows) : nullptr;
+        m.na_row = cons ? out(r->na_row, n_rows) : nullptr;
+        m.participation_rows = cons ? out(r->participation_rows, n_rows) : nullptr;
+        m.relative_part = cons ? out(r->relative_part, n_rows) : nullptr;
+        m.reporter_bonus = cons ? out(r->reporter_bonus, n_rows) : nullptr;
+        m.adj_first_loadings = cons ? out(r->adj_first_loadings, E) : nullptr;
+        m.outcomes_raw = cons ? out(r->outcomes_raw, E) : nullptr;
+        m.outcomes_adjusted = cons ? out(r->outcomes_adjusted, E) : nullptr;
+        m.outcomes_final = cons ? out(r->outcomes_final, E) : nullptr;
+        m.certainty = cons ? out(r->certainty, E) : nullptr;
+        m.consensus_reward = cons ? out(r->consensus_reward, E) : nullptr;
+        m.nas_filled = cons ? out(r->nas_filled, E) : nullptr;
+        m.participation_columns = cons ? out(r->participation_columns, E) : nullptr;
+        m.author_bonus = cons ? out(r->author_bonus, E) : nullptr;
+        m.original = (cons || entry == 1) ? out(r->original, n_rows * E) : nullptr;
+        m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
+        m.weighted_mean = entry == 2 ? out(r->weighted_mean, E) : nullptr;
+        m.nc_out = entry == 4 ? out(nc_out, n_rows) : nullptr;
+        double* cov_out = entry == 2 ? out(r->covariance, E * E) : nullptr;
+        double* ld_out = (entry == 2 || lie) ? out(r->adj_first_loadings, E) : nullptr;
+        double* sc_out = entry == 2 ? out(r->scores, n_rows) : nullptr;
+
+        // ---- the kernel view
+        m.n_rows = n_rows;
+        m.n_events = E;
+        m.n_total = N;
+        m.row_offset = p->row_offset;
+        m.world = world;
+        m.rank = rank;
+        m.int_dtype = filled_input ? 0 : (p->int_dtype ? 1 : 0);
+        m.algorithm = alg;
+        m.catch_tolerance = p->catch_tolerance;
+        m.alpha = p->alpha;
+        m.n_scaled = n_scaled;
+        m.sel_phase = 1;
+        m.col_blocks = (int32_t)w->col_blocks;
+        m.cov_tiles = (int32_t)w->cov_tiles;
+        m.cov_kslices = (int32_t)w->cov_kslices;
+        m.no_fill = filled_input ? 1 : 0;
+        m.rank_rule = entry == 4 ? (rank_rule ? 1 : 0) : (alg == PCX_ALG_PCA ? 1 : 0);
+        m.scores_given = (entry == 4 || alg == PCX_ALG_COKURTOSIS) ? 1 : 0;
+        m.reports = reports;
+        m.scaled = scaled;
+        m.lo = lo;
+        m.hi = hi;
+        m.rep_raw = rep_raw;
+        m.scaled_cols = w->scols;
+        m.scaled_index = w->sidx;
+        m.rep = w->rep;
+        m.tok = w->tok;
+        m.T = w->T;
+        m.part = w->part;
+        m.mpart = w->mpart;
+        m.cstat = w->cstat;
+        m.cmax = w->cmax;
+        m.scal = w->scal;
+        m.spart = w->spart;
+        m.ev = w->ev;
+        m.cslab = w->cslab;
+        m.C = w->C;
+        m.Mw = w->Mw;
+        m.pvec = w->pvec;
+        m.rowv = w->rowv;
+        m.rowstat = w->rowstat;
+        m.skey = w->skey;
+        m.info = w->info;
+        m.sel_state = w->sel_state;
+        m.sel_isum = w->sel_isum;
+        m.sel_imin = w->sel_imin;
+        m.sel_imax = w->sel_imax;
+        m.hist_sum = w->hist_sum;
+        m.hist_min = w->hist_min;
+        m.hist_max = w->hist_max;
+        m.sel_arg = w->sel_arg;
+        m.sel_act = w->sel_act;
+        m.hard = w->hard;
+        m.scalars = w->scalars;
+        m.wcd = w->wcd;
+        m.tokp = w->tokp;
+        m.wcd_rows = w->wcd_rows;
+        m.wcd_ld = w->wcd_ld;
+        m.rowpart = w->rowpart;
+        m.max_components = p->max_components < 1 ? 1 : (p->max_components > E ? (int32_t)E : p->max_components);
+        m.components = -1;
+        m.variance_threshold = p->variance_threshold;
+        m.aux_scores = aux;
+        r->n_hard = 0;
+        r->sel_passes = 0;
+
+        const double* cstat = w->cstat;
+        (void)cstat;
+        const int64_t cpitch = CS * 2;
+        // a1: reputation, tokens (:138-146)
+        R.stage(m, M_REPUTATION);
+        R.gather_slots(w->scal, 1, SS * 2, 0, 2, w);
+        // a2/a3: rescale + NA + present sums (:266-299)
+        R.stage(m, M_COLSTATS);
+        R.gather_slots(w->cstat, E, cpitch, 0, 4, w);
+        R.gather_block(w->cmax, E * 4 * 8);
+        R.stage(m, M_GUESS);  // binary fills (:304-309)
+        if (!filled_input) select(R, m, w, 1, r);  // scaled fills: weighted median (:300-303)
+        if (entry == 1) {      // interpolate: rescaled + filled matrices (:266-313)
+            R.stage(m, M_MATRICES);
+        } else {
+            R.stage(m, M_MEAN);
+            const bool wpca = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;
+            const bool run_wpca = entry == 2 || (entry != 4 && wpca);
+            int64_t flags = 0;
+            if (run_wpca) {
+                // a5: wcd materialised (:322); a6: covariance on fp64 MFMA (:326); a7: power iteration (:330-336)
+                R.stage(m, M_WCD);
+                R.stage(m, M_COV);
+                R.stage(m, M_COV_REDUCE);
+                R.allreduce(w->C, E * E, PCX_F64, PCX_SUM);
+                R.stage(m, M_COV_FINISH);
+                R.stage(m, M_POWER);
+                flags = R.read(m.info + INFO_FLAGS);
+                // big-five / fixed-variance components (:373-390, :429-451); a non-finite
+                // covariance makes the reference's second svd raise (Oracle: LinAlgError)
+                if (entry != 2 && alg != PCX_ALG_PCA && !(flags & PCX_FLAG_SVD_FAIL)) R.stage(m, M_EIG);
+            } else {
+                R.stage(m, M_ZERO_LOADING);
+            }
+            if (entry == 2 && alg != PCX_ALG_PCA) m.algorithm = PCX_ALG_PCA;  // wpca: the first loading's scores
+            R.stage(m, M_SCORES);
+            R.gather_block(w->skey, 4 * 8);
+            if (entry == 2) {
+                R.stage(m, M_WMEAN_OUT);
+                if (cov_out) R.hip(hipMemcpyAsync(cov_out, w->C, E * E * 8, hipMemcpyDeviceToDevice, R.st), "cov");
+                if (ld_out) R.hip(hipMemcpyAsync(ld_out, w->ev + 3 * E, E * 8, hipMemcpyDeviceToDevice, R.st), "ld");
+                if (sc_out) R.hip(hipMemcpyAsync(sc_out, w->rowv, n_rows * 8, hipMemcpyDeviceToDevice, R.st), "scores");
+            } else {
+                if (alg != PCX_ALG_ABSOLUTE || entry == 4) {
+                    // a8/a9: sign-choice rule (:487-500; the other algorithms: nonconformity, :475-485)
+                    R.stage(m, M_NCSUMS);
+                    R.gather_slots(w->scal, 1, SS * 2, 2, 6, w);
+                    R.stage(m, M_GEMV2);
+                    R.gather_slots(w->cstat, E, cpitch, 4, 6, w);
+                    R.stage(m, M_DECIDE);
+                }
+                if (entry == 4) {
+                    R.stage(m, M_NC_OUT);
+                } else {
+                    // a10: reputation update (:460-472)
+                    R.stage(m, M_REPU);
+                    R.gather_slots(w->scal, 1, SS * 2, 6, 8, w);
+                    R.stage(m, M_SMOOTH);
+                    if (lie) {
+                        R.stage(m, M_AGENTS);
+                        if (ld_out)
+                            R.hip(hipMemcpyAsync(ld_out, w->ev + 3 * E, E * 8, hipMemcpyDeviceToDevice, R.st), "ld");
+                    } else {
+                        // a12-a14: outcomes, participation, certainty (:510-546)
+                        R.stage(m, M_OUTCOMES);
+                        R.gather_slots(w->cstat, E, cpitch, 6, 14, w);
+                        R.hip(hipMemsetAsync(w->hard, 0, E * 4, R.st), "hipMemset(hard)");
+                        R.stage(m, M_EVENTS);
+                        select(R, m, w, 2, r);  // scaled outcomes: weighted median (:519-523)
+                        R.stage(m, M_SCALED_CERT);
+                        R.gather_slots(w->cstat, E, cpitch, 14, 16, w);
+                        R.stage(m, M_FINAL);
+                        R.stage(m, M_ROWSUMS);
+                        R.gather_slots(w->scal, 1, SS * 2, 8, 10, w);
+                        R.stage(m, M_AGENTS);
+                        R.stage(m, M_MATRICES);
+                    }
+                }
+            }
+        }
+        // ---- scalars and host outputs
+        int64_t info[4];
+        double sc2[2];
+        R.hip(hipMemcpyAsync(info, w->info, sizeof(info), hipMemcpyDeviceToHost, R.st), "D2H info");
+        R.hip(hipMemcpyAsync(sc2, w->scalars, sizeof(sc2), hipMemcpyDeviceToHost, R.st), "D2H scalars");
+        R.mark(M_D2H);
+        for (auto& o : outs)
+            R.hip(hipMemcpyAsync(o.user, o.dev, o.n * 8, hipMemcpyDeviceToHost, R.st), "D2H output");
+        R.mark(-1);
+        R.sync();
+        r->participation = sc2[0];
+        r->avg_certainty = sc2[1];
+        const bool branchless = (alg == PCX_ALG_ABSOLUTE && entry != 4) || entry == 1 || entry == 2;
+        r->branch = branchless ? PCX_BRANCH_NONE : (int32_t)info[INFO_BRANCH];
+        r->pi_iters = (int32_t)info[INFO_PI_ITERS];
+        r->flags = (int32_t)info[INFO_FLAGS];
+        r->components = m.components;
+        // per-stage device time
+        if (c->profile && !R.evs.empty()) {
+            for (int k = 0; k < PCX_NSTAGES; k++) c->stage_ms[k] = 0.0;
+            for (size_t i = 0; i + 1 < R.evs.size(); i++) {
+                if (R.ev_stage[i] < 0) continue;
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, R.evs[i], R.evs[i + 1]) == hipSuccess)
+                    c->stage_ms[R.ev_stage[i]] += ms;
+            }
+        }
+        for (hipEvent_t e : R.evs) (void)hipEventDestroy(e);
+        return PCX_OK;
+    } catch (const Fail& f) {
+        (void)hipStreamSynchronize(R.st);
+        for (hipEvent_t e : R.evs) (void)hipEventDestroy(e);
+        if (err.empty()) err = "single-matrix run failed";
+        return f.code;
+    } catch (const std::bad_alloc&) {
+        err = "out of host memory";
+        return PCX_ENOMEM;
+    }
+}
+
+}  // namespace pcx

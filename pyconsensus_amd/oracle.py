@@ -94,6 +94,93 @@ class Oracle(object):
             return self.YES
         return self.BAD
 
+    def _device_index(self):
+        if self.device is None:
+            return 0
+        import torch
+
+        d = torch.device(self.device)
+        return d.index or 0
+
+    def _kw(self):
+        return dict(catch_tolerance=self.catch_tolerance, alpha=self.alpha, algorithm=self._stage_algorithm(),
+                    max_components=self.max_components, variance_threshold=self.variance_threshold)
+
+    def _stage_algorithm(self):
+        return self.algorithm if self.algorithm in ("PCA", "absolute", "big-five", "fixed-variance",
+                                                    "cokurtosis") else "PCA"
+
+    # -- stage methods (:260-500), each one call of the single-matrix ABI ------
+    def interpolate(self, reports):
+        """Oracle.interpolate (:260-313): rescales the scaled events of ``reports`` IN PLACE
+        (as the reference does, Q2) and returns the filled matrix (same dtype; an integer
+        dtype truncates the fills, Q3).  Fills: weighted median (scaled) / catch of the
+        weighted mean (binary), computed on the GPU (pcx_interpolate_f64)."""
+        from .pipeline import interpolate_host
+
+        data = np.ma.getdata(reports) if isinstance(reports, np.ma.MaskedArray) else np.asarray(reports)
+        ints = np.issubdtype(data.dtype, np.integer)
+        sc, lo, hi = self._bounds_arrays()
+        outs, _ = interpolate_host(np.asarray(data, dtype=np.float64), self._rep_raw, sc, lo, hi,
+                                   device_index=self._device_index(), int_dtype=ints, **self._kw())
+        if sc is not None and sc.any():
+            cols = np.nonzero(sc)[0]
+            reports[:, cols] = outs["original"][:, cols].astype(data.dtype) if ints else outs["original"][:, cols]
+        return outs["filled"].astype(data.dtype) if ints else outs["filled"]
+
+    def wpca(self, reports_filled):
+        """Oracle.wpca (:315-339) on the GPU (pcx_wpca_f64): returns (weighted_mean, wcd,
+        covariance_matrix, first_loading, first_score).  The covariance is the token-weighted
+        fp64-MFMA SYRK, the loading the power-iteration leading eigenvector (its sign follows
+        the SPEC rule, which may differ from LAPACK's, Q8)."""
+        from .pipeline import wpca_host
+
+        F = np.asarray(np.ma.getdata(reports_filled), dtype=np.float64)
+        outs, _ = wpca_host(F, self._rep_raw, device_index=self._device_index(), **self._kw())
+        weighted_mean = np.ma.masked_array(outs["weighted_mean"])
+        wcd = np.asmatrix(F - outs["weighted_mean"])
+        first_loading = np.ma.masked_array(outs["adj_first_loadings"])
+        first_score = np.asmatrix(outs["scores"])
+        return weighted_mean, wcd, np.ma.masked_array(outs["covariance"]), first_loading, first_score
+
+    def lie_detector(self, reports_filled):
+        """Oracle.lie_detector (:341-473) on the GPU (pcx_lie_detector_f64): the algorithm's
+        scores and sign choice, then this_rep / smooth_rep."""
+        from .pipeline import lie_detector_host
+
+        F = np.asarray(np.ma.getdata(reports_filled), dtype=np.float64)
+        aux = None
+        if self.algorithm == "cokurtosis":
+            aux = np.asarray(self.aux["cokurt"], dtype=np.float64).ravel()
+        outs, meta = lie_detector_host(F, self._rep_raw, device_index=self._device_index(), aux_scores=aux,
+                                       **self._kw())
+        self.convergence = self.algorithm != "absolute"
+        self.last_info = {"branch": meta["branch"], "path": "matrix"}
+        ma = np.ma.masked_array if self.algorithm == "PCA" else np.asarray
+        return {"first_loading": np.ma.masked_array(outs["adj_first_loadings"]),
+                "scores": ma(outs["scores"]) if aux is None else self.aux["cokurt"],
+                "old_rep": self.reputation.T, "this_rep": ma(outs["this_rep"]),
+                "smooth_rep": ma(outs["smooth_rep"])}
+
+    def nonconformity(self, scores, reports):
+        """Oracle.nonconformity (:475-485): the continuous sign choice, on the GPU."""
+        return self._nonconformity(scores, reports, False)
+
+    def nonconformity_rank(self, scores, reports):
+        """Oracle.nonconformity_rank (:487-500): the rank rule with its continuous fallback."""
+        return self._nonconformity(scores, reports, True)
+
+    def _nonconformity(self, scores, reports, rank_rule):
+        from .pipeline import nonconformity_host
+
+        F = np.asarray(np.ma.getdata(reports), dtype=np.float64)
+        s = np.asarray(np.ma.getdata(scores), dtype=np.float64).ravel()
+        nc, meta = nonconformity_host(s, F, self._rep_raw, rank_rule=rank_rule,
+                                      device_index=self._device_index(), **self._kw())
+        self.convergence = True
+        self.last_info = {"branch": meta["branch"], "path": "matrix"}
+        return nc
+
     # -- consensus (:502-611) ---------------------------------------------------
     def _bounds_arrays(self):
         if self.event_bounds is None:
@@ -133,16 +220,15 @@ class Oracle(object):
             self.last_info = {"branch": int(g["branch"]), "flags": int(g["flags"]),
                               "pi_iters": int(g["pi_iters"]), "path": "batched"}
         else:
-            from .pipeline import consensus_matrix
+            from .pipeline import consensus_host
 
-            ev, ag, meta = consensus_matrix(self._data, self._rep_raw, sc, lo, hi, matrices=True, n_total=N,
-                                            row_offset=0, aux_scores=aux, **kw)
-            g = {k: v.cpu().numpy() for k, v in list(ev.items()) + list(ag.items())}
+            g, meta = consensus_host(self._data, self._rep_raw, sc, lo, hi, device_index=self._device_index(),
+                                     aux_scores=aux, **{k: v for k, v in kw.items() if k != "device"})
             participation = float(meta["participation"])
             avg_certainty = float(meta["avg_certainty"])
             comps = int(meta["components"])
             self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
-                              "path": "matrix"}
+                              "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"], "path": "matrix"}
         if self.algorithm in ("big-five", "fixed-variance") and self.last_info["flags"] & _abi.FLAG_SVD_FAIL:
             # the reference's second svd (:375, :431) is outside the try of :329-333
             raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")
@@ -151,7 +237,42 @@ class Oracle(object):
         self.convergence = self.algorithm != "absolute"  # nonconformity(_rank) / the clusterings set it
         if self.algorithm == "clusterfeck":  # cluster() rewrites zero tokens in the caller's list (:202-204)
             self.reptokens = [0.00001 if t == 0 else t for t in self.reptokens]
-        return self._result(g, participation, avg_certainty)
+        res = self._result(g, participation, avg_certainty)
+        if self.verbose:
+            self._print_verbose(res)
+        return res
+
+    def _print_verbose(self, res):
+        """The reference's verbose=True trace (:349-357, :363-365, :463-466, :552-572),
+        printed from the GPU results."""
+        print("Reports:")
+        print(self.reports)
+        print("Total rep:")
+        print(self.total_rep)
+        print("Num reporters:")
+        print(self.num_reports)
+        print("Rep tokens:")
+        print(self.reptokens)
+        print("pyconsensus [%s]:\n" % self.algorithm)
+        s = np.asarray(np.ma.getdata(res["agents"]["scores"]), dtype=np.float64)
+        b = self.last_info.get("branch", _abi.BRANCH_NONE)
+        if b in (_abi.BRANCH_SET1, _abi.BRANCH_TIE_SET1):
+            nc = s + np.abs(np.min(s))
+        elif b in (_abi.BRANCH_SET2, _abi.BRANCH_TIE_SET2):
+            nc = s - np.max(s)
+        else:
+            nc = np.zeros(self.num_reports)
+        print("  Adjusted:  ", nc)
+        print("  Reputation:", res["agents"]["this_rep"])
+        print()
+        na = np.ma.masked_array(np.asarray(res["agents"]["na_row"]))
+        print("NA Mat:")
+        print(np.isnan(np.ma.getdata(self.reports).astype(np.float64)) | (np.ma.getdata(self.reports) == NA))
+        print()
+        print("Sum:")
+        print(na)
+        print()
+        print(1 - res["participation"])
 
     def _result(self, g, participation, avg_certainty):
         original = g["original"]

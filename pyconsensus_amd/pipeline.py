@@ -1,12 +1,17 @@
-"""Single-matrix consensus pipeline: stage sequencing, workspace and cross-rank exchange.
+"""Single-matrix consensus: tensor handoff to ``pcx_consensus_f64`` and the rank contexts.
 
-One N x E report matrix, sharded by reporter rows over ``comm.world`` GPUs (one
-process per GPU; ``world == 1`` on a single GPU).  Each stage is one call of
-``pcx_mat_stage`` (include/pcx.h, kernels in csrc/pcx_matrix.hip).  Stages that
-produce per-rank partial sums write slot ``[rank]`` of a ``[world, ...]`` buffer;
-:class:`Comm` sums those buffers over ranks (RCCL all-reduce via torch.distributed)
-and the next stage combines the ranks in rank order, so every rank ends with the
-same event-level results whatever the collective's internal order.
+One N x E report matrix, sharded by contiguous reporter rows over ``comm.world``
+ranks (one process per GPU, or threads of one process).  The whole consensus --
+stage order, scratch, and the exchange between stages -- runs inside libpcx
+(``csrc/pcx_runner.cpp``); this module only builds the ``pcx_problem`` /
+``pcx_result`` structs from torch tensors or numpy arrays and picks the context:
+
+* :class:`Comm`        one rank;
+* :class:`RcclComm`    one process per GPU, RCCL over xGMI inside libpcx (the unique
+                       id is broadcast with torch.distributed, any backend);
+* :class:`ThreadComm`  virtual ranks as threads of one process (``ThreadGroup``),
+                       exchanging through host memory -- the 1-GPU rehearsal;
+* :class:`CallbackComm` torch.distributed (e.g. gloo) behind libpcx's callback ops.
 
 Reference (pyconsensus/__init__.py): interpolate :260-313, wpca :315-339,
 nonconformity_rank :487-500, lie_detector tail :459-473, consensus :502-611.
@@ -16,85 +21,156 @@ from __future__ import annotations
 import ctypes as C
 import threading
 
-from . import _abi, _device, _lib
+import numpy as np
 
-COL_THREADS = 256
-COV_TILE = 128
-COV_STAGE = 16
+from . import _abi, _device, _lib
 
 
 class Comm:
-    """Cross-rank exchange used between stages.  world == 1: every call is a no-op."""
+    """One rank: the per-(thread, device) context of _lib."""
 
-    def __init__(self, world=1, rank=0, group=None):
-        self.world = int(world)
-        self.rank = int(rank)
-        self.group = group
+    world, rank = 1, 0
 
-    def all_reduce_sum(self, t):
-        if self.world == 1:
-            return
-        import torch.distributed as dist
-
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-
-    # [world, ...] slot buffers: other ranks' slots are zeroed before the stage writes
-    # its own, so the SUM leaves every slot with exactly one contribution.
-    def clear_slots(self, buf, sl=()):
-        if self.world == 1:
-            return
-        buf[(slice(None),) + tuple(sl)] = 0
-
-    def reduce_slots(self, buf, sl=()):
-        if self.world == 1:
-            return
-        idx = (slice(None),) + tuple(sl)
-        t = buf[idx].contiguous()
-        self.all_reduce_sum(t)
-        buf[idx] = t
+    def context(self, device_index):
+        return _lib.context(device_index)
 
     @staticmethod
-    def from_env():
+    def from_env(device_index=None):
+        """The communicator of an initialised torch.distributed job: RCCL for the
+        ``nccl`` backend (RCCL on ROCm), callbacks for any other (gloo)."""
         import torch.distributed as dist
 
-        if dist.is_available() and dist.is_initialized():
-            return Comm(dist.get_world_size(), dist.get_rank())
-        return Comm()
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return Comm()
+        if device_index is None:
+            device_index = _device.torch().cuda.current_device()
+        if dist.get_backend() == "nccl":
+            return RcclComm(dist.get_world_size(), dist.get_rank(), device_index)
+        return CallbackComm(dist.get_world_size(), dist.get_rank())
+
+
+class _OwnedCtx(Comm):
+    _ctx = None
+
+    def context(self, device_index):
+        return self._ctx
+
+    def close(self):
+        if self._ctx:
+            _lib.lib().pcx_destroy(self._ctx)
+            self._ctx = None
+
+
+class RcclComm(_OwnedCtx):
+    """libpcx's own RCCL communicator (ncclCommInitRank); collective construction."""
+
+    def __init__(self, world, rank, device_index):
+        import torch.distributed as dist
+
+        self.world, self.rank = int(world), int(rank)
+        cid = _abi.CommId()
+        if self.rank == 0:
+            _lib.check(_lib.lib().pcx_comm_unique_id(C.byref(cid)))
+        box = [bytes(cid.internal) if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        C.memmove(C.addressof(cid), box[0], 128)
+        self.device_index = int(device_index)
+        self._ctx = _lib.new_context(_lib.lib().pcx_create_rank(self.device_index, self.world, self.rank,
+                                                                C.byref(cid)), "pcx_create_rank")
 
 
 class ThreadGroup:
-    """Shared state of :class:`ThreadComm` ranks (one thread per virtual shard)."""
+    """Shared exchange of :class:`ThreadComm` ranks (pcx_group)."""
 
     def __init__(self, world):
         self.world = int(world)
+        self.handle = _lib.new_context(_lib.lib().pcx_group_create(self.world), "pcx_group_create")
         self.barrier = threading.Barrier(self.world)
-        self.bufs = [None] * self.world
-        self.result = None
+
+    def __del__(self):
+        try:
+            _lib.lib().pcx_group_destroy(self.handle)
+        except Exception:  # pragma: no cover
+            pass
 
 
-class ThreadComm(Comm):
-    """Virtual shards in ONE process (one thread per rank, same or different GPUs):
-    exercises the sharded stages and the slot reductions without a multi-GPU node."""
+class ThreadComm(_OwnedCtx):
+    """Virtual rank ``rank`` of a :class:`ThreadGroup` (one thread per rank, any device)."""
 
     def __init__(self, group, rank):
-        super().__init__(group.world, rank)
         self.g = group
+        self.world, self.rank = group.world, int(rank)
+        self._dev = None
 
-    def all_reduce_sum(self, t):
-        torch = _device.torch()
-        torch.cuda.synchronize()
-        self.g.bufs[self.rank] = t
-        self.g.barrier.wait()
-        if self.rank == 0:
-            acc = self.g.bufs[0].clone()
-            for r in range(1, self.world):
-                acc += self.g.bufs[r].to(acc.device)
-            torch.cuda.synchronize()
-            self.g.result = acc
-        self.g.barrier.wait()
-        t.copy_(self.g.result.to(t.device))
-        torch.cuda.synchronize()
-        self.g.barrier.wait()
+    def context(self, device_index):
+        if self._ctx is None or self._dev != device_index:
+            self.close()
+            self._ctx = _lib.new_context(_lib.lib().pcx_create_grouped(int(device_index), self.g.handle, self.rank),
+                                         "pcx_create_grouped")
+            self._dev = device_index
+        return self._ctx
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+
+class CallbackComm(_OwnedCtx):
+    """torch.distributed (any backend, CPU tensors) behind libpcx's callback exchange."""
+
+    def __init__(self, world, rank, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.world, self.rank, self.group = int(world), int(rank), group
+        self._dev = None
+
+        def allreduce(user, buf, count, dtype, op):
+            try:
+                a = np.ctypeslib.as_array(C.cast(buf, C.POINTER(C.c_double if dtype == _abi.F64 else C.c_uint64)),
+                                          shape=(count,))
+                if dtype == _abi.F64:
+                    t = torch.from_numpy(a)
+                    o = {_abi.RED_SUM: dist.ReduceOp.SUM, _abi.RED_MIN: dist.ReduceOp.MIN,
+                         _abi.RED_MAX: dist.ReduceOp.MAX}[op]
+                    dist.all_reduce(t, op=o, group=self.group)
+                else:  # u64: gather all ranks and reduce exactly on the host (torch has no uint64 reduce)
+                    t = torch.from_numpy(a.view(np.int64).copy())
+                    parts = [torch.empty_like(t) for _ in range(self.world)]
+                    dist.all_gather(parts, t, group=self.group)
+                    st = np.stack([p.numpy().view(np.uint64) for p in parts])
+                    r = st.sum(axis=0, dtype=np.uint64) if op == _abi.RED_SUM else (
+                        st.min(axis=0) if op == _abi.RED_MIN else st.max(axis=0))
+                    a[:] = r
+                return 0
+            except Exception:  # pragma: no cover
+                return 1
+
+        def allgather(user, send, recv, nbytes):
+            try:
+                s = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,))
+                r = np.ctypeslib.as_array(C.cast(recv, C.POINTER(C.c_uint8)), shape=(nbytes * self.world,))
+                t = torch.from_numpy(s.copy())
+                parts = [torch.empty_like(t) for _ in range(self.world)]
+                dist.all_gather(parts, t, group=self.group)
+                for w, p in enumerate(parts):
+                    r[w * nbytes:(w + 1) * nbytes] = p.numpy()
+                return 0
+            except Exception:  # pragma: no cover
+                return 1
+
+        self._cbs = (_abi.ALLREDUCE_CB(allreduce), _abi.ALLGATHER_CB(allgather))  # keep alive
+        self._ops = _abi.CommOps(None, self._cbs[0], self._cbs[1])
+
+    def context(self, device_index):
+        if self._ctx is None or self._dev != device_index:
+            self.close()
+            self._ctx = _lib.new_context(_lib.lib().pcx_create_custom(int(device_index), self.world, self.rank,
+                                                                      C.byref(self._ops)), "pcx_create_custom")
+            self._dev = device_index
+        return self._ctx
 
 
 def shard_rows(N, world, rank):
@@ -105,117 +181,56 @@ def shard_rows(N, world, rank):
     return offset, count
 
 
-class MatWorkspace:
-    """Device buffers of one rank for an (n_rows x E) shard of an N x E matrix."""
-
-    def __init__(self, n_rows, E, n_scaled, world, device):
-        t = _device.torch()
-        f64, u64 = t.float64, t.int64
-        self.device = device
-        self.n_rows, self.E, self.n_scaled, self.world = n_rows, E, n_scaled, world
-        ceb = (E + COL_THREADS - 1) // COL_THREADS
-        # enough row chunks to give ~2048 column-pass blocks, at least 32 rows each
-        self.col_blocks = max(1, min(max(1, 2048 // ceb), (n_rows + 31) // 32, 4096))
-        nb = (E + COV_TILE - 1) // COV_TILE
-        self.cov_tiles = nb * (nb + 1) // 2
-        # covariance operand wcd, materialised [wcd_rows][wcd_ld] (16-row stages, 128-col tiles)
-        self.wcd_rows = (n_rows + COV_STAGE - 1) // COV_STAGE * COV_STAGE
-        self.wcd_ld = nb * COV_TILE
-        # row slices: >= ~16 workgroups per CU slot (3 per CU), each slice >= 8 stages
-        stages = self.wcd_rows // COV_STAGE
-        ks = -(-16 * 3 * 256 // self.cov_tiles)
-        self.cov_kslices = max(1, min(32, ks, stages // 8 if stages >= 8 else 1))
-        z = lambda *shape, dt=f64: t.zeros(shape, dtype=dt, device=device)
-        self.rep = z(n_rows)
-        self.tok = z(n_rows)
-        self.T = z(max(1, n_scaled), n_rows)
-        self.part = z(self.col_blocks, E, 8, 2)
-        self.mpart = z(self.col_blocks, E, 4)
-        self.cstat = z(world, E, 16, 2)
-        self.cmax = z(world, E, 4)
-        self.scal = z(world, 16, 2)
-        self.spart = z(4096, 4, 2)
-        self.ev = z(16, E)
-        self.cslab = z(self.cov_kslices, E, E)
-        self.wcd = t.empty((self.wcd_rows, self.wcd_ld), dtype=f64, device=device)
-        self.tokp = t.empty((self.wcd_rows + 64,), dtype=f64, device=device)
-        self.rowpart = t.empty(((self.wcd_ld + 511) // 512, self.wcd_rows, 2), dtype=t.int32, device=device)
-        self.C = z(E, E)
-        self.Mw = z(2 * E * E + 8 * E + 64)  # power-iteration matrices; PCX_M_EIG scratch
-        self.pvec = z(4, E + 64)
-        self.rowv = z(6, n_rows)
-        self.rowstat = z(n_rows, 2, dt=t.int32)
-        self.skey = z(world, 4, dt=u64)
-        self.info = z(16, dt=u64)
-        S = max(1, n_scaled)
-        self.sel_sum = z(world, S, 256, 4, dt=u64)
-        self.sel_min = z(world, S, 256, 2, dt=u64)
-        self.sel_max = z(world, S, 256, dt=u64)
-        self.sel_state = z(S, 16, dt=u64)
-        self.sel_val = z(world, S, 4)
-
-    # buffers every stage writes in full before reading: not re-zeroed on reuse
-    _NO_RESET = ("wcd", "tokp", "rowpart", "T", "cslab", "C", "Mw")
-
-    def reset(self):
-        """Zero the scratch for another consensus of the same shape (reuse across calls)."""
-        for name, v in vars(self).items():
-            if name not in self._NO_RESET and hasattr(v, "zero_"):
-                v.zero_()
-
-    def new_outputs(self):
-        """Fresh result tensors for one call (results outlive the reused scratch)."""
-        t = _device.torch()
-        z = lambda n: t.zeros(n, dtype=t.float64, device=self.device)
-        out = {k: z(self.n_rows) for k in _abi.MAT_OUTPUT_AGENTS}
-        out.update({k: z(self.E) for k in _abi.MAT_OUTPUT_EVENTS})
-        return out, z(4)
+def release_workspace(comm=None, device=None):
+    """Free the single-matrix scratch cached in this thread's context (tens of GB at C5)."""
+    t = _device.torch()
+    comm = comm or Comm()
+    dev = t.device(device) if device is not None else t.device("cuda", t.cuda.current_device())
+    _lib.check(_lib.lib().pcx_release_workspace(comm.context(dev.index)))
 
 
-_WS_CACHE = {}       # (n_rows, E, n_scaled, world, rank, device) -> MatWorkspace
-_WS_CACHE_MAX = 4
-_WS_LOCK = threading.Lock()
+clear_workspace_cache = release_workspace
 
 
-def _workspace(n_rows, E, n_scaled, world, rank, device):
-    """Scratch of one rank, reused across calls of the same shape (allocating and first-touching
-    tens of GB per call costs ~0.1 s at C5 sizes).  Least recently used entries are dropped."""
-    key = (int(n_rows), int(E), int(n_scaled), int(world), int(rank), str(device))
-    with _WS_LOCK:
-        ws = _WS_CACHE.pop(key, None)
-        if ws is not None and getattr(ws, "_busy", False):
-            ws = None  # the same key in use on another thread: build a private one
-        if ws is None:
-            while len(_WS_CACHE) >= _WS_CACHE_MAX:
-                _WS_CACHE.pop(next(iter(_WS_CACHE)))
-            ws = MatWorkspace(n_rows, E, n_scaled, world, device)
-        else:
-            ws.reset()
-        ws._busy = True
-        _WS_CACHE[key] = ws
-    return ws
+def _bounds(scaled, lo, hi, conv):
+    if scaled is None:
+        return None, None, None
+    return conv(scaled, np.uint8), conv(lo, np.float64), conv(hi, np.float64)
 
 
-def clear_workspace_cache():
-    """Release every cached single-matrix workspace (device memory returns to torch's allocator)."""
-    with _WS_LOCK:
-        _WS_CACHE.clear()
+def _problem(n_rows, E, N, r0, P, rep, sc, lo, hi, catch_tolerance, alpha, int_dtype, algorithm, max_components,
+             variance_threshold, aux, mem_kind):
+    alg = _abi.ALGORITHMS.get(algorithm)
+    if alg is None or algorithm in _abi.CLUSTER_ALGORITHMS:
+        raise NotImplementedError("algorithm %r is not on the single-matrix path" % (algorithm,))
+    if alg == _abi.ALG_COKURTOSIS and aux is None:
+        raise ValueError("cokurtosis needs aux_scores (this rank's rows of aux['cokurt'])")
+    mc = int(max_components) if E >= int(max_components) else E  # __init__.py:134-137
+    return _abi.Problem(n_rows, E, N, r0, P, rep, sc, lo, hi, float(catch_tolerance), float(alpha),
+                        int(bool(int_dtype)), alg, mc, mem_kind, float(variance_threshold), aux)
 
+
+def _shape_args(n_rows, comm, n_total, row_offset):
+    if comm.world == 1:
+        return n_rows, 0
+    if n_total is None or row_offset is None:
+        raise ValueError("a sharded call needs n_total and row_offset (see shard_rows)")
+    return int(n_total), int(row_offset)
 
 
 def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, catch_tolerance=0.1,
                      alpha=0.1, int_dtype=False, algorithm="PCA", comm=None, n_total=None,
                      row_offset=None, device=None, matrices=False, profile=None, max_components=5,
                      variance_threshold=0.9, aux_scores=None):
-    """Consensus of one report matrix on the GPU(s).
+    """Consensus of one report matrix on the GPU(s), device-resident (torch tensors).
 
     reports:    this rank's rows, (n_rows, E) float64 (torch tensor on the GPU, or numpy)
     reputation: RAW reputation of ALL N reporters (every rank passes the full vector), or None
     scaled/lo/hi: event bounds (E,), or None (every event binary)
-    comm:       :class:`Comm` (default: single GPU)
+    comm:       :class:`Comm` (default: single GPU); sharded calls also give n_total, row_offset
     matrices:   also return this rank's rescaled ("original") and filled reports
     profile:    optional dict; receives per-stage device milliseconds (HIP events on the
-                launching stream) under the stage names of include/pcx.h
+                launching stream, pcx_profile_read) under the stage names of libpcx
     algorithm:  "PCA", "absolute", "big-five" (max_components, capped at E), "fixed-variance"
                 (variance_threshold), "cokurtosis" (aux_scores: this rank's rows of aux["cokurt"])
 
@@ -227,204 +242,124 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     dev = t.device(device) if device is not None else t.device("cuda", t.cuda.current_device())
     R = _device.as_device(reports, t.float64, dev)
     n_rows, E = R.shape
-    N = int(n_total) if n_total is not None else n_rows * comm.world
-    r0 = int(row_offset) if row_offset is not None else comm.rank * n_rows
+    N, r0 = _shape_args(n_rows, comm, n_total, row_offset)
     rep = _device.as_device(reputation, t.float64, dev)
     if rep is not None and rep.numel() != N:
         raise ValueError("reputation must hold all N=%d reporters (got %d)" % (N, rep.numel()))
-    sc = lo_ = hi_ = None
-    scols = sidx = None
-    n_scaled = 0
-    if scaled is not None:
-        sc = _device.as_device(scaled, t.uint8, dev)
-        lo_ = _device.as_device(lo, t.float64, dev)
-        hi_ = _device.as_device(hi, t.float64, dev)
-        scl = sc.to("cpu").bool()
-        cols = t.nonzero(scl).flatten().to(t.int32)
-        n_scaled = int(cols.numel())
-        idx = t.full((E,), -1, dtype=t.int32)
-        idx[cols.long()] = t.arange(n_scaled, dtype=t.int32)
-        scols = cols.to(dev)
-        sidx = idx.to(dev)
-    alg = _abi.ALGORITHMS.get(algorithm)
-    if alg is None or algorithm in _abi.CLUSTER_ALGORITHMS:
-        raise NotImplementedError("algorithm %r is not on the single-matrix path" % (algorithm,))
-    aux = None
-    if alg == _abi.ALG_COKURTOSIS:
-        if aux_scores is None:
-            raise ValueError("cokurtosis needs aux_scores (this rank's rows of aux['cokurt'])")
-        aux = _device.as_device(aux_scores, t.float64, dev).reshape(-1)
-        if aux.numel() != n_rows:
-            raise ValueError("aux_scores must hold this rank's %d rows" % n_rows)
-    algo = (alg, int(max_components) if E >= int(max_components) else E, float(variance_threshold), aux)
-
-    ws = _workspace(n_rows, E, n_scaled, comm.world, comm.rank, dev)
-    try:
-        return _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, algo, comm, dev, catch_tolerance,
-                    alpha, int_dtype, matrices, profile)
-    finally:
-        ws._busy = False
-
-
-def _run(ws, R, rep, sc, lo_, hi_, scols, sidx, n_scaled, N, r0, algo, comm, dev, catch_tolerance, alpha,
-         int_dtype, matrices, profile):
-    t = _device.torch()
-    alg, max_components, variance_threshold, aux = algo
-    n_rows, E = R.shape
-    out, scalars = ws.new_outputs()
-    m = _abi.Mat()
-    m.n_rows, m.n_events, m.n_total, m.row_offset = n_rows, E, N, r0
-    m.world, m.rank, m.int_dtype, m.algorithm = comm.world, comm.rank, int(bool(int_dtype)), alg
-    m.catch_tolerance, m.alpha = float(catch_tolerance), float(alpha)
-    m.n_scaled, m.sel_phase, m.col_blocks = n_scaled, 1, ws.col_blocks
-    m.cov_tiles, m.cov_kslices = ws.cov_tiles, ws.cov_kslices
-    m.wcd_rows, m.wcd_ld = ws.wcd_rows, ws.wcd_ld
-    m.max_components, m.components, m.variance_threshold = max_components, -1, variance_threshold
-    m.aux_scores = _device.ptr(aux)
+    conv = lambda a, dt: _device.as_device(a, {np.uint8: t.uint8, np.float64: t.float64}[dt], dev)
+    sc, lo_, hi_ = _bounds(scaled, lo, hi, conv)
+    aux = None if aux_scores is None else _device.as_device(aux_scores, t.float64, dev).reshape(-1)
+    if aux is not None and aux.numel() != n_rows:
+        raise ValueError("aux_scores must hold this rank's %d rows" % n_rows)
     P = _device.ptr
-    m.reports, m.scaled, m.lo, m.hi, m.rep_raw = P(R), P(sc), P(lo_), P(hi_), P(rep)
-    m.scaled_cols, m.scaled_index = P(scols), P(sidx)
-    for name in ("wcd", "tokp", "rowpart", "rep", "tok", "T", "part", "mpart", "cstat", "cmax", "scal", "spart", "ev", "cslab", "C",
-                 "Mw", "pvec", "rowv", "rowstat", "skey", "info", "sel_sum", "sel_min", "sel_max", "sel_state",
-                 "sel_val"):
-        setattr(m, name, P(getattr(ws, name)))
+    prob = _problem(n_rows, E, N, r0, P(R), P(rep), P(sc), P(lo_), P(hi_), catch_tolerance, alpha, int_dtype,
+                    algorithm, max_components, variance_threshold, P(aux), _abi.MEM_DEVICE)
+    z = lambda *shape: t.empty(shape, dtype=t.float64, device=dev)
+    out = {k: z(n_rows) for k in _abi.MAT_OUTPUT_AGENTS}
+    out.update({k: z(E) for k in _abi.MAT_OUTPUT_EVENTS})
+    if matrices:
+        out["original"], out["filled"] = z(n_rows, E), z(n_rows, E)
+    res = _abi.Result()
     for k, v in out.items():
-        setattr(m, k, P(v))
-    m.scalars = P(scalars)
-    mats = {}
-    if matrices:
-        mats = {"original": t.empty((n_rows, E), dtype=t.float64, device=dev),
-                "filled": t.empty((n_rows, E), dtype=t.float64, device=dev)}
-        m.original, m.filled = P(mats["original"]), P(mats["filled"])
-
-    h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev))
+        setattr(res, k, v.data_ptr())
     lib = _lib.lib()
-
-    names = {v: k for k, v in vars(_abi).items() if k.startswith("M_") and isinstance(v, int)}
-    events = []
-
-    def stage(s):
-        if profile is not None:
-            e0 = t.cuda.Event(enable_timing=True)
-            e0.record()
-        _lib.check(lib.pcx_mat_stage(h, C.byref(m), int(s)))
-        if profile is not None:
-            e1 = t.cuda.Event(enable_timing=True)
-            e1.record()
-            events.append((names.get(int(s), str(s)), e0, e1))
-
-    S = slice
-    # a1: reputation, tokens (__init__.py:138-146)
-    comm.clear_slots(ws.scal, (S(0, 2),))
-    stage(_abi.M_REPUTATION)
-    comm.reduce_slots(ws.scal, (S(0, 2),))
-    # a2/a3: rescale + NA + present sums (:266-299)
-    comm.clear_slots(ws.cstat, (S(None), S(0, 4)))
-    comm.clear_slots(ws.cmax)
-    stage(_abi.M_COLSTATS)
-    comm.reduce_slots(ws.cstat, (S(None), S(0, 4)))
-    comm.reduce_slots(ws.cmax)
-    stage(_abi.M_GUESS)
-    _select(stage, m, ws, comm, phase=1)                 # scaled fills: weighted median (:300-303)
-    stage(_abi.M_MEAN)
-    pca = alg == _abi.ALG_PCA
-    wpca = alg in (_abi.ALG_PCA, _abi.ALG_BIG_FIVE, _abi.ALG_FIXED_VARIANCE)
-    if wpca:
-        # a5: wcd materialised (:322); a6: covariance on fp64 MFMA (:326); a7: power iteration (:330-336)
-        stage(_abi.M_WCD)
-        stage(_abi.M_COV)
-        stage(_abi.M_COV_REDUCE)
-        comm.all_reduce_sum(ws.C)
-        stage(_abi.M_COV_FINISH)
-        stage(_abi.M_POWER)
-        if not pca:  # big-five / fixed-variance components (:373-390, :429-451)
-            stage(_abi.M_EIG)
-    else:
-        stage(_abi.M_ZERO_LOADING)
-    comm.clear_slots(ws.skey)
-    stage(_abi.M_SCORES)
-    comm.reduce_slots(ws.skey)
-    if alg != _abi.ALG_ABSOLUTE:
-        # a8/a9: sign-choice rule (:487-500; the other algorithms: nonconformity, :475-485)
-        comm.clear_slots(ws.scal, (S(2, 6),))
-        stage(_abi.M_NCSUMS)
-        comm.reduce_slots(ws.scal, (S(2, 6),))
-        comm.clear_slots(ws.cstat, (S(None), S(4, 6)))
-        stage(_abi.M_GEMV2)
-        comm.reduce_slots(ws.cstat, (S(None), S(4, 6)))
-        stage(_abi.M_DECIDE)
-    # a10: reputation update (:460-472)
-    comm.clear_slots(ws.scal, (S(6, 8),))
-    stage(_abi.M_REPU)
-    comm.reduce_slots(ws.scal, (S(6, 8),))
-    stage(_abi.M_SMOOTH)
-    # a12-a14: outcomes, participation, certainty (:510-546)
-    comm.clear_slots(ws.cstat, (S(None), S(6, 14)))
-    stage(_abi.M_OUTCOMES)
-    comm.reduce_slots(ws.cstat, (S(None), S(6, 14)))
-    stage(_abi.M_EVENTS)
-    _select(stage, m, ws, comm, phase=2)                 # scaled outcomes: weighted median (:519-523)
-    comm.clear_slots(ws.cstat, (S(None), S(14, 16)))
-    stage(_abi.M_SCALED_CERT)
-    comm.reduce_slots(ws.cstat, (S(None), S(14, 16)))
-    stage(_abi.M_FINAL)
-    comm.clear_slots(ws.scal, (S(8, 10),))
-    stage(_abi.M_ROWSUMS)
-    comm.reduce_slots(ws.scal, (S(8, 10),))
-    stage(_abi.M_AGENTS)
-    if matrices:
-        stage(_abi.M_MATRICES)
-
-    info = ws.info.cpu().tolist()
+    h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev), comm.context(dev.index))
     if profile is not None:
-        t.cuda.synchronize(dev)
-        for name, e0, e1 in events:
-            profile[name] = profile.get(name, 0.0) + e0.elapsed_time(e1)
-    scal = scalars.cpu().tolist()
+        _lib.check(lib.pcx_profile_enable(h, 1))
+    _lib.check(lib.pcx_consensus_f64(h, C.byref(prob), C.byref(res)))
+    if profile is not None:
+        ms = (C.c_double * _abi.NSTAGES)()
+        _lib.check(lib.pcx_profile_read(h, ms))
+        _lib.check(lib.pcx_profile_enable(h, 0))
+        for k in range(_abi.NSTAGES):
+            if ms[k] > 0:
+                name = "M_" + lib.pcx_stage_name(k).decode()
+                profile[name] = profile.get(name, 0.0) + ms[k]
     events = {k: out[k] for k in _abi.MAT_OUTPUT_EVENTS}
     agents = {k: out[k] for k in _abi.MAT_OUTPUT_AGENTS}
-    agents.update(mats)
-    meta = {"participation": scal[0], "avg_certainty": scal[1],
-            "branch": int(info[_abi.INFO_BRANCH]) if alg != _abi.ALG_ABSOLUTE else _abi.BRANCH_NONE,
-            "pi_iters": int(info[_abi.INFO_PI_ITERS]), "flags": int(info[_abi.INFO_FLAGS]) if wpca else 0,
-            "components": int(m.components),
-            "filled_guess": ws.ev[0].clone(), "workspace": ws, "inputs": (R, rep, sc, lo_, hi_)}
+    for k in ("original", "filled"):
+        if k in out:
+            agents[k] = out[k]
+    meta = _meta(res, algorithm)
+    meta["inputs"] = (R, rep, sc, lo_, hi_)
     return events, agents, meta
 
 
-def _select(stage, m, ws, comm, phase):
-    """Exact weighted medians of the scaled events (weightedstats semantics)."""
-    if m.n_scaled == 0:
-        return
-    m.sel_phase = phase
-    if comm.world == 1 and m.n_rows <= _abi.SEL_EXACT_MAX:
-        # small matrices: replay the reference's float walk exactly (ties included)
-        stage(_abi.M_SEL_EXACT)
-        stage(_abi.M_SEL_FINISH)
-        return
-    for b in (ws.sel_sum, ws.sel_min, ws.sel_max, ws.sel_val):
-        comm.clear_slots(b)
-    stage(_abi.M_SEL_INIT)
-    for b in (ws.sel_sum, ws.sel_min, ws.sel_max, ws.sel_val):
-        comm.reduce_slots(b)
-    stage(_abi.M_SEL_START)
-    if int(ws.info[_abi.INFO_SEL_ARGMAX].item()):
-        comm.clear_slots(ws.sel_val)
-        stage(_abi.M_SEL_ARGMAX)
-        comm.reduce_slots(ws.sel_val)
-        comm.clear_slots(ws.sel_val, (S_ALL, slice(2, 3)))
-        stage(_abi.M_SEL_VALUE)
-        comm.reduce_slots(ws.sel_val, (S_ALL, slice(2, 3)))
-    for _ in range(16):  # <= 8 passes of 8 key bits each
-        for b in (ws.sel_sum, ws.sel_min, ws.sel_max):
-            comm.clear_slots(b)
-        stage(_abi.M_SEL_HIST)
-        for b in (ws.sel_sum, ws.sel_min, ws.sel_max):
-            comm.reduce_slots(b)
-        stage(_abi.M_SEL_STEP)
-        if int(ws.info[_abi.INFO_SEL_ACTIVE].item()) == 0:
-            break
-    stage(_abi.M_SEL_FINISH)
+def _meta(res, algorithm):
+    return {"participation": res.participation, "avg_certainty": res.avg_certainty,
+            "branch": int(res.branch), "pi_iters": int(res.pi_iters), "flags": int(res.flags),
+            "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes)}
 
 
-S_ALL = slice(None)
+# ---------------------------------------------------------------- host-memory entry points
+def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outputs, catch_tolerance=0.1,
+               alpha=0.1, int_dtype=False, algorithm="PCA", max_components=5, variance_threshold=0.9,
+               aux_scores=None, extra=()):
+    """Call a single-matrix entry point with numpy inputs / outputs (PCX_MEM_HOST: libpcx
+    copies in and out).  ``outputs``: {result field: shape}."""
+    _device.require_gpu()
+    R = np.ascontiguousarray(reports, dtype=np.float64)
+    n_rows, E = R.shape
+    keep = [R]
+
+    def ptr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data
+
+    sc, lo_, hi_ = (None, None, None) if scaled is None else (ptr(scaled, np.uint8), ptr(lo, np.float64),
+                                                              ptr(hi, np.float64))
+    prob = _problem(n_rows, E, n_rows, 0, R.ctypes.data, ptr(reputation, np.float64), sc, lo_, hi_,
+                    catch_tolerance, alpha, int_dtype, algorithm, max_components, variance_threshold,
+                    ptr(aux_scores, np.float64), _abi.MEM_HOST)
+    res = _abi.Result()
+    outs = {}
+    for k, shape in outputs.items():
+        outs[k] = np.empty(shape, dtype=np.float64)
+        setattr(res, k, outs[k].ctypes.data)
+    h = _lib.context(device_index)
+    _lib.check(getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res)))
+    return outs, _meta(res, algorithm)
+
+
+def consensus_host(reports, reputation=None, scaled=None, lo=None, hi=None, device_index=0, matrices=True, **kw):
+    """Whole consensus from host arrays (the drop-in Oracle's large-matrix path)."""
+    n, E = np.shape(reports)
+    shapes = {k: (n,) for k in _abi.MAT_OUTPUT_AGENTS}
+    shapes.update({k: (E,) for k in _abi.MAT_OUTPUT_EVENTS})
+    if matrices:
+        shapes.update(original=(n, E), filled=(n, E))
+    return _host_call("pcx_consensus_f64", reports, reputation, scaled, lo, hi, device_index, shapes, **kw)
+
+
+def interpolate_host(reports, reputation=None, scaled=None, lo=None, hi=None, device_index=0, **kw):
+    n, E = np.shape(reports)
+    return _host_call("pcx_interpolate_f64", reports, reputation, scaled, lo, hi, device_index,
+                      {"original": (n, E), "filled": (n, E)}, **kw)
+
+
+def wpca_host(filled, reputation=None, device_index=0, **kw):
+    n, E = np.shape(filled)
+    return _host_call("pcx_wpca_f64", filled, reputation, None, None, None, device_index,
+                      {"weighted_mean": (E,), "covariance": (E, E), "adj_first_loadings": (E,), "scores": (n,)},
+                      **kw)
+
+
+def lie_detector_host(filled, reputation=None, device_index=0, **kw):
+    n, E = np.shape(filled)
+    return _host_call("pcx_lie_detector_f64", filled, reputation, None, None, None, device_index,
+                      {"adj_first_loadings": (E,), "scores": (n,), "old_rep": (n,), "this_rep": (n,),
+                       "smooth_rep": (n,)}, **kw)
+
+
+def nonconformity_host(scores, filled, reputation=None, rank_rule=True, device_index=0, **kw):
+    n, E = np.shape(filled)
+    s = np.ascontiguousarray(np.asarray(scores, dtype=np.float64).ravel())
+    if s.size != n:
+        raise ValueError("scores must hold one value per reporter")
+    nc = np.empty(n, dtype=np.float64)
+    outs, meta = _host_call("pcx_nonconformity_f64", filled, reputation, None, None, None, device_index, {},
+                            extra=(s.ctypes.data, int(bool(rank_rule)), nc.ctypes.data), **kw)
+    return nc, meta

@@ -28,7 +28,7 @@ def test_c5_full_size_properties_and_shard_invariance(gpu_lib):
     import torch
 
     from pyconsensus_amd import synthetic
-    from pyconsensus_amd.pipeline import clear_workspace_cache, consensus_matrix
+    from pyconsensus_amd.pipeline import consensus_matrix, release_workspace
 
     dev = torch.device("cuda:0")
     R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, device=dev)
@@ -37,7 +37,7 @@ def test_c5_full_size_properties_and_shard_invariance(gpu_lib):
     scaled = sc.cpu().numpy().astype(bool)
     lo_, hi_ = lo.cpu().numpy(), hi.cpu().numpy()
     del R, ev, ag, meta
-    clear_workspace_cache()
+    release_workspace()
     torch.cuda.empty_cache()
 
     # reputation vectors are distributions
@@ -60,7 +60,7 @@ def _check_world(world, dev, ref_ev, ref_ag, branch):
     import torch
 
     from pyconsensus_amd import synthetic
-    from pyconsensus_amd.pipeline import ThreadComm, ThreadGroup, clear_workspace_cache, consensus_matrix, shard_rows
+    from pyconsensus_amd.pipeline import ThreadComm, ThreadGroup, consensus_matrix, shard_rows
 
     grp = ThreadGroup(world)
     res = [None] * world
@@ -74,9 +74,11 @@ def _check_world(world, dev, ref_ev, ref_ag, branch):
                                                            shards=list(range(r * per, (r + 1) * per)), device=dev)
             off, cnt = shard_rows(N, world, r)
             assert Rr.shape[0] == cnt
-            e, a, m = consensus_matrix(Rr, None, scr, lor, hir, comm=ThreadComm(grp, r), n_total=N,
-                                       row_offset=off, device=dev)
+            comm = ThreadComm(grp, r)
+            e, a, m = consensus_matrix(Rr, None, scr, lor, hir, comm=comm, n_total=N, row_offset=off, device=dev)
             res[r] = (_np(e), _np(a), m["branch"])
+            del Rr, e, a
+            comm.close()  # frees this virtual rank's scratch
         except Exception as ex:  # pragma: no cover
             errs.append(ex)
             grp.barrier.abort()
@@ -84,7 +86,6 @@ def _check_world(world, dev, ref_ev, ref_ag, branch):
     th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
     [x.start() for x in th]
     [x.join() for x in th]
-    clear_workspace_cache()
     torch.cuda.empty_cache()
     assert not errs, errs
     for r in range(world):

@@ -1,20 +1,22 @@
-"""The N>1 path's host protocol on CPU with torch.distributed gloo, world_size 2.
+"""The N>1 host path on CPU with torch.distributed gloo, world_size 2.
 
-pipeline.Comm is what the sharded consensus uses between stages: each rank writes
-its partial into slot [rank] of a [world, ...] buffer; clear_slots + reduce_slots
-(all-reduce SUM) must leave every slot holding exactly its owner's values on every
-rank, for whole buffers and for sub-slices (the stages reuse one buffer for several
-slot ranges), and a full-buffer SUM (the covariance) must add the ranks.
-"""
+libpcx's sharded consensus exchanges per-rank partials through a communicator; the
+callback backend (pipeline.CallbackComm) carries those exchanges over torch.distributed.
+Its two callbacks are exercised here exactly as libpcx calls them -- host buffers, in
+place -- with the data kinds the consensus exchanges: u64 selection limbs / counts (SUM,
+exact even near 2^64), u64 key ranges (MIN / MAX), f64 covariance partials (SUM) and
+rank-ordered all-gathers of dd slot blocks.  Row sharding math is checked too."""
+import ctypes as C
 import os
 import socket
 
+import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pyconsensus_amd.pipeline import Comm, shard_rows
+from pyconsensus_amd import _abi
+from pyconsensus_amd.pipeline import CallbackComm, shard_rows
 
 
 def _free_port():
@@ -29,48 +31,40 @@ def _worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = Comm.from_env()
-        assert comm.world == world and comm.rank == rank
-        # a [world, E, 16, 2] column-stat buffer reused for two slot ranges
-        E = 5
-        buf = torch.zeros(world, E, 16, 2, dtype=torch.float64)
-        comm.clear_slots(buf, (slice(None), slice(0, 4)))
-        buf[rank, :, 0:4] = rank + 1.0
-        comm.reduce_slots(buf, (slice(None), slice(0, 4)))
-        for w in range(world):
-            assert torch.all(buf[w, :, 0:4] == w + 1.0)
-        # second stage writes another slot range; the first range must stay intact
-        comm.clear_slots(buf, (slice(None), slice(4, 6)))
-        buf[rank, :, 4:6] = 10.0 * (rank + 1)
-        comm.reduce_slots(buf, (slice(None), slice(4, 6)))
-        for w in range(world):
-            assert torch.all(buf[w, :, 0:4] == w + 1.0)
-            assert torch.all(buf[w, :, 4:6] == 10.0 * (w + 1))
-        # uint64 key slots (score min/max) survive the SUM exactly
-        sk = torch.zeros(world, 4, dtype=torch.int64)
-        comm.clear_slots(sk)
-        sk[rank, 0] = -1 - rank  # ~0ull-style patterns
-        sk[rank, 1] = (1 << 62) + rank
-        comm.reduce_slots(sk)
-        for w in range(world):
-            assert sk[w, 0].item() == -1 - w and sk[w, 1].item() == (1 << 62) + w
-        # plain all-reduce (covariance partials)
-        C = torch.full((3, 3), float(rank + 1), dtype=torch.float64)
-        comm.all_reduce_sum(C)
-        assert torch.all(C == sum(range(1, world + 1)))
-        # row shards tile [0, N)
-        N = 1001
-        spans = [shard_rows(N, world, r) for r in range(world)]
-        assert spans[0][0] == 0 and sum(c for _, c in spans) == N
-        assert all(spans[r][0] + spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+        comm = CallbackComm(world, rank)
+        ar, ag = comm._cbs
+        p = lambda a: a.ctypes.data_as(C.c_void_p)
+        # u64 limbs and counts: exact SUM (no float rounding, no int64 overflow issues)
+        big = np.array([2 ** 62 + rank, 12345 + rank, (1 << 43) - 1], dtype=np.uint64)
+        assert ar(None, p(big), big.size, _abi.U64, _abi.RED_SUM) == 0
+        assert big.tolist() == [sum(2 ** 62 + r for r in range(world)), sum(12345 + r for r in range(world)),
+                                world * ((1 << 43) - 1)]
+        keys = np.array([0xFFFF000000000000 - rank, 5 + rank], dtype=np.uint64)
+        mn = keys.copy()
+        assert ar(None, p(mn), 2, _abi.U64, _abi.RED_MIN) == 0
+        assert mn.tolist() == [0xFFFF000000000000 - (world - 1), 5]
+        mx = keys.copy()
+        assert ar(None, p(mx), 2, _abi.U64, _abi.RED_MAX) == 0
+        assert mx.tolist() == [0xFFFF000000000000, 5 + world - 1]
+        # f64 covariance partials
+        cov = np.full((3, 3), rank + 1.0)
+        assert ar(None, p(cov), cov.size, _abi.F64, _abi.RED_SUM) == 0
+        assert np.all(cov == sum(range(1, world + 1)))
+        # all-gather of dd slot blocks: rank order
+        blk = np.arange(6, dtype=np.float64) + 100 * rank
+        out = np.zeros(6 * world)
+        assert ag(None, p(blk), p(out), blk.nbytes) == 0
+        assert np.array_equal(out, np.concatenate([np.arange(6.0) + 100 * r for r in range(world)]))
         dist.destroy_process_group()
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover
-        q.put((rank, repr(e)))
+        import traceback
+
+        q.put((rank, traceback.format_exc() + repr(e)))
 
 
 @pytest.mark.parametrize("world", [2])
-def test_slot_protocol_gloo(world):
+def test_callback_exchange_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -87,5 +81,6 @@ def test_shard_rows_uneven():
             if N < world:
                 continue
             spans = [shard_rows(N, world, r) for r in range(world)]
-            assert sum(c for _, c in spans) == N
+            assert spans[0][0] == 0 and sum(c for _, c in spans) == N
+            assert all(spans[r][0] + spans[r][1] == spans[r + 1][0] for r in range(world - 1))
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
