@@ -96,6 +96,69 @@ static double dot2(const double* a, int sa, const double* b, int sb, int n) {
     return s + c;
 }
 
+/* np.dot(v, F) for v (N,), F (N, E) row-major with row stride ES, column j, in the exact
+ * operation order numpy 2.2 / OpenBLAS 0.3.29 use in the build container (DYNAMIC_ARCH,
+ * SkylakeX kernels), the machine the golden vectors come from.  Measured, not documented:
+ * tests/golden/probe_openblas_order.py fits this model bit for bit on random inputs with a
+ * wide exponent range (every N <= 139, E <= 32).  numpy calls cblas_dgemv(RowMajor, Trans),
+ * i.e. column-major dgemv_n on the E x N matrix (single-threaded at these sizes):
+ *   - events j < E & ~3 (the 4-row vector kernel): reporters in blocks of 4, each block
+ *     t = v1*F1 rounded, then fma with reporters 0, 2, 3; y = y + t; a tail of 2 the same
+ *     with reporters (1, 0); a tail of 1: y = y + v*F;
+ *   - the last E % 4 events (scalar code): y = fma(F_i, v_i, y) over i, except lda == 2 or 3
+ *     (E == 2, 3), unrolled by 4 as y = y + fma(F_i, v_i, F_i+1 v_i+1) per pair;
+ *   - E == 1: numpy's ddot (4 x 8-lane fma accumulators per 32, folded to 4 x 4 lanes, 16 per
+ *     step, lanes summed (0+2)+(1+3), then a sequential fma tail). */
+static double ob_ddot(const double* a, const double* x, int sx, int n) {
+    double acc8[4][8] = {{0}}, acc4[4][4];
+    const int n32 = n & -32, n16 = n & -16;
+    for (int i = 0; i < n32; i += 32)
+        for (int k = 0; k < 32; k++) acc8[k / 8][k % 8] = fma(a[i + k], x[(int64_t)(i + k) * sx], acc8[k / 8][k % 8]);
+    for (int r = 0; r < 4; r++)
+        for (int l = 0; l < 4; l++) acc4[r][l] = acc8[r][l] + acc8[r][l + 4];
+    for (int i = n32; i < n16; i += 16)
+        for (int k = 0; k < 16; k++) acc4[k / 4][k % 4] = fma(a[i + k], x[(int64_t)(i + k) * sx], acc4[k / 4][k % 4]);
+    double A[4];
+    for (int l = 0; l < 4; l++) A[l] = ((acc4[0][l] + acc4[1][l]) + acc4[2][l]) + acc4[3][l];
+    double d = (A[0] + A[2]) + (A[1] + A[3]);
+    for (int i = n16; i < n; i++) d = fma(a[i], x[(int64_t)i * sx], d);
+    return d;
+}
+
+static double ob_vecmat(const double* v, const double* Fj, int ld, int N, int E, int j) {
+    if (E == 1) return ob_ddot(v, Fj, ld, N);
+#define FJ(i) Fj[(int64_t)(i) * ld]
+    if (j < (E & ~3)) {
+        double y = 0.0;
+        int n = 0;
+        for (; n + 4 <= N; n += 4) {
+            double t = FJ(n + 1) * v[n + 1];
+            t = fma(FJ(n), v[n], t);
+            t = fma(FJ(n + 2), v[n + 2], t);
+            t = fma(FJ(n + 3), v[n + 3], t);
+            y = y + t;
+        }
+        if (n + 2 <= N) {
+            double t = FJ(n + 1) * v[n + 1];
+            t = fma(FJ(n), v[n], t);
+            y = y + t;
+            n += 2;
+        }
+        if (n < N) y = y + FJ(n) * v[n];
+        return y;
+    }
+    double t = 0.0;
+    int i = 0;
+    if (E == 2 || E == 3)
+        for (; i + 4 <= N; i += 4) {
+            t = t + fma(FJ(i), v[i], FJ(i + 1) * v[i + 1]);
+            t = t + fma(FJ(i + 2), v[i + 2], FJ(i + 3) * v[i + 3]);
+        }
+    for (; i < N; i++) t = fma(FJ(i), v[i], t);
+    return t;
+#undef FJ
+}
+
 static double catch_(double x, double tol) {  /* __init__.py:251-258 */
     if (x < 1.5 - tol) return 1.0;
     if (x > 1.5 + tol) return 2.0;
@@ -799,7 +862,7 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     double loading[EMAX], s[NMAX], nc[NMAX];
     int flags = 0, iters = 0, branch = PCX_BRANCH_NONE;
     double old[EMAX];
-    for (int j = 0; j < E; j++) old[j] = dot2(rep, 1, &F[0][j], ES, N);  /* np.dot(rep, F) */
+    for (int j = 0; j < E; j++) old[j] = ob_vecmat(rep, &F[0][j], ES, N, E, j);  /* np.dot(rep, F) */
     const int alg = in->algorithm;
     const int pca_like = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;
     int comps = -1;
@@ -879,8 +942,8 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         normalize_(set2, N, n2);
         double d1[EMAX], d2[EMAX], new1[EMAX], new2[EMAX], r0[EMAX], r1[EMAX], r2[EMAX];
         for (int j = 0; j < E; j++) {
-            double a1 = dot2(n1, 1, &F[0][j], ES, N);
-            double a2 = dot2(n2, 1, &F[0][j], ES, N);
+            double a1 = ob_vecmat(n1, &F[0][j], ES, N, E, j);  /* np.dot(normalize(set), F) */
+            double a2 = ob_vecmat(n2, &F[0][j], ES, N, E, j);
             d1[j] = a1;
             d2[j] = a2;
             double t = 0.01 * old[j];
@@ -925,7 +988,7 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     /* --- a12/a13: outcomes (:510-538) --- */
     double raw[EMAX], adj[EMAX], fin[EMAX], cert[EMAX];
     for (int j = 0; j < E; j++) {
-        raw[j] = dot2(smooth, 1, &F[0][j], ES, N);
+        raw[j] = ob_vecmat(smooth, &F[0][j], ES, N, E, j);  /* np.dot(smooth_rep, F) (:510) */
         if (scaled[j]) {
             double col[NMAX];
             for (int i = 0; i < N; i++) col[i] = F[i][j];

@@ -185,6 +185,70 @@ __device__ __forceinline__ double dot2(const double* a, const double* b, int bs,
     return s + c;
 }
 
+// np.dot(v, F) for one event column j, in the operation order of numpy 2.2 / OpenBLAS
+// 0.3.29 (SkylakeX kernels) in the build container, where the goldens come from -- the
+// SPEC's ob_vecmat (oracle/pcx_oracle_batched.c), fitted bit for bit by
+// tests/golden/probe_openblas_order.py.  Events j < E & ~3: reporters in blocks of 4, the
+// second product rounded then fma with the 1st, 3rd, 4th, y = y + block; tails of 2 / 1.
+// The last E % 4 events: a sequential fma chain (E == 2, 3: pairs y + fma(a, x, a' x')).
+// E == 1: numpy's ddot (32-wide, then 16-wide fma accumulators, lanes (0+2)+(1+3), fma tail).
+__device__ __noinline__ double ob_ddot(const double* v, const double* f, int ld, int n) {
+    double acc8[4][8], acc4[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc8[r][q] = 0.0;
+    const int n32 = n & -32, n16 = n & -16;
+    for (int i = 0; i < n32; i += 32)
+#pragma unroll
+        for (int k = 0; k < 32; k++) acc8[k / 8][k % 8] = fma(v[i + k], f[(i + k) * ld], acc8[k / 8][k % 8]);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc4[r][q] = acc8[r][q] + acc8[r][q + 4];
+    for (int i = n32; i < n16; i += 16)
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc4[k / 4][k % 4] = fma(v[i + k], f[(i + k) * ld], acc4[k / 4][k % 4]);
+    double A[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) A[q] = ((acc4[0][q] + acc4[1][q]) + acc4[2][q]) + acc4[3][q];
+    double d = (A[0] + A[2]) + (A[1] + A[3]);
+    for (int i = n16; i < n; i++) d = fma(v[i], f[i * ld], d);
+    return d;
+}
+
+__device__ __forceinline__ double ob_vecmat(const double* v, const double* f, int ld, int N, int E, int j) {
+    if (E == 1) return ob_ddot(v, f, ld, N);
+    if (j < (E & ~3)) {
+        double y = 0.0;
+        int n = 0;
+        for (; n + 4 <= N; n += 4) {
+            double t = f[(n + 1) * ld] * v[n + 1];
+            t = fma(f[n * ld], v[n], t);
+            t = fma(f[(n + 2) * ld], v[n + 2], t);
+            t = fma(f[(n + 3) * ld], v[n + 3], t);
+            y = y + t;
+        }
+        if (n + 2 <= N) {
+            double t = f[(n + 1) * ld] * v[n + 1];
+            t = fma(f[n * ld], v[n], t);
+            y = y + t;
+            n += 2;
+        }
+        if (n < N) y = y + f[n * ld] * v[n];
+        return y;
+    }
+    double t = 0.0;
+    int i = 0;
+    if (E == 2 || E == 3)
+        for (; i + 4 <= N; i += 4) {
+            t = t + fma(f[i * ld], v[i], f[(i + 1) * ld] * v[i + 1]);
+            t = t + fma(f[(i + 2) * ld], v[i + 2], f[(i + 3) * ld] * v[i + 3]);
+        }
+    for (; i < N; i++) t = fma(f[i * ld], v[i], t);
+    return t;
+}
+
 // weightedstats.weighted_median restated (oracle/pcx_oracle.py): lane i holds the
 // pair (x, w) if `sel`; W is the builtin sequential sum of the selected weights in
 // lane order (computed by the caller).  Scratch: sx, sw (64 doubles each).
@@ -1173,7 +1237,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
 
     STAMP(3);
     // ---- old = rep . F (np.dot) -------------------------------------------
-    double oldj = col ? dot2(S.rep, S.F + l, ES, N) : 0.0;
+    double oldj = col ? ob_vecmat(S.rep, S.F + l, ES, N, E, l) : 0.0;  // np.dot(rep, F) (:490)
 
     double sc_i = 0.0, nc_i = 0.0, ld_j = 0.0;
     int branch = 5, flags = 0, iters = 0, comps = -1;
@@ -1411,8 +1475,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         wsync();
         double d1 = 0.0, d2 = 0.0;
         if (col) {
-            d1 = dot2(S.n1, S.F + l, ES, N);
-            d2 = dot2(S.n2, S.F + l, ES, N);
+            d1 = ob_vecmat(S.n1, S.F + l, ES, N, E, l);  // np.dot(normalize(set1), F) (:492)
+            d2 = ob_vecmat(S.n2, S.F + l, ES, N, E, l);
             const double t = 0.01 * oldj;
             S.nv1[l] = d1 + t;
             S.nv2[l] = d2 + t;
@@ -1456,7 +1520,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
 
     STAMP(8);
     // ---- a12/a13: outcomes (:510-538) -------------------------------------
-    double rawj = col ? dot2(S.smooth, S.F + l, ES, N) : 0.0;
+    double rawj = col ? ob_vecmat(S.smooth, S.F + l, ES, N, E, l) : 0.0;  // np.dot(smooth_rep, F) (:510)
     STAMP(15);
     if (scaled_mask) {
         const double Wsm = [&] {  // builtin sequential sum of smooth_rep (weightedstats)

@@ -41,16 +41,73 @@ SIGNED = {"agents.scores", "events.adj_first_loadings"}
 EXCLUDED = {"q_all_missing_scaled_col"}
 
 
-def is_neartie(case, path="exact"):
-    """Is this round's discrete outcome decided by rounding on ``path``?
+# Every golden case a path does NOT reproduce, with the kind of mismatch and its cause.
+# The suites assert that the set of mismatching cases they ran EQUALS this list (restricted
+# to the cases run): a new mismatch and a stale entry both fail, so the list only changes
+# deliberately.  Kinds: "branch" (the sign-choice branch code differs but every output
+# matches), "outputs" (some output is outside the north_star tolerance).
+LAPACK_PAIR = ("LAPACK's leading eigenvector gives two structurally symmetric events "
+               "components that differ in the last ulp; the exact eigenvector (power iteration) "
+               "keeps them equal, so new1/new2 tie where the reference's do not")
+LAPACK_EIG = ("two eigenvalues within 1e-9 (a degenerate eigenspace): the component basis and "
+              "order are LAPACK's rounding, any basis is an exact eigen-decomposition")
+BLAS_ORDER = ("the single-matrix path sums np.dot(v, F) in double-double (within an ulp of "
+              "exact); the reference's OpenBLAS dgemv order rounds a tie between events apart "
+              "(replayed only in the batched path, where the sizes keep OpenBLAS single-threaded)")
+KNOWN_MISMATCH = {
+    # batched kernel == C SPEC (N <= 64, E <= 32): OpenBLAS np.dot order replayed (ob_vecmat)
+    "exact": {
+        "q_scaled_eq_min": ("branch", LAPACK_PAIR + "; the continuous fallback then picks set1 like the "
+                                                    "reference's rank rule: identical outputs"),
+    },
+    "algos_exact": {
+        "t8@big-five": ("outputs", LAPACK_EIG),
+        "t8@fixed-variance": ("outputs", LAPACK_EIG),
+    },
+    # the single-matrix pipeline FORCED onto the tiny golden cases (tests/test_matrix_gpu.py,
+    # test_algos_gpu.py); the drop-in Oracle runs every one of these shapes (<= 64 x 32) on the
+    # batched kernel above.  Its sums are double-double, not OpenBLAS's order.
+    "matrix": {
+        "t11": ("outputs", BLAS_ORDER),
+        "q_int_fill": ("outputs", BLAS_ORDER),
+        "q_int_scaled": ("branch", BLAS_ORDER),
+        "q_scaled_eq_min": ("branch", LAPACK_PAIR),
+        "m000": ("branch", BLAS_ORDER),
+        "m024": ("outputs", BLAS_ORDER),
+        "m096": ("outputs", BLAS_ORDER),
+    },
+    "algos_matrix": {
+        "t8@big-five": ("outputs", LAPACK_EIG),
+        "t8@fixed-variance": ("outputs", LAPACK_EIG),
+    },
+}
 
-    exact:  replays the reference's float order wherever it is defined by Python/numpy
-            (batched kernel, C oracle): only decisions fed by OpenBLAS/LAPACK results
-            are near ties -- the rank rule, catch of outcomes, outcome medians.
-    matrix_small: single-matrix path with N <= 8192 (medians replayed exactly, binary
-            fills from compensated sums): also binary fills at a catch threshold.
-    matrix_large: single-matrix path (exact-arithmetic medians): also fill medians.
-    """
+
+def mismatch_kind(case, ours, components=False):
+    """None, "branch" or "outputs" (with the first bad outputs)."""
+    bad, sign = compare(case, ours)
+    if bad:
+        return "outputs", bad
+    if "branch" in ours and not branch_matches(case, ours, sign):
+        return "branch", []
+    if components and int(ours["components"]) != int(case["components"]):
+        return "outputs", [("components", int(ours["components"]), int(case["components"]))]
+    return None, []
+
+
+def assert_known(path, observed, ran):
+    """observed: {case: kind} of the mismatching cases among the names in ``ran``."""
+    ran = set(ran)
+    expected = {k: v[0] for k, v in KNOWN_MISMATCH[path].items() if k in ran}
+    got = {k: v for k, v in observed.items()}
+    assert got == expected, {"new or changed": {k: v for k, v in got.items() if expected.get(k) != v},
+                             "stale (now matching)": sorted(set(expected) - set(got))}
+
+
+def is_neartie(case, path="exact"):
+    """Fixture flag: does the reference's decision on this round hinge on BLAS/LAPACK
+    rounding (make_golden.py)?  Reported in suite statistics only; pass/fail is decided
+    by KNOWN_MISMATCH."""
     f = lambda k: bool(case.get(k, False))
     nt = f("neartie_rank") or f("neartie_catch") or f("neartie_median") or f("neartie_eig")
     if path in ("matrix_small", "matrix_large"):
@@ -104,6 +161,6 @@ def branch_matches(case, ours, sign_agrees):
     """Branch codes name set1/set2 relative to the eigenvector sign; with the
     opposite sign, set1 and set2 swap roles (and so do the codes)."""
     b = int(ours["branch"])
-    if not sign_agrees:
+    if not sign_agrees and str(case.get("in_algorithm", "PCA")) == "PCA":  # other scores are sign-fixed
         b = _FLIP.get(b, b)
     return b == int(case["branch"])

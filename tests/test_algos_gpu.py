@@ -13,21 +13,18 @@ import parity as P
 pytestmark = pytest.mark.gpu
 
 
-def _check(cases, run):
-    stats = dict(n=0, neartie=0, neartie_match=0)
-    fails = []
+def _check(cases, run, path_of):
+    observed = {p: {} for p in ("algos_exact", "algos_matrix")}
+    ran = {p: [] for p in observed}
     for name, case in cases:
         ours = run(case)
-        bad, _ = P.compare(case, ours)
-        ok = not bad and int(ours["branch"]) == int(case["branch"])
-        ok = ok and int(ours["components"]) == int(case["components"])
-        stats["n"] += 1
-        if P.is_neartie(case):
-            stats["neartie"] += 1
-            stats["neartie_match"] += ok
-        elif not ok:
-            fails.append((name, int(ours["branch"]), int(case["branch"]), bad[:3]))
-    return stats, fails
+        path = path_of(case, ours)
+        ran[path].append(name)
+        kind, _ = P.mismatch_kind(case, ours, components=True)
+        if kind:
+            observed[path][name] = kind
+    for p in observed:
+        P.assert_known(p, observed[p], ran[p])
 
 
 def run_oracle(case):
@@ -40,6 +37,7 @@ def run_oracle(case):
     ours = {P.ABI_NAME[k]: v for k, v in G.flat_result(res).items() if k in P.ABI_NAME}
     ours["branch"] = np.array(o.last_info["branch"])
     ours["components"] = np.array(res["components"])
+    ours["path"] = o.last_info["path"]
     assert res["convergence"] == bool(case["convergence"])
     return ours
 
@@ -70,15 +68,11 @@ def run_matrix(case):
 @pytest.mark.parametrize("alg", ["big-five", "fixed-variance", "cokurtosis", "absolute"])
 def test_oracle_algos_golden(gpu_lib, alg):
     cases = [(n, c) for n, c in sorted(G.algos().items()) if n.endswith("@" + alg)]
-    stats, fails = _check(cases, run_oracle)
-    print(alg, stats)
-    assert not fails, fails[:4]
+    _check(cases, run_oracle, lambda case, ours: "algos_exact" if ours.pop("path") == "batched" else "algos_matrix")
 
 
 @pytest.mark.parametrize("alg", ["big-five", "fixed-variance", "cokurtosis"])
 def test_matrix_path_algos_golden(gpu_lib, alg):
     """The staged pipeline on every case of the algorithm (small ones forced through it)."""
     cases = [(n, c) for n, c in sorted(G.algos().items()) if n.endswith("@" + alg)]
-    stats, fails = _check(cases[::3], run_matrix)
-    print(alg, stats)
-    assert not fails, fails[:4]
+    _check(cases[::3], run_matrix, lambda case, ours: "algos_matrix")

@@ -36,46 +36,33 @@ def _run_gpu(case_list):
 
 
 def _score(cases, outs):
-    stats = dict(n=0, neartie=0, neartie_match=0, sign=0)
-    fails = []
+    """{name: mismatch kind} of the rounds of one launch, and the names run."""
+    observed, ran = {}, []
     for b, (name, case) in enumerate(cases):
-        ours = {k: v[b] for k, v in outs.items()}
-        bad, sign = P.compare(case, ours)
-        stats["n"] += 1
-        stats["sign"] += sign
-        ok = not bad and P.branch_matches(case, ours, sign)
-        if P.is_neartie(case):
-            stats["neartie"] += 1
-            stats["neartie_match"] += ok
-        elif not ok:
-            fails.append((name, int(ours["branch"]), int(case["branch"]), bad[:3]))
-    return stats, fails
+        ran.append(name)
+        kind, _ = P.mismatch_kind(case, {k: v[b] for k, v in outs.items()})
+        if kind:
+            observed[name] = kind
+    return observed, ran
 
 
 def test_golden_synth_50x20(gpu_lib):
     st = G.synth()
-    cases = [(b, G.unstack(st, b)) for b in range(st["branch"].shape[0])]
-    outs = _run_gpu([c for _, c in cases])
-    stats, fails = _score(cases, outs)
-    print("synth_50x20", stats)
-    assert not fails, fails[:5]
-    assert stats["neartie"] <= 0.08 * stats["n"]
+    cases = [("s%03d" % b, G.unstack(st, b)) for b in range(st["branch"].shape[0])]
+    P.assert_known("exact", *_score(cases, _run_gpu([c for _, c in cases])))
 
 
 def test_golden_kat_and_mixed(gpu_lib):
     allc = list(G.kat().items()) + list(G.mixed().items())
-    fails = []
-    tot = dict(n=0, neartie=0, neartie_match=0, sign=0)
+    observed, ran = {}, []
     for name, case in allc:
         N, E = case["in_reports"].shape
         if name in P.EXCLUDED or N > 64 or E > 32:
             continue
-        stats, f = _score([(name, case)], _run_gpu([case]))
-        fails += f
-        for k in tot:
-            tot[k] += stats[k]
-    print("kat+mixed", tot)
-    assert not fails, fails[:5]
+        o, r = _score([(name, case)], _run_gpu([case]))
+        observed.update(o)
+        ran += r
+    P.assert_known("exact", observed, ran)
 
 
 def test_bitexact_vs_c_oracle_c3(gpu_lib):

@@ -50,26 +50,16 @@ def run_c(case):
 
 
 def test_c_oracle_vs_golden():
-    stats = dict(n=0, neartie=0, neartie_match=0)
-    fails = []
+    observed, ran = {}, []
     for name, case in sorted(G.algos().items()):
         N, E = case["in_reports"].shape
         if N > 64 or E > 64:
             continue
-        ours = run_c(case)
-        bad, sign = P.compare(case, ours)
-        ok = not bad and int(ours["branch"]) == int(case["branch"])
-        ok = ok and int(ours["components"]) == int(case["components"])
-        stats["n"] += 1
-        if P.is_neartie(case):
-            stats["neartie"] += 1
-            stats["neartie_match"] += ok
-        elif not ok:
-            fails.append((name, int(ours["branch"]), int(case["branch"]), int(ours["components"]),
-                          int(case["components"]), bad[:3]))
-    print("algos C oracle", stats)
-    assert not fails, fails[:5]
-    assert stats["neartie"] <= 0.05 * stats["n"]
+        ran.append(name)
+        kind, _ = P.mismatch_kind(case, run_c(case), components=True)
+        if kind:
+            observed[name] = kind
+    P.assert_known("algos_exact", observed, ran)
 
 
 @pytest.mark.parametrize("alg", ["big-five", "fixed-variance"])
