@@ -79,8 +79,7 @@ pcx_ctx* pcx_create_rank(int device_id, int world, int rank, const pcx_comm_id* 
     }
     pcx_ctx* c = new_ctx(device_id, "pcx_create_rank");
     if (!c) return nullptr;
-    if (world == 1) return c;
-    std::string err;
+    std::string err;  // world == 1 too: a one-rank RCCL communicator (every exchange still runs)
     return with_comm(c, pcx::comm_rccl(device_id, world, rank, id, err), err);
 }
 

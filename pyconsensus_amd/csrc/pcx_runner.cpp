@@ -118,14 +118,14 @@ struct Run {
 
     // ---- exchanges
     void allreduce(void* buf, int64_t count, int dtype, int op) {
-        if (world == 1 || count <= 0) return;
+        if (!comm || count <= 0) return;
         mark(M_EXCHANGE);
         comm_rc(comm->allreduce(buf, count, dtype, op, st, err));
         mark(-1);
     }
     // dd slots [s0, s1) of every column of a [world][rows][pitch/2] dd buffer
     void gather_slots(double* buf, int64_t rows, int64_t pitch, int s0, int s1, pcx_workspace* w) {
-        if (world == 1) return;
+        if (!comm) return;
         mark(M_EXCHANGE);
         const int64_t width = (int64_t)(s1 - s0) * 2, blk = rows * pitch;
         if (width * rows > w->xcap) {
@@ -143,7 +143,7 @@ struct Run {
     }
     // whole per-rank blocks of a [world][bytes] buffer (in place)
     void gather_block(void* buf, int64_t bytes) {
-        if (world == 1) return;
+        if (!comm) return;
         mark(M_EXCHANGE);
         comm_rc(comm->allgather(static_cast<char*>(buf) + (int64_t)rank * bytes, buf, bytes, st, err));
         mark(-1);
@@ -330,13 +330,13 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
     HardArgs h{};
     h.cap = cap;
     h.send = (double*)carve(Hb * cap * 16);
-    h.recv = R.world == 1 ? h.send : (double*)carve(R.world * Hb * cap * 16);
+    h.recv = !R.comm ? h.send : (double*)carve(R.world * Hb * cap * 16);
     h.keys = (uint64_t*)carve(Hb * P_max * 16);
     h.X = (double*)carve(Hb * N * 8);
     h.W = (double*)carve(Hb * N * 8);
     h.hs = (double*)carve(Hb * 4 * 8);
     h.send_cnt = (int64_t*)carve(Hb * 8);
-    h.recv_cnt = R.world == 1 ? h.send_cnt : (int64_t*)carve(R.world * Hb * 8);
+    h.recv_cnt = !R.comm ? h.send_cnt : (int64_t*)carve(R.world * Hb * 8);
     for (int64_t b0 = 0; b0 < H; b0 += Hb) {
         h.n_hard = (int32_t)std::min<int64_t>(Hb, H - b0);
         h.cols = w->hard_cols + b0;
@@ -344,7 +344,7 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
         R.mark(M_HARD_GATHER);
         R.check_err(hard_stage(m, h, M_HARD_GATHER, R.st, R.err), "hard gather");
         R.mark(-1);
-        if (R.world > 1) {
+        if (R.comm) {
             // compact the send rows of the batch: [n_hard][cap] pairs, counts
             R.mark(M_EXCHANGE);
             R.comm_rc(R.comm->allgather(h.send, h.recv, (int64_t)h.n_hard * cap * 16, R.st, R.err));
@@ -380,7 +380,7 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
 void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
     m.sel_phase = phase;
     const int S = m.n_scaled;
-    if (R.world == 1 && m.n_rows <= SEL_EXACT_MAX) {
+    if (!R.comm && m.n_rows <= SEL_EXACT_MAX) {
         // small matrices: replay the reference's float walk directly
         if (S) R.stage(m, M_SEL_EXACT);
     } else if (S) {

@@ -125,7 +125,10 @@ class Oracle(object):
                                    device_index=self._device_index(), int_dtype=ints, **self._kw())
         if sc is not None and sc.any():
             cols = np.nonzero(sc)[0]
-            reports[:, cols] = outs["original"][:, cols].astype(data.dtype) if ints else outs["original"][:, cols]
+            val = outs["original"][:, cols].astype(data.dtype) if ints else outs["original"][:, cols]
+            if isinstance(reports, np.ma.MaskedArray):  # a masked column stays masked where NaN
+                val = np.ma.masked_array(val, np.isnan(outs["original"][:, cols]))
+            reports[:, cols] = val
         return outs["filled"].astype(data.dtype) if ints else outs["filled"]
 
     def wpca(self, reports_filled):

@@ -71,7 +71,7 @@ class RcclComm(_OwnedCtx):
         cid = _abi.CommId()
         if self.rank == 0:
             _lib.check(_lib.lib().pcx_comm_unique_id(C.byref(cid)))
-        box = [bytes(cid.internal) if self.rank == 0 else None]
+        box = [C.string_at(C.addressof(cid), C.sizeof(cid)) if self.rank == 0 else None]  # all 128 bytes
         dist.broadcast_object_list(box, src=0)
         C.memmove(C.addressof(cid), box[0], 128)
         self.device_index = int(device_index)
