@@ -13,7 +13,8 @@ import threading
 from . import _abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpcx.so")
+# PCX_LIB: load another build of the same ABI (A/B performance runs, tools/ab_build.sh)
+LIB_PATH = os.environ.get("PCX_LIB") or os.path.join(HERE, "libpcx.so")
 
 _lock = threading.Lock()
 _lib = None
