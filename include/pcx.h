@@ -242,6 +242,7 @@ typedef struct {
     int32_t components;           /* result["components"]: fixed-variance count, else -1 (:449, :610) */
     int32_t n_hard;               /* weighted medians / binary fills replayed in sequential float order */
     int32_t sel_passes;           /* weighted-selection histogram passes                 */
+    double  comm_bytes;           /* bytes this rank passed to collectives (all-reduce buffers + all-gather sends) */
 } pcx_result;
 
 /* The whole consensus (__init__.py:502-611) on this rank's rows; collective over

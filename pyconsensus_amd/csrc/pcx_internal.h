@@ -60,8 +60,9 @@ typedef struct {
     uint64_t* sel_isum;           /* [n_scaled][4] total weight limbs, count       (SUM) */
     uint64_t* sel_imin;           /* [n_scaled][2] min key, min weight bits        (MIN) */
     uint64_t* sel_imax;           /* [n_scaled][2] max key, max weight bits        (MAX) */
-    uint64_t* hist_sum;           /* [n_active][256][4] bucket weight limbs, count (SUM) */
-    uint64_t* hist_min;           /* [n_active][256][2] bucket min key, min weight (MIN) */
+    uint64_t* hist_w;             /* [n_active][256][3] bucket weight limbs (SUM; weight-mode events) */
+    uint64_t* hist_n;             /* [n_active][256] bucket element count          (SUM) */
+    uint64_t* hist_min;           /* [n_active][256] bucket min key                (MIN) */
     uint64_t* hist_max;           /* [n_active][256] bucket max key                (MAX) */
     uint64_t* sel_arg;            /* [2][n_scaled] first dominant row (MIN), its value key (MAX) */
     int32_t*  sel_act;            /* [n_scaled] active scaled events, compacted in event order */
@@ -169,7 +170,8 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st);
 hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner
 enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
-                     INFO_PICK1 = 5, INFO_HARD = 6 };
+                     INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7 };
+hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st);
 
 // pack / unpack of strided dd slot ranges for the slot exchange (runner)
 hipError_t copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch, int64_t width, int64_t rows,

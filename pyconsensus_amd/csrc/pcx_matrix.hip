@@ -52,7 +52,7 @@ enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ,
                EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP };
-enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD };
+enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -1559,12 +1559,22 @@ __device__ int64_t block_compact(int64_t n, PRED pred, EMIT emit) {
     return base_s;
 }
 
-// active events (status 1) in event order -> sel_act, count -> info[IN_SEL_ACTIVE]
+// active events (status 1) in event order -> sel_act, count -> info[IN_SEL_ACTIVE]; how many
+// of them walk weights (not counts) -> info[IN_SEL_WACTIVE] (their limb histograms are exchanged)
 __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
+    __shared__ unsigned long long nw;
+    if (threadIdx.x == 0) nw = 0;
+    __syncthreads();
     const int64_t cnt = block_compact(
         m.n_scaled, [&](int64_t s) { return m.sel_state[s * SELS + SW_STATUS] == 1; },
-        [&](int64_t s, int64_t pos) { m.sel_act[pos] = (int32_t)s; });
-    if (threadIdx.x == 0) m.info[IN_SEL_ACTIVE] = cnt;
+        [&](int64_t s, int64_t pos) {
+            m.sel_act[pos] = (int32_t)s;
+            if (m.sel_state[s * SELS + SW_MODE] == 0) atomicAdd(&nw, 1ull);
+        });
+    if (threadIdx.x == 0) {
+        m.info[IN_SEL_ACTIVE] = cnt;
+        m.info[IN_SEL_WACTIVE] = (int64_t)nw;
+    }
 }
 
 // exact weight / count histogram of the keys inside [lo, hi] (NB buckets) of active event a
@@ -1572,12 +1582,11 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     const int s = m.sel_act[a];
     const uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB], hw[NB];
+    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB];
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
         hmin[b] = ~0ull;
         hmax[b] = 0;
-        hw[b] = ~0ull;
     }
     __syncthreads();
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
@@ -1595,7 +1604,6 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             atomicAdd(&ha[b], (unsigned long long)L.l0);
             atomicAdd(&hb[b], (unsigned long long)L.l1);
             atomicAdd(&hc[b], (unsigned long long)L.l2);
-            atomicMin(&hw[b], (unsigned long long)__double_as_longlong(w));
         }
         atomicAdd(&hn[b], 1ull);
         atomicMin(&hmin[b], (unsigned long long)k);
@@ -1604,12 +1612,13 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     __syncthreads();
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
-        m.hist_sum[(o + b) * 4 + 0] = ha[b];
-        m.hist_sum[(o + b) * 4 + 1] = hb[b];
-        m.hist_sum[(o + b) * 4 + 2] = hc[b];
-        m.hist_sum[(o + b) * 4 + 3] = hn[b];
-        m.hist_min[(o + b) * 2 + 0] = hmin[b];
-        m.hist_min[(o + b) * 2 + 1] = hw[b];
+        if (wmode) {
+            m.hist_w[(o + b) * 3 + 0] = ha[b];
+            m.hist_w[(o + b) * 3 + 1] = hb[b];
+            m.hist_w[(o + b) * 3 + 2] = hc[b];
+        }
+        m.hist_n[o + b] = hn[b];
+        m.hist_min[o + b] = hmin[b];
         m.hist_max[o + b] = hmax[b];
     }
 }
@@ -1631,11 +1640,11 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
     bool has_below = st[SW_HAS_BELOW] != 0;
     const int64_t o = (int64_t)a * NB;
     for (int b = 0; b < NB; b++) {
-        const uint64_t* hs = m.hist_sum + (o + b) * 4;
-        const uint64_t n = hs[3];
+        const uint64_t n = m.hist_n[o + b];
         if (n == 0) continue;
-        const L3 hw = l3_norm({hs[0], hs[1], hs[2]});
-        const uint64_t kmin = m.hist_min[(o + b) * 2], kmax = m.hist_max[o + b];
+        const uint64_t* hs = m.hist_w + (o + b) * 3;
+        const L3 hw = wmode ? l3_norm({hs[0], hs[1], hs[2]}) : L3{0, 0, 0};
+        const uint64_t kmin = m.hist_min[o + b], kmax = m.hist_max[o + b];
         const L3 upto = l3_add(below, hw);
         const bool cross = wmode ? l3_cmp(l3_twice(upto), tot) > 0 : cbelow + n > target;
         if (cross) {
@@ -2261,6 +2270,25 @@ __global__ void __launch_bounds__(BT) k_wmean_out(pcx_mat m) {
     if (c < m.n_events) m.weighted_mean[c] = m.ev[EV_MU * m.n_events + c];
 }
 
+// lower triangle of the E x E covariance <-> packed buffer (row-major p >= q): the
+// cross-rank SUM then moves E (E + 1) / 2 doubles instead of E^2; unpack mirrors
+__global__ void __launch_bounds__(BT) k_tri_pack(double* C, double* buf, int64_t E, int unpack) {
+    const int64_t n = E * (E + 1) / 2;
+    for (int64_t t = blockIdx.x * (int64_t)BT + threadIdx.x; t < n; t += (int64_t)gridDim.x * BT) {
+        int64_t p = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+        while ((p + 1) * (p + 2) / 2 <= t) p++;
+        while (p * (p + 1) / 2 > t) p--;
+        const int64_t q = t - p * (p + 1) / 2;
+        if (unpack) {
+            const double v = buf[t];
+            C[p * E + q] = v;
+            C[q * E + p] = v;
+        } else {
+            buf[t] = C[p * E + q];
+        }
+    }
+}
+
 // strided 2-D copy (slot exchange pack / unpack)
 __global__ void __launch_bounds__(BT) k_copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch,
                                                int64_t width, int64_t rows) {
@@ -2426,6 +2454,12 @@ const char* stage_name(int k) {
         "SEL_STEP", "SEL_FINISH", "HARD_LIST", "HARD_GATHER", "HARD_PREP", "HARD_SORT", "HARD_WALK", "EXCHANGE",
         "H2D", "D2H"};
     return (k >= 0 && k < M_NSTAGE) ? names[k] : "";
+}
+
+hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st) {
+    const int64_t n = E * (E + 1) / 2;
+    hipLaunchKernelGGL(k_tri_pack, dim3(grid_rows(n, BT)), dim3(BT), 0, st, (double*)C, buf, E, unpack);
+    return hipGetLastError();
 }
 
 hipError_t copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch, int64_t width, int64_t rows,

@@ -53,7 +53,7 @@ struct pcx_workspace {
     uint32_t* rowstat;
     uint64_t* skey;
     int64_t* info;
-    uint64_t *sel_state, *sel_isum, *sel_imin, *sel_imax, *hist_sum, *hist_min, *hist_max, *sel_arg;
+    uint64_t *sel_state, *sel_isum, *sel_imin, *sel_imax, *hist_w, *hist_n, *hist_min, *hist_max, *sel_arg;
     int32_t *sel_act, *hard, *hard_cols, *hard_modes, *scols, *sidx;
     double *wcd, *tokp, *scalars, *xsend, *xrecv;
     uint32_t* rowpart;
@@ -79,6 +79,7 @@ struct Run {
     int world, rank;
     std::vector<hipEvent_t> evs;
     std::vector<int> ev_stage;
+    double comm_bytes = 0.0;
 
     void hip(hipError_t e, const char* what) {
         if (e != hipSuccess) {
@@ -120,6 +121,7 @@ struct Run {
     void allreduce(void* buf, int64_t count, int dtype, int op) {
         if (!comm || count <= 0) return;
         mark(M_EXCHANGE);
+        comm_bytes += 8.0 * (double)count;
         comm_rc(comm->allreduce(buf, count, dtype, op, st, err));
         mark(-1);
     }
@@ -133,6 +135,7 @@ struct Run {
             throw Fail{PCX_EINVAL};
         }
         hip(copy2d(w->xsend, width, buf + (int64_t)rank * blk + 2 * s0, pitch, width, rows, st), "pack");
+        comm_bytes += 8.0 * (double)(width * rows);
         comm_rc(comm->allgather(w->xsend, w->xrecv, width * rows * 8, st, err));
         for (int r = 0; r < world; r++)
             if (r != rank)
@@ -145,6 +148,7 @@ struct Run {
     void gather_block(void* buf, int64_t bytes) {
         if (!comm) return;
         mark(M_EXCHANGE);
+        comm_bytes += (double)bytes;
         comm_rc(comm->allgather(static_cast<char*>(buf) + (int64_t)rank * bytes, buf, bytes, st, err));
         mark(-1);
     }
@@ -218,8 +222,9 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->scols, (size_t)S * 4, false},
         {(void**)&w->sidx, (size_t)E * 4, false},
         {(void**)&w->scalars, (size_t)4 * 8, true},
-        {(void**)&w->hist_sum, (size_t)(S * SEL_NB * 4) * 8, false},
-        {(void**)&w->hist_min, (size_t)(S * SEL_NB * 2) * 8, false},
+        {(void**)&w->hist_w, (size_t)(S * SEL_NB * 3) * 8, false},
+        {(void**)&w->hist_n, (size_t)(S * SEL_NB) * 8, false},
+        {(void**)&w->hist_min, (size_t)(S * SEL_NB) * 8, false},
         {(void**)&w->hist_max, (size_t)(S * SEL_NB) * 8, false},
         {(void**)&w->xsend, (size_t)w->xcap * 8, false},
         {(void**)&w->xrecv, (size_t)(w->xcap * world) * 8, false},
@@ -347,6 +352,7 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
         if (R.comm) {
             // compact the send rows of the batch: [n_hard][cap] pairs, counts
             R.mark(M_EXCHANGE);
+            R.comm_bytes += (double)h.n_hard * (double)(cap * 16 + 8);
             R.comm_rc(R.comm->allgather(h.send, h.recv, (int64_t)h.n_hard * cap * 16, R.st, R.err));
             R.comm_rc(R.comm->allgather(h.send_cnt, h.recv_cnt, (int64_t)h.n_hard * 8, R.st, R.err));
             R.mark(-1);
@@ -390,11 +396,11 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         R.allreduce(w->sel_imax, (int64_t)S * 2, PCX_U64, PCX_MAX);
         R.stage(m, M_SEL_START);
         R.stage(m, M_SEL_COMPACT);
-        int64_t inf2[2];
-        R.hip(hipMemcpyAsync(inf2, m.info + INFO_SEL_ACTIVE, 16, hipMemcpyDeviceToHost, R.st), "D2H");
+        int64_t inf5[5];  // active, argmax, (pick1), (hard), weight-mode active
+        R.hip(hipMemcpyAsync(inf5, m.info + INFO_SEL_ACTIVE, sizeof(inf5), hipMemcpyDeviceToHost, R.st), "D2H");
         R.sync();
-        int64_t active = inf2[0];
-        if (inf2[1] > 0) {  // dominant weights: the first row holding the max weight (all ranks)
+        int64_t active = inf5[0], wactive = inf5[4];
+        if (inf5[1] > 0) {  // dominant weights: the first row holding the max weight (all ranks)
             R.stage(m, M_SEL_ARGMAX);
             R.allreduce(w->sel_arg, S, PCX_U64, PCX_MIN);
             R.stage(m, M_SEL_VALUE);
@@ -410,14 +416,19 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
             R.mark(M_SEL_HIST);
             R.check_err(sel_hist(m, (int)active, R.st), "k_sel_hist");
             R.mark(-1);
-            R.allreduce(w->hist_sum, active * SEL_NB * 4, PCX_U64, PCX_SUM);
-            R.allreduce(w->hist_min, active * SEL_NB * 2, PCX_U64, PCX_MIN);
+            // exact integers: order-independent reductions (limbs only when some event walks weights)
+            if (wactive > 0) R.allreduce(w->hist_w, active * SEL_NB * 3, PCX_U64, PCX_SUM);
+            R.allreduce(w->hist_n, active * SEL_NB, PCX_U64, PCX_SUM);
+            R.allreduce(w->hist_min, active * SEL_NB, PCX_U64, PCX_MIN);
             R.allreduce(w->hist_max, active * SEL_NB, PCX_U64, PCX_MAX);
             R.mark(M_SEL_STEP);
             R.check_err(sel_step(m, (int)active, R.st), "k_sel_step");
             R.mark(-1);
             R.stage(m, M_SEL_COMPACT);
-            active = R.read(m.info + INFO_SEL_ACTIVE);
+            R.hip(hipMemcpyAsync(inf5, m.info + INFO_SEL_ACTIVE, sizeof(inf5), hipMemcpyDeviceToHost, R.st), "D2H");
+            R.sync();
+            active = inf5[0];
+            wactive = inf5[4];
             passes++;
         }
         res->sel_passes += passes;
@@ -608,7 +619,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.sel_isum = w->sel_isum;
         m.sel_imin = w->sel_imin;
         m.sel_imax = w->sel_imax;
-        m.hist_sum = w->hist_sum;
+        m.hist_w = w->hist_w;
+        m.hist_n = w->hist_n;
         m.hist_min = w->hist_min;
         m.hist_max = w->hist_max;
         m.sel_arg = w->sel_arg;
@@ -651,7 +663,11 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 R.stage(m, M_WCD);
                 R.stage(m, M_COV);
                 R.stage(m, M_COV_REDUCE);
-                R.allreduce(w->C, E * E, PCX_F64, PCX_SUM);
+                if (R.comm) {  // the partial covariance: one SUM of its lower triangle (cslab is free now)
+                    R.hip(tri_pack(w->C, w->cslab, E, 0, R.st), "tri pack");
+                    R.allreduce(w->cslab, E * (E + 1) / 2, PCX_F64, PCX_SUM);
+                    R.hip(tri_pack(w->C, w->cslab, E, 1, R.st), "tri unpack");
+                }
                 R.stage(m, M_COV_FINISH);
                 R.stage(m, M_POWER);
                 flags = R.read(m.info + INFO_FLAGS);
@@ -724,6 +740,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         r->pi_iters = (int32_t)info[INFO_PI_ITERS];
         r->flags = (int32_t)info[INFO_FLAGS];
         r->components = m.components;
+        r->comm_bytes = R.comm_bytes;
         // per-stage device time
         if (c->profile && !R.evs.empty()) {
             for (int k = 0; k < PCX_NSTAGES; k++) c->stage_ms[k] = 0.0;

@@ -288,7 +288,8 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
 def _meta(res, algorithm):
     return {"participation": res.participation, "avg_certainty": res.avg_certainty,
             "branch": int(res.branch), "pi_iters": int(res.pi_iters), "flags": int(res.flags),
-            "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes)}
+            "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes),
+            "comm_bytes": float(res.comm_bytes)}
 
 
 # ---------------------------------------------------------------- host-memory entry points
