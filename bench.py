@@ -28,11 +28,33 @@ SEED = 20261015
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def round_bytes(N, E):
-    """Algorithmic HBM bytes per round: inputs read once, outputs written once."""
+def round_bytes(N, E, matrices=True):
+    """Algorithmic HBM bytes per round: inputs read once, outputs written once (the whole
+    result dict of __init__.py:583-611, including the N x E "original" and "filled")."""
     reads = 8 * N * E + 8 * N + E * (1 + 8 + 8)          # reports, reputation, scaled/lo/hi
     writes = 8 * N * 8 + 8 * E * 9 + 8 * 2 + 4 * 3       # 8 N-vectors, 9 E-vectors, 2 f64 + 3 i32 scalars
+    if matrices:
+        writes += 2 * 8 * N * E                           # result["original"], result["filled"]
     return reads + writes
+
+
+def host_threads():
+    """The host cores this job may use: the box's share (OMP_NUM_THREADS, 16 per GPU on the
+    pool) when set, else every CPU."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return max(1, os.cpu_count() or 1)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(seconds=12.0):
@@ -41,7 +63,7 @@ def cpu_baseline(seconds=12.0):
     from oracle import pcx_oracle_c as OC
     from pyconsensus_amd import synthetic
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_threads()
     R, sc, lo, hi, rep = synthetic.rounds(4096, N_REP, N_EV, seed=SEED)
     OC.batched(R[:256], sc[:256], lo[:256], hi[:256], rep[:256], threads=threads)  # warm
     done, t0 = 0, time.perf_counter()
@@ -51,7 +73,8 @@ def cpu_baseline(seconds=12.0):
     el = time.perf_counter() - t0
     out = {"value": done / el, "unit": "rounds/s", "cores": threads, "kind": "port",
            "sample": "%d rounds of the C3 workload (50x20, seed %d) in %.1f s, C oracle, %d OpenMP threads"
-                     % (done, SEED, el, threads)}
+                     % (done, SEED, el, threads),
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
     # the numpy restatement (same per-round structure as the reference) for context
     from oracle.pcx_oracle import OracleCPU
     bl = synthetic.bounds_list
@@ -85,7 +108,7 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
 
     def run(profile=None):
         return consensus_matrix(R, None, sc, lo, hi, comm=comm, n_total=N, row_offset=off, device=dev,
-                                profile=profile)
+                                profile=profile, matrices=True)
 
     for _ in range(warmup):
         run()
@@ -108,7 +131,7 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     cov_flops_rank = float(cnt) * E * (E + 1)  # one MAC per unique (j, k<=j) pair per row
     tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms else None
     del R
-    return {"metric": "1M x 4k consensus latency", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
+    return {"metric": "1M x 4k consensus latency (every output, original and filled included)", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
             "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
             "branch": meta["branch"], "pi_iters": meta["pi_iters"], "flags": meta["flags"],
             "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
@@ -119,15 +142,67 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
                     "reputation=None"}
 
 
-def load_traffic(kernel="batched_round_kernel"):
-    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, tools/gpu_profile.sh), or None."""
+def bench_c4(dev, steps=3, oracle=True):
+    """Config C4: one 100k x 1k matrix (seed 2, integer reputations),
+    device-resident consensus latency; the host->device copy of the reports timed apart; the
+    numpy restatement (the reference's algorithm, OpenBLAS on the host cores) timed beside it on
+    the same inputs, and the largest relative difference of smooth_rep against it."""
+    import numpy as np
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.pipeline import consensus_matrix
+
+    R, sc, lo, hi, rep = synthetic.matrix(100_000, 1000, seed=2)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    Rd = torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize(dev)
+    h2d = time.perf_counter() - t0
+    args = (Rd, torch.from_numpy(rep).to(dev), torch.from_numpy(sc.astype(np.uint8)).to(dev),
+            torch.from_numpy(lo).to(dev), torch.from_numpy(hi).to(dev))
+    consensus_matrix(*args, device=dev, matrices=True)  # warm (workspace)
+    times = []
+    for _ in range(steps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev, ag, meta = consensus_matrix(*args, device=dev, matrices=True)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    out = {"metric": "100k x 1k consensus latency", "latency_ms": 1e3 * sorted(times)[len(times) // 2],
+           "h2d_ms": 1e3 * h2d, "h2d_gbs": R.nbytes / h2d / 1e9, "branch": meta["branch"],
+           "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"],
+           "data": "synthetic (SURVEY.md 8(d), seed 2, integer reputations U[1,99])"}
+    smooth = ag["smooth_rep"].cpu().numpy()
+    del Rd, args, ev, ag
+    torch.cuda.empty_cache()
+    if oracle:
+        from oracle.pcx_oracle import OracleCPU
+
+        t0 = time.perf_counter()
+        ref = OracleCPU(reports=R, event_bounds=synthetic.bounds_list(sc, lo, hi), reputation=rep).consensus()
+        el = time.perf_counter() - t0
+        rs = np.asarray(ref["agents"]["smooth_rep"], dtype=float)
+        out["cpu_baseline"] = {"value": el * 1e3, "unit": "ms", "kind": "port", "cores": host_threads(),
+                               "sample": "the whole C4 consensus, numpy restatement (oracle/pcx_oracle.py)",
+                               "cpu_model": cpu_model()}
+        out["smooth_rep_max_rel_diff"] = float(np.max(np.abs(smooth - rs) / np.maximum(np.abs(rs), 1e-300)))
+    return out
+
+
+def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
+    """Per-launch PMC figure of `kernel` (HBM bytes, VALU instructions) from the committed
+    rocprofv3 passes (profiles/pmc_traffic.json, tools/gpu_profile.sh), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
-        return d.get(kernel, {}).get("bytes_per_launch")
+        return d.get(kernel, {}).get(key)
     except Exception:
         return None
+
+
+VALU_ISSUE_CYCLES = 4      # a wave64 VALU instruction holds its SIMD 4 cycles
+SIMDS, CLOCK_GHZ = 1024, 2.4
 
 
 def main():
@@ -138,6 +213,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=ROUNDS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c5-steps", type=int, default=3, help="timed 1M x 4k consensus runs (0 = skip)")
+    ap.add_argument("--no-c4", dest="c4", action="store_false", help="skip the 100k x 1k (C4) entry")
     args = ap.parse_args()
 
     import torch
@@ -170,12 +246,20 @@ def main():
     Rd, scd, lod, hid, repd = t(R), t(sc, torch.uint8), t(lo), t(hi), t(rep)
     del R
 
-    def step():
-        return consensus_batched(Rd, repd, scd, lod, hid, device=dev)
+    def step(matrices=True):  # the whole result dict, "original" and "filled" included
+        return consensus_batched(Rd, repd, scd, lod, hid, device=dev, filled=matrices, original=matrices)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    # the vector outputs only (no N x E matrices), for reference
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(torch.cuda.current_stream(dev))
+    for _ in range(5):
+        step(False)
+    e1.record(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize(dev)
+    vec_ms = e0.elapsed_time(e1) / 5
 
     def barrier():
         if world > 1:
@@ -209,6 +293,8 @@ def main():
         bpl = round_bytes(N_REP, N_EV) * B
         achieved = bpl / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic()
+        valu = load_traffic(key="insts_valu_per_launch")
+        valu_ms = valu * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_GHZ * 1e9) * 1e3 if valu else None
         line = {
             "metric": "oracle rounds/sec (batched 50x20, 1 GPU)",
             "value": value,
@@ -224,27 +310,39 @@ def main():
             "data": ("synthetic (SURVEY.md 8(d) generator: 10%% NaN, 25%% scaled events, 70/30 honest/liar, "
                      "integer reputation; seed %d + rank)") % SEED,
             "config": {"workload": "C3: %d independent 50x20 oracle rounds per GPU per step (one wavefront "
-                                   "per round), inputs resident in HBM" % B,
+                                   "per round), inputs resident in HBM, every output of the result dict "
+                                   "written (original and filled included)" % B,
                        "rounds_per_gpu": B, "reporters": N_REP, "events": N_EV,
                        "parallelism": "rounds sharded across %d GPU(s), no collective" % world},
             "roofline": {"bound": "hbm", "kernel": "batched_round_kernel", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bpl,
-                         "limiter": ("latency / VALU issue, not HBM: one wave64 per LDS-resident round, "
-                                     "10 rounds per CU, SQ VALU busy ~55% "
-                                     "(profiles/r1/sq_counters_batched_pass*.csv, DESIGN.md 5)")},
+                         "limiter": ("latency / instruction issue, not HBM: one wave64 per LDS-resident "
+                                     "round, 10 rounds per CU (DESIGN.md 5)"),
+                         "valu": {"insts_per_launch": valu, "issue_ms": valu_ms,
+                                  "frac": (valu_ms / kern_ms) if valu_ms else None,
+                                  "note": "VALU issue time of the launch's instructions (SQ_INSTS_VALU, "
+                                          "profiles/pmc_traffic.json) at 4 cycles each on 1024 SIMDs at "
+                                          "2.4 GHz, over the kernel time"}},
+            "vectors_only_kernel_ms": vec_ms,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
     del Rd, out
     torch.cuda.empty_cache()
-    c5 = None
+    c5 = c4 = None
     if args.c5_steps > 0:
         c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
+    if args.c4 and world == 1:
+        c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)
     if rank == 0:
         if c5 is not None:
             line["c5"] = c5
+        if c4 is not None:
+            line["c4"] = c4
+        if c4 is not None and c5 is not None:  # pageable host->device rate measured on C4's reports
+            c5["h2d_ms_estimate"] = 8.0 * c5["rows_per_gpu"] * c5["events"] / (c4["h2d_gbs"] * 1e9) * 1e3
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

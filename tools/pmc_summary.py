@@ -3,6 +3,7 @@
     python tools/pmc_summary.py --stats DIR/kt_kernel_stats.csv --fetch DIR/pmc_counter_collection.csv \
         --write DIR2/pmc_counter_collection.csv --out profiles/pmc_traffic.json
 
+SQ_INSTS_VALU (optional, its own pass) is the launch's wave-level VALU instruction count.
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced streaming read, so
 bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  Each counter comes from its own
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
+    ap.add_argument("--valu", help="pmc_counter_collection.csv of an SQ_INSTS_VALU pass")
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
     a = ap.parse_args()
@@ -51,6 +53,9 @@ def main():
         res[k] = {"fetch_size_kib": fk, "write_size_kib": wk,
                   "bytes_per_launch": (2 * fk * 1024 if fk is not None else 0) + (wk * 1024 if wk is not None else 0),
                   "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves wide reads)"}
+    if a.valu:
+        for k, v in per_kernel(a.valu, "SQ_INSTS_VALU").items():
+            res.setdefault(k, {})["insts_valu_per_launch"] = v
     if a.stats:
         for r in csv.DictReader(open(a.stats)):
             if not ours(r["Name"]):
