@@ -128,8 +128,17 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
         times.append(el)
     prof = {k: v / steps for k, v in prof.items()}
     cov_ms = prof.get("M_COV", float("nan"))
-    cov_flops_rank = float(cnt) * E * (E + 1)  # one MAC per unique (j, k<=j) pair per row
-    tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms else None
+    i8_ms = prof.get("M_COV_I8", float("nan"))
+    # unique (j, k<=j) covariance pairs: those with a general event on fp64 MFMA (k_syrk),
+    # the grid-grid pairs on int8 MFMA (k_syrk_i8); one multiply-add per pair per row
+    ng = meta["grid_events"]
+    G = E - ng
+    fp_pairs = G * (G + 1) // 2 + G * ng
+    i8_pairs = ng * (ng + 1) // 2
+    cov_flops_rank = 2.0 * cnt * fp_pairs
+    i8_ops_rank = 2.0 * cnt * i8_pairs
+    tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms and fp_pairs else None
+    tops = i8_ops_rank / (i8_ms * 1e-3) / 1e12 if i8_ms == i8_ms and i8_pairs else None
     del R
     return {"metric": "1M x 4k consensus latency (every output, original and filled included)", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
             "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
@@ -137,7 +146,12 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
             "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
             "roofline_cov": {"bound": "mfma", "kernel": "k_syrk", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
                              "unit": "TFLOP/s", "frac": (tfs / FP64_MFMA_PEAK_TFS) if tfs else None,
-                             "flops_per_launch": cov_flops_rank, "traffic": load_traffic("k_syrk")},
+                             "flops_per_launch": cov_flops_rank, "traffic": load_traffic("k_syrk"),
+                             "pairs": "fp64: pairs with a general event (%d general, %d grid events)" % (G, ng)},
+            "roofline_cov_i8": {"bound": "mfma", "kernel": "k_syrk_i8", "achieved": tops, "peak": I8_MFMA_PEAK_TOPS,
+                                "unit": "TOP/s", "frac": (tops / I8_MFMA_PEAK_TOPS) if tops else None,
+                                "ops_per_launch": i8_ops_rank, "traffic": load_traffic("k_syrk_i8")},
+            "grid_events": ng,
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}
 
@@ -201,6 +215,7 @@ def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
         return None
 
 
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 VALU_ISSUE_CYCLES = 4      # a wave64 VALU instruction holds its SIMD 4 cycles
 SIMDS, CLOCK_GHZ = 1024, 2.4
 

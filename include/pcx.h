@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 5
+#define PCX_ABI_VERSION 6
 
 enum pcx_status {
     PCX_OK = 0,
@@ -243,6 +243,8 @@ typedef struct {
     int32_t n_hard;               /* weighted medians / binary fills replayed in sequential float order */
     int32_t sel_passes;           /* weighted-selection histogram passes                 */
     double  comm_bytes;           /* bytes this rank passed to collectives (all-reduce buffers + all-gather sends) */
+    int32_t grid_events;          /* events whose covariance block ran on int8 MFMA (binary, filled values on {1, 1.5, 2}) */
+    int32_t reserved;
 } pcx_result;
 
 /* The whole consensus (__init__.py:502-611) on this rank's rows; collective over

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
@@ -110,4 +110,5 @@ class Result(C.Structure):
     _fields_ = [(n, _vp) for n in RESULT_VECTORS] + [
         ("participation", C.c_double), ("avg_certainty", C.c_double),
         ("branch", C.c_int32), ("flags", C.c_int32), ("pi_iters", C.c_int32), ("components", C.c_int32),
-        ("n_hard", C.c_int32), ("sel_passes", C.c_int32), ("comm_bytes", C.c_double)]
+        ("n_hard", C.c_int32), ("sel_passes", C.c_int32), ("comm_bytes", C.c_double),
+        ("grid_events", C.c_int32), ("reserved", C.c_int32)]

@@ -83,6 +83,18 @@ typedef struct {
     int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
     int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
     uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
+    /* wcd column order (M_COV_PLAN): general events first, then the grid events (binary,
+       every filled value in {1, 1.5, 2}), each group in event order; the pure-grid tiles
+       of the covariance run on int8 MFMA over z = 2 (F - 1) */
+    int32_t* cov_perm;            /* [wcd_ld] event at each wcd position, -1 past E                 */
+    int32_t* cov_pos;             /* [E] wcd position of each event                                 */
+    int8_t*  zA;                  /* [wcd_rows/16][zq][16] tok * z of the pure-grid positions        */
+    int8_t*  zB;                  /* [wcd_rows/16][zq][16] z                                        */
+    int64_t* zsum;                /* [E] sum over this rank's rows of tok * z (grid events, exact)   */
+    int64_t  zq;                  /* pure-grid positions: wcd_ld - 128 * cov_jb                      */
+    int32_t  cov_jb;              /* first pure-grid 128-column tile (= wcd_ld / 128: none)          */
+    int32_t  cov_fp_tiles;        /* fp64 tiles (the trapezoid J < cov_jb of the lower triangle)     */
+    int32_t  cov_i8_tiles;        /* int8 tiles (the lower triangle of the tiles >= cov_jb)          */
     /* algorithms other than PCA (enum pcx_algorithm) */
     int32_t max_components;       /* "big-five" component count                                     */
     int32_t components;           /* out ("fixed-variance"): components used, else -1               */
@@ -134,7 +146,7 @@ enum mat_stage_id {
     M_AGENTS, M_MATRICES, M_WCD, M_EIG, M_ZERO_LOADING, M_NC_OUT, M_WMEAN_OUT,
     M_SEL_EXACT, M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_VALUE_FINISH, M_SEL_COMPACT,
     M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH, M_HARD_LIST, M_HARD_GATHER, M_HARD_PREP, M_HARD_SORT, M_HARD_WALK,
-    M_EXCHANGE, M_H2D, M_D2H, M_NSTAGE
+    M_EXCHANGE, M_H2D, M_D2H, M_COV_PLAN, M_COV_I8, M_NSTAGE
 };
 static_assert(M_NSTAGE <= PCX_NSTAGES, "stage table");
 const char* stage_name(int k);
@@ -170,7 +182,7 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st);
 hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner
 enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
-                     INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7 };
+                     INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7, INFO_COV_GENERAL = 8 };
 hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st);
 
 // pack / unpack of strided dd slot ranges for the slot exchange (runner)

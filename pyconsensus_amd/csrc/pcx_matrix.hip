@@ -47,12 +47,14 @@ constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
 constexpr int SELS = 24;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
+constexpr int CM = 8;            // doubles per column in mpart / cmax
 
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
                EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
-enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP };
-enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE };
+enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK };
+enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
+                 IN_COV_GENERAL };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -156,6 +158,7 @@ __global__ void __launch_bounds__(1024) k_rep_total(pcx_mat m) {
 __global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
     __shared__ dd lds[8];
     acc2 at, ar;
+    double big = 0.0;  // tokens outside [0, 63]: the int8 covariance path needs tok * z <= 126
     const double tot = m.rep_raw ? m.pvec[0] : 0.0;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         const double r = m.rep_raw ? m.rep_raw[m.row_offset + i] / tot : 1.0 / (double)m.n_total;
@@ -164,21 +167,24 @@ __global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
         m.tok[i] = t;
         at.add(t);
         ar.add(r);
+        big += (t >= 0.0 && t <= 63.0) ? 0.0 : 1.0;
     }
     dd st = block_sum_dd<BT>(at.get(), lds);
     dd sr = block_sum_dd<BT>(ar.get(), lds);
+    dd sb = block_sum_dd<BT>(dd{big, 0.0}, lds);
     if (threadIdx.x == 0) {
         st_dd(m.spart + blockIdx.x * 8 + 0, st);
         st_dd(m.spart + blockIdx.x * 8 + 2, sr);
+        st_dd(m.spart + blockIdx.x * 8 + 4, sb);
     }
 }
 
-// reduce spart[nblk][4 dd] into scal[rank][slot0 .. slot0+k)
-__global__ void __launch_bounds__(64) k_spart_finish(pcx_mat m, int nblk, int k, int slot0) {
+// reduce spart[nblk][4 dd] slots src0 .. src0+k into scal[rank][slot0 .. slot0+k)
+__global__ void __launch_bounds__(64) k_spart_finish(pcx_mat m, int nblk, int k, int slot0, int src0 = 0) {
     const int j = threadIdx.x;
     if (j >= k) return;
     dd r{0.0, 0.0};
-    for (int b = 0; b < nblk; b++) r = dd_add(r, ld_dd(m.spart + b * 8 + 2 * j));
+    for (int b = 0; b < nblk; b++) r = dd_add(r, ld_dd(m.spart + b * 8 + 2 * (src0 + j)));
     st_dd(m.scal + ((int64_t)m.rank * SS + slot0 + j) * 2, r);
 }
 
@@ -245,6 +251,7 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     row_range(m, r0, r1, 16);
     acc2 sr, srx;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+    bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
     rows_unrolled<16>(
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
         [&](int64_t i, XW v) {
@@ -264,17 +271,19 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             }
             mn_x = fmin(mn_x, x);
             mx_x = fmax(mx_x, x);
+            offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);
         });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, {cnt, 0.0});
     st_dd(pp + 2, sr.get());
     st_dd(pp + 4, srx.get());
     st_dd(pp + 6, {nz, 0.0});
-    double* mp = m.mpart + ((int64_t)blockIdx.y * E + c) * 4;
+    double* mp = m.mpart + ((int64_t)blockIdx.y * E + c) * CM;
     mp[0] = mx;
     mp[1] = arg;
     mp[2] = mn_x;
     mp[3] = mx_x;
+    mp[4] = offgrid ? 1.0 : 0.0;
 }
 
 // reduce part[G][E][k] over G (in order) into cstat[rank][E][base + k]; optional max partials
@@ -288,21 +297,23 @@ __global__ void __launch_bounds__(BT) k_col_finish(pcx_mat m, int G, int k, int 
         st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + base + j) * 2, r);
     }
     if (with_max) {
-        double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+        double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf(), og = 0.0;
         for (int g = 0; g < G; g++) {
-            const double* mp = m.mpart + ((int64_t)g * E + c) * 4;
+            const double* mp = m.mpart + ((int64_t)g * E + c) * CM;
             if (mp[0] > mx) {
                 mx = mp[0];
                 arg = mp[1];
             }
             mn_x = fmin(mn_x, mp[2]);
             mx_x = fmax(mx_x, mp[3]);
+            og = fmax(og, mp[4]);
         }
-        double* o = m.cmax + ((int64_t)m.rank * E + c) * 4;
+        double* o = m.cmax + ((int64_t)m.rank * E + c) * CM;
         o[0] = mx;
         o[1] = arg;
         o[2] = mn_x;
         o[3] = mx_x;
+        o[4] = og;
     }
 }
 
@@ -325,8 +336,8 @@ __global__ void __launch_bounds__(BT) k_guess(pcx_mat m) {
     const double miss = (double)m.n_total - present;
     double mn_x = __builtin_inf(), mx_x = -__builtin_inf();
     for (int w = 0; w < m.world; w++) {
-        mn_x = fmin(mn_x, m.cmax[((int64_t)w * E + c) * 4 + 2]);
-        mx_x = fmax(mx_x, m.cmax[((int64_t)w * E + c) * 4 + 3]);
+        mn_x = fmin(mn_x, m.cmax[((int64_t)w * E + c) * CM + 2]);
+        mx_x = fmax(mx_x, m.cmax[((int64_t)w * E + c) * CM + 3]);
     }
     m.ev[EV_MINX * E + c] = mn_x;
     m.ev[EV_MAXX * E + c] = mx_x;
@@ -436,69 +447,169 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
 }
 
 // ---------------------------------------------------------------- covariance operands
-// PCX_M_COV step 1: wcd = F - mu (:317-322) materialised once, [wcd_rows][wcd_ld] with
-// zero padding, plus the tokens zero-padded past n_rows.  The SYRK then streams plain
-// rows (every element is re-read by nb/2 tiles; the transform runs once).
-constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread, 16-byte accesses)
+// PCX_M_COV_PLAN: the wcd column order.  A "grid" event is binary with every filled value
+// in {1, 1.5, 2} (present reports on the grid -- k_colstats -- and a fill, if any, on it),
+// while every token lies in [0, 63] (so tok * z fits int8).  General events take the
+// first wcd positions, grid events the rest, each group in event order; the covariance
+// tiles made only of grid positions run on int8 MFMA over z = 2 (F - 1) in {0, 1, 2}:
+//   sum_i tok_i (F_ij - mu_j)(F_ik - mu_k) = c_j c_k T + (c_j Z_k + c_k Z_j) / 2 + P_jk / 4
+// with c = 1 - mu, T = sum tok, Z_j = sum tok z_ij, P_jk = sum tok z_ij z_ik (exact integers).
+__device__ __forceinline__ bool grid_event(const pcx_mat& m, int c, bool big) {
+    const int64_t E = m.n_events;
+    if (big || (m.scaled && m.scaled[c])) return false;
+    for (int w = 0; w < m.world; w++)
+        if (m.cmax[((int64_t)w * E + c) * CM + 4] != 0.0) return false;
+    const double g = m.ev[EV_GUESS * E + c];
+    return m.ev[EV_MISS * E + c] == 0.0 || g == 1.0 || g == 1.5 || g == 2.0;
+}
 
-// Blocks own a contiguous row range of a 512-column block; each wave also counts the
-// NaN / zero rescaled reports of its 128 columns per row (ballots), the block folds its
-// four waves in LDS and writes the counts of 64 rows at a time to rowpart[column block]
-// (k_scores adds the column blocks up: rowstat for na_row / participation, :549-567).
+__global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
+    __shared__ int wg[16], wb[16];
+    __shared__ int base[2];
+    const int E = (int)m.n_events;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool big = dd_to_double(scl(m, SC_BIGTOK)) > 0.0;
+    int ng = 0;
+    for (int c = tid; c < E; c += 1024) ng += grid_event(m, c, big) ? 0 : 1;
+    for (int s = 32; s >= 1; s >>= 1) ng += __shfl_xor(ng, s, WAVE);
+    if (lane == 0) wg[wv] = ng;
+    __syncthreads();
+    if (tid == 0) {
+        int G = 0;
+        for (int w = 0; w < 16; w++) G += wg[w];
+        base[0] = 0;
+        base[1] = G;
+        m.info[IN_COV_GENERAL] = G;
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int c0 = 0; c0 < E; c0 += 1024) {
+        const int c = c0 + tid;
+        const bool valid = c < E;
+        const bool gr = valid && grid_event(m, c, big);
+        const uint64_t bg = __ballot(valid && !gr), bb = __ballot(gr);
+        if (lane == 0) {
+            wg[wv] = __popcll(bg);
+            wb[wv] = __popcll(bb);
+        }
+        __syncthreads();
+        int pg = base[0], pb = base[1];
+        for (int w = 0; w < wv; w++) {
+            pg += wg[w];
+            pb += wb[w];
+        }
+        if (valid) {
+            const int pos = gr ? pb + __popcll(bb & lt) : pg + __popcll(bg & lt);
+            m.cov_perm[pos] = c;
+            m.cov_pos[c] = pos;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 0; w < 16; w++) {
+                base[0] += wg[w];
+                base[1] += wb[w];
+            }
+        }
+        __syncthreads();
+    }
+    for (int64_t p = E + tid; p < m.wcd_ld; p += 1024) m.cov_perm[p] = -1;
+}
+
+// PCX_M_WCD: wcd = F - mu (:317-322) materialised once, [wcd_rows][wcd_ld] in the
+// M_COV_PLAN column order with zero padding, plus the tokens zero-padded past n_rows, and
+// for the pure-grid positions (>= 128 cov_jb) the int8 operands tok * z (zA) and z (zB) in
+// 16-row interleaved column-major blocks [row / 16][position][16] -- one 16-byte MFMA
+// fragment per (position, 16 rows) -- and Z_j = sum tok z_ij (zsum, exact).
+constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread)
+
+// Blocks own a contiguous row range (a multiple of 64 rows) of a 512-event block; each
+// wave also counts the NaN / zero rescaled reports of its 128 events per row (ballots),
+// the block folds its four waves in LDS and writes the counts of 64 rows at a time to
+// rowpart[column block] (k_scores adds the column blocks up: rowstat for na_row /
+// participation, :549-567).
 __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     __shared__ uint32_t cnt[4][64][2];
     const int E = (int)m.n_events;
     const int64_t ld = m.wcd_ld;
     const int c0 = blockIdx.y * WCD_COLS + 2 * threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t gb = (int64_t)m.cov_jb * CT;
     ColParam p[2];
-    bool ok[2];
+    bool ok[2], zc[2];
+    int64_t pos[2];
     for (int k = 0; k < 2; k++) {
-        ok[k] = c0 + k < E;
-        p[k] = ok[k] ? col_param(m, c0 + k, true) : ColParam{false, 0.0, 1.0, 0.0, 0.0};
+        const int c = c0 + k;
+        ok[k] = c < E;
+        p[k] = ok[k] ? col_param(m, c, true) : ColParam{false, 0.0, 1.0, 0.0, 0.0};
+        pos[k] = ok[k] ? m.cov_pos[c] : (c < ld ? c : -1);  // padding positions keep their index
+        zc[k] = ok[k] && pos[k] >= gb;
     }
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
         m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
-    const int64_t per = (m.wcd_rows + gridDim.x - 1) / gridDim.x;
-    const int64_t r0 = blockIdx.x * per, r1 = r0 + per < m.wcd_rows ? r0 + per : m.wcd_rows;
-    const bool in = c0 < ld;
+    const int64_t per = ((m.wcd_rows + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;
+    int64_t r0 = blockIdx.x * per;
+    r0 = r0 < m.wcd_rows ? r0 : m.wcd_rows;
+    const int64_t r1 = r0 + per < m.wcd_rows ? r0 + per : m.wcd_rows;
     uint32_t* part = m.rowpart + (int64_t)blockIdx.y * m.wcd_rows * 2;
+    int64_t zs[2] = {0, 0};
     for (int64_t g0 = r0; g0 < r1; g0 += 64) {
-        const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;
-        for (int u0 = 0; u0 < gn; u0 += 4) {
-            double rv[4][2];
+        const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;  // a multiple of 16 (wcd_rows % 16 == 0)
+        for (int q0 = 0; q0 < gn; q0 += 16) {
+            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int64_t i = g0 + u0 + u;
-                const bool live = u0 + u < gn && i < m.n_rows;
-                const double* r = m.reports + (live ? i : 0) * E + c0;
-                rv[u][0] = (live && ok[0]) ? r[0] : 0.0;
-                rv[u][1] = (live && ok[1]) ? r[1] : 0.0;
-            }
+            for (int h = 0; h < 4; h++) {
+                double rv[4][2];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (u0 + u >= gn) break;
-                const int64_t i = g0 + u0 + u;
-                const bool live = i < m.n_rows;
-                double w[2] = {0.0, 0.0};
-                int nn = 0, nz = 0;
-                for (int k = 0; k < 2; k++) {
-                    if (live && ok[k]) {
-                        const double x = rescale(rv[u][k], p[k], m.int_dtype);
-                        nn += __builtin_isnan(x) ? 1 : 0;
-                        nz += x == 0.0 ? 1 : 0;
-                        w[k] = (missing(x) ? p[k].guess : x) - p[k].mu;
+                for (int u = 0; u < 4; u++) {
+                    const int64_t i = g0 + q0 + 4 * h + u;
+                    const bool live = i < m.n_rows;
+                    const double* r = m.reports + (live ? i : 0) * E + c0;
+                    rv[u][0] = (live && ok[0]) ? r[0] : 0.0;
+                    rv[u][1] = (live && ok[1]) ? r[1] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t i = g0 + q0 + 4 * h + u;
+                    const bool live = i < m.n_rows;
+                    const int tk = (live && (zc[0] || zc[1])) ? (int)m.tok[i] : 0;
+                    double w[2] = {0.0, 0.0};
+                    int nn = 0, nz = 0;
+#pragma unroll
+                    for (int k = 0; k < 2; k++) {
+                        if (live && ok[k]) {
+                            const double x = rescale(rv[u][k], p[k], m.int_dtype);
+                            nn += __builtin_isnan(x) ? 1 : 0;
+                            nz += x == 0.0 ? 1 : 0;
+                            const double f = missing(x) ? p[k].guess : x;
+                            w[k] = f - p[k].mu;
+                            if (zc[k]) {
+                                const int z = (int)((f - 1.0) * 2.0);
+                                za[k][h] |= (uint32_t)(uint8_t)(int8_t)(tk * z) << (8 * u);
+                                zb[k][h] |= (uint32_t)z << (8 * u);
+                                zs[k] += tk * z;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 2; k++)
+                        if (pos[k] >= 0) m.wcd[i * ld + pos[k]] = w[k];
+                    const uint64_t b0 = __ballot(nn >= 1), b1 = __ballot(nn == 2);
+                    const uint64_t z0 = __ballot(nz >= 1), z1 = __ballot(nz == 2);
+                    if (lane == 0) {
+                        cnt[wv][q0 + 4 * h + u][0] = __popcll(b0) + __popcll(b1);
+                        cnt[wv][q0 + 4 * h + u][1] = __popcll(z0) + __popcll(z1);
                     }
                 }
-                if (in) *(double2*)(m.wcd + i * ld + c0) = double2{w[0], w[1]};
-                const uint64_t b0 = __ballot(nn >= 1), b1 = __ballot(nn == 2);
-                const uint64_t z0 = __ballot(nz >= 1), z1 = __ballot(nz == 2);
-                if (lane == 0) {
-                    cnt[wv][u0 + u][0] = __popcll(b0) + __popcll(b1);
-                    cnt[wv][u0 + u][1] = __popcll(z0) + __popcll(z1);
-                }
             }
+            const int64_t grp = (g0 + q0) >> 4;
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                if (zc[k]) {
+                    const int64_t o = (grp * m.zq + (pos[k] - gb)) * 16;
+                    *(uint4*)(m.zA + o) = uint4{za[k][0], za[k][1], za[k][2], za[k][3]};
+                    *(uint4*)(m.zB + o) = uint4{zb[k][0], zb[k][1], zb[k][2], zb[k][3]};
+                }
         }
         __syncthreads();
         if (threadIdx.x < gn) {
@@ -509,6 +620,9 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
         }
         __syncthreads();
     }
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+        if (zc[k] && zs[k] != 0) atomicAdd((unsigned long long*)&m.zsum[c0 + k], (unsigned long long)zs[k]);
 }
 
 // PCX_M_COV step 2: partial C = wcd^T diag(tok) wcd (:326) over one row slice, one
@@ -615,15 +729,21 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// one work item = (lower-triangle tile (I,J), row slice ks) -> cslab[ks] (lower part)
+// one work item = (tile (I,J) of the trapezoid J < cov_jb of the lower triangle, row
+// slice ks) -> cslab[ks] (lower part, wcd positions); the pure-grid tiles are k_syrk_i8's
 __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
     extern __shared__ __attribute__((aligned(16))) double sy_lds[];
     const int E = (int)m.n_events;
-    const int ntiles = m.cov_tiles, nks = m.cov_kslices;
+    const int ntiles = m.cov_fp_tiles, nks = m.cov_kslices;
+    const int nb = (int)(m.wcd_ld / CT);
     const int item = xcd_remap(blockIdx.x, gridDim.x);
-    const int ks = item / ntiles, t = item % ntiles;
-    int I, J;
-    tri_index(t, I, J);
+    const int ks = item / ntiles;
+    int J = 0, I = item % ntiles;
+    while (I >= nb - J) {  // column J of the trapezoid holds tiles I = J .. nb-1
+        I -= nb - J;
+        J++;
+    }
+    I += J;
     const int64_t nst = m.wcd_rows / SY_BK;
     const int64_t per = (nst + nks - 1) / nks;
     const int64_t s0 = ks * per < nst ? ks * per : nst;
@@ -642,6 +762,70 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
                 const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
                 const int64_t q = (int64_t)J * CT + wc * 64 + b * 16 + (lane & 15);
                 if (p < E && q <= p) out[p * E + q] = acc[a][b][r];
+            }
+}
+
+// PCX_M_COV_I8: P = zA^T zB over one row slice for one 128x128 tile of the pure-grid
+// positions (lower triangle), on int8 MFMA (v_mfma_i32_16x16x64_i8, exact int32
+// accumulation: |P| <= 4 sum tok <= 4e6).  Each lane's A / B fragment is 16 rows of one
+// position -- one 16-byte load from the [row / 16][position][16] blocks, no LDS -- and the
+// next k-step's fragments are loaded while this step's 16 MFMAs run.  4 waves in 2x2,
+// 64x64 per wave.  P goes to cslab[ks] as exact doubles; k_cov_reduce combines.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) k_syrk_i8(pcx_mat m) {
+    const int E = (int)m.n_events;
+    const int ntiles = m.cov_i8_tiles, nks = m.cov_kslices;
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / ntiles, t = item % ntiles;
+    int I, J;
+    tri_index(t, I, J);
+    const int64_t RG = m.wcd_rows / 16;  // 16-row groups
+    const int64_t nst = (RG + 3) / 4;     // 64-row k-steps
+    const int64_t per = (nst + nks - 1) / nks;
+    const int64_t s0 = ks * per < nst ? ks * per : nst;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int lc = lane & 15, lg = lane >> 4;
+    const v4i* A = (const v4i*)m.zA + I * CT + wr * 64 + lc;
+    const v4i* B = (const v4i*)m.zB + J * CT + wc * 64 + lc;
+    const int64_t zq = m.zq;
+    v4i acc[4][4];
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
+    v4i af[4], bf[4];
+    auto load = [&](int64_t s) {
+        const int64_t g = s * 4 + lg;
+        const bool okg = g < RG;
+#pragma unroll
+        for (int a = 0; a < 4; a++) af[a] = okg ? A[g * zq + a * 16] : v4i{0, 0, 0, 0};
+#pragma unroll
+        for (int b = 0; b < 4; b++) bf[b] = okg ? B[g * zq + b * 16] : v4i{0, 0, 0, 0};
+    };
+    if (s0 < s1) load(s0);
+    for (int64_t s = s0; s < s1; s++) {
+        v4i ca[4], cb[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            ca[a] = af[a];
+            cb[a] = bf[a];
+        }
+        if (s + 1 < s1) load(s + 1);
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ca[a], cb[b], acc[a][b], 0, 0, 0);
+    }
+    // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    double* out = m.cslab + (int64_t)ks * E * E;
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++)
+            for (int r = 0; r < 4; r++) {
+                const int64_t p = gb + I * CT + wr * 64 + a * 16 + 4 * lg + r;
+                const int64_t q = gb + J * CT + wc * 64 + b * 16 + lc;
+                if (p < E && q <= p) out[p * E + q] = (double)acc[a][b][r];
             }
 }
 
@@ -690,7 +874,15 @@ __global__ void __launch_bounds__(BT) k_scale(double* M, int64_t n, const unsign
         M[i] = mx > 0.0 ? M[i] / mx : M[i];
 }
 
-// PCX_M_COV_REDUCE: C = sum of slabs over the lower triangle, mirrored (unnormalised)
+__device__ __forceinline__ dd two_prod(double a, double b) {
+    const double p = a * b;
+    return fast_two_sum(p, fma(a, b, -p));
+}
+
+// PCX_M_COV_REDUCE: C = sum of slabs over the lower triangle of wcd positions, in event
+// order (cov_perm) and mirrored (unnormalised).  Pure-grid entries hold the exact integer
+// P_jk: C_jk = c_j c_k T + (c_j Z_k + c_k Z_j) / 2 + P_jk / 4 with this rank's T, Z, P
+// (c = 1 - mu is exact for mu in [1, 2]), evaluated in double-double.
 __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
     const int64_t E = m.n_events;
     const int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x;
@@ -699,8 +891,19 @@ __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
     if (q > p) return;
     double s = 0.0;
     for (int k = 0; k < m.cov_kslices; k++) s += m.cslab[(int64_t)k * E * E + p * E + q];
-    m.C[p * E + q] = s;
-    m.C[q * E + p] = s;
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    const int64_t cp = m.cov_perm[p], cq = m.cov_perm[q];
+    if (q >= gb) {
+        const double T = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
+        const double ap = 1.0 - m.ev[EV_MU * E + cp], aq = 1.0 - m.ev[EV_MU * E + cq];
+        const double Zp = 0.5 * (double)m.zsum[cp], Zq = 0.5 * (double)m.zsum[cq];
+        dd r = dd_mul_d(two_prod(ap, aq), T);
+        r = dd_add(r, dd_add(two_prod(ap, Zq), two_prod(aq, Zp)));
+        r = dd_add(r, dd{0.25 * s, 0.0});
+        s = dd_to_double(r);
+    }
+    m.C[cp * E + cq] = s;
+    m.C[cq * E + cp] = s;
 }
 
 // PCX_M_COV_FINISH: divide by (sum tokens - 1) (:326)
@@ -879,10 +1082,11 @@ __global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
         const double* w = m.wcd + i * ld;
         double acc = 0.0;
 #pragma unroll 4
-        for (int c = 2 * lane; c < ld; c += 2 * WAVE) {
+        for (int c = 2 * lane; c < ld; c += 2 * WAVE) {  // wcd positions (M_COV_PLAN order)
             const double2 x = *(const double2*)(w + c);
-            const double v0 = c < m.n_events ? LD[c] : 0.0;
-            const double v1 = c + 1 < m.n_events ? LD[c + 1] : 0.0;
+            const int e0 = m.cov_perm[c], e1 = m.cov_perm[c + 1];
+            const double v0 = e0 >= 0 ? LD[e0] : 0.0;
+            const double v1 = e1 >= 0 ? LD[e1] : 0.0;
             acc = fma(x.x, v0, acc);
             acc = fma(x.y, v1, acc);
         }
@@ -2452,7 +2656,7 @@ const char* stage_name(int k) {
         "ROWSUMS", "AGENTS", "MATRICES", "WCD", "EIG", "ZERO_LOADING", "NC_OUT", "WMEAN_OUT", "SEL_EXACT",
         "SEL_INIT", "SEL_START", "SEL_ARGMAX", "SEL_VALUE", "SEL_VALUE_FINISH", "SEL_COMPACT", "SEL_HIST",
         "SEL_STEP", "SEL_FINISH", "HARD_LIST", "HARD_GATHER", "HARD_PREP", "HARD_SORT", "HARD_WALK", "EXCHANGE",
-        "H2D", "D2H"};
+        "H2D", "D2H", "COV_PLAN", "COV_I8"};
     return (k >= 0 && k < M_NSTAGE) ? names[k] : "";
 }
 
@@ -2513,7 +2717,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_REPUTATION:
             if (m.rep_raw) hipLaunchKernelGGL(k_rep_total, dim3(1), dim3(1024), 0, st, m);
             hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_TOK);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_TOK, 0);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 1, (int)SC_BIGTOK, 2);
             break;
         case M_COLSTATS:
             hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
@@ -2525,11 +2730,32 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_MEAN:
             hipLaunchKernelGGL(k_mean, dim3(ceb), dim3(BT), 0, st, m);
             break;
+        case M_COV_PLAN:
+            if (!m.cov_perm || !m.cov_pos) {
+                err = "M_COV_PLAN: permutation workspace missing";
+                return hipErrorInvalidValue;
+            }
+            hipLaunchKernelGGL(k_cov_plan, dim3(1), dim3(1024), 0, st, m);
+            break;
+        case M_COV_I8: {
+            const int nb = (int)(m.wcd_ld / CT);
+            if (!m.zA || !m.zB || !m.zsum || m.cov_jb < 0 || m.cov_jb > nb || m.zq != (int64_t)(nb - m.cov_jb) * CT ||
+                m.cov_i8_tiles != (nb - m.cov_jb) * (nb - m.cov_jb + 1) / 2 || m.wcd_rows % 16) {
+                err = "M_COV_I8: int8 operands missing or plan inconsistent";
+                return hipErrorInvalidValue;
+            }
+            if (m.cov_i8_tiles > 0)
+                hipLaunchKernelGGL(k_syrk_i8, dim3(m.cov_i8_tiles * m.cov_kslices), dim3(256), 0, st, m);
+            break;
+        }
         case M_WCD:
         case M_COV: {
-            if (!m.wcd || !m.tokp || !m.rowpart || m.wcd_rows % SY_BK || m.wcd_rows < m.n_rows || m.wcd_ld % CT ||
-                m.wcd_ld < m.n_events) {
-                err = "M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128)";
+            const int nb = (int)(m.wcd_ld / CT);
+            if (!m.wcd || !m.tokp || !m.rowpart || !m.cov_perm || !m.cov_pos || m.wcd_rows % 16 ||
+                m.wcd_rows < m.n_rows || m.wcd_ld % CT || m.wcd_ld < m.n_events || m.cov_jb < 0 || m.cov_jb > nb ||
+                m.cov_fp_tiles != m.cov_jb * nb - m.cov_jb * (m.cov_jb - 1) / 2 ||
+                (m.cov_jb < nb && (!m.zA || !m.zB || !m.zsum))) {
+                err = "M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128) or no plan";
                 return hipErrorInvalidValue;
             }
             if (stage == M_WCD) {
@@ -2546,7 +2772,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                                               (int)SY_LDS_BYTES);
             });
             if (lds_err != hipSuccess) return lds_err;
-            hipLaunchKernelGGL(k_syrk, dim3(m.cov_tiles * m.cov_kslices), dim3(256), SY_LDS_BYTES, st, m);
+            if (m.cov_fp_tiles > 0)
+                hipLaunchKernelGGL(k_syrk, dim3(m.cov_fp_tiles * m.cov_kslices), dim3(256), SY_LDS_BYTES, st, m);
             break;
         }
         case M_COV_REDUCE: {
@@ -2561,7 +2788,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         }
         case M_SCORES:
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
-            if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart)
+            if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart &&
+                m.cov_perm)
                 hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             else
                 hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);

@@ -26,7 +26,9 @@
 namespace {
 constexpr int BT = 256;
 constexpr int CS = 16;  // dd slots per column in cstat
+constexpr int CM = 8;   // doubles per column in mpart / cmax
 constexpr int SS = 16;  // dd slots in scal
+constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
 constexpr int COV_STAGE = 16;
 constexpr int SELS = 24;
@@ -57,6 +59,9 @@ struct pcx_workspace {
     int32_t *sel_act, *hard, *hard_cols, *hard_modes, *scols, *sidx;
     double *wcd, *tokp, *scalars, *xsend, *xrecv;
     uint32_t* rowpart;
+    int32_t *cov_perm, *cov_pos;
+    int8_t *zA, *zB;
+    int64_t* zsum;
     int64_t xcap = 0;  // doubles per rank in xsend
 
     ~pcx_workspace() {
@@ -199,9 +204,12 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->rep, (size_t)n_rows * 8, true},
         {(void**)&w->tok, (size_t)n_rows * 8, true},
         {(void**)&w->part, (size_t)(w->col_blocks * E * 16) * 8, true},
-        {(void**)&w->mpart, (size_t)(w->col_blocks * E * 4) * 8, true},
+        {(void**)&w->mpart, (size_t)(w->col_blocks * E * CM) * 8, true},
         {(void**)&w->cstat, (size_t)(world * E * CS * 2) * 8, true},
-        {(void**)&w->cmax, (size_t)(world * E * 4) * 8, true},
+        {(void**)&w->cmax, (size_t)(world * E * CM) * 8, true},
+        {(void**)&w->cov_perm, (size_t)w->wcd_ld * 4, true},
+        {(void**)&w->cov_pos, (size_t)E * 4, true},
+        {(void**)&w->zsum, (size_t)E * 8, true},
         {(void**)&w->scal, (size_t)(world * SS * 2) * 8, true},
         {(void**)&w->spart, (size_t)(4096 * 8) * 8, true},
         {(void**)&w->ev, (size_t)(16 * E) * 8, true},
@@ -235,6 +243,8 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
         {(void**)&w->tokp, (size_t)(w->wcd_rows + 64) * 8, false},
         {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
+        {(void**)&w->zA, (size_t)(w->wcd_rows * w->wcd_ld), false},
+        {(void**)&w->zB, (size_t)(w->wcd_rows * w->wcd_ld), false},
     };
     auto align = [](size_t b) { return (b + 255) / 256 * 256; };
     size_t zb = 0;
@@ -638,17 +648,18 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.aux_scores = aux;
         r->n_hard = 0;
         r->sel_passes = 0;
+        r->grid_events = 0;
 
         const double* cstat = w->cstat;
         (void)cstat;
         const int64_t cpitch = CS * 2;
         // a1: reputation, tokens (:138-146)
         R.stage(m, M_REPUTATION);
-        R.gather_slots(w->scal, 1, SS * 2, 0, 2, w);
+        R.gather_slots(w->scal, 1, SS * 2, 0, SC_BIGTOK_SLOT + 1, w);
         // a2/a3: rescale + NA + present sums (:266-299)
         R.stage(m, M_COLSTATS);
         R.gather_slots(w->cstat, E, cpitch, 0, 4, w);
-        R.gather_block(w->cmax, E * 4 * 8);
+        R.gather_block(w->cmax, E * CM * 8);
         R.stage(m, M_GUESS);  // binary fills (:304-309)
         if (!filled_input) select(R, m, w, 1, r);  // scaled fills: weighted median (:300-303)
         if (entry == 1) {      // interpolate: rescaled + filled matrices (:266-313)
@@ -659,9 +670,25 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             const bool run_wpca = entry == 2 || (entry != 4 && wpca);
             int64_t flags = 0;
             if (run_wpca) {
-                // a5: wcd materialised (:322); a6: covariance on fp64 MFMA (:326); a7: power iteration (:330-336)
+                // a5: wcd materialised (:322) in the M_COV_PLAN column order; a6: covariance (:326),
+                // general tiles on fp64 MFMA, pure-grid tiles on int8 MFMA; a7: power iteration (:330-336)
+                m.cov_perm = w->cov_perm;
+                m.cov_pos = w->cov_pos;
+                m.zA = w->zA;
+                m.zB = w->zB;
+                m.zsum = w->zsum;
+                R.stage(m, M_COV_PLAN);
+                const int64_t n_general = R.read(m.info + INFO_COV_GENERAL);
+                r->grid_events = (int32_t)(E - n_general);
+                const int64_t nb = w->wcd_ld / COV_TILE;
+                const int64_t jb = (n_general + COV_TILE - 1) / COV_TILE;
+                m.cov_jb = (int32_t)jb;
+                m.zq = (nb - jb) * COV_TILE;
+                m.cov_fp_tiles = (int32_t)(jb * nb - jb * (jb - 1) / 2);
+                m.cov_i8_tiles = (int32_t)((nb - jb) * (nb - jb + 1) / 2);
                 R.stage(m, M_WCD);
                 R.stage(m, M_COV);
+                R.stage(m, M_COV_I8);
                 R.stage(m, M_COV_REDUCE);
                 if (R.comm) {  // the partial covariance: one SUM of its lower triangle (cslab is free now)
                     R.hip(tri_pack(w->C, w->cslab, E, 0, R.st), "tri pack");

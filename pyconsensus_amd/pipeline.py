@@ -289,7 +289,7 @@ def _meta(res, algorithm):
     return {"participation": res.participation, "avg_certainty": res.avg_certainty,
             "branch": int(res.branch), "pi_iters": int(res.pi_iters), "flags": int(res.flags),
             "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes),
-            "comm_bytes": float(res.comm_bytes)}
+            "comm_bytes": float(res.comm_bytes), "grid_events": int(res.grid_events)}
 
 
 # ---------------------------------------------------------------- host-memory entry points
