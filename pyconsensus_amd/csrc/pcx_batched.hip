@@ -334,6 +334,13 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
 // scr: MED_SCR doubles of LDS (sx | sw | ox | ow | 64 int counters).
 constexpr int MED_SCR = 288;
 
+// top 32 bits of the order-preserving key of a double (-0.0 folded onto +0.0)
+__device__ __forceinline__ uint32_t key_hi32(double x) {
+    uint64_t u = __double_as_longlong(x == 0.0 ? 0.0 : x);
+    u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+    return (uint32_t)(u >> 32);
+}
+
 template <int NR>
 __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
                                                     long long* prof = nullptr) {
@@ -341,6 +348,9 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     double *sx = scr, *sw = scr + 64, *ox = scr + 128, *ow = scr + 192;
     int* cnt = reinterpret_cast<int*>(scr + 256);
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#ifdef PCX_X_NOMED  // ablation (tools/ab_variant.sh): wrong results, time without the medians
+    return bcast(x, 0) + 0.0 * Wtot;
+#endif
     const double mid = 0.5 * Wtot;
     if (ballot(sel && w > mid)) {  // weightedstats: a weight above half the total wins outright
         const double mx = wave_max(sel ? w : -__builtin_inf());
@@ -349,22 +359,53 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
     if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
     const int n = popc(ballot(sel));
+    // rank by the top 32 bits of x's order-preserving key (one 32-bit compare per row,
+    // four keys per LDS read; unselected rows hold the largest key, below no selected
+    // one); pairs whose keys collide -- the atomic hands a rank out twice -- are rare and
+    // take the (x, w) lexicographic pass
+    uint32_t* kx = reinterpret_cast<uint32_t*>(ox);
+    const uint32_t key = sel ? key_hi32(x) : 0xffffffffu;
     wsync();
     sx[l] = sel ? x : __builtin_inf();
     sw[l] = sel ? w : __builtin_inf();
     cnt[l] = 0;
+    ow[l] = 0.0;  // slots past n add +0.0 in the walk
+    kx[l] = key;
     wsync();
     int r = 0;
+#ifdef PCX_X_NORANK  // ablation: no rank loop
+    r = l;
+#else
 #pragma unroll
     for (int m = 0; m < NR; m++) {
         if (NR == 64 && m >= N) break;
-        const double xm = sx[m], wm = sw[m];
-        r += ((xm < x) | ((xm == x) & (wm < w))) ? 1 : 0;
+        r += kx[m] < key ? 1 : 0;
+    }
+#endif
+    if (sel) atomicAdd(&cnt[r], 1);
+    wsync();
+    // rows sharing a key (equal x: e.g. the filled guesses of the outcome median, or a
+    // 32-bit key collision) are ordered among themselves by (x, w, row), one step per
+    // such row
+    const bool tied = sel && cnt[r] > 1;
+    uint64_t T = ballot(tied);
+    int sub = 0;
+    if (T) {
+        int* rk = reinterpret_cast<int*>(kx);  // the keys are dead
+        rk[l] = r;
+        wsync();
+        while (T) {
+            const int m = __builtin_ctzll(T);
+            T &= T - 1;
+            const double xm = sx[m], wm = sw[m];
+            const bool before = (xm < x) | ((xm == x) & ((wm < w) | ((wm == w) & (m < l))));
+            sub += (tied && rk[m] == r && before) ? 1 : 0;
+        }
+        wsync();
     }
     if (sel) {
-        const int slot = r + atomicAdd(&cnt[r], 1);
-        ox[slot] = x;
-        ow[slot] = w;
+        ox[r + sub] = x;
+        ow[r + sub] = w;
     }
     wsync();
     if (prof) {
@@ -377,9 +418,38 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     // the current group's dependent adds
     double cum = 0.0, before = 0.0;
     int k = 0;
+#ifdef PCX_X_NOWALK  // ablation: no walk
+    return ox[n >> 1] + 0.0 * mid;
+#endif
     double v[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) v[q] = ow[q];
+    if (!ballot(sel && !(w >= 0.0))) {
+        // non-negative weights: the running sums only grow (slots past n add +0.0), so a
+        // group holds the first cum > mid iff its last sum exceeds mid
+        for (int t = 0; t < n; t += 8) {
+            double nv[8], c[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) nv[q] = ow[(t + 8 + q) & 63];
+            c[0] = cum + v[0];
+#pragma unroll
+            for (int q = 1; q < 8; q++) c[q] = c[q - 1] + v[q];
+            if (c[7] > mid) {
+                int hit = 7;
+#pragma unroll
+                for (int q = 6; q >= 0; q--)
+                    if (c[q] > mid) hit = q;
+                k = t + hit + 1;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q == hit) before = c[q] - v[q];
+                break;
+            }
+            cum = c[7];
+#pragma unroll
+            for (int q = 0; q < 8; q++) v[q] = nv[q];
+        }
+    } else
     for (int t = 0; t < n; t += 8) {
         double nv[8], c[8];
 #pragma unroll
@@ -1204,8 +1274,12 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             ws[l] = w;
             wsync();
             Wsum = 0.0;
+#ifdef PCX_X_TREEW  // ablation: tree sum instead of the sequential one
+            Wsum = wave_pw_sum(w, row);
+#else
 #pragma unroll 8
             for (int i = 0; i < N; i++) Wsum = Wsum + ws[i];
+#endif
         };
         auto finish = [&](int j, double g) {
             if (a.int_dtype) g = trunc(g);
@@ -1319,6 +1393,10 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         } else if (!any_nz) {
             xv = l == 0 ? 1.0 : 0.0;
             flags |= 1;
+#ifdef PCX_X_NOPI  // ablation: wrong results, time without the power iteration
+        } else if (true) {
+            xv = col ? S.C[l * ES] : 0.0;
+#endif
         } else {
             // start: the column with the largest diagonal entry (first max; C is finite here)
             const double dg = col ? S.C[l * ES + l] : -__builtin_inf();
