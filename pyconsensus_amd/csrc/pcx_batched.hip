@@ -53,7 +53,14 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x; }
         }                                                                         \
     } while (0)
 
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// One wave per workgroup: the LDS operations of a wave execute in issue order, so a
+// compiler-ordering wave barrier suffices between an LDS write and another lane's read
+// (no lgkmcnt(0) drain, which __syncthreads() emits).
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
@@ -266,8 +273,10 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
     const uint64_t selm = ballot(sel);
     const int n = popc(selm);
     wsync();
-    sx[l] = x;
-    sw[l] = w;
+    if (sel) {
+        sx[l] = x;
+        sw[l] = w;
+    }
     wsync();
     int r = 0;
     if (sel) {  // stable rank by (x, w)
@@ -331,8 +340,10 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
 //    cum > mid: the SPEC's sequential sums bit for bit; `before` is the same subtraction.
 // NaN keys have no total order: rounds with a NaN among the selected pairs take
 // wave_wmedian.  NR = compile-time row count bound (64 when the shape is dynamic).
-// scr: MED_SCR doubles of LDS (sx | sw | ox | ow | 64 int counters).
-constexpr int MED_SCR = 288;
+// scr: med_scr(NR) doubles of LDS: sx | sw | ox [NR] | ow [med_ow(NR)] | NR int counters
+// (ow holds the zero-padded walk groups: every prefetched group of eight).
+__host__ __device__ constexpr int med_ow(int NR) { return (NR + 7) / 8 * 8 + 8; }
+__host__ __device__ constexpr int med_scr(int NR) { return 3 * NR + med_ow(NR) + (NR + 1) / 2; }
 
 // top 32 bits of the order-preserving key of a double (-0.0 folded onto +0.0)
 __device__ __forceinline__ uint32_t key_hi32(double x) {
@@ -345,8 +356,8 @@ template <int NR>
 __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
                                                     long long* prof = nullptr) {
     const int l = lane_id();
-    double *sx = scr, *sw = scr + 64, *ox = scr + 128, *ow = scr + 192;
-    int* cnt = reinterpret_cast<int*>(scr + 256);
+    double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
+    int* cnt = reinterpret_cast<int*>(scr + 3 * NR + med_ow(NR));
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #ifdef PCX_X_NOMED  // ablation (tools/ab_variant.sh): wrong results, time without the medians
     return bcast(x, 0) + 0.0 * Wtot;
@@ -366,11 +377,13 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     uint32_t* kx = reinterpret_cast<uint32_t*>(ox);
     const uint32_t key = sel ? key_hi32(x) : 0xffffffffu;
     wsync();
-    sx[l] = sel ? x : __builtin_inf();
-    sw[l] = sel ? w : __builtin_inf();
-    cnt[l] = 0;
-    ow[l] = 0.0;  // slots past n add +0.0 in the walk
-    kx[l] = key;
+    if (l < NR) {
+        sx[l] = sel ? x : __builtin_inf();
+        sw[l] = sel ? w : __builtin_inf();
+        cnt[l] = 0;
+        kx[l] = key;
+    }
+    for (int q = l; q < med_ow(NR); q += 64) ow[q] = 0.0;  // slots past n add +0.0 in the walk
     wsync();
     int r = 0;
 #ifdef PCX_X_NORANK  // ablation: no rank loop
@@ -430,7 +443,7 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
         for (int t = 0; t < n; t += 8) {
             double nv[8], c[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) nv[q] = ow[(t + 8 + q) & 63];
+            for (int q = 0; q < 8; q++) nv[q] = ow[t + 8 + q];
             c[0] = cum + v[0];
 #pragma unroll
             for (int q = 1; q < 8; q++) c[q] = c[q - 1] + v[q];
@@ -453,7 +466,7 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     for (int t = 0; t < n; t += 8) {
         double nv[8], c[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) nv[q] = ow[(t + 8 + q) & 63];
+        for (int q = 0; q < 8; q++) nv[q] = ow[t + 8 + q];
         c[0] = cum + v[0];
 #pragma unroll
         for (int q = 1; q < 8; q++) c[q] = c[q - 1] + v[q];
@@ -536,26 +549,40 @@ __host__ __device__ inline int smem_f_size(int N, int E, int ES) {
     return N * ES > E * (N | 1) ? N * ES : E * (N | 1);
 }
 __host__ __device__ inline int smem_evs(int E) { return (E + 1) & ~1; }
-__host__ __device__ inline int smem_c_size(int N, int E, int ES) {
+// C and M: full [E][ES] (the Jacobi eigenpairs of big-five / fixed-variance need a
+// general V), or -- every other algorithm -- packed lower triangles (both are symmetric:
+// the squared M bitwise too), which brings a 50 x 20 round to 13.2 KB, twelve per CU.
+__host__ __device__ inline int smem_mat(int E, int ES, bool pk) { return pk ? E * (E + 1) / 2 : E * ES; }
+__host__ __device__ inline int smem_c_size(int N, int E, int ES, bool pk) {
     const int need = 3 * smem_rows(N) + 2 * smem_evs(E);
-    return E * ES > need ? E * ES : need;
+    return smem_mat(E, ES, pk) > need ? smem_mat(E, ES, pk) : need;
 }
-__host__ __device__ inline int smem_m_size(int E, int ES) {
-    const int need = MED_SCR > 2 * smem_evs(E) ? MED_SCR : 2 * smem_evs(E);
-    return E * ES > need ? E * ES : need;
-}
-
-__host__ __device__ inline size_t smem_doubles(int N, int E, int ES) {
-    return (size_t)smem_f_size(N, E, ES) + smem_c_size(N, E, ES) + smem_m_size(E, ES) + smem_rows(N) + 5 * (size_t)smem_evs(E);
+__host__ __device__ inline int smem_m_size(int E, int ES, int NR, bool pk) {
+    const int need = med_scr(NR) > 2 * smem_evs(E) ? med_scr(NR) : 2 * smem_evs(E);
+    return smem_mat(E, ES, pk) > need ? smem_mat(E, ES, pk) : need;
 }
 
-__device__ Smem carve(double* base, int N, int E, int ES) {
+__host__ __device__ inline size_t smem_doubles(int N, int E, int ES, int NR, bool pk) {
+    return (size_t)smem_f_size(N, E, ES) + smem_c_size(N, E, ES, pk) + smem_m_size(E, ES, NR, pk) + smem_rows(N) +
+           5 * (size_t)smem_evs(E);
+}
+
+// entry (j, k) of the symmetric C / M
+template <bool PK>
+__device__ __forceinline__ int sym_at(int j, int k, int ES) {
+    if constexpr (PK)
+        return j >= k ? j * (j + 1) / 2 + k : k * (k + 1) / 2 + j;
+    else
+        return j * ES + k;
+}
+
+__device__ Smem carve(double* base, int N, int E, int ES, int NR, bool pk) {
     const int nr = smem_rows(N), ne = smem_evs(E);
     Smem s;
     double* p = base;
     s.F = p; p += smem_f_size(N, E, ES);
-    s.C = p; p += smem_c_size(N, E, ES);
-    s.M = p; p += smem_m_size(E, ES);
+    s.C = p; p += smem_c_size(N, E, ES, pk);
+    s.M = p; p += smem_m_size(E, ES, NR, pk);
     s.rep = p; p += nr;
     s.mu = p; p += ne;
     s.x = p; p += ne;
@@ -575,13 +602,13 @@ __device__ Smem carve(double* base, int N, int E, int ES) {
 }
 
 // y = normalize(M x) for lane j < E, x in LDS; returns y_j (0 on other lanes)
+template <bool PK>
 __device__ __forceinline__ double matvec_unit(const double* M, int ES, const double* x, int E) {
     const int l = lane_id();
     double y = 0.0;
     if (l < E) {
         double acc = 0.0;
-        const double* row = M + l * ES;
-        for (int k = 0; k < E; k++) acc = fma(row[k], x[k], acc);
+        for (int k = 0; k < E; k++) acc = fma(M[sym_at<PK>(l, k, ES)], x[k], acc);
         y = acc;
     }
     const double nrm = sqrt(tree_sum(l < E ? y * y : 0.0));
@@ -598,6 +625,8 @@ __device__ __forceinline__ d4v mfma_f64(double a, double b, d4v c) {
 // accumulates exactly like the SPEC's fma chain over m (tools/probes/mfma_f64_order:
 // bitwise equal), and the zero padding of the 32 x 32 tile adds exact zeros, so every
 // entry is bit-identical to the VALU loop.  E <= 32: a 2 x 2 grid of 16 x 16 tiles.
+// M symmetric: A[ml][mm] = B[mm][ml], one read per operand pair.
+template <bool PK>
 __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
     const int l = lane_id(), ml = l & 15, kq = l >> 4;
     const bool two = E > 16;
@@ -605,12 +634,12 @@ __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
     for (int m0 = 0; m0 < E; m0 += 4) {
         const int mm = m0 + kq;
         const bool ok = mm < E;
-        const double a0 = (ok && ml < E) ? M[ml * ES + mm] : 0.0;
-        const double b0 = (ok && ml < E) ? M[mm * ES + ml] : 0.0;
+        const double a0 = (ok && ml < E) ? M[sym_at<PK>(ml, mm, ES)] : 0.0;
+        const double b0 = a0;
         t00 = mfma_f64(a0, b0, t00);
         if (two) {
-            const double a1 = (ok && 16 + ml < E) ? M[(16 + ml) * ES + mm] : 0.0;
-            const double b1 = (ok && 16 + ml < E) ? M[mm * ES + 16 + ml] : 0.0;
+            const double a1 = (ok && 16 + ml < E) ? M[sym_at<PK>(16 + ml, mm, ES)] : 0.0;
+            const double b1 = a1;
             t01 = mfma_f64(a0, b1, t01);
             t10 = mfma_f64(a1, b0, t10);
             t11 = mfma_f64(a1, b1, t11);
@@ -635,10 +664,10 @@ __device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
-        if (j0 < E && k0 < E) M[j0 * ES + k0] = scaled(t00[r]);
-        if (j0 < E && k1 < E) M[j0 * ES + k1] = scaled(t01[r]);
-        if (j1 < E && k0 < E) M[j1 * ES + k0] = scaled(t10[r]);
-        if (j1 < E && k1 < E) M[j1 * ES + k1] = scaled(t11[r]);
+        if (j0 < E && k0 < E && (!PK || k0 <= j0)) M[sym_at<PK>(j0, k0, ES)] = scaled(t00[r]);
+        if (j0 < E && k1 < E && !PK) M[sym_at<PK>(j0, k1, ES)] = scaled(t01[r]);
+        if (j1 < E && k0 < E) M[sym_at<PK>(j1, k0, ES)] = scaled(t10[r]);
+        if (j1 < E && k1 < E && (!PK || k1 <= j1)) M[sym_at<PK>(j1, k1, ES)] = scaled(t11[r]);
     }
     wsync();
 }
@@ -1121,13 +1150,14 @@ __device__ __noinline__ double feck_nc(const BatchArgs& a, const double* F, int 
 // launcher specialises, e.g. the 50 x 20 of config C3): every loop bound is known, so
 // the sequential column/row loops unroll and their LDS reads issue ahead of the
 // dependent adds.  NT = ET = 0: any N <= 64, E <= 32 at run time.  Same arithmetic.
-template <int NT, int ET, bool CLUS>
+template <int NT, int ET, bool CLUS, bool PK>
 __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? (ET | 1) : a.ES;
     const int l = lane_id();
     const int64_t b = blockIdx.x;
-    Smem S = carve(smem, N, E, ES);
+    constexpr int NRM = NT > 0 ? NT : 64;  // median scratch rows
+    Smem S = carve(smem, N, E, ES, NRM, PK);
     const bool row = l < N, col = l < E;
     const int64_t bo = a.bounds_shared ? 0 : b * E;
     const bool has_bounds = a.scaled != nullptr;
@@ -1363,12 +1393,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                     }
                 }
             }
-            auto put = [&](int j, int k, double acc) {
+            auto put = [&](int j, int k, double acc) {  // j >= k
                 const double c = acc / denom;
-                S.C[j * ES + k] = c;
-                S.C[k * ES + j] = c;
-                S.M[j * ES + k] = c;
-                S.M[k * ES + j] = c;
+                S.C[sym_at<PK>(j, k, ES)] = c;
+                S.M[sym_at<PK>(j, k, ES)] = c;
+                if (!PK) {
+                    S.C[k * ES + j] = c;
+                    S.M[k * ES + j] = c;
+                }
                 nonzero |= c != 0.0;
                 finite &= __builtin_isfinite(c) != 0;
             };
@@ -1395,22 +1427,22 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             flags |= 1;
 #ifdef PCX_X_NOPI  // ablation: wrong results, time without the power iteration
         } else if (true) {
-            xv = col ? S.C[l * ES] : 0.0;
+            xv = col ? S.C[sym_at<PK>(l, 0, ES)] : 0.0;
 #endif
         } else {
             // start: the column with the largest diagonal entry (first max; C is finite here)
-            const double dg = col ? S.C[l * ES + l] : -__builtin_inf();
+            const double dg = col ? S.C[sym_at<PK>(l, l, ES)] : -__builtin_inf();
             const int kd = __builtin_ctzll(ballot(col && dg == wave_max(dg)));
-            double x0 = col ? S.C[l * ES + kd] : 0.0;
+            double x0 = col ? S.C[sym_at<PK>(l, kd, ES)] : 0.0;
             const double n0 = sqrt(tree_sum(x0 * x0));
             xv = col ? x0 / n0 : 0.0;
             int sqn = 0;
-            for (; sqn < PI_PRESQUARE; sqn++) square_scaled(S.M, ES, E);
+            for (; sqn < PI_PRESQUARE; sqn++) square_scaled<PK>(S.M, ES, E);
             if (col) S.x[l] = xv;
             wsync();
             int it = 0, since = 0;
             for (;;) {
-                const double y = matvec_unit(S.M, ES, S.x, E);
+                const double y = matvec_unit<PK>(S.M, ES, S.x, E);
                 const double d = wave_max(col ? fabs(y - xv) : 0.0);
                 xv = y;
                 wsync();
@@ -1424,13 +1456,13 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                     break;
                 }
                 if (since >= PI_SQUARE_EVERY && sqn < PI_MAX_SQUARINGS) {
-                    square_scaled(S.M, ES, E);
+                    square_scaled<PK>(S.M, ES, E);
                     sqn++;
                     since = 0;
                 }
             }
             for (int p = 0; p < PI_POLISH; p++) {
-                xv = matvec_unit(S.C, ES, S.x, E);
+                xv = matvec_unit<PK>(S.C, ES, S.x, E);
                 wsync();
                 if (col) S.x[l] = xv;
                 wsync();
@@ -1461,7 +1493,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             }
         } else if (flags & 2) {
             sc_i = __builtin_nan("");  // the reference's second svd raises (:375, :431)
-        } else {
+        } else if constexpr (!PK) {  // (the packed layout is never launched for these)
             // ---- big-five (:373-390) / fixed-variance (:429-451): net score =
             // sum_c Sigma_c * (wcd . loading_c); Sigma, loadings from Jacobi (SPEC)
             const double trace = wave_pw_sum(col ? S.C[l * ES + l] : 0.0, col);  // np.trace
@@ -1511,7 +1543,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(6);
     if constexpr (CLUS) {
         if (clus) {
-            double* X = smem + smem_doubles(N, E, ES);
+            double* X = smem + smem_doubles(N, E, ES, NRM, PK);
             if (alg == 6)
                 nc_i = hier_nc(S.F, S.mu, ES, N, E, a.hierarchy_threshold, reinterpret_cast<uint64_t*>(X));
             else if (alg == 5)
@@ -1774,9 +1806,16 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     }
 }
 
-size_t batched_lds_bytes(int N, int E) {
+// the launch's instantiation: <50, 20> for the C3 shape, else the dynamic one; packed
+// C / M unless the algorithm needs the Jacobi eigenpairs (big-five, fixed-variance) or
+// is a clustering one
+static bool shape_50x20(int N, int E, int ES) { return N == 50 && E == 20 && ES == 21; }
+static bool packed_alg(int alg) { return alg == 0 || alg == 1 || alg == 4; }
+
+size_t batched_lds_bytes(int N, int E, int alg) {
     const int ES = E | 1;
-    return smem_doubles(N, E, ES) * sizeof(double);
+    const int NR = shape_50x20(N, E, ES) && alg < 5 ? 50 : 64;
+    return smem_doubles(N, E, ES, NR, packed_alg(alg)) * sizeof(double);
 }
 
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
@@ -1786,20 +1825,28 @@ hipError_t launch_batched(const BatchArgs& a, hipStream_t stream) {
         const char* e = getenv("PCX_BATCHED_LDS_PAD");
         return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
     }();
-    size_t lds = batched_lds_bytes(a.N, a.E) + pad;
+    size_t lds = batched_lds_bytes(a.N, a.E, a.algorithm) + pad;
     if (a.B <= 0) return hipSuccess;
+    const dim3 grid((unsigned)a.B), block(64);
+    const bool pk = packed_alg(a.algorithm);
     if (a.algorithm >= 5) {  // clustering algorithms: their own instantiation and LDS region
-        lds = batched_lds_bytes(a.N, a.E) + sizeof(double) * (size_t)cluster_lds_doubles(a.N, a.E, a.ES);
+        lds += sizeof(double) * (size_t)cluster_lds_doubles(a.N, a.E, a.ES);
         static bool attr = [] {
-            return hipFuncSetAttribute(reinterpret_cast<const void*>(&batched_round_kernel<0, 0, true>),
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(&batched_round_kernel<0, 0, true, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
         }();
         (void)attr;
-        hipLaunchKernelGGL((batched_round_kernel<0, 0, true>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
-    } else if (a.N == 50 && a.E == 20 && a.ES == 21)
-        hipLaunchKernelGGL((batched_round_kernel<50, 20, false>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
-    else
-        hipLaunchKernelGGL((batched_round_kernel<0, 0, false>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((batched_round_kernel<0, 0, true, false>), grid, block, lds, stream, a);
+    } else if (shape_50x20(a.N, a.E, a.ES)) {
+        if (pk)
+            hipLaunchKernelGGL((batched_round_kernel<50, 20, false, true>), grid, block, lds, stream, a);
+        else
+            hipLaunchKernelGGL((batched_round_kernel<50, 20, false, false>), grid, block, lds, stream, a);
+    } else if (pk) {
+        hipLaunchKernelGGL((batched_round_kernel<0, 0, false, true>), grid, block, lds, stream, a);
+    } else {
+        hipLaunchKernelGGL((batched_round_kernel<0, 0, false, false>), grid, block, lds, stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -135,7 +135,7 @@ struct BatchArgs {
     long long* stamps;  // diagnostic phase clocks [B][16] (PCX_STAMPS), normally NULL
 };
 
-size_t batched_lds_bytes(int N, int E);
+size_t batched_lds_bytes(int N, int E, int algorithm);
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream);
 
 // ---------------------------------------------------------------- single-matrix stages

@@ -42,9 +42,10 @@ def child():
 
 
 def main():
-    ES = 21  # batched_lds_bytes(50, 20): smem_doubles() in pcx_batched.hip
-    base = 8 * (50 * ES + 2 * 20 * ES + 50 + 5 * 20)
-    for k in (10, 9, 8, 6):
+    # batched_lds_bytes(50, 20, PCA): smem_doubles() in pcx_batched.hip -- F [50][21], packed C
+    # (210), M (the median scratch, 239), rep, five event vectors
+    base = 8 * (50 * 21 + 210 + 239 + 50 + 5 * 20)
+    for k in (12, 10, 9, 8, 6):
         pad = max(0, LDS_CU // k - base - 256) if k < LDS_CU // base else 0
         env = dict(os.environ, PCX_BATCHED_LDS_PAD=str(pad))
         r = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
