@@ -519,7 +519,9 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
 // M_COV_PLAN column order with zero padding, plus the tokens zero-padded past n_rows, and
 // for the pure-grid positions (>= 128 cov_jb) the int8 operands tok * z (zA) and z (zB) in
 // 16-row interleaved column-major blocks [row / 16][position][16] -- one 16-byte MFMA
-// fragment per (position, 16 rows) -- and Z_j = sum tok z_ij (zsum, exact).
+// fragment per (position, 16 rows) -- and Z_j = sum tok z_ij (zsum, exact).  The
+// consensus entry's "original" / "filled" matrices are written here too (no M_MATRICES
+// pass over the reports).
 constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread)
 
 // Blocks own a contiguous row range (a multiple of 64 rows) of a 512-event block; each
@@ -534,6 +536,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     const int c0 = blockIdx.y * WCD_COLS + 2 * threadIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t gb = (int64_t)m.cov_jb * CT;
+    const bool even_e = (E & 1) == 0;  // 16-byte aligned event pairs in the N x E outputs
     ColParam p[2];
     bool ok[2], zc[2];
     int64_t pos[2];
@@ -573,7 +576,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     const int64_t i = g0 + q0 + 4 * h + u;
                     const bool live = i < m.n_rows;
                     const int tk = (live && (zc[0] || zc[1])) ? (int)m.tok[i] : 0;
-                    double w[2] = {0.0, 0.0};
+                    double w[2] = {0.0, 0.0}, xo[2] = {0.0, 0.0}, fo[2] = {0.0, 0.0};
                     int nn = 0, nz = 0;
 #pragma unroll
                     for (int k = 0; k < 2; k++) {
@@ -583,6 +586,8 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                             nz += x == 0.0 ? 1 : 0;
                             const double f = missing(x) ? p[k].guess : x;
                             w[k] = f - p[k].mu;
+                            xo[k] = x;
+                            fo[k] = f;
                             if (zc[k]) {
                                 const int z = (int)((f - 1.0) * 2.0);
                                 za[k][h] |= (uint32_t)(uint8_t)(int8_t)(tk * z) << (8 * u);
@@ -594,6 +599,21 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
 #pragma unroll
                     for (int k = 0; k < 2; k++)
                         if (pos[k] >= 0) m.wcd[i * ld + pos[k]] = w[k];
+                    // result["original"] / result["filled"] (:266-313), event order
+                    if (live && (m.original || m.filled)) {
+                        const int64_t o = i * E + c0;
+                        if (even_e && ok[1]) {
+                            if (m.original) *(double2*)(m.original + o) = double2{xo[0], xo[1]};
+                            if (m.filled) *(double2*)(m.filled + o) = double2{fo[0], fo[1]};
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 2; k++)
+                                if (ok[k]) {
+                                    if (m.original) m.original[o + k] = xo[k];
+                                    if (m.filled) m.filled[o + k] = fo[k];
+                                }
+                        }
+                    }
                     const uint64_t b0 = __ballot(nn >= 1), b1 = __ballot(nn == 2);
                     const uint64_t z0 = __ballot(nz >= 1), z1 = __ballot(nz == 2);
                     if (lane == 0) {
@@ -2443,16 +2463,22 @@ __global__ void __launch_bounds__(BT) k_agents(pcx_mat m) {
 }
 
 // PCX_M_MATRICES: rescaled (result["original"]) and filled (result["filled"]) reports
+// grid (ceil(E/BT), G): thread = one event column over a chunk of rows (the column
+// parameters loaded once)
 __global__ void __launch_bounds__(BT) k_matrices(pcx_mat m) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c >= m.n_events) return;
     const int E = (int)m.n_events;
-    const int64_t tot = m.n_rows * m.n_events;
-    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < tot; idx += (int64_t)gridDim.x * BT) {
-        const int c = (int)(idx % E);
-        const ColParam p = col_param(m, c, true);
-        const double x = rescale(m.reports[idx], p, m.int_dtype);
-        if (m.original) m.original[idx] = x;
-        if (m.filled) m.filled[idx] = missing(x) ? p.guess : x;
-    }
+    const ColParam p = col_param(m, c, true);
+    int64_t r0, r1;
+    row_range(m, r0, r1);
+    rows_unrolled<ROW_UNROLL>(
+        r0, r1, [&](int64_t i) { return m.reports[i * E + c]; },
+        [&](int64_t i, double v) {
+            const double x = rescale(v, p, m.int_dtype);
+            if (m.original) m.original[i * E + c] = x;
+            if (m.filled) m.filled[i * E + c] = missing(x) ? p.guess : x;
+        });
 }
 
 __global__ void k_info_clear(pcx_mat m, int slot) { m.info[slot] = 0; }
@@ -2954,7 +2980,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         }
         case M_MATRICES:
             if (m.original || m.filled)
-                hipLaunchKernelGGL(k_matrices, dim3(grid_rows(m.n_rows * m.n_events, BT)), dim3(BT), 0, st, m);
+                hipLaunchKernelGGL(k_matrices, colgrid, dim3(BT), 0, st, m);
             break;
         case M_EIG:
             if (m.algorithm != 2 && m.algorithm != 3) break;

@@ -669,6 +669,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             const bool wpca = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;
             const bool run_wpca = entry == 2 || (entry != 4 && wpca);
             int64_t flags = 0;
+            bool mats_written = false;  // k_wcd writes "original" / "filled" on the way
             if (run_wpca) {
                 // a5: wcd materialised (:322) in the M_COV_PLAN column order; a6: covariance (:326),
                 // general tiles on fp64 MFMA, pure-grid tiles on int8 MFMA; a7: power iteration (:330-336)
@@ -687,6 +688,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.cov_fp_tiles = (int32_t)(jb * nb - jb * (jb - 1) / 2);
                 m.cov_i8_tiles = (int32_t)((nb - jb) * (nb - jb + 1) / 2);
                 R.stage(m, M_WCD);
+                mats_written = true;
                 R.stage(m, M_COV);
                 R.stage(m, M_COV_I8);
                 R.stage(m, M_COV_REDUCE);
@@ -745,7 +747,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                         R.stage(m, M_ROWSUMS);
                         R.gather_slots(w->scal, 1, SS * 2, 8, 10, w);
                         R.stage(m, M_AGENTS);
-                        R.stage(m, M_MATRICES);
+                        if (!mats_written) R.stage(m, M_MATRICES);
                     }
                 }
             }
