@@ -65,15 +65,16 @@ static double pw_sum(const double* a, int n) {
     return pw_sum(a, n2) + pw_sum(a + n2, n - n2);
 }
 
-/* SPEC tree64: butterfly over 64 slots (zero padded), xor distance 32..1. */
+/* SPEC tree64: over 64 slots (zero padded), a butterfly inside each row of 16 (xor
+ * distance 1, 2, 4, 8), then (R0 + R1) + (R2 + R3) of the four row sums. */
 static double tree64(const double* a, int n) {
     double t[64], u[64];
     for (int i = 0; i < 64; i++) t[i] = i < n ? a[i] : 0.0;
-    for (int s = 32; s >= 1; s >>= 1) {
+    for (int s = 1; s <= 8; s <<= 1) {
         for (int i = 0; i < 64; i++) u[i] = t[i] + t[i ^ s];
         memcpy(t, u, sizeof t);
     }
-    return t[0];
+    return (t[0] + t[16]) + (t[32] + t[48]);
 }
 
 /* SPEC dot2: compensated dot product (Ogita-Rump-Oishi Dot2: TwoProduct by fma,

@@ -66,17 +66,30 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
 __device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
 
-__device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, W); }
+// broadcast from a wave-uniform lane: v_readlane into SGPRs (no LDS-pipe round trip)
+__device__ __forceinline__ double bcast(double v, int src) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
-// lane l <- lane l ^ S, by the cheapest cross-lane path for each distance: DPP
-// quad_perm (1, 2) and row_ror:8 (8), ds_swizzle xor mode (4, 16), ds_bpermute (32)
+// lane l <- lane l ^ S inside a 16-lane row, DPP only (VALU, no LDS-pipe round trip):
+// quad_perm (1, 2), row_shr:4 / row_shl:4 selected by lane bit 2 (4), row_ror:8 (8)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
 template <int S>
 __device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
-    if constexpr (S == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
-    else if constexpr (S == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
-    else if constexpr (S == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
-    else if constexpr (S == 4 || S == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (S << 10) | 0x1F);
-    else return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ S) * 4), (int)v);
+    if constexpr (S == 1) return dpp32<0xB1>(v);
+    else if constexpr (S == 2) return dpp32<0x4E>(v);
+    else if constexpr (S == 8) return dpp32<0x128>(v);
+    else {
+        static_assert(S == 4, "row-local distances only");
+        const uint32_t up = dpp32<0x114>(v), dn = dpp32<0x104>(v);  // lane l-4 | lane l+4
+        return (threadIdx.x & 4) ? up : dn;
+    }
 }
 
 template <int S>
@@ -86,25 +99,29 @@ __device__ __forceinline__ double xor_lane(double v) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// SPEC tree64: butterfly, xor distance 32..1 (every lane ends with the same sum)
+__device__ __forceinline__ double lane_value(double v, int k) {  // lane k's v (k wave-uniform)
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// SPEC tree64: a butterfly inside each 16-lane row (xor 1, 2, 4, 8: every lane of a row
+// ends with the same row sum R_r), then (R0 + R1) + (R2 + R3) from lanes 0, 16, 32, 48
 __device__ __forceinline__ double tree_sum(double v) {
-    v = v + xor_lane<32>(v);
-    v = v + xor_lane<16>(v);
-    v = v + xor_lane<8>(v);
-    v = v + xor_lane<4>(v);
-    v = v + xor_lane<2>(v);
     v = v + xor_lane<1>(v);
-    return v;
+    v = v + xor_lane<2>(v);
+    v = v + xor_lane<4>(v);
+    v = v + xor_lane<8>(v);
+    return (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-    v = fmax(v, xor_lane<32>(v));
-    v = fmax(v, xor_lane<16>(v));
-    v = fmax(v, xor_lane<8>(v));
-    v = fmax(v, xor_lane<4>(v));
-    v = fmax(v, xor_lane<2>(v));
     v = fmax(v, xor_lane<1>(v));
-    return v;
+    v = fmax(v, xor_lane<2>(v));
+    v = fmax(v, xor_lane<4>(v));
+    v = fmax(v, xor_lane<8>(v));
+    return fmax(fmax(lane_value(v, 0), lane_value(v, 16)), fmax(lane_value(v, 32), lane_value(v, 48)));
 }
 
 __device__ __forceinline__ double catch_(double x, double tol) {  // __init__.py:251-258
