@@ -334,7 +334,7 @@ def main():
                          "traffic": traffic, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bpl,
                          "limiter": ("latency / instruction issue, not HBM: one wave64 per LDS-resident "
-                                     "round, 10 rounds per CU (DESIGN.md 5)"),
+                                     "round, 12 rounds per CU (DESIGN.md 5.2)"),
                          "valu": {"insts_per_launch": valu, "issue_ms": valu_ms,
                                   "frac": (valu_ms / kern_ms) if valu_ms else None,
                                   "note": "VALU issue time of the launch's instructions (SQ_INSTS_VALU, "
@@ -348,15 +348,23 @@ def main():
     torch.cuda.empty_cache()
     c5 = c4 = None
     if args.c5_steps > 0:
-        c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
+        # a failure here is recorded in the line; the C3 headline above stands
+        try:
+            c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
+        except Exception as e:  # noqa: BLE001
+            c5 = {"metric": "1M x 4k consensus latency", "n_gpus": world, "error": repr(e)[:400]}
     if args.c4 and world == 1:
-        c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)
+        try:
+            c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001
+            c4 = {"metric": "100k x 1k consensus latency", "error": repr(e)[:400]}
     if rank == 0:
         if c5 is not None:
             line["c5"] = c5
         if c4 is not None:
             line["c4"] = c4
-        if c4 is not None and c5 is not None:  # pageable host->device rate measured on C4's reports
+        if c4 is not None and c5 is not None and "h2d_gbs" in c4 and "rows_per_gpu" in c5:
+            # pageable host->device rate measured on C4's reports
             c5["h2d_ms_estimate"] = 8.0 * c5["rows_per_gpu"] * c5["events"] / (c4["h2d_gbs"] * 1e9) * 1e3
         print(json.dumps(line), flush=True)
     if world > 1:
