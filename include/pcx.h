@@ -243,8 +243,9 @@ typedef struct {
     int32_t n_hard;               /* weighted medians / binary fills replayed in sequential float order */
     int32_t sel_passes;           /* weighted-selection histogram passes                 */
     double  comm_bytes;           /* bytes this rank passed to collectives (all-reduce buffers + all-gather sends) */
-    int32_t grid_events;          /* events whose covariance block ran on int8 MFMA (binary, filled values on {1, 1.5, 2}) */
-    int32_t reserved;
+    int32_t grid_events;          /* grid events (binary, filled values on {1, 1.5, 2}) past the general 128-event tiles:
+                                     their covariance block ran on int8 MFMA */
+    int32_t mixed_int8;           /* 1: general x grid pairs ran on int8 digit slices too (else fp64 MFMA) */
 } pcx_result;
 
 /* The whole consensus (__init__.py:502-611) on this rank's rows; collective over

@@ -111,4 +111,4 @@ class Result(C.Structure):
         ("participation", C.c_double), ("avg_certainty", C.c_double),
         ("branch", C.c_int32), ("flags", C.c_int32), ("pi_iters", C.c_int32), ("components", C.c_int32),
         ("n_hard", C.c_int32), ("sel_passes", C.c_int32), ("comm_bytes", C.c_double),
-        ("grid_events", C.c_int32), ("reserved", C.c_int32)]
+        ("grid_events", C.c_int32), ("mixed_int8", C.c_int32)]

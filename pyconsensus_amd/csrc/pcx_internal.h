@@ -88,13 +88,23 @@ typedef struct {
        of the covariance run on int8 MFMA over z = 2 (F - 1) */
     int32_t* cov_perm;            /* [wcd_ld] event at each wcd position, -1 past E                 */
     int32_t* cov_pos;             /* [E] wcd position of each event                                 */
-    int8_t*  zA;                  /* [wcd_rows/16][zq][16] tok * z of the pure-grid positions        */
-    int8_t*  zB;                  /* [wcd_rows/16][zq][16] z                                        */
+    int8_t*  zA;                  /* [wcd_rows/16][zq][16] tok * z of the positions >= 128 cov_jb, then the token column */
+    int8_t*  zB;                  /* [wcd_rows/16][zq][16] z (the token column: 1)                  */
     int64_t* zsum;                /* [E] sum over this rank's rows of tok * z (grid events, exact)   */
-    int64_t  zq;                  /* pure-grid positions: wcd_ld - 128 * cov_jb                      */
+    int64_t  zq;                  /* int8 operand width: E - 128 cov_jb + 1 rounded up to 256, or 0  */
     int32_t  cov_jb;              /* first pure-grid 128-column tile (= wcd_ld / 128: none)          */
-    int32_t  cov_fp_tiles;        /* fp64 tiles (the trapezoid J < cov_jb of the lower triangle)     */
-    int32_t  cov_i8_tiles;        /* int8 tiles (the lower triangle of the tiles >= cov_jb)          */
+    int32_t  cov_fp_tiles;        /* fp64 tiles: the Jb x Jb triangle (mixed pairs on int8) or the trapezoid J < cov_jb */
+    int32_t  cov_mixed;           /* general x grid pairs on int8 slices of w (M_COV_I8)             */
+    int32_t  tokpos;              /* local int8 position of the token column: E - 128 cov_jb          */
+    /* mixed pairs: w of the general positions (< 128 cov_jb) in 8 balanced int8 digits of 7 bits,
+       fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */
+    int8_t*  zD;                  /* [wcd_rows/16][8 * 128 cov_jb][16] digit s of position q at s * 128 cov_jb + q */
+    double*  dscale;              /* [wcd_ld] 2^-e per general position                               */
+    int32_t* Pgg;                 /* [ks_gg][zq][zq] int32 zA^T zB per k-slice (lower part)           */
+    int32_t* Pmx;                 /* [ks_mx][zq][8 * 128 cov_jb] int32 zA^T zD per k-slice            */
+    int32_t  ks_gg, ks_mx;        /* k-slices of the two int8 products (int32-exact row ranges)       */
+    int32_t  fp_ks;               /* k-slices of the fp64 tiles (k_syrk)                              */
+    int64_t  fp_ld;               /* row length of one fp64 slab: E, or 128 cov_jb when mixed          */
     /* algorithms other than PCA (enum pcx_algorithm) */
     int32_t max_components;       /* "big-five" component count                                     */
     int32_t components;           /* out ("fixed-variance"): components used, else -1               */
@@ -182,7 +192,8 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st);
 hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner
 enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
-                     INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7, INFO_COV_GENERAL = 8 };
+                     INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7, INFO_COV_GENERAL = 8,
+                     INFO_COV_MIXED = 9 };
 hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st);
 
 // pack / unpack of strided dd slot ranges for the slot exchange (runner)

@@ -54,7 +54,7 @@ enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ,
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
-                 IN_COV_GENERAL };
+                 IN_COV_GENERAL, IN_COV_MIXED };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -179,13 +179,17 @@ __global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
     }
 }
 
-// reduce spart[nblk][4 dd] slots src0 .. src0+k into scal[rank][slot0 .. slot0+k)
-__global__ void __launch_bounds__(64) k_spart_finish(pcx_mat m, int nblk, int k, int slot0, int src0 = 0) {
-    const int j = threadIdx.x;
+// reduce spart[nblk][4 dd] slots src0 .. src0+k into scal[rank][slot0 .. slot0+k): one
+// block per slot, a fixed strided assignment of the row-pass blocks to threads and a fixed
+// dd tree (deterministic)
+__global__ void __launch_bounds__(BT) k_spart_finish(pcx_mat m, int nblk, int k, int slot0, int src0 = 0) {
+    __shared__ dd lds[BT / WAVE];
+    const int j = blockIdx.x;
     if (j >= k) return;
     dd r{0.0, 0.0};
-    for (int b = 0; b < nblk; b++) r = dd_add(r, ld_dd(m.spart + b * 8 + 2 * (src0 + j)));
-    st_dd(m.scal + ((int64_t)m.rank * SS + slot0 + j) * 2, r);
+    for (int b = threadIdx.x; b < nblk; b += BT) r = dd_add(r, ld_dd(m.spart + b * 8 + 2 * (src0 + j)));
+    r = block_sum_dd<BT>(r, lds);
+    if (threadIdx.x == 0) st_dd(m.scal + ((int64_t)m.rank * SS + slot0 + j) * 2, r);
 }
 
 // ================================================================== column passes
@@ -513,6 +517,34 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
         __syncthreads();
     }
     for (int64_t p = E + tid; p < m.wcd_ld; p += 1024) m.cov_perm[p] = -1;
+    // mixed pairs (a general position q < 128 jb with a grid one) on int8 slices of w: the
+    // fixed-point exponent of each general position from the bound of |F - mu| over its
+    // present values (all ranks) and its fill; any non-finite bound keeps them on fp64
+    __syncthreads();
+    const int G = base[0];
+    const int gb = (G + CT - 1) / CT * CT;
+    int bad = 0;
+    if (!big && gb > 0 && gb < E) {
+        for (int q = tid; q < gb; q += 1024) {
+            const int c = m.cov_perm[q];
+            const double mu = m.ev[EV_MU * E + c];
+            double bnd = 0.0;
+            if (m.ev[EV_MISS * E + c] < (double)m.n_total) {  // some present report
+                double mn = __builtin_inf(), mx = -__builtin_inf();
+                for (int w = 0; w < m.world; w++) {
+                    mn = fmin(mn, m.cmax[((int64_t)w * E + c) * CM + 2]);
+                    mx = fmax(mx, m.cmax[((int64_t)w * E + c) * CM + 3]);
+                }
+                bnd = fmax(fabs(mx - mu), fabs(mn - mu));
+            }
+            if (m.ev[EV_MISS * E + c] > 0.0) bnd = fmax(bnd, fabs(m.ev[EV_GUESS * E + c] - mu));
+            if (!__builtin_isfinite(bnd) || __builtin_isnan(mu)) bad = 1;
+            // |w| <= bnd < 2^(ilogb + 1): |w| 2^-e <= 1/2 with e = ilogb + 2 (first digit |d| <= 64)
+            m.dscale[q] = bnd > 0.0 && __builtin_isfinite(bnd) ? ldexp(1.0, -(ilogb(bnd) + 2)) : 1.0;
+        }
+    }
+    bad = __syncthreads_or(bad);
+    if (tid == 0) m.info[IN_COV_MIXED] = (!big && gb > 0 && gb < E && !bad) ? 1 : 0;
 }
 
 // PCX_M_WCD: wcd = F - mu (:317-322) materialised once, [wcd_rows][wcd_ld] in the
@@ -754,16 +786,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
     extern __shared__ __attribute__((aligned(16))) double sy_lds[];
     const int E = (int)m.n_events;
-    const int ntiles = m.cov_fp_tiles, nks = m.cov_kslices;
+    const int ntiles = m.cov_fp_tiles, nks = m.fp_ks;
     const int nb = (int)(m.wcd_ld / CT);
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / ntiles;
     int J = 0, I = item % ntiles;
-    while (I >= nb - J) {  // column J of the trapezoid holds tiles I = J .. nb-1
-        I -= nb - J;
-        J++;
+    if (m.cov_mixed) {
+        tri_index(I, I, J);  // the Jb x Jb triangle of general tiles
+    } else {
+        while (I >= nb - J) {  // column J of the trapezoid holds tiles I = J .. nb-1
+            I -= nb - J;
+            J++;
+        }
+        I += J;
     }
-    I += J;
     const int64_t nst = m.wcd_rows / SY_BK;
     const int64_t per = (nst + nks - 1) / nks;
     const int64_t s0 = ks * per < nst ? ks * per : nst;
@@ -775,78 +811,169 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
         syrk_tile<false>(m.wcd, m.tokp, m.wcd_ld, I, J, s0, s1 - s0, sy_lds, acc);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wr = wv >> 1, wc = wv & 1;
-    double* out = m.cslab + (int64_t)ks * E * E;
+    const int64_t ld = m.fp_ld, pmax = ld < E ? ld : E;
+    double* out = m.cslab + (int64_t)ks * ld * ld;
     for (int a = 0; a < 4; a++)
         for (int b = 0; b < 4; b++)
             for (int r = 0; r < 4; r++) {
                 const int64_t p = (int64_t)I * CT + wr * 64 + a * 16 + (lane >> 4) + 4 * r;
                 const int64_t q = (int64_t)J * CT + wc * 64 + b * 16 + (lane & 15);
-                if (p < E && q <= p) out[p * E + q] = acc[a][b][r];
+                if (p < pmax && q <= p) out[p * ld + q] = acc[a][b][r];
             }
 }
 
-// PCX_M_COV_I8: P = zA^T zB over one row slice for one 128x128 tile of the pure-grid
-// positions (lower triangle), on int8 MFMA (v_mfma_i32_16x16x64_i8, exact int32
-// accumulation: |P| <= 4 sum tok <= 4e6).  Each lane's A / B fragment is 16 rows of one
-// position -- one 16-byte load from the [row / 16][position][16] blocks, no LDS -- and the
-// next k-step's fragments are loaded while this step's 16 MFMAs run.  4 waves in 2x2,
-// 64x64 per wave.  P goes to cslab[ks] as exact doubles; k_cov_reduce combines.
+// PCX_M_COV_I8: exact integer products on int8 MFMA (v_mfma_i32_16x16x64_i8).  Operands are
+// [row / 16][position][16] int8 blocks, so one 16-byte load is one lane's MFMA fragment (16
+// rows of one position).  256 x 256 output tiles, 8 waves of 128 x 64 (32 int32
+// accumulators each); 64-row stages of both 16 KB panels go to LDS by global_load_lds in a
+// four-stage ring (three stages in flight under the MFMAs -- the loads' latency is several
+// stages long -- one barrier per stage, counted vmcnt); each k-slice's int32 tile is stored
+// to its own slab (k_cov_reduce sums the slabs in int64).  Tiles run k-slice major and
+// XCD-grouped, so the WGs resident at once stream the same rows through L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int GT = 256;                              // output tile edge
+constexpr int G_NBUF = 4;                            // LDS ring depth
+constexpr int G_LPW = 4;                             // global_load_lds per wave per stage
+constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one operand's 64-row stage: 16 KB
+constexpr size_t G_LDS_BYTES = G_NBUF * 2 * G_PANEL; // 128 KB
 
-__global__ void __launch_bounds__(256) k_syrk_i8(pcx_mat m) {
-    const int E = (int)m.n_events;
-    const int ntiles = m.cov_i8_tiles, nks = m.cov_kslices;
+struct GemmI8 {
+    const int8_t* A;
+    int64_t lda;  // positions per row group
+    const int8_t* B;
+    int64_t ldb;
+    int32_t* out;  // [kslices][slab]: row p at p * ldo
+    int64_t ldo, slab;
+    int np, nq, tp, tq, lower, kslices;
+    int64_t rg;  // row groups, a multiple of 4
+};
+
+constexpr int G_THREADS = 512;  // 2 x 4 waves of 128 x 64
+
+__global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
+    extern __shared__ __attribute__((aligned(16))) char glds[];
+    const int ntiles = g.tp * g.tq;
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / ntiles, t = item % ntiles;
-    int I, J;
-    tri_index(t, I, J);
-    const int64_t RG = m.wcd_rows / 16;  // 16-row groups
-    const int64_t nst = (RG + 3) / 4;     // 64-row k-steps
-    const int64_t per = (nst + nks - 1) / nks;
+    const int ip = t / g.tq, iq = t % g.tq;
+    if (g.lower && iq > ip) return;  // above the diagonal (square tiles)
+    const int64_t nst = g.rg / 4;
+    const int64_t per = (nst + g.kslices - 1) / g.kslices;
     const int64_t s0 = ks * per < nst ? ks * per : nst;
-    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;  // (an empty slice stores zeros)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int wr = wv >> 1, wc = wv & 1;
+    const int wr = wv >> 2, wc = wv & 3;  // 2 x 4 waves: 128 p x 64 q each
     const int lc = lane & 15, lg = lane >> 4;
-    const v4i* A = (const v4i*)m.zA + I * CT + wr * 64 + lc;
-    const v4i* B = (const v4i*)m.zB + J * CT + wc * 64 + lc;
-    const int64_t zq = m.zq;
-    v4i acc[4][4];
-    for (int a = 0; a < 4; a++)
-        for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
-    v4i af[4], bf[4];
-    auto load = [&](int64_t s) {
-        const int64_t g = s * 4 + lg;
-        const bool okg = g < RG;
+    // this wave moves row group (wv & 3) of each stage, half (wv >> 2) of both panels
+    const int mg = wv & 3, mh = wv >> 2;
+    const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 128 + lane) * 16;
+    const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 128 + lane) * 16;
+    auto issue = [&](int64_t st, int buf) {
+        char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 128) * 16;
+        const int64_t grp = st * 4 + mg;
 #pragma unroll
-        for (int a = 0; a < 4; a++) af[a] = okg ? A[g * zq + a * 16] : v4i{0, 0, 0, 0};
+        for (int j = 0; j < 2; j++)
+            __builtin_amdgcn_global_load_lds((const void*)(Ab + (grp * g.lda + j * 64) * 16),
+                                             (lds_ptr_t)(base + (size_t)j * 64 * 16), 16, 0, 0);
 #pragma unroll
-        for (int b = 0; b < 4; b++) bf[b] = okg ? B[g * zq + b * 16] : v4i{0, 0, 0, 0};
+        for (int j = 0; j < 2; j++)
+            __builtin_amdgcn_global_load_lds((const void*)(Bb + (grp * g.ldb + j * 64) * 16),
+                                             (lds_ptr_t)(base + G_PANEL + (size_t)j * 64 * 16), 16, 0, 0);
     };
-    if (s0 < s1) load(s0);
-    for (int64_t s = s0; s < s1; s++) {
-        v4i ca[4], cb[4];
+    v4i acc[8][4];
 #pragma unroll
-        for (int a = 0; a < 4; a++) {
-            ca[a] = af[a];
-            cb[a] = bf[a];
-        }
-        if (s + 1 < s1) load(s + 1);
+    for (int a = 0; a < 8; a++)
 #pragma unroll
-        for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
+    const int64_t n = s1 - s0;
 #pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ca[a], cb[b], acc[a][b], 0, 0, 0);
+    for (int k = 0; k < G_NBUF - 1; k++)
+        if (k < n) issue(s0 + k, k);
+    for (int64_t t = 0; t < n; t++) {
+        const int buf = (int)(t % G_NBUF);
+        if (t + G_NBUF - 2 < n)
+            wait_vmcnt<G_LPW * (G_NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
+        else
+            wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + G_NBUF - 1 < n) issue(s0 + t + G_NBUF - 1, (int)((t + G_NBUF - 1) % G_NBUF));
+        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * 128 + lc;
+        const v4i* Bs = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL + G_PANEL) + lg * GT + wc * 64 + lc;
+        v4i af[8], bf[4];
+#pragma unroll
+        for (int a = 0; a < 8; a++) af[a] = As[a * 16];
+#pragma unroll
+        for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+        asm volatile("" ::: "memory");
     }
     // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
-    const int64_t gb = (int64_t)m.cov_jb * CT;
-    double* out = m.cslab + (int64_t)ks * E * E;
-    for (int a = 0; a < 4; a++)
+    const int p0 = ip * GT + wr * 128 + 4 * lg, q0 = iq * GT + wc * 64 + lc;
+    int32_t* out = g.out + (int64_t)ks * g.slab;
+#pragma unroll
+    for (int a = 0; a < 8; a++)
+#pragma unroll
         for (int b = 0; b < 4; b++)
+#pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int64_t p = gb + I * CT + wr * 64 + a * 16 + 4 * lg + r;
-                const int64_t q = gb + J * CT + wc * 64 + b * 16 + lc;
-                if (p < E && q <= p) out[p * E + q] = (double)acc[a][b][r];
+                const int p = p0 + a * 16 + r, q = q0 + b * 16;
+                if (p < g.np && q < g.nq && (!g.lower || q <= p)) out[(int64_t)p * g.ldo + q] = acc[a][b][r];
             }
+}
+
+// the token column of the int8 operands: zA = tok (<= 63), zB = 1 on live rows
+__global__ void __launch_bounds__(BT) k_tokcol(pcx_mat m) {
+    const int64_t grp = blockIdx.x * (int64_t)BT + threadIdx.x;
+    if (grp >= m.wcd_rows / 16) return;
+    uint32_t ta[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int64_t i = grp * 16 + r;
+        if (i < m.n_rows) {
+            ta[r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)m.tok[i] << (8 * (r & 3));
+            tb[r >> 2] |= 1u << (8 * (r & 3));
+        }
+    }
+    const int64_t o = (grp * m.zq + m.tokpos) * 16;
+    *(uint4*)(m.zA + o) = uint4{ta[0], ta[1], ta[2], ta[3]};
+    *(uint4*)(m.zB + o) = uint4{tb[0], tb[1], tb[2], tb[3]};
+}
+
+// w of the general positions q < gb as 8 balanced base-128 digits of w 2^-e (|w 2^-e| <= 1/2):
+// t = 128 v, d = rint(t), v = t - d -- every step exact, |d| <= 64, residue <= 2^-57 2^e
+__global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
+    const int gb = m.cov_jb * CT;
+    const int q = blockIdx.x * BT + threadIdx.x;
+    if (q >= gb) return;
+    const double sc = m.dscale[q];
+    const int64_t ng = m.wcd_rows / 16;
+    const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
+    const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
+    const int64_t ldd = (int64_t)8 * gb;
+    for (int64_t grp = g0; grp < g1; grp++) {
+        uint32_t d[8][4];
+#pragma unroll
+        for (int k = 0; k < 8; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            double v = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const double t = v * 128.0;
+                const double di = rint(t);
+                v = t - di;
+                d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
+    }
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -910,17 +1037,42 @@ __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
     const int64_t p = idx / E, q = idx % E;
     if (q > p) return;
     double s = 0.0;
-    for (int k = 0; k < m.cov_kslices; k++) s += m.cslab[(int64_t)k * E * E + p * E + q];
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int64_t cp = m.cov_perm[p], cq = m.cov_perm[q];
-    if (q >= gb) {
+    if (q < gb && (!m.cov_mixed || p < gb)) {  // fp64 tiles: the slabs of k_syrk
+        const int64_t ld = m.fp_ld;
+        for (int k = 0; k < m.fp_ks; k++) s += m.cslab[(int64_t)k * ld * ld + p * ld + q];
+    } else if (q >= gb) {  // grid x grid: P from the int8 products
+        int64_t Pi = 0;
+        for (int k = 0; k < m.ks_gg; k++) Pi += m.Pgg[(int64_t)k * m.zq * m.zq + (p - gb) * m.zq + (q - gb)];
+        const double P = (double)Pi;
         const double T = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
         const double ap = 1.0 - m.ev[EV_MU * E + cp], aq = 1.0 - m.ev[EV_MU * E + cq];
         const double Zp = 0.5 * (double)m.zsum[cp], Zq = 0.5 * (double)m.zsum[cq];
         dd r = dd_mul_d(two_prod(ap, aq), T);
         r = dd_add(r, dd_add(two_prod(ap, Zq), two_prod(aq, Zp)));
-        r = dd_add(r, dd{0.25 * s, 0.0});
+        r = dd_add(r, dd{0.25 * P, 0.0});
         s = dd_to_double(r);
+    } else if (p >= gb && m.cov_mixed) {
+        // general q x grid p: sum tok w_q (c_p + z_p / 2) = c_p S_q + Q_pq / 2, with S_q (the
+        // token column) and Q_pq = sum tok z_p w_q from the digit products, Horner in dd
+        const int64_t ldm = (int64_t)8 * gb;
+        const double sc = ldexp(0x1p-7, -ilogb(m.dscale[q]));  // 2^(e - 7)
+        auto comb = [&](int64_t row) {
+            const int32_t* P = m.Pmx + row * ldm + q;
+            const int64_t slab = m.zq * ldm;
+            auto digit = [&](int d) {  // sum over the k-slice slabs
+                int64_t v = 0;
+                for (int k = 0; k < m.ks_mx; k++) v += P[(int64_t)k * slab + (int64_t)d * gb];
+                return (double)v;
+            };
+            dd a{digit(7), 0.0};
+            for (int d = 6; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{digit(d), 0.0});
+            return dd_mul_d(a, sc);
+        };
+        const dd S = comb(m.tokpos), Q = comb(p - gb);
+        const double ap = 1.0 - m.ev[EV_MU * E + cp];
+        s = dd_to_double(dd_add(dd_mul_d(S, ap), dd_mul_d(Q, 0.5)));
     }
     m.C[cp * E + cq] = s;
     m.C[cq * E + cp] = s;
@@ -2743,8 +2895,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_REPUTATION:
             if (m.rep_raw) hipLaunchKernelGGL(k_rep_total, dim3(1), dim3(1024), 0, st, m);
             hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_TOK, 0);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 1, (int)SC_BIGTOK, 2);
+            hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_TOK, 0);
+            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(BT), 0, st, m, rg, 1, (int)SC_BIGTOK, 2);
             break;
         case M_COLSTATS:
             hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
@@ -2765,21 +2917,47 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_COV_I8: {
             const int nb = (int)(m.wcd_ld / CT);
-            if (!m.zA || !m.zB || !m.zsum || m.cov_jb < 0 || m.cov_jb > nb || m.zq != (int64_t)(nb - m.cov_jb) * CT ||
-                m.cov_i8_tiles != (nb - m.cov_jb) * (nb - m.cov_jb + 1) / 2 || m.wcd_rows % 16) {
+            if (m.cov_jb >= nb && m.zq == 0) break;  // no grid events
+            const int gb = m.cov_jb * CT;
+            const int np = (int)(m.n_events - gb) + 1;  // grid positions + the token column
+            if (!m.zA || !m.zB || !m.zsum || !m.Pgg || m.cov_jb < 0 || m.cov_jb > nb || m.zq < np || m.ks_gg < 1 ||
+                (m.cov_mixed && m.ks_mx < 1) ||
+                m.zq % GT || m.tokpos != np - 1 || m.wcd_rows % 64 || (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale))) {
                 err = "M_COV_I8: int8 operands missing or plan inconsistent";
                 return hipErrorInvalidValue;
             }
-            if (m.cov_i8_tiles > 0)
-                hipLaunchKernelGGL(k_syrk_i8, dim3(m.cov_i8_tiles * m.cov_kslices), dim3(256), 0, st, m);
+            static std::once_flag g_once;
+            static hipError_t g_err = hipSuccess;
+            std::call_once(g_once, [] {
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)G_LDS_BYTES);
+            });
+            if (g_err != hipSuccess) return g_err;
+            const int64_t rg = m.wcd_rows / 16;
+            hipLaunchKernelGGL(k_tokcol, dim3((unsigned)((rg + BT - 1) / BT)), dim3(BT), 0, st, m);
+            {  // grid x grid (lower tiles): |tok z z| <= 252 per row
+                GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg};
+                g.tp = g.tq = (np + GT - 1) / GT;
+                hipLaunchKernelGGL(k_gemm_i8, dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(G_THREADS), G_LDS_BYTES, st, g);
+            }
+            if (m.cov_mixed) {  // grid x general digits: |tok z d| <= 126 * 64 per row
+                const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
+                hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
+                GemmI8 g{m.zA, m.zq, m.zD, (int64_t)8 * gb, m.Pmx, (int64_t)8 * gb, m.zq * 8 * gb, np, 8 * gb,
+                         0, 0, 0, m.ks_mx, rg};
+                g.tp = (np + GT - 1) / GT;
+                g.tq = (8 * gb + GT - 1) / GT;
+                hipLaunchKernelGGL(k_gemm_i8, dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(G_THREADS), G_LDS_BYTES, st, g);
+            }
             break;
         }
         case M_WCD:
         case M_COV: {
             const int nb = (int)(m.wcd_ld / CT);
-            if (!m.wcd || !m.tokp || !m.rowpart || !m.cov_perm || !m.cov_pos || m.wcd_rows % 16 ||
+            if (!m.wcd || !m.tokp || !m.rowpart || !m.cov_perm || !m.cov_pos || m.wcd_rows % 64 ||
                 m.wcd_rows < m.n_rows || m.wcd_ld % CT || m.wcd_ld < m.n_events || m.cov_jb < 0 || m.cov_jb > nb ||
-                m.cov_fp_tiles != m.cov_jb * nb - m.cov_jb * (m.cov_jb - 1) / 2 ||
+                m.cov_fp_tiles != (m.cov_mixed ? m.cov_jb * (m.cov_jb + 1) / 2
+                                                : m.cov_jb * nb - m.cov_jb * (m.cov_jb - 1) / 2) ||
                 (m.cov_jb < nb && (!m.zA || !m.zB || !m.zsum))) {
                 err = "M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128) or no plan";
                 return hipErrorInvalidValue;
@@ -2799,7 +2977,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             });
             if (lds_err != hipSuccess) return lds_err;
             if (m.cov_fp_tiles > 0)
-                hipLaunchKernelGGL(k_syrk, dim3(m.cov_fp_tiles * m.cov_kslices), dim3(256), SY_LDS_BYTES, st, m);
+                hipLaunchKernelGGL(k_syrk, dim3(m.cov_fp_tiles * m.fp_ks), dim3(256), SY_LDS_BYTES, st, m);
             break;
         }
         case M_COV_REDUCE: {
@@ -2822,7 +3000,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_NCSUMS:
             hipLaunchKernelGGL(k_ncsums, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 4, (int)SC_A1);
+            hipLaunchKernelGGL(k_spart_finish, dim3(4), dim3(BT), 0, st, m, rg, 4, (int)SC_A1);
             break;
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
@@ -2836,7 +3014,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_REPU:
             hipLaunchKernelGGL(k_repu, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_U);
+            hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_U);
             break;
         case M_SMOOTH:
             hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);
@@ -2856,7 +3034,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_ROWSUMS:
             hipLaunchKernelGGL(k_rowsums, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(64), 0, st, m, rg, 2, (int)SC_AR);
+            hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_AR);
             break;
         case M_AGENTS:
             hipLaunchKernelGGL(k_agents, dim3(rg), dim3(BT), 0, st, m);

@@ -30,7 +30,7 @@ constexpr int CM = 8;   // doubles per column in mpart / cmax
 constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
-constexpr int COV_STAGE = 16;
+constexpr int COV_STAGE = 64;  // wcd rows: whole 64-row stages of the int8 GEMM
 constexpr int SELS = 24;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
@@ -62,10 +62,27 @@ struct pcx_workspace {
     int32_t *cov_perm, *cov_pos;
     int8_t *zA, *zB;
     int64_t* zsum;
+    double* dscale;
+    // sized by the data (the grid / general split), grown on demand
+    struct Grow {
+        void* p = nullptr;
+        size_t bytes = 0;
+    } pgg, zd, pmx;
+    bool grow(Grow& g, size_t need) {
+        if (g.bytes >= need) return true;
+        if (g.p) (void)hipFree(g.p);
+        g.p = nullptr;
+        g.bytes = 0;
+        if (hipMalloc(&g.p, need) != hipSuccess) return false;
+        g.bytes = need;
+        return true;
+    }
     int64_t xcap = 0;  // doubles per rank in xsend
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
+        for (Grow* g : {&pgg, &zd, &pmx})
+            if (g->p) (void)hipFree(g->p);
     }
 };
 
@@ -243,8 +260,9 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
         {(void**)&w->tokp, (size_t)(w->wcd_rows + 64) * 8, false},
         {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
-        {(void**)&w->zA, (size_t)(w->wcd_rows * w->wcd_ld), false},
-        {(void**)&w->zB, (size_t)(w->wcd_rows * w->wcd_ld), false},
+        {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
+        {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
+        {(void**)&w->dscale, (size_t)w->wcd_ld * 8, false},
     };
     auto align = [](size_t b) { return (b + 255) / 256 * 256; };
     size_t zb = 0;
@@ -649,6 +667,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         r->n_hard = 0;
         r->sel_passes = 0;
         r->grid_events = 0;
+        r->mixed_int8 = 0;
 
         const double* cstat = w->cstat;
         (void)cstat;
@@ -678,15 +697,54 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.zA = w->zA;
                 m.zB = w->zB;
                 m.zsum = w->zsum;
+                m.dscale = w->dscale;
                 R.stage(m, M_COV_PLAN);
-                const int64_t n_general = R.read(m.info + INFO_COV_GENERAL);
-                r->grid_events = (int32_t)(E - n_general);
+                int64_t plan[2];  // general events, mixed pairs on int8
+                R.hip(hipMemcpyAsync(plan, m.info + INFO_COV_GENERAL, sizeof(plan), hipMemcpyDeviceToHost, R.st),
+                      "D2H plan");
+                R.sync();
+                const int64_t n_general = plan[0];
                 const int64_t nb = w->wcd_ld / COV_TILE;
-                const int64_t jb = (n_general + COV_TILE - 1) / COV_TILE;
+                const int64_t jb = (n_general + COV_TILE - 1) / COV_TILE, gb = jb * COV_TILE;
                 m.cov_jb = (int32_t)jb;
-                m.zq = (nb - jb) * COV_TILE;
-                m.cov_fp_tiles = (int32_t)(jb * nb - jb * (jb - 1) / 2);
-                m.cov_i8_tiles = (int32_t)((nb - jb) * (nb - jb + 1) / 2);
+                const int64_t np = gb < E ? E - gb + 1 : 0;  // grid positions + the token column
+                m.zq = (np + 255) / 256 * 256;
+                m.tokpos = (int32_t)(np - 1);
+                r->grid_events = (int32_t)(np > 0 ? E - gb : 0);  // grid events past the general tiles
+                // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
+                // |tok z d| <= 126 * 64 per row) and at least two WGs per CU
+                const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (8 * gb + 255) / 256;
+                auto ks_for = [&](int64_t tiles, int64_t max_rows) {
+                    tiles = std::max<int64_t>(1, tiles);
+                    int64_t k = std::max<int64_t>((w->wcd_rows + max_rows - 1) / max_rows, (512 + tiles - 1) / tiles);
+                    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(k, nst));
+                };
+                m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000);
+                m.ks_mx = ks_for(tp * tq, 250000);
+                if (np > 0 && !w->grow(w->pgg, (size_t)(m.ks_gg * m.zq * m.zq * 4))) {
+                    err = "workspace: hipMalloc of the int8 covariance products failed";
+                    throw Fail{PCX_ENOMEM};
+                }
+                m.Pgg = (int32_t*)w->pgg.p;
+                // mixed pairs on int8 digits when the bounds are finite and the memory is there
+                m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * 8 * gb)) &&
+                                      w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * 8 * gb * 4))
+                                  ? 1
+                                  : 0;
+                r->mixed_int8 = m.cov_mixed;
+                m.zD = (int8_t*)w->zd.p;
+                m.Pmx = (int32_t*)w->pmx.p;
+                m.cov_fp_tiles = (int32_t)(m.cov_mixed ? jb * (jb + 1) / 2 : jb * nb - jb * (jb - 1) / 2);
+                // fp64 slabs: [E][E] for the trapezoid; the mixed triangle's [gb][gb] slabs are
+                // small, so it takes more k-slices (~16 WGs per CU) within the same cslab
+                m.fp_ld = m.cov_mixed ? gb : E;
+                m.fp_ks = (int32_t)w->cov_kslices;
+                if (m.cov_mixed && m.cov_fp_tiles > 0) {
+                    const int64_t want = (16 * 256 + m.cov_fp_tiles - 1) / m.cov_fp_tiles;
+                    const int64_t cap = std::min<int64_t>(w->cov_kslices * E * E / (gb * gb),
+                                                          std::max<int64_t>(1, w->wcd_rows / (8 * 8)));
+                    m.fp_ks = (int32_t)std::max<int64_t>(1, std::min(want, cap));
+                }
                 R.stage(m, M_WCD);
                 mats_written = true;
                 R.stage(m, M_COV);

@@ -289,7 +289,8 @@ def _meta(res, algorithm):
     return {"participation": res.participation, "avg_certainty": res.avg_certainty,
             "branch": int(res.branch), "pi_iters": int(res.pi_iters), "flags": int(res.flags),
             "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes),
-            "comm_bytes": float(res.comm_bytes), "grid_events": int(res.grid_events)}
+            "comm_bytes": float(res.comm_bytes), "grid_events": int(res.grid_events),
+            "mixed_int8": int(res.mixed_int8)}
 
 
 # ---------------------------------------------------------------- host-memory entry points

@@ -2,7 +2,8 @@
 
 Binary events whose filled values all lie on {1, 1.5, 2} ("grid" events) take the wcd
 positions after the general events; the covariance tiles made only of grid positions are
-P = sum tok z z^T on int8 MFMA with z = 2 (F - 1), combined with the exact T and Z sums.
+P = sum tok z z^T on int8 MFMA with z = 2 (F - 1), combined with the exact T and Z sums;
+the general x grid pairs multiply eight int8 digit slices of w = F - mu with tok z.
 The wpca entry's covariance is checked against the reference formula
 (pyconsensus/__init__.py:317-326) evaluated in numpy: all-general, mixed, all-grid,
 varying tokens (tok * z operand), off-grid values and tokens above 63 (no int8 path).
@@ -43,7 +44,8 @@ CASES = {
     "mixed_int_rep": (40000, 300, 0.25, "int", (), True),
     "offgrid_events": (40000, 300, 0.25, None, (3, 150, 299), True),
     "tokens_above_63": (3000, 300, 0.25, "int", (), False),
-    "single_tile": (20000, 100, 0.3, None, (), True),
+    "single_tile": (20000, 100, 0.3, None, (), True),  # general and grid share the one tile: fp64
+    "two_tiles": (20000, 200, 0.3, None, (), True),
 }
 
 
@@ -57,7 +59,10 @@ def test_wpca_covariance_grid(name):
     outs, meta = wpca_host(F, rep)
     mu, cov = _ref(F, rep)
     n_grid = int(E - sc.sum() - len([c for c in og if not sc[c]]))
-    assert meta["grid_events"] == (n_grid if expect else 0), (meta["grid_events"], n_grid)
+    gb = -(-(E - n_grid) // 128) * 128  # general events take the first 128-event tiles
+    assert meta["grid_events"] == (max(0, E - gb) if expect else 0), (meta["grid_events"], n_grid)
+    # general x grid pairs on int8 digit slices whenever both kinds of tile are present
+    assert meta["mixed_int8"] == (1 if expect and 0 < gb < E else 0)
     np.testing.assert_allclose(outs["weighted_mean"], mu, rtol=1e-14, atol=0)
     scale = np.abs(cov).max()
     err = np.abs(outs["covariance"] - cov).max() / scale
