@@ -219,6 +219,7 @@ def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
         return None
 
 
+C5_TIMEOUT_S = 300          # multi-rank C5 watchdog (bench main)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 VALU_ISSUE_CYCLES = 4      # a wave64 VALU instruction holds its SIMD 4 cycles
 SIMDS, CLOCK_GHZ = 1024, 2.4
@@ -352,11 +353,29 @@ def main():
     torch.cuda.empty_cache()
     c5 = c4 = None
     if args.c5_steps > 0:
-        # a failure here is recorded in the line; the C3 headline above stands
+        # a failure here is recorded in the line; the C3 headline above stands.  With several
+        # ranks a watchdog also guards against a stuck collective: after C5_TIMEOUT_S every rank
+        # exits, rank 0 first printing the C3 line with the C5 entry marked.
+        watchdog = None
+        if world > 1:
+            import threading
+
+            def on_timeout():
+                if rank == 0:
+                    line["c5"] = {"metric": "1M x 4k consensus latency", "n_gpus": world,
+                                  "error": "timed out after %d s" % C5_TIMEOUT_S}
+                    print(json.dumps(line), flush=True)
+                os._exit(0)
+
+            watchdog = threading.Timer(C5_TIMEOUT_S, on_timeout)
+            watchdog.daemon = True
+            watchdog.start()
         try:
             c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
         except Exception as e:  # noqa: BLE001
             c5 = {"metric": "1M x 4k consensus latency", "n_gpus": world, "error": repr(e)[:400]}
+        if watchdog is not None:
+            watchdog.cancel()
     if args.c4 and world == 1:
         try:
             c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)

@@ -629,8 +629,8 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                         }
                     }
 #pragma unroll
-                    for (int k = 0; k < 2; k++)
-                        if (pos[k] >= 0) m.wcd[i * ld + pos[k]] = w[k];
+                    for (int k = 0; k < 2; k++)  // mixed_int8: the grid positions live in zA / zB only
+                        if (pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb)) m.wcd[i * ld + pos[k]] = w[k];
                     // result["original"] / result["filled"] (:266-313), event order
                     if (live && (m.original || m.filled)) {
                         const int64_t o = i * E + c0;
@@ -1274,6 +1274,84 @@ __global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
         kmin = k < kmin ? k : kmin;
         kmax = k > kmax ? k : kmax;
     }
+    if (lane == 0) {
+        uint64_t* sk = m.skey + (int64_t)m.rank * 4;
+        atomicMin((unsigned long long*)&sk[0], (unsigned long long)kmin);
+        atomicMax((unsigned long long*)&sk[1], (unsigned long long)kmax);
+        if (anynan) atomicOr((unsigned long long*)&sk[2], 1ull);
+    }
+}
+
+// PCX_M_SCORES with mixed_int8 (wcd holds only the general positions): one wave per 16-row
+// group; general positions from wcd, grid positions from the int8 codes, F - mu = c + z / 2:
+//   s_i = sum_{q < gb} wcd_iq ld_q + K + (1/2) sum_{q >= gb} z_iq ld_q,  K = sum_{q >= gb} c_q ld_q
+__global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
+    const int lane = threadIdx.x % WAVE, wv = threadIdx.x / WAVE;
+    const int64_t ld = m.wcd_ld;
+    const int ncb = (int)((ld + WCD_COLS - 1) / WCD_COLS);
+    const int E = (int)m.n_events;
+    const double* LD = m.ev + (m.algorithm == 0 ? EV_LD : EV_SPARE) * E;
+    const int gb = m.cov_jb * CT, ng = E - gb;
+    double kk = 0.0;
+    for (int q = lane; q < ng; q += WAVE) {
+        const int c = m.cov_perm[gb + q];
+        kk = fma(1.0 - m.ev[EV_MU * E + c], LD[c], kk);
+    }
+    const double K = wave_sum_d(kk);
+    uint64_t kmin = ~0ull, kmax = 0;
+    bool anynan = false;
+    const int64_t ngrp = (m.n_rows + 15) / 16;
+    for (int64_t g = blockIdx.x * (int64_t)(BT / WAVE) + wv; g < ngrp; g += (int64_t)gridDim.x * (BT / WAVE)) {
+        double a[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) a[r] = 0.0;
+        for (int q = lane; q < gb; q += WAVE) {
+            const double l = LD[m.cov_perm[q]];
+            const double* w = m.wcd + g * 16 * ld + q;
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
+        }
+        double z[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) z[r] = 0.0;
+        for (int q = lane; q < ng; q += WAVE) {
+            const double l = LD[m.cov_perm[gb + q]];
+            const uint4 zb = *(const uint4*)(m.zB + (g * m.zq + q) * 16);
+            const uint32_t wd[4] = {zb.x, zb.y, zb.z, zb.w};
+#pragma unroll
+            for (int r = 0; r < 16; r++) z[r] = fma((double)((wd[r >> 2] >> (8 * (r & 3))) & 0xffu), l, z[r]);
+        }
+        double mine = 0.0;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const double sr = wave_sum_d(fma(0.5, z[r], a[r])) + K;
+            if (lane == r) mine = sr;
+        }
+        const int64_t i = g * 16 + (lane & 15);
+        if (lane < 16 && i < m.n_rows) {
+            m.rowv[RV_S * m.n_rows + i] = mine;
+            if (__builtin_isnan(mine)) anynan = true;
+            const uint64_t k = dkey(mine);
+            kmin = k < kmin ? k : kmin;
+            kmax = k > kmax ? k : kmax;
+        }
+        if (lane < 32) {  // row NaN / zero counts from k_wcd's column-block partials
+            const int64_t ir = g * 16 + (lane >> 1);
+            if (ir < m.n_rows) {
+                uint32_t t = 0;
+                for (int b = 0; b < ncb; b++) t += m.rowpart[((int64_t)b * m.wcd_rows + ir) * 2 + (lane & 1)];
+                m.rowstat[2 * ir + (lane & 1)] = t;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t a = (uint64_t)__shfl_xor((long long)kmin, o, WAVE);
+        const uint64_t b = (uint64_t)__shfl_xor((long long)kmax, o, WAVE);
+        kmin = a < kmin ? a : kmin;
+        kmax = b > kmax ? b : kmax;
+    }
+    anynan = __ballot(anynan) != 0;
     if (lane == 0) {
         uint64_t* sk = m.skey + (int64_t)m.rank * 4;
         atomicMin((unsigned long long*)&sk[0], (unsigned long long)kmin);
@@ -2993,7 +3071,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_SCORES:
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
             if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart &&
-                m.cov_perm)
+                m.cov_perm && m.cov_mixed)
+                hipLaunchKernelGGL(k_scores_grid, dim3(grid_rows((m.n_rows + 15) / 16, BT / WAVE)), dim3(BT), 0, st, m);
+            else if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd &&
+                     m.rowpart && m.cov_perm)
                 hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
             else
                 hipLaunchKernelGGL(k_scores, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);
