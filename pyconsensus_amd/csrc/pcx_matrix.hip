@@ -1624,7 +1624,10 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
     const ColParam p = col_param(m, c, true);
     int64_t r0, r1;
     row_range(m, r0, r1);
-    acc2 raw, pc, b1, b15, b2;
+    // raw (np.dot(smooth_rep, F), :510) decides the catch: compensated.  The participation and
+    // certainty sums (:542, :558) are continuous outputs: plain sums (error ~N ulp << 1e-9)
+    acc2 raw;
+    double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     double n1 = 0, n15 = 0, n2 = 0;
     // explicit unroll (a lambda capturing five accumulators pushed them to scratch)
     int64_t i = r0;
@@ -1645,26 +1648,22 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
             const double f = ms ? p.guess : x;
             const double w = wv[u];
             raw.add_prod(w, f);
-            if (ms) pc.add(w);
-            if (f == 1.0) {
-                b1.add(w);
-                n1 += 1;
-            } else if (f == 1.5) {
-                b15.add(w);
-                n15 += 1;
-            } else if (f == 2.0) {
-                b2.add(w);
-                n2 += 1;
-            }
+            pc += ms ? w : 0.0;
+            b1 += f == 1.0 ? w : 0.0;
+            b15 += f == 1.5 ? w : 0.0;
+            b2 += f == 2.0 ? w : 0.0;
+            n1 += f == 1.0 ? 1.0 : 0.0;
+            n15 += f == 1.5 ? 1.0 : 0.0;
+            n2 += f == 2.0 ? 1.0 : 0.0;
         }
         i += u_n;
     }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, raw.get());
-    st_dd(pp + 2, pc.get());
-    st_dd(pp + 4, b1.get());
-    st_dd(pp + 6, b15.get());
-    st_dd(pp + 8, b2.get());
+    st_dd(pp + 2, {pc, 0.0});
+    st_dd(pp + 4, {b1, 0.0});
+    st_dd(pp + 6, {b15, 0.0});
+    st_dd(pp + 8, {b2, 0.0});
     st_dd(pp + 10, {n1, 0.0});
     st_dd(pp + 12, {n15, 0.0});
     st_dd(pp + 14, {n2, 0.0});

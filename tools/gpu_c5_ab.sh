@@ -8,6 +8,6 @@ mkdir -p $O
 for i in 1 2; do
   for L in "$@"; do
     PCX_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-c4 --c5-steps 3 --steps 3 > $O/b.json 2> $O/b.err || { echo "bench rc=$? ($L)"; tail -3 $O/b.err; exit 1; }
-    python3 -c "import json,sys; c=json.load(open('$O/b.json'))['c5']; s=c['stage_ms']; print('%-24s C5 %.1f ms  COV %.1f  COV_I8 %.1f  WCD %.1f' % (sys.argv[1], c['latency_ms'], s.get('M_COV',0), s.get('M_COV_I8',0), s.get('M_WCD',0)))" "$L"
+    python3 -c "import json,sys; c=json.load(open('$O/b.json'))['c5']; s=c['stage_ms']; print('%-24s C5 %.1f ms ' % (sys.argv[1], c['latency_ms']) + ' '.join('%s %.1f' % (k[2:], v) for k, v in list(s.items())[:9]))" "$L"
   done
 done
