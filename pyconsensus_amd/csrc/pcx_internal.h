@@ -67,6 +67,9 @@ typedef struct {
     uint64_t* sel_arg;            /* [2][n_scaled] first dominant row (MIN), its value key (MAX) */
     int32_t*  sel_act;            /* [n_scaled] active scaled events, compacted in event order */
     int32_t*  hard;               /* [E] 0 / hard-replay mode per event (binary fill mean, median) */
+    uint64_t* cbuf;               /* [n_scaled][ccap][2] compacted (key, weight bits) of the range (k_sel_hist) */
+    int64_t*  ccount;             /* [n_scaled] compacted elements of this rank                    */
+    int64_t   ccap;               /* compaction capacity per event (0: none)                       */
     /* outputs ([E] events, [n_rows] agents of this rank) */
     double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
         *reporter_bonus;

@@ -45,7 +45,7 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
-constexpr int SELS = 24;         // sel_state words per scaled event
+constexpr int SELS = 32;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
 
@@ -1723,6 +1723,10 @@ enum sel_word {
     SW_TARGET,                        // count mode: 0-based rank of the crossing element
     SW_CNT_BELOW,                     // count mode: elements before the range
     SW_HALF,                          // count mode: 1 exact half (mean with predecessor), 2 half at k*=1
+    SW_INRANGE,                       // elements (all ranks) in [LO, HI] after the last step
+    SW_CMODE,                         // 1: this rank's in-range elements are compacted in cbuf
+    SW_GN, SW_GW0, SW_GW1, SW_GW2,    // phase 2, this rank: filled (missing) rows -- all at the fill
+                                      // value -- count and raw weight limb sums, binned once per pass
     SW_NWORDS
 };
 static_assert(SW_NWORDS <= SELS, "sel_state words");
@@ -1810,9 +1814,10 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     const int s = blockIdx.x;
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     if (st[SW_STATUS] != 1) return;
-    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wminb, wmaxb;
+    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wminb, wmaxb, ga_s, gb_s, gc_s, gn_s;
     if (threadIdx.x == 0) {
         la = lb = lc = cnt = 0;
+        ga_s = gb_s = gc_s = gn_s = 0;
         kmin = ~0ull;
         kmax = 0;
         wminb = ~0ull;
@@ -1820,6 +1825,7 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     }
     __syncthreads();
     uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0, wlo = ~0ull, whi = 0;
+    uint64_t ga = 0, gb = 0, gc = 0, gn = 0;
     rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
                              [&](int64_t, XW v) {
                                  double x, w;
@@ -1828,6 +1834,12 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
                                  a += L.l0;
                                  b += L.l1;
                                  c += L.l2;
+                                 if (m.sel_phase == 2 && __builtin_isnan(v.x)) {
+                                     ga += L.l0;
+                                     gb += L.l1;
+                                     gc += L.l2;
+                                     gn++;
+                                 }
                                  const uint64_t k = dkey(x);
                                  mn = k < mn ? k : mn;
                                  mx = k > mx ? k : mx;
@@ -1844,8 +1856,18 @@ __global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
     atomicMax(&kmax, (unsigned long long)mx);
     atomicMin(&wminb, (unsigned long long)wlo);
     atomicMax(&wmaxb, (unsigned long long)whi);
+    if (gn) {
+        atomicAdd(&ga_s, (unsigned long long)ga);
+        atomicAdd(&gb_s, (unsigned long long)gb);
+        atomicAdd(&gc_s, (unsigned long long)gc);
+        atomicAdd(&gn_s, (unsigned long long)gn);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
+        st[SW_GN] = gn_s;  // this rank's only: added to its own histograms
+        st[SW_GW0] = ga_s;
+        st[SW_GW1] = gb_s;
+        st[SW_GW2] = gc_s;
         // limbs stay unnormalised here (carries are exact under the cross-rank SUM)
         m.sel_isum[s * 4 + 0] = la;
         m.sel_isum[s * 4 + 1] = lb;
@@ -1892,6 +1914,7 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
     st[SW_LO] = kmin;
     st[SW_HI] = kmax;
     st[SW_SHIFT] = shift_for(kmin, kmax);
+    st[SW_INRANGE] = n;
     if (n == 0 || !(tot.a | tot.b | tot.c)) {  // weighted_median returns None -> NaN
         sel_done(st, __builtin_nan(""));
         return;
@@ -2031,26 +2054,36 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
 }
 
 // exact weight / count histogram of the keys inside [lo, hi] (NB buckets) of active event a
+// One block per active event.  Once the key range holds at most ccap elements (all ranks),
+// the pass that reads the whole column also compacts this rank's in-range (key, weight)
+// pairs into cbuf; later passes read only those (the histogram is a set of exact integer
+// sums / minima / maxima, so the compacted order does not matter).
 __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     const int s = m.sel_act[a];
-    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
     __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB];
+    __shared__ unsigned long long gcount;
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
         hmin[b] = ~0ull;
         hmax[b] = 0;
     }
+    if (threadIdx.x == 0) gcount = 0;
     __syncthreads();
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
     const int sh = (int)st[SW_SHIFT];
     const bool wmode = st[SW_MODE] == 0;
-    rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
-                             [&](int64_t, XW v) {
-        double x, w;
-        if (!sel_decode(m, s, v, x, w)) return;
-        const uint64_t k = dkey(x);
-        if (k < lo || k > hi) return;
+    const bool from_buf = st[SW_CMODE] == 1;
+    // phase 2: the filled rows all sit at the fill value -- binned once, not per element
+    const bool gties = m.sel_phase == 2 && st[SW_GN] > 0;
+    const uint64_t gk = gties ? dkey(m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]]) : 0;
+    const bool gin = gties && gk >= lo && gk <= hi;
+    const uint64_t ties_all = gin ? (uint64_t)m.ev[EV_MISS * m.n_events + m.scaled_cols[s]] : 0;  // all ranks
+    const uint64_t need = st[SW_INRANGE] > ties_all ? st[SW_INRANGE] - ties_all : 0;
+    const bool gather = !from_buf && m.cbuf && st[SW_INRANGE] > 0 && need <= (uint64_t)m.ccap;
+    uint64_t* cb = m.cbuf ? m.cbuf + (int64_t)s * m.ccap * 2 : nullptr;
+    auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh);
         if (wmode) {
             const limbs3 L = to_limbs(w);
@@ -2061,8 +2094,46 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         atomicAdd(&hn[b], 1ull);
         atomicMin(&hmin[b], (unsigned long long)k);
         atomicMax(&hmax[b], (unsigned long long)k);
-    });
+    };
+    if (from_buf) {
+        const int64_t nc = m.ccount[s];
+        for (int64_t j = threadIdx.x; j < nc; j += BT) {
+            const uint64_t k = cb[2 * j];
+            if (k < lo || k > hi) continue;
+            bin(k, __longlong_as_double(cb[2 * j + 1]));
+        }
+    } else {
+        rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
+                                 [&](int64_t, XW v) {
+            double x, w;
+            if (gties && __builtin_isnan(v.x)) return;  // a filled row
+            if (!sel_decode(m, s, v, x, w)) return;
+            const uint64_t k = dkey(x);
+            if (k < lo || k > hi) return;
+            bin(k, w);
+            if (gather) {
+                const unsigned long long j = atomicAdd(&gcount, 1ull);
+                cb[2 * j] = k;
+                cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
+            }
+        });
+    }
+    if (gin && threadIdx.x == 0) {
+        const int b = (int)((gk - lo) >> sh);
+        if (wmode) {
+            atomicAdd(&ha[b], (unsigned long long)st[SW_GW0]);
+            atomicAdd(&hb[b], (unsigned long long)st[SW_GW1]);
+            atomicAdd(&hc[b], (unsigned long long)st[SW_GW2]);
+        }
+        atomicAdd(&hn[b], (unsigned long long)st[SW_GN]);
+        atomicMin(&hmin[b], (unsigned long long)gk);
+        atomicMax(&hmax[b], (unsigned long long)gk);
+    }
     __syncthreads();
+    if (gather && threadIdx.x == 0) {
+        m.ccount[s] = (int64_t)gcount;
+        st[SW_CMODE] = 1;
+    }
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
         if (wmode) {
@@ -2123,6 +2194,7 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
                 st[SW_LO] = kmin;
                 st[SW_HI] = kmax;
                 st[SW_SHIFT] = shift_for(kmin, kmax);
+                st[SW_INRANGE] = n;
                 st_l3(st + SW_BELOW0, below);
                 st[SW_CNT_BELOW] = cbelow;
                 st[SW_BELOW_MAX] = below_max;

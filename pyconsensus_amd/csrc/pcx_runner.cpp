@@ -31,7 +31,7 @@ constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
 constexpr int COV_STAGE = 64;  // wcd rows: whole 64-row stages of the int8 GEMM
-constexpr int SELS = 24;
+constexpr int SELS = 32;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
 template <class T>
@@ -63,6 +63,9 @@ struct pcx_workspace {
     int8_t *zA, *zB;
     int64_t* zsum;
     double* dscale;
+    uint64_t* cbuf;
+    int64_t* ccount;
+    int64_t ccap = 0;
     // sized by the data (the grid / general split), grown on demand
     struct Grow {
         void* p = nullptr;
@@ -210,6 +213,8 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
     const int64_t ks = (16 * 3 * 256 + w->cov_tiles - 1) / w->cov_tiles;
     w->cov_kslices = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(32, ks), stages >= 8 ? stages / 8 : 1));
     w->xcap = E * CS * 2;
+    // selection compaction: up to 256k (key, weight) pairs per scaled event and rank (4 GB at C5)
+    w->ccap = n_scaled > 0 ? std::min<int64_t>(262144, n_rows) : 0;
 
     // small buffers (zeroed per call) in one block, the big ones in their own
     struct Item {
@@ -242,6 +247,8 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->sel_arg, (size_t)(S * 2) * 8, true},
         {(void**)&w->sel_act, (size_t)S * 4, true},
         {(void**)&w->hard, (size_t)E * 4, true},
+        {(void**)&w->ccount, (size_t)S * 8, true},
+        {(void**)&w->cbuf, (size_t)(S * w->ccap * 2) * 8, false},
         {(void**)&w->hard_cols, (size_t)E * 4, true},
         {(void**)&w->hard_modes, (size_t)E * 4, true},
         {(void**)&w->scols, (size_t)S * 4, false},
@@ -654,6 +661,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.sel_arg = w->sel_arg;
         m.sel_act = w->sel_act;
         m.hard = w->hard;
+        m.cbuf = w->ccap > 0 ? w->cbuf : nullptr;
+        m.ccount = w->ccount;
+        m.ccap = w->ccap;
         m.scalars = w->scalars;
         m.wcd = w->wcd;
         m.tokp = w->tokp;
