@@ -824,8 +824,8 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
 
 // PCX_M_COV_I8: exact integer products on int8 MFMA (v_mfma_i32_16x16x64_i8).  Operands are
 // [row / 16][position][16] int8 blocks, so one 16-byte load is one lane's MFMA fragment (16
-// rows of one position).  256 x 256 output tiles, 8 waves of 128 x 64 (32 int32
-// accumulators each); 64-row stages of both 16 KB panels go to LDS by global_load_lds in a
+// rows of one position).  256 x 256 output tiles, 16 waves of 64 x 64 (16 int32
+// accumulators each, four waves per SIMD); 64-row stages of both 16 KB panels go to LDS by global_load_lds in a
 // four-stage ring (three stages in flight under the MFMAs -- the loads' latency is several
 // stages long -- one barrier per stage, counted vmcnt); each k-slice's int32 tile is stored
 // to its own slab (k_cov_reduce sums the slabs in int64).  Tiles run k-slice major and
@@ -833,7 +833,7 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int GT = 256;                              // output tile edge
 constexpr int G_NBUF = 4;                            // LDS ring depth
-constexpr int G_LPW = 4;                             // global_load_lds per wave per stage
+constexpr int G_LPW = 2;                             // global_load_lds per wave per stage
 constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one operand's 64-row stage: 16 KB
 constexpr size_t G_LDS_BYTES = G_NBUF * 2 * G_PANEL; // 128 KB
 
@@ -848,7 +848,7 @@ struct GemmI8 {
     int64_t rg;  // row groups, a multiple of 4
 };
 
-constexpr int G_THREADS = 512;  // 2 x 4 waves of 128 x 64
+constexpr int G_THREADS = 1024;  // 4 x 4 waves of 64 x 64
 
 __global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
     extern __shared__ __attribute__((aligned(16))) char glds[];
@@ -862,27 +862,21 @@ __global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
     const int64_t s0 = ks * per < nst ? ks * per : nst;
     const int64_t s1 = s0 + per < nst ? s0 + per : nst;  // (an empty slice stores zeros)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int wr = wv >> 2, wc = wv & 3;  // 2 x 4 waves: 128 p x 64 q each
+    const int wr = wv >> 2, wc = wv & 3;  // 4 x 4 waves: 64 p x 64 q each
     const int lc = lane & 15, lg = lane >> 4;
-    // this wave moves row group (wv & 3) of each stage, half (wv >> 2) of both panels
+    // this wave moves row group (wv & 3) of each stage, quarter (wv >> 2) of both panels
     const int mg = wv & 3, mh = wv >> 2;
-    const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 128 + lane) * 16;
-    const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 128 + lane) * 16;
+    const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
+    const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
     auto issue = [&](int64_t st, int buf) {
-        char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 128) * 16;
+        char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 64) * 16;
         const int64_t grp = st * 4 + mg;
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-            __builtin_amdgcn_global_load_lds((const void*)(Ab + (grp * g.lda + j * 64) * 16),
-                                             (lds_ptr_t)(base + (size_t)j * 64 * 16), 16, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-            __builtin_amdgcn_global_load_lds((const void*)(Bb + (grp * g.ldb + j * 64) * 16),
-                                             (lds_ptr_t)(base + G_PANEL + (size_t)j * 64 * 16), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16, 0, 0);
     };
-    v4i acc[8][4];
+    v4i acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 8; a++)
+    for (int a = 0; a < 4; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
     const int64_t n = s1 - s0;
@@ -899,24 +893,24 @@ __global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (t + G_NBUF - 1 < n) issue(s0 + t + G_NBUF - 1, (int)((t + G_NBUF - 1) % G_NBUF));
-        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * 128 + lc;
+        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * 64 + lc;
         const v4i* Bs = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL + G_PANEL) + lg * GT + wc * 64 + lc;
-        v4i af[8], bf[4];
+        v4i af[4], bf[4];
 #pragma unroll
-        for (int a = 0; a < 8; a++) af[a] = As[a * 16];
+        for (int a = 0; a < 4; a++) af[a] = As[a * 16];
 #pragma unroll
         for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
 #pragma unroll
-        for (int a = 0; a < 8; a++)
+        for (int a = 0; a < 4; a++)
 #pragma unroll
             for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
         asm volatile("" ::: "memory");
     }
     // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
-    const int p0 = ip * GT + wr * 128 + 4 * lg, q0 = iq * GT + wc * 64 + lc;
+    const int p0 = ip * GT + wr * 64 + 4 * lg, q0 = iq * GT + wc * 64 + lc;
     int32_t* out = g.out + (int64_t)ks * g.slab;
 #pragma unroll
-    for (int a = 0; a < 8; a++)
+    for (int a = 0; a < 4; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++)
 #pragma unroll
