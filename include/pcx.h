@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 6
+#define PCX_ABI_VERSION 7
 
 enum pcx_status {
     PCX_OK = 0,
@@ -72,11 +72,13 @@ int      pcx_set_stream(pcx_ctx* ctx, void* hip_stream);  /* NULL = default stre
 int      pcx_synchronize(pcx_ctx* ctx);
 
 /* ------------------------------------------------------------------------ */
-/* Batched regime: B independent rounds of equal shape N x E, one round per    */
-/* wavefront (Simulator.jl-style Monte Carlo, README.rst:52-56).  Each round is */
-/* the complete Oracle(reports, event_bounds, reputation).consensus() of       */
-/* __init__.py:102-611.                                                          */
-/* Limits: 1 <= N <= 64, 1 <= E <= 32.                                          */
+/* Batched regime: B independent rounds of equal shape N x E (Simulator.jl-    */
+/* style Monte Carlo, README.rst:52-56).  Each round is the complete            */
+/* Oracle(reports, event_bounds, reputation).consensus() of __init__.py:102-611. */
+/* N <= 64, E <= 32: one round per wavefront, asynchronous on the stream.      */
+/* Larger rounds (E <= 65536; not the clustering algorithms): each round is one */
+/* single-matrix consensus, a pool of worker streams keeps many in flight       */
+/* (PCX_ROUND_WORKERS, default 16); the call is then synchronous.              */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     int64_t n_rounds;             /* B                                           */
@@ -190,6 +192,19 @@ typedef struct {
     int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);
 } pcx_comm_ops;
 pcx_ctx* pcx_create_custom(int device_id, int world, int rank, const pcx_comm_ops* ops);
+
+/* One process driving several GPUs (pcx_create(n_devices,
+ * device_ids); replaces the reference's single-process Oracle(...).consensus(),
+ * __init__.py:502-611, at sizes one GPU cannot hold).  A single-matrix call on this
+ * context takes the WHOLE matrix in host memory (PCX_MEM_HOST, n_total == n_rows,
+ * row_offset 0) and shards its rows over the devices in contiguous blocks (the
+ * first N % n_devices blocks one row longer), one worker thread per device.  The
+ * devices exchange through RCCL (ncclCommInitAll, xGMI) when the ids are distinct,
+ * through host memory when an id repeats (rehearsal on fewer GPUs).  Results are
+ * the one-device call's, bit for bit; the scalars of pcx_result are device 0's
+ * (comm_bytes: summed over the devices).  pcx_consensus_batched_f64 on this
+ * context runs on device_ids[0]. */
+pcx_ctx* pcx_create_devices(int n_devices, const int* device_ids);
 
 int pcx_ctx_world(const pcx_ctx* ctx);
 int pcx_ctx_rank(const pcx_ctx* ctx);

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5

@@ -45,6 +45,7 @@ def _declare(lib):
         ("pcx_group_destroy", None, [vp]),
         ("pcx_create_grouped", vp, [i32, vp, i32]),
         ("pcx_create_custom", vp, [i32, i32, i32, C.POINTER(_abi.CommOps)]),
+        ("pcx_create_devices", vp, [i32, C.POINTER(C.c_int)]),
         ("pcx_ctx_world", i32, [vp]),
         ("pcx_ctx_rank", i32, [vp]),
         ("pcx_release_workspace", i32, [vp]),
@@ -97,6 +98,19 @@ def context(device_index):
         h = lib().pcx_create(int(device_index))
         if not h:
             raise PcxError("pcx_create(%d) failed: %s" % (device_index, lib().pcx_last_error().decode()))
+        _ctx[key] = h
+    return h
+
+
+def devices_context(device_ids):
+    """The per-thread multi-device pcx_ctx (pcx_create_devices) of ``device_ids``: the
+    single-matrix calls on it shard the rows over those GPUs inside libpcx."""
+    ids = tuple(int(d) for d in device_ids)
+    key = (threading.get_ident(), ids)
+    h = _ctx.get(key)
+    if h is None:
+        arr = (C.c_int * len(ids))(*ids)
+        h = new_context(lib().pcx_create_devices(len(ids), arr), "pcx_create_devices(%s)" % (ids,))
         _ctx[key] = h
     return h
 

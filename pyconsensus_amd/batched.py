@@ -1,10 +1,11 @@
 """Batched Monte Carlo regime: B independent oracle rounds in one launch.
 
 Each round is exactly ``Oracle(reports[b], event_bounds_b, reputation[b]).consensus()``
-(pyconsensus/__init__.py:102-611) and runs in one wavefront of
-``batched_round_kernel`` (csrc/pcx_batched.hip).  This is the regime of
-Simulator.jl-style Monte Carlo drivers (README.rst:52-56), which loop consensus()
-over many small random rounds.
+(pyconsensus/__init__.py:102-611).  This is the regime of Simulator.jl-style Monte
+Carlo drivers (README.rst:52-56), which loop consensus() over many random rounds.
+Rounds of at most 64 reporters x 32 events run in one wavefront each of
+``batched_round_kernel`` (csrc/pcx_batched.hip); larger rounds run as single-matrix
+consensuses, many in flight on a pool of worker streams (csrc/pcx_rounds.cpp).
 """
 from __future__ import annotations
 
@@ -14,7 +15,7 @@ import numpy as np
 
 from . import _abi, _device, _lib
 
-MAX_REPORTERS = 64
+MAX_REPORTERS = 64  # one wavefront per round up to here (and MAX_EVENTS)
 MAX_EVENTS = 32
 
 
@@ -65,7 +66,8 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     cluster_threshold: clusterfeck's cut (default: the reference's log10(E)/1.77 rule)
 
     Returns a dict of torch tensors on the device, named like the ABI fields
-    (``smooth_rep``, ``outcomes_final``, ...).  Asynchronous on torch's current stream.
+    (``smooth_rep``, ``outcomes_final``, ...).  Asynchronous on torch's current stream
+    for rounds up to 64 x 32; larger rounds return when every output is written.
     """
     t = _device.require_gpu()
     dev = t.device(device) if device is not None else t.device("cuda", t.cuda.current_device())
@@ -73,9 +75,11 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     if R.dim() != 3:
         raise ValueError("reports must be (B, N, E)")
     B, N, E = R.shape
-    if not (1 <= N <= MAX_REPORTERS and 1 <= E <= MAX_EVENTS):
-        raise ValueError("batched rounds need 1 <= N <= %d and 1 <= E <= %d (got %d x %d)"
-                         % (MAX_REPORTERS, MAX_EVENTS, N, E))
+    if N < 1 or E < 1:
+        raise ValueError("batched rounds need N >= 1 and E >= 1 (got %d x %d)" % (N, E))
+    if (N > MAX_REPORTERS or E > MAX_EVENTS) and algorithm in _abi.CLUSTER_ALGORITHMS:
+        raise NotImplementedError("algorithm %r runs on rounds of at most %d x %d (got %d x %d)"
+                                  % (algorithm, MAX_REPORTERS, MAX_EVENTS, N, E))
     rep = _device.as_device(reputation, t.float64, dev)
     if rep is not None and tuple(rep.shape) != (B, N):
         raise ValueError("reputation must be (B, N)")

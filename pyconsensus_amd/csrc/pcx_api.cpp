@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <thread>
 
 #include "../../include/pcx.h"
 #include "pcx_internal.h"
@@ -105,11 +106,66 @@ pcx_ctx* pcx_create_custom(int device_id, int world, int rank, const pcx_comm_op
     return with_comm(c, pcx::comm_custom(world, rank, ops, err), err);
 }
 
-int pcx_ctx_world(const pcx_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->world : 1; }
+pcx_ctx* pcx_create_devices(int n_devices, const int* device_ids) {
+    if (n_devices < 1 || !device_ids) {
+        g_err = "pcx_create_devices: need n_devices >= 1 and device_ids";
+        return nullptr;
+    }
+    pcx_ctx* c = new_ctx(device_ids[0], "pcx_create_devices");
+    if (!c) return nullptr;
+    for (int k = 1; k < n_devices; k++) {
+        pcx_ctx* probe = new_ctx(device_ids[k], "pcx_create_devices");
+        if (!probe) {
+            delete c;
+            return nullptr;
+        }
+        delete probe;
+    }
+    bool distinct = true;
+    for (int a = 0; a < n_devices; a++)
+        for (int b = a + 1; b < n_devices; b++) distinct = distinct && device_ids[a] != device_ids[b];
+    std::string err;
+    std::vector<pcx::Comm*> comms;
+    if (distinct) {
+        const int rc = pcx::comm_rccl_all(n_devices, device_ids, comms, err);
+        if (rc) {
+            g_err = "pcx_create_devices: " + err;
+            delete c;
+            return nullptr;
+        }
+    } else {
+        c->group = pcx::group_create(n_devices);
+        for (int k = 0; k < n_devices && c->group; k++) comms.push_back(pcx::comm_group(c->group, k, err));
+    }
+    for (int k = 0; k < n_devices; k++) {
+        pcx_ctx* s = (k < (int)comms.size() && comms[k]) ? new (std::nothrow) pcx_ctx : nullptr;
+        if (s) {
+            s->device = device_ids[k];
+            s->comm = comms[k];
+        } else if (k < (int)comms.size()) {
+            delete comms[k];
+        }
+        c->sub.push_back(s);
+    }
+    for (pcx_ctx* s : c->sub)
+        if (!s) {
+            g_err = "pcx_create_devices: communicator setup failed" + (err.empty() ? std::string() : ": " + err);
+            pcx_destroy(c);
+            return nullptr;
+        }
+    return c;
+}
+
+int pcx_ctx_world(const pcx_ctx* ctx) {
+    if (ctx && !ctx->sub.empty()) return (int)ctx->sub.size();
+    return ctx && ctx->comm ? ctx->comm->world : 1;
+}
 int pcx_ctx_rank(const pcx_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }
 
 int pcx_release_workspace(pcx_ctx* ctx) {
     if (!ctx) return fail(PCX_EINVAL, "pcx_release_workspace: null context");
+    for (pcx_ctx* s : ctx->sub) pcx_release_workspace(s);
+    pcx::rounds_free(ctx);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
     return PCX_OK;
@@ -117,6 +173,9 @@ int pcx_release_workspace(pcx_ctx* ctx) {
 
 void pcx_destroy(pcx_ctx* ctx) {
     if (!ctx) return;
+    for (pcx_ctx* s : ctx->sub) pcx_destroy(s);
+    if (ctx->group) pcx::group_destroy(ctx->group);
+    pcx::rounds_free(ctx);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
     delete ctx->comm;
@@ -140,9 +199,12 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     if (!ctx || !in || !out) return fail(PCX_EINVAL, "pcx_consensus_batched_f64: null argument");
     if (in->n_rounds < 0 || in->n_rounds > 0x7fffffff)
         return fail(PCX_EINVAL, "batched: n_rounds must be in [0, 2^31)");
-    if (in->n_reporters < 1 || in->n_reporters > 64)
-        return fail(PCX_EINVAL, "batched: n_reporters must be in [1, 64]");
-    if (in->n_events < 1 || in->n_events > 32) return fail(PCX_EINVAL, "batched: n_events must be in [1, 32]");
+    if (in->n_reporters < 1 || in->n_reporters > 0x7fffffff)
+        return fail(PCX_EINVAL, "batched: n_reporters must be in [1, 2^31)");
+    if (in->n_events < 1 || in->n_events > 65536) return fail(PCX_EINVAL, "batched: n_events must be in [1, 65536]");
+    const bool large = in->n_reporters > 64 || in->n_events > 32;  // beyond one wavefront per round
+    if (large && in->algorithm >= PCX_ALG_KMEANS)
+        return fail(PCX_EINVAL, "batched: the clustering algorithms need rounds of at most 64 x 32");
     if (!in->reports) return fail(PCX_EINVAL, "batched: reports is NULL");
     if (in->scaled && (!in->lo || !in->hi)) return fail(PCX_EINVAL, "batched: scaled given without lo/hi");
     if (in->algorithm < PCX_ALG_PCA || in->algorithm > PCX_ALG_CLUSTERFECK)
@@ -161,6 +223,11 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
         return fail(PCX_EINVAL, "batched: cokurtosis needs aux_scores (aux[\"cokurt\"])");
     if (!std::isfinite(in->catch_tolerance) || !std::isfinite(in->alpha))
         return fail(PCX_EINVAL, "batched: catch_tolerance/alpha must be finite");
+    if (large) {  // one single-matrix consensus per round, many rounds in flight (pcx_rounds.cpp)
+        std::string err;
+        const int rc = pcx::run_rounds(ctx, in, out, err);
+        return rc ? fail(rc, "pcx_consensus_batched_f64: " + err) : PCX_OK;
+    }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     pcx::BatchArgs a{};
@@ -247,10 +314,108 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
 }
 
 namespace {
+// pcx_create_devices context: shard the host matrix's rows over the devices, one
+// worker thread per device running the rank's consensus (collective over the ranks)
+int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, const double* scores, int rank_rule,
+                double* nc, std::string& err) {
+    const int n = (int)ctx->sub.size();
+    const int64_t N = p->n_rows, E = p->n_events;
+    if (p->mem_kind != PCX_MEM_HOST) {
+        err = "a multi-device context takes the matrix in host memory (PCX_MEM_HOST)";
+        return PCX_EINVAL;
+    }
+    if (p->n_total != N || p->row_offset != 0) {
+        err = "a multi-device context takes the whole matrix (n_total == n_rows, row_offset 0)";
+        return PCX_EINVAL;
+    }
+    if (N < n || E < 1 || !p->reports) {
+        err = "bad shape (fewer rows than devices) or missing reports";
+        return PCX_EINVAL;
+    }
+    std::vector<pcx_problem> ps(n, *p);
+    std::vector<pcx_result> rs(n);
+    std::vector<std::string> errs(n);
+    std::vector<int> rcs(n, 0);
+    const int64_t base = N / n, rem = N % n;
+    auto at = [](double* a, int64_t off) { return a ? a + off : nullptr; };
+    for (int k = 0; k < n; k++) {
+        const int64_t off = k * base + (k < rem ? k : rem), cnt = base + (k < rem ? 1 : 0);
+        pcx_problem& q = ps[k];
+        q.n_rows = cnt;
+        q.n_total = N;
+        q.row_offset = off;
+        q.reports = p->reports + off * E;
+        q.aux_scores = p->aux_scores ? p->aux_scores + off : nullptr;
+        pcx_result& o = rs[k];
+        o = pcx_result{};
+        o.old_rep = at(r->old_rep, off);
+        o.this_rep = at(r->this_rep, off);
+        o.smooth_rep = at(r->smooth_rep, off);
+        o.scores = at(r->scores, off);
+        o.na_row = at(r->na_row, off);
+        o.participation_rows = at(r->participation_rows, off);
+        o.relative_part = at(r->relative_part, off);
+        o.reporter_bonus = at(r->reporter_bonus, off);
+        o.original = at(r->original, off * E);
+        o.filled = at(r->filled, off * E);
+        if (k == 0) {  // event vectors are identical on every rank: device 0 writes them
+            o.adj_first_loadings = r->adj_first_loadings;
+            o.outcomes_raw = r->outcomes_raw;
+            o.outcomes_adjusted = r->outcomes_adjusted;
+            o.outcomes_final = r->outcomes_final;
+            o.certainty = r->certainty;
+            o.consensus_reward = r->consensus_reward;
+            o.nas_filled = r->nas_filled;
+            o.participation_columns = r->participation_columns;
+            o.author_bonus = r->author_bonus;
+            o.weighted_mean = r->weighted_mean;
+            o.covariance = r->covariance;
+        }
+    }
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; k++) {
+        const int64_t off = ps[k].row_offset;
+        th.emplace_back([&, k, off] {
+            rcs[k] = pcx::run_matrix(ctx->sub[k], &ps[k], &rs[k], entry, scores ? scores + off : nullptr, rank_rule,
+                                     nc ? nc + off : nullptr, errs[k]);
+            if (rcs[k] && ctx->group) pcx::group_abort(ctx->group);  // release the ranks waiting on this one
+        });
+    }
+    for (auto& t : th) t.join();
+    if (ctx->group) pcx::group_reset(ctx->group);  // every worker has left the exchange
+    int first = -1;
+    for (int k = 0; k < n && first < 0; k++)
+        if (rcs[k] && errs[k].find("exchange aborted") == std::string::npos) first = k;
+    for (int k = first < 0 ? 0 : first; k < n; k++)
+        if (rcs[k]) {
+            err = "device " + std::to_string(ctx->sub[k]->device) + " (rank " + std::to_string(k) + "): " + errs[k];
+            return rcs[k];
+        }
+    double bytes = 0;
+    for (int k = 0; k < n; k++) bytes += rs[k].comm_bytes;
+    const pcx_result& z = rs[0];
+    r->participation = z.participation;
+    r->avg_certainty = z.avg_certainty;
+    r->branch = z.branch;
+    r->flags = z.flags;
+    r->pi_iters = z.pi_iters;
+    r->components = z.components;
+    r->n_hard = z.n_hard;
+    r->sel_passes = z.sel_passes;
+    r->comm_bytes = bytes;
+    r->grid_events = z.grid_events;
+    r->mixed_int8 = z.mixed_int8;
+    return 0;
+}
+
 int run(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, const double* scores, int rank_rule, double* nc,
         const char* who) {
     if (!ctx || !p || !r) return fail(PCX_EINVAL, std::string(who) + ": null argument");
     std::string err;
+    if (!ctx->sub.empty()) {
+        const int rc = run_devices(ctx, p, r, entry, scores, rank_rule, nc, err);
+        return rc ? fail(rc, std::string(who) + ": " + err) : PCX_OK;
+    }
     const int rc = pcx::run_matrix(ctx, p, r, entry, scores, rank_rule, nc, err);
     return rc ? fail(rc, std::string(who) + ": " + err) : PCX_OK;
 }
@@ -280,13 +445,15 @@ int pcx_nonconformity_f64(pcx_ctx* ctx, const pcx_problem* p, const double* scor
 
 int pcx_profile_enable(pcx_ctx* ctx, int on) {
     if (!ctx) return fail(PCX_EINVAL, "pcx_profile_enable: null context");
+    for (pcx_ctx* s : ctx->sub) s->profile = on ? 1 : 0;
     ctx->profile = on ? 1 : 0;
     return PCX_OK;
 }
 
 int pcx_profile_read(pcx_ctx* ctx, double* ms) {
     if (!ctx || !ms) return fail(PCX_EINVAL, "pcx_profile_read: null argument");
-    for (int k = 0; k < PCX_NSTAGES; k++) ms[k] = ctx->stage_ms[k];
+    const pcx_ctx* src = ctx->sub.empty() ? ctx : ctx->sub[0];  // multi-device: device 0's stages
+    for (int k = 0; k < PCX_NSTAGES; k++) ms[k] = src->stage_ms[k];
     return PCX_OK;
 }
 

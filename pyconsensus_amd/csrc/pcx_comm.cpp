@@ -30,16 +30,25 @@ struct pcx_group {
     std::vector<std::vector<char>> slot;  // per rank host staging
     std::vector<char> result;             // reduced data (written by the last arriver)
 
-    void barrier() {
+    bool aborted = false;                 // a rank failed: every waiting and later exchange fails
+
+    bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return false;
         const int64_t g = generation;
         if (++arrived == world) {
             arrived = 0;
             generation++;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return generation != g; });
+            cv.wait(lk, [&] { return generation != g || aborted; });
         }
+        return !aborted;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
     }
 };
 
@@ -120,11 +129,15 @@ struct StagedComm : Comm {
 
 struct GroupComm : StagedComm {
     pcx_group* g = nullptr;
+    static int aborted(std::string& err) {
+        err = "exchange aborted: another rank of the group failed";
+        return PCX_ECOMM;
+    }
     int allreduce(void* buf, int64_t count, int dtype, int op, hipStream_t st, std::string& err) override {
         if (count <= 0) return 0;
         const int64_t bytes = count * (int64_t)dtype_size(dtype);
         int rc = stage_out(buf, bytes, g->slot[rank], st, err);
-        g->barrier();
+        if (!g->barrier()) return aborted(err);
         if (rc == 0) {
             // every rank reduces in rank order: identical results everywhere
             std::vector<char>& acc = h1;
@@ -132,19 +145,19 @@ struct GroupComm : StagedComm {
             memcpy(acc.data(), g->slot[0].data(), bytes);
             for (int w = 1; w < world; w++) host_reduce(acc.data(), g->slot[w].data(), count, dtype, op);
         }
-        g->barrier();
+        if (!g->barrier()) return aborted(err);
         if (rc == 0) rc = stage_in(buf, h1.data(), bytes, st, err);
         return rc;
     }
     int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) override {
         if (bytes <= 0) return 0;
         int rc = stage_out(send, bytes, g->slot[rank], st, err);
-        g->barrier();
+        if (!g->barrier()) return aborted(err);
         if (rc == 0) {
             if ((int64_t)h1.size() < bytes * world) h1.resize(bytes * world);
             for (int w = 0; w < world; w++) memcpy(h1.data() + (int64_t)w * bytes, g->slot[w].data(), bytes);
         }
-        g->barrier();
+        if (!g->barrier()) return aborted(err);
         if (rc == 0) rc = stage_in(recv, h1.data(), bytes * world, st, err);
         return rc;
     }
@@ -214,6 +227,28 @@ Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::str
     return c;
 }
 
+int comm_rccl_all(int n, const int* devices, std::vector<Comm*>& out, std::string& err) {
+    std::vector<ncclComm_t> comms(n, nullptr);
+    ncclResult_t r = ncclCommInitAll(comms.data(), n, devices);
+    if (r != ncclSuccess) {
+        err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+        return PCX_ECOMM;
+    }
+    for (int k = 0; k < n; k++) {
+        RcclComm* c = new (std::nothrow) RcclComm;
+        if (!c) {
+            for (int j = k; j < n; j++) ncclCommDestroy(comms[j]);
+            err = "out of host memory";
+            return PCX_ENOMEM;
+        }
+        c->comm = comms[k];
+        c->world = n;
+        c->rank = k;
+        out.push_back(c);
+    }
+    return 0;
+}
+
 pcx_group* group_create(int world) {
     if (world < 1) return nullptr;
     pcx_group* g = new (std::nothrow) pcx_group;
@@ -224,6 +259,17 @@ pcx_group* group_create(int world) {
 }
 
 void group_destroy(pcx_group* g) { delete g; }
+
+void group_abort(pcx_group* g) {
+    if (g) g->abort();
+}
+
+void group_reset(pcx_group* g) {
+    if (!g) return;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->aborted = false;
+    g->arrived = 0;
+}
 
 Comm* comm_group(pcx_group* g, int rank, std::string& err) {
     if (!g || rank < 0 || rank >= g->world) {

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/pcx.h"
 
@@ -28,6 +29,9 @@ typedef struct {
     int32_t no_fill;              /* reports are already filled (stage entries): no NA fill */
     int32_t rank_rule;            /* sign choice by nonconformity_rank (:487-500), else nonconformity */
     int32_t scores_given;         /* scores come from aux_scores (nonconformity entries, cokurtosis) */
+    int32_t ob_order;             /* one rank and N*E < 9216 (OpenBLAS dgemv single-threaded): the np.dot
+                                     vectors (:489-492, :510) and np.sum totals (:144, :244-249, :461) in
+                                     the reference's own operation order */
     /* inputs */
     const double*  reports;       /* [n_rows][E]                                  */
     const uint8_t* scaled;        /* [E] or NULL (event_bounds None)              */
@@ -217,8 +221,12 @@ Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::str
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);
 Comm* comm_group(pcx_group* g, int rank, std::string& err);
 Comm* comm_custom(int world, int rank, const pcx_comm_ops* ops, std::string& err);
+// one communicator per listed device, all in this process (ncclCommInitAll); 0 = ok
+int comm_rccl_all(int n, const int* devices, std::vector<Comm*>& out, std::string& err);
 pcx_group* group_create(int world);
 void group_destroy(pcx_group* g);
+void group_abort(pcx_group* g);  // wake and fail every waiting / later exchange of g
+void group_reset(pcx_group* g);  // clear an abort once no rank is inside an exchange
 
 }  // namespace pcx
 
@@ -231,6 +239,12 @@ struct pcx_ctx {
     pcx_workspace* ws = nullptr;   // single-matrix scratch, cached between calls
     int profile = 0;
     double stage_ms[PCX_NSTAGES] = {0};
+    int scaled_floor = 0;          // allocate the workspace for at least this many scaled events
+    // batched rounds above the one-wave kernel's limits: worker contexts of the round scheduler
+    std::vector<pcx_ctx*> pool;
+    // pcx_create_devices: one rank context per device, driven by worker threads
+    std::vector<pcx_ctx*> sub;
+    pcx_group* group = nullptr;    // host exchange of `sub` when a device id repeats
 };
 
 namespace pcx {
@@ -238,4 +252,8 @@ void workspace_free(pcx_ctx* c);
 // entry: 0 consensus, 1 interpolate, 2 wpca, 3 lie_detector, 4 nonconformity
 int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const double* scores_in, int rank_rule,
                double* nc_out, std::string& err);
+// batched rounds of any N x E (pcx_rounds.cpp): each round one single-matrix consensus on a
+// pool of worker contexts with their own streams; synchronous
+int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::string& err);
+void rounds_free(pcx_ctx* c);
 }  // namespace pcx

@@ -87,6 +87,138 @@ __device__ __forceinline__ double filled(double r, const ColParam& p, int int_dt
     return missing(x) ? p.guess : x;
 }
 
+// ------------------------------------------------------------------ the reference's own order
+// For one rank with N*E < 9216 the reference's np.dot runs single-threaded OpenBLAS dgemv and
+// its np.sum numpy's pairwise sum; m.ob_order replays both (oracle/pcx_oracle_batched.c
+// ob_vecmat / pw_sum, fitted bit for bit on the goldens' host), so rank ties that rounding
+// makes or breaks (e.g. np.dot(rep, F) of two events with equal counts under uniform weights,
+// :489-490) fall as in the reference.  One thread runs each whole sum (N*E < 9216: short).
+
+// numpy pairwise_sum: blocks of <= 128 with 8 accumulators, halves rounded to multiples of 8
+template <class G>
+__device__ double pw_leaf(G g, int64_t off, int64_t n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; i++) r += g(off + i);
+        return r;
+    }
+    double r[8];
+    for (int k = 0; k < 8; k++) r[k] = g(off + k);
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int k = 0; k < 8; k++) r[k] += g(off + i + k);
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += g(off + i);
+    return res;
+}
+
+template <class G>
+__device__ double pw_sum_dev(G g, int64_t n) {  // the recursion of pw_sum, as an explicit stack
+    int64_t off_[32], n_[32];
+    double left_[32];
+    int state_[32];  // 0 = fresh, 1 = left half pending, 2 = right half pending
+    int sp = 0;
+    off_[0] = 0;
+    n_[0] = n;
+    state_[0] = 0;
+    for (;;) {
+        double ret;
+        if (n_[sp] > 128) {  // split: evaluate the left half first
+            int64_t n2 = n_[sp] / 2;
+            n2 -= n2 % 8;
+            state_[sp] = 1;
+            off_[sp + 1] = off_[sp];
+            n_[sp + 1] = n2;
+            state_[sp + 1] = 0;
+            sp++;
+            continue;
+        }
+        ret = pw_leaf(g, off_[sp], n_[sp]);
+        for (;;) {  // hand ret to the parent frames
+            if (sp == 0) return ret;
+            sp--;
+            if (state_[sp] == 1) {
+                int64_t n2 = n_[sp] / 2;
+                n2 -= n2 % 8;
+                left_[sp] = ret;
+                state_[sp] = 2;
+                off_[sp + 1] = off_[sp] + n2;
+                n_[sp + 1] = n_[sp] - n2;
+                state_[sp + 1] = 0;
+                sp++;
+                break;
+            }
+            ret = left_[sp] + ret;
+        }
+    }
+}
+
+// numpy's ddot (E == 1): 4 x 8-lane fma accumulators per 32 terms, folded to 4 x 4 lanes,
+// 16 per step, lanes (0 + 2) + (1 + 3), then a sequential fma tail
+template <class V, class X>
+__device__ double ob_ddot(V v, X x, int64_t n) {
+    double acc8[4][8], acc4[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int l = 0; l < 8; l++) acc8[r][l] = 0.0;
+    const int64_t n32 = n & ~(int64_t)31, n16 = n & ~(int64_t)15;
+    for (int64_t i = 0; i < n32; i += 32)
+        for (int k = 0; k < 32; k++) acc8[k / 8][k % 8] = fma(v(i + k), x(i + k), acc8[k / 8][k % 8]);
+    for (int r = 0; r < 4; r++)
+        for (int l = 0; l < 4; l++) acc4[r][l] = acc8[r][l] + acc8[r][l + 4];
+    for (int64_t i = n32; i < n16; i += 16)
+        for (int k = 0; k < 16; k++) acc4[k / 4][k % 4] = fma(v(i + k), x(i + k), acc4[k / 4][k % 4]);
+    double A[4];
+    for (int l = 0; l < 4; l++) A[l] = ((acc4[0][l] + acc4[1][l]) + acc4[2][l]) + acc4[3][l];
+    double d = (A[0] + A[2]) + (A[1] + A[3]);
+    for (int64_t i = n16; i < n; i++) d = fma(v(i), x(i), d);
+    return d;
+}
+
+// np.dot(v, F)[j] as cblas_dgemv(RowMajor, Trans) = column-major dgemv_n on the E x N matrix:
+// events j < E & ~3 in the 4-row vector kernel (reporters in blocks of 4: the second product
+// rounded, fma with the first, third, fourth; y = y + block; tails of 2 and 1), the last E % 4
+// events a sequential fma chain (E = 2, 3: unrolled pairs), E = 1 numpy's ddot
+template <class V, class X>
+__device__ double ob_vecmat(V v, X F, int64_t N, int64_t E, int64_t j) {
+    if (E == 1) return ob_ddot(v, F, N);
+    if (j < (E & ~(int64_t)3)) {
+        double y = 0.0;
+        int64_t n = 0;
+        for (; n + 4 <= N; n += 4) {
+            double t = F(n + 1) * v(n + 1);
+            t = fma(F(n), v(n), t);
+            t = fma(F(n + 2), v(n + 2), t);
+            t = fma(F(n + 3), v(n + 3), t);
+            y = y + t;
+        }
+        if (n + 2 <= N) {
+            double t = F(n + 1) * v(n + 1);
+            t = fma(F(n), v(n), t);
+            y = y + t;
+            n += 2;
+        }
+        if (n < N) y = y + F(n) * v(n);
+        return y;
+    }
+    double t = 0.0;
+    int64_t i = 0;
+    if (E == 2 || E == 3)
+        for (; i + 4 <= N; i += 4) {
+            t = t + fma(F(i), v(i), F(i + 1) * v(i + 1));
+            t = t + fma(F(i + 2), v(i + 2), F(i + 3) * v(i + 3));
+        }
+    for (; i < N; i++) t = fma(F(i), v(i), t);
+    return t;
+}
+
+// np.dot(w, F)[c] of the filled column c, weights w[i] (ob_order)
+__device__ __forceinline__ double ob_col_dot(const pcx_mat& m, const double* w, int c) {
+    const ColParam p = col_param(m, c, true);
+    const int64_t E = m.n_events;
+    return ob_vecmat([&](int64_t i) { return w[i]; },
+                     [&](int64_t i) { return filled(m.reports[i * E + c], p, m.int_dtype); }, m.n_rows, E, c);
+}
+
 // ------------------------------------------------------------------ block reductions
 template <int NT>
 __device__ dd block_sum_dd(dd v, dd* lds) {
@@ -147,6 +279,10 @@ __device__ __forceinline__ double l3_to_double(L3 x) {
 // ================================================================== PCX_M_REPUTATION
 __global__ void __launch_bounds__(1024) k_rep_total(pcx_mat m) {
     __shared__ dd lds[16];
+    if (m.ob_order) {  // np.sum's own pairwise order
+        if (threadIdx.x == 0) m.pvec[0] = pw_sum_dev([&](int64_t i) { return m.rep_raw[i]; }, m.n_total);
+        return;
+    }
     acc2 a;
     for (int64_t i = threadIdx.x; i < m.n_total; i += blockDim.x) a.add(m.rep_raw[i]);
     dd v = block_sum_dd<1024>(a.get(), lds);
@@ -377,7 +513,7 @@ __global__ void __launch_bounds__(BT) k_mean(pcx_mat m) {
     const double g = m.ev[EV_GUESS * E + c];
     const dd miss_w = dd_sub(R_tot, S_r);  // reputation of the filled cells
     const dd num = m.ev[EV_MISS * E + c] > 0 ? dd_add(S_rx, dd_mul_d(miss_w, g)) : S_rx;
-    m.ev[EV_OLD * E + c] = dd_to_double(num);
+    m.ev[EV_OLD * E + c] = m.ob_order ? ob_col_dot(m, m.rep, c) : dd_to_double(num);  // np.dot(rep, F) (:489)
     m.ev[EV_MU * E + c] = dd_div(num, R_tot);
 }
 
@@ -1485,6 +1621,32 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
     st_dd(pp + 2, a2.get());
 }
 
+// ob_order: the scalar sums of the reference in numpy's pairwise order, written over the dd
+// totals of scal[rank] (one thread; N < 9216).  which 0: sum(rep) (np.mean(rep), :461, and
+// np.ma.average's denominator, :317); 1: normalize(set1 / set2) totals (:244-249, :491-492);
+// 2: normalize(nc * rep / mean) totals (:462)
+__global__ void k_ob_sums(pcx_mat m, int which) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t N = m.n_rows;
+    double* sc = m.scal + (int64_t)m.rank * SS * 2;
+    auto put = [&](int slot, double v) { st_dd(sc + slot * 2, dd{v, 0.0}); };
+    if (which == 0) {
+        put(SC_REP, pw_sum_dev([&](int64_t i) { return m.rep[i]; }, N));
+    } else if (which == 1) {
+        double mn, mx;
+        score_minmax(m, mn, mx);
+        const double* s = m.rowv + RV_S * N;
+        put(SC_A1, pw_sum_dev([&](int64_t i) { return fabs(s[i] + fabs(mn)); }, N));
+        put(SC_A1P, pw_sum_dev([&](int64_t i) { return fabs(s[i] + fabs(mn)) + 1.0; }, N));
+        put(SC_A2, pw_sum_dev([&](int64_t i) { return fabs(s[i] - mx); }, N));
+        put(SC_A2P, pw_sum_dev([&](int64_t i) { return fabs(s[i] - mx) + 1.0; }, N));
+    } else {
+        const double* u = m.rowv + RV_U * N;
+        put(SC_U, pw_sum_dev([&](int64_t i) { return u[i]; }, N));
+        put(SC_UP, pw_sum_dev([&](int64_t i) { return u[i] + 1.0; }, N));
+    }
+}
+
 // PCX_M_DECIDE: ranks of old, new1, new2 (scipy rankdata 'average') and the rule (:487-500)
 // PCX_M_DECIDE (:491-498): new1/new2, then the three average ranks (scipy rankdata),
 // O(E^2) comparisons spread over E/256 blocks; the rank-distance sums are half-integers,
@@ -1499,8 +1661,8 @@ __global__ void __launch_bounds__(BT) k_decide_prep(pcx_mat m) {
     const int c = blockIdx.x * BT + threadIdx.x;
     if (c == 0) pv_s(m)[8] = 0.0;
     if (c >= E) return;
-    const double a = dd_to_double(cst(m, c, 4));
-    const double b = dd_to_double(cst(m, c, 5));
+    const double a = m.ob_order ? ob_col_dot(m, m.rowv + RV_N1 * m.n_rows, c) : dd_to_double(cst(m, c, 4));
+    const double b = m.ob_order ? ob_col_dot(m, m.rowv + RV_N2 * m.n_rows, c) : dd_to_double(cst(m, c, 5));
     const double t = 0.01 * old[c];
     n1[c] = a + t;
     n2[c] = b + t;
@@ -1548,7 +1710,17 @@ __global__ void __launch_bounds__(1024) k_decide(pcx_mat m) {
     const double* raw2 = pv_y(m);
     const double ref = m.rank_rule ? pv_s(m)[8] : 0.0;  // no rank rule: nonconformity directly
     int branch, pick1;
-    if (ref == 0) {
+    if (ref == 0 && m.ob_order) {  // np.sum((new - old)**2) pairwise (:480-481)
+        __shared__ int pk;
+        if (threadIdx.x == 0) {
+            const double s1 = pw_sum_dev([&](int64_t c) { const double a = raw1[c] - old[c]; return a * a; }, E);
+            const double s2 = pw_sum_dev([&](int64_t c) { const double b = raw2[c] - old[c]; return b * b; }, E);
+            pk = (s1 - s2) <= 0 ? 1 : 0;
+        }
+        __syncthreads();
+        pick1 = pk;
+        branch = pick1 ? 3 : 4;
+    } else if (ref == 0) {
         acc2 q1, q2;
         for (int c = threadIdx.x; c < E; c += 1024) {
             const double a = raw1[c] - old[c];
@@ -1677,7 +1849,8 @@ __global__ void __launch_bounds__(BT) k_events(pcx_mat m) {
     const bool sc = m.scaled && m.scaled[c];
     m.ev[EV_PC * E + c] = 1.0 - dd_to_double(cst(m, c, 7));
     if (sc) return;  // scaled events: phase-2 median
-    const double raw = dd_to_double(cst(m, c, 6));
+    // np.dot(smooth_rep, F) (:510)
+    const double raw = m.ob_order ? ob_col_dot(m, m.rowv + RV_SMOOTH * m.n_rows, c) : dd_to_double(cst(m, c, 6));
     const double adj = catch_value(raw, m.catch_tolerance);
     const int slot = adj == 1.0 ? 8 : (adj == 1.5 ? 9 : 10);
     const double cnt = dd_to_double(cst(m, c, slot + 3));
@@ -3040,6 +3213,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_TOK, 0);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(BT), 0, st, m, rg, 1, (int)SC_BIGTOK, 2);
+            if (m.ob_order) hipLaunchKernelGGL(k_ob_sums, dim3(1), dim3(64), 0, st, m, 0);
             break;
         case M_COLSTATS:
             hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
@@ -3147,6 +3321,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_NCSUMS:
             hipLaunchKernelGGL(k_ncsums, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(4), dim3(BT), 0, st, m, rg, 4, (int)SC_A1);
+            if (m.ob_order) hipLaunchKernelGGL(k_ob_sums, dim3(1), dim3(64), 0, st, m, 1);
             break;
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
@@ -3161,6 +3336,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_REPU:
             hipLaunchKernelGGL(k_repu, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_U);
+            if (m.ob_order) hipLaunchKernelGGL(k_ob_sums, dim3(1), dim3(64), 0, st, m, 2);
             break;
         case M_SMOOTH:
             hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);

@@ -1,0 +1,167 @@
+// pcx_rounds.cpp -- batched rounds above the one-wave round kernel's limits (N > 64
+// reporters or E > 32 events).
+//
+// The Monte Carlo regime (README.rst:52-56) loops Oracle(...).consensus()
+// (__init__.py:102-611) over many independent rounds.  Rounds up to 64 x 32 are one
+// wavefront each (pcx_batched.hip).  Larger rounds run here: each is one single-matrix
+// consensus (pcx_runner.cpp, the same kernels and arithmetic as pcx_consensus_f64 on
+// that round alone), and a pool of worker threads -- each with its own context, cached
+// workspace and non-blocking HIP stream -- keeps many rounds' stage chains in flight on
+// the GPU at once, so the per-stage launch and host-sync latency of one round overlaps
+// the others.  Rounds are handed out by an atomic counter; the per-round scalars are
+// gathered on the host and copied to the caller's [B] arrays once at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pcx_internal.h"
+
+namespace pcx {
+
+namespace {
+// worker contexts (streams) kept in flight: each round is a chain of ~30 dependent stage
+// launches and a few host polls, so throughput grows with the rounds in flight
+int pool_size() {
+    const char* e = getenv("PCX_ROUND_WORKERS");
+    const int n = e ? atoi(e) : 16;
+    return std::max(1, std::min(n, 64));
+}
+
+double* at(double* base, int64_t off) { return base ? base + off : nullptr; }
+}  // namespace
+
+void rounds_free(pcx_ctx* c) {
+    for (pcx_ctx* w : c->pool) {
+        (void)hipSetDevice(w->device);
+        workspace_free(w);
+        if (w->stream) (void)hipStreamDestroy(w->stream);
+        delete w;
+    }
+    c->pool.clear();
+}
+
+int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::string& err) {
+    const int64_t B = in->n_rounds, N = in->n_reporters, E = in->n_events;
+    if (B == 0) return 0;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // inputs produced on the caller's stream
+    if (e != hipSuccess) {
+        err = std::string("rounds: ") + hipGetErrorString(e);
+        return PCX_EHIP;
+    }
+    const int K = (int)std::min<int64_t>(pool_size(), B);
+    while ((int)c->pool.size() < K) {
+        pcx_ctx* w = new (std::nothrow) pcx_ctx;
+        if (!w) {
+            err = "rounds: out of host memory";
+            return PCX_ENOMEM;
+        }
+        w->device = c->device;
+        w->scaled_floor = (int)E;  // one workspace serves every round's bounds
+        e = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete w;
+            err = std::string("rounds: hipStreamCreate: ") + hipGetErrorString(e);
+            return PCX_EHIP;
+        }
+        c->pool.push_back(w);
+    }
+    std::vector<double> part(B), avg(B);
+    std::vector<int32_t> branch(B), flags(B), iters(B), comps(B);
+    std::atomic<int64_t> next{0};
+    std::atomic<int> failed{0};
+    std::vector<std::string> errs(K);
+    std::vector<int> rcs(K, 0);
+    auto worker = [&](int k) {
+        pcx_ctx* w = c->pool[k];
+        for (;;) {
+            const int64_t b = next.fetch_add(1);
+            if (b >= B || failed.load()) return;
+            pcx_problem p{};
+            p.n_rows = N;
+            p.n_events = E;
+            p.n_total = N;
+            p.row_offset = 0;
+            p.reports = in->reports + b * N * E;
+            p.reputation = in->reputation ? in->reputation + b * N : nullptr;
+            const int64_t bo = in->bounds_shared ? 0 : b * E;
+            p.scaled = in->scaled ? in->scaled + bo : nullptr;
+            p.lo = in->scaled ? in->lo + bo : nullptr;
+            p.hi = in->scaled ? in->hi + bo : nullptr;
+            p.catch_tolerance = in->catch_tolerance;
+            p.alpha = in->alpha;
+            p.int_dtype = in->int_dtype;
+            p.algorithm = in->algorithm;
+            p.max_components = in->max_components;
+            p.mem_kind = PCX_MEM_DEVICE;
+            p.variance_threshold = in->variance_threshold;
+            p.aux_scores = in->aux_scores ? in->aux_scores + b * N : nullptr;
+            pcx_result r{};
+            r.old_rep = at(out->old_rep, b * N);
+            r.this_rep = at(out->this_rep, b * N);
+            r.smooth_rep = at(out->smooth_rep, b * N);
+            r.scores = at(out->scores, b * N);
+            r.na_row = at(out->na_row, b * N);
+            r.participation_rows = at(out->participation_rows, b * N);
+            r.relative_part = at(out->relative_part, b * N);
+            r.reporter_bonus = at(out->reporter_bonus, b * N);
+            r.adj_first_loadings = at(out->adj_first_loadings, b * E);
+            r.outcomes_raw = at(out->outcomes_raw, b * E);
+            r.outcomes_adjusted = at(out->outcomes_adjusted, b * E);
+            r.outcomes_final = at(out->outcomes_final, b * E);
+            r.certainty = at(out->certainty, b * E);
+            r.consensus_reward = at(out->consensus_reward, b * E);
+            r.nas_filled = at(out->nas_filled, b * E);
+            r.participation_columns = at(out->participation_columns, b * E);
+            r.author_bonus = at(out->author_bonus, b * E);
+            r.original = at(out->original, b * N * E);
+            r.filled = at(out->filled, b * N * E);
+            const int rc = run_matrix(w, &p, &r, 0, nullptr, 0, nullptr, errs[k]);
+            if (rc) {
+                rcs[k] = rc;
+                errs[k] = "round " + std::to_string(b) + ": " + errs[k];
+                failed.store(1);
+                return;
+            }
+            part[b] = r.participation;
+            avg[b] = r.avg_certainty;
+            branch[b] = r.branch;
+            flags[b] = r.flags;
+            iters[b] = r.pi_iters;
+            comps[b] = r.components;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int k = 0; k < K; k++) th.emplace_back(worker, k);
+    for (auto& t : th) t.join();
+    for (int k = 0; k < K; k++)
+        if (rcs[k]) {
+            err = errs[k];
+            return rcs[k];
+        }
+    (void)hipSetDevice(c->device);
+    auto put = [&](void* dst, const void* src, size_t bytes) {
+        if (dst && e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+    };
+    put(out->participation, part.data(), B * 8);
+    put(out->avg_certainty, avg.data(), B * 8);
+    put(out->branch, branch.data(), B * 4);
+    put(out->flags, flags.data(), B * 4);
+    put(out->pi_iters, iters.data(), B * 4);
+    put(out->components, comps.data(), B * 4);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the host arrays die with this call
+    if (e != hipSuccess) {
+        err = std::string("rounds: scalar copy: ") + hipGetErrorString(e);
+        return PCX_EHIP;
+    }
+    return 0;
+}
+
+}  // namespace pcx

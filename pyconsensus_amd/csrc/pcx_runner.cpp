@@ -183,9 +183,12 @@ struct Run {
 pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total, int n_scaled, int world,
                          std::string& err, int& rc) {
     pcx_workspace* w = c->ws;
-    if (w && w->n_rows == n_rows && w->E == E && w->n_scaled == n_scaled && w->world == world &&
+    // capacity semantics in the scaled-event count: a context that runs many shapes of
+    // bounds (the batched-rounds scheduler sets scaled_floor = E) reuses one workspace
+    if (w && w->n_rows == n_rows && w->E == E && w->n_scaled >= n_scaled && w->world == world &&
         w->n_total == n_total)
         return w;
+    n_scaled = std::max(n_scaled, (int)std::min<int64_t>(c->scaled_floor, E));
     delete c->ws;  // one cached workspace per context (a C5 shard's is ~50 GB)
     c->ws = nullptr;
     w = new (std::nothrow) pcx_workspace;
@@ -624,6 +627,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.cov_kslices = (int32_t)w->cov_kslices;
         m.no_fill = filled_input ? 1 : 0;
         m.rank_rule = entry == 4 ? (rank_rule ? 1 : 0) : (alg == PCX_ALG_PCA ? 1 : 0);
+        // numpy/OpenBLAS run np.dot single-threaded below m*n = 9216 (interface/gemv.c: 2304 x
+        // GEMM_MULTITHREAD_THRESHOLD): there the reference's summation order is known and replayed
+        m.ob_order = (world == 1 && N * E < 9216) ? 1 : 0;
         m.scores_given = (entry == 4 || alg == PCX_ALG_COKURTOSIS) ? 1 : 0;
         m.reports = reports;
         m.scaled = scaled;

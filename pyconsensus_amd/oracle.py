@@ -8,8 +8,10 @@ result is computed by libpcx's HIP kernels:
 * rounds with N <= 64 reporters and E <= 32 events run the one-wavefront round
   kernel (csrc/pcx_batched.hip) -- the same kernel as the batched Monte Carlo
   regime, with a batch of one;
-* larger matrices run the staged single-matrix pipeline (pipeline.py,
-  csrc/pcx_matrix.hip).
+* larger matrices run the single-matrix pipeline (one call of pcx_consensus_f64,
+  csrc/pcx_runner.cpp + csrc/pcx_matrix.hip) on one GPU, or -- with
+  ``devices=[0, 1, ...]`` -- row-sharded over several GPUs of this process
+  (pcx_create_devices: one worker thread per GPU, RCCL over xGMI inside libpcx).
 
 There is no CPU fallback: without the library or a GPU, ``consensus()`` raises.
 """
@@ -40,7 +42,7 @@ class Oracle(object):
     def __init__(self, reports=None, event_bounds=None, reputation=None,
                  catch_tolerance=0.1, alpha=0.1, verbose=False,
                  aux=None, algorithm="PCA", variance_threshold=0.9,
-                 max_components=5, hierarchy_threshold=0.5, device=None):
+                 max_components=5, hierarchy_threshold=0.5, device=None, devices=None):
         self.NO, self.YES, self.BAD, self.NA = NO, YES, BAD, NA
         data = np.ma.getdata(reports) if isinstance(reports, np.ma.MaskedArray) else reports
         arr = np.asarray(data)
@@ -65,6 +67,10 @@ class Oracle(object):
         self.aux = aux
         self.max_components = max_components if self.num_events >= max_components else self.num_events
         self.device = device
+        # extension: shard the single-matrix path's rows over these GPUs (one process)
+        self.devices = None if devices is None else [int(d) for d in devices]
+        if self.devices is not None and not self.devices:
+            raise ValueError("devices must list at least one GPU")
         n = self.num_reports
         if reputation is None:  # :138-141
             self.weighted = False
@@ -95,6 +101,8 @@ class Oracle(object):
         return self.BAD
 
     def _device_index(self):
+        if self.devices is not None:
+            return self.devices[0]
         if self.device is None:
             return 0
         import torch
@@ -104,7 +112,8 @@ class Oracle(object):
 
     def _kw(self):
         return dict(catch_tolerance=self.catch_tolerance, alpha=self.alpha, algorithm=self._stage_algorithm(),
-                    max_components=self.max_components, variance_threshold=self.variance_threshold)
+                    max_components=self.max_components, variance_threshold=self.variance_threshold,
+                    devices=self.devices)
 
     def _stage_algorithm(self):
         return self.algorithm if self.algorithm in ("PCA", "absolute", "big-five", "fixed-variance",
@@ -205,8 +214,8 @@ class Oracle(object):
             if aux.size != N:
                 raise ValueError("aux['cokurt'] must hold one score per reporter")
         kw = dict(catch_tolerance=self.catch_tolerance, alpha=self.alpha, int_dtype=self._int_dtype,
-                  algorithm=self.algorithm, device=self.device, max_components=self.max_components,
-                  variance_threshold=self.variance_threshold)
+                  algorithm=self.algorithm, device=self.device if self.devices is None else self.devices[0],
+                  max_components=self.max_components, variance_threshold=self.variance_threshold)
         small = N <= MAX_REPORTERS and E <= MAX_EVENTS
         if self.algorithm in _abi.CLUSTER_ALGORITHMS and not small:
             raise NotImplementedError("algorithm %r runs in the batched regime only (N <= %d, E <= %d; got %d x %d)"
@@ -226,12 +235,14 @@ class Oracle(object):
             from .pipeline import consensus_host
 
             g, meta = consensus_host(self._data, self._rep_raw, sc, lo, hi, device_index=self._device_index(),
-                                     aux_scores=aux, **{k: v for k, v in kw.items() if k != "device"})
+                                     aux_scores=aux, devices=self.devices,
+                                     **{k: v for k, v in kw.items() if k != "device"})
             participation = float(meta["participation"])
             avg_certainty = float(meta["avg_certainty"])
             comps = int(meta["components"])
             self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
-                              "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"], "path": "matrix"}
+                              "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"], "path": "matrix",
+                              "devices": self.devices or [self._device_index()], "comm_bytes": meta["comm_bytes"]}
         if self.algorithm in ("big-five", "fixed-variance") and self.last_info["flags"] & _abi.FLAG_SVD_FAIL:
             # the reference's second svd (:375, :431) is outside the try of :329-333
             raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")

@@ -296,9 +296,10 @@ def _meta(res, algorithm):
 # ---------------------------------------------------------------- host-memory entry points
 def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outputs, catch_tolerance=0.1,
                alpha=0.1, int_dtype=False, algorithm="PCA", max_components=5, variance_threshold=0.9,
-               aux_scores=None, extra=()):
+               aux_scores=None, extra=(), devices=None):
     """Call a single-matrix entry point with numpy inputs / outputs (PCX_MEM_HOST: libpcx
-    copies in and out).  ``outputs``: {result field: shape}."""
+    copies in and out).  ``outputs``: {result field: shape}.  ``devices``: a list of device
+    ids -- libpcx shards the rows over them (pcx_create_devices), else one GPU."""
     _device.require_gpu()
     R = np.ascontiguousarray(reports, dtype=np.float64)
     n_rows, E = R.shape
@@ -321,7 +322,7 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
     for k, shape in outputs.items():
         outs[k] = np.empty(shape, dtype=np.float64)
         setattr(res, k, outs[k].ctypes.data)
-    h = _lib.context(device_index)
+    h = _lib.context(device_index) if devices is None else _lib.devices_context(devices)
     _lib.check(getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res)))
     return outs, _meta(res, algorithm)
 

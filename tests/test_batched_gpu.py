@@ -118,3 +118,59 @@ def test_variants_bitexact_vs_c_oracle(gpu_lib, variant):
     for k, v in g.items():
         same = (v == c[k]) | (np.isnan(v) & np.isnan(c[k])) if v.dtype.kind == "f" else (v == c[k])
         assert np.all(same), (variant, k, int(np.size(same) - np.count_nonzero(same)))
+
+
+@pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "200x24_big-five"])
+def test_rounds_above_one_wave(gpu_lib, variant):
+    """Rounds beyond the one-wavefront kernel (N > 64 or E > 32): the batched entry runs
+    each as a single-matrix consensus on a pool of worker streams (csrc/pcx_rounds.cpp).
+    Every round equals its own pcx_consensus_f64 call bit for bit and the numpy
+    restatement of the reference within the north_star tolerances."""
+    import torch
+
+    from oracle.pcx_oracle import OracleCPU
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+    from pyconsensus_amd.pipeline import consensus_matrix
+
+    shape, *rest = variant.split("_")
+    N, E = map(int, shape.split("x"))
+    B = 40
+    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=77)
+    kw = dict(reputation=rep, scaled=sc, lo=lo, hi=hi)
+    if "uniform" in rest:
+        kw["reputation"] = None
+    if "shared" in rest:
+        kw.update(scaled=sc[0], lo=lo[0], hi=hi[0])
+    alg = "big-five" if "big-five" in rest else "PCA"
+    g = _np(consensus_batched(R, filled=True, original=True, algorithm=alg, **kw))
+    torch.cuda.synchronize()
+    for b in [0, 1, B // 2, B - 1]:
+        s_b = kw["scaled"] if kw["scaled"].ndim == 1 else kw["scaled"][b]
+        lo_b = kw["lo"] if kw["lo"].ndim == 1 else kw["lo"][b]
+        hi_b = kw["hi"] if kw["hi"].ndim == 1 else kw["hi"][b]
+        rep_b = None if kw["reputation"] is None else kw["reputation"][b]
+        ev, ag, meta = consensus_matrix(R[b], rep_b, s_b, lo_b, hi_b, algorithm=alg, matrices=True)
+        one = {k: v.cpu().numpy() for d in (ev, ag) for k, v in d.items()}
+        for k, v in one.items():
+            np.testing.assert_array_equal(g[k][b], v, err_msg="%s round %d" % (k, b))
+        assert int(g["branch"][b]) == meta["branch"] and g["participation"][b] == meta["participation"]
+    for b in range(B):
+        s_b = kw["scaled"] if kw["scaled"].ndim == 1 else kw["scaled"][b]
+        lo_b = kw["lo"] if kw["lo"].ndim == 1 else kw["lo"][b]
+        hi_b = kw["hi"] if kw["hi"].ndim == 1 else kw["hi"][b]
+        rep_b = None if kw["reputation"] is None else kw["reputation"][b]
+        ref = G.flat_result(OracleCPU(reports=R[b].copy(), event_bounds=synthetic.bounds_list(s_b, lo_b, hi_b),
+                                      reputation=rep_b, algorithm=alg).consensus())
+        ours = {k: v[b] for k, v in g.items()}
+        bad, _ = P.compare(ref, ours)
+        assert not bad, (b, bad)
+
+
+def test_rounds_above_one_wave_refuse_clustering(gpu_lib):
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, sc, lo, hi, rep = synthetic.rounds(2, 70, 10, seed=1)
+    with pytest.raises(NotImplementedError):
+        consensus_batched(R, rep, sc, lo, hi, algorithm="hierarchical")

@@ -79,6 +79,65 @@ def test_c_program_calls_single_matrix_abi(gpu_lib, c_exe, world):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("devices", ["0", "0,0", "0,0,0"])
+def test_c_program_multi_device_context(gpu_lib, c_exe, devices):
+    """ONE pcx_consensus_f64 call on a pcx_create_devices context with the whole host matrix:
+    the library shards the rows over the listed devices (worker threads; RCCL ncclCommInitAll
+    for distinct ids -- "0" is a one-rank RCCL communicator -- host exchange when an id
+    repeats).  Equals the one-device call: discrete outputs exactly, continuous ones within the
+    north_star tolerance (the covariance partials are summed across ranks)."""
+    from pyconsensus_amd import synthetic
+
+    exe, d = c_exe
+    N, E = 9000, 130
+    R, sc, lo, hi, rep = synthetic.matrix(N, E, seed=31)
+    inp = str(d / "in_dev.bin")
+    _write_case(inp, R, rep, sc, lo, hi)
+    o1, on = str(d / "out_dev1.bin"), str(d / ("out_dev_%s.bin" % devices.replace(",", "_")))
+    r = subprocess.run([exe, inp, o1, "1"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    world = devices.count(",") + 1
+    r = subprocess.run([exe, inp, on, str(world), devices], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    print(r.stdout.strip())
+    # the sharded covariance is one f64 SUM all-reduce of per-rank partials: continuous
+    # outputs agree with the one-device call to rounding, discrete ones exactly
+    one, _ = _read_out(o1, N, E)
+    many, info = _read_out(on, N, E)
+    ref = {g: one[a] for g, a in P.ABI_NAME.items() if a in one}
+    bad, _ = P.compare(ref, many)
+    assert not bad, bad
+    for k in ("na_row", "nas_filled", "outcomes_adjusted", "outcomes_final", "filled"):
+        np.testing.assert_array_equal(many[k], one[k], err_msg=k)
+    assert info["branch"] == _read_out(o1, N, E)[1]["branch"]
+
+
+def test_oracle_devices_matches_one_gpu(gpu_lib):
+    """Oracle(devices=[0, 0]): the drop-in's row-sharded multi-GPU path (rehearsed on one
+    GPU: two ranks on device 0) equals Oracle() -- fills and discrete outputs exactly, the
+    rest within the north_star tolerance -- for consensus and the stage methods."""
+    from pyconsensus_amd import Oracle, _lib, synthetic
+
+    R, sc, lo, hi, rep = synthetic.matrix(3001, 70, seed=12)
+    eb = synthetic.bounds_list(sc, lo, hi)
+    one = Oracle(reports=R.copy(), event_bounds=eb, reputation=rep).consensus()
+    o2 = Oracle(reports=R.copy(), event_bounds=eb, reputation=rep, devices=[0, 0])
+    two = o2.consensus()
+    assert o2.last_info["devices"] == [0, 0] and o2.last_info["comm_bytes"] > 0
+    f1, f2 = G.flat_result(one), G.flat_result(two)
+    bad, _ = P.compare(f1, {a: f2[g] for g, a in P.ABI_NAME.items()})
+    assert not bad, bad
+    g1 = Oracle(reports=R.copy(), event_bounds=eb, reputation=rep)
+    g2 = Oracle(reports=R.copy(), event_bounds=eb, reputation=rep, devices=[0, 0, 0])
+    F1, F2 = g1.interpolate(g1.reports), g2.interpolate(g2.reports)
+    np.testing.assert_array_equal(F2, F1)  # fills are exact on any rank count
+    s1, s2 = g1.lie_detector(F1), g2.lie_detector(F2)
+    for k in ("this_rep", "smooth_rep"):
+        np.testing.assert_allclose(np.asarray(s2[k]), np.asarray(s1[k]), rtol=1e-9, atol=1e-12, err_msg=k)
+    with pytest.raises(_lib.PcxError, match="fewer rows than devices"):
+        Oracle(reports=np.ones((66, 2)), devices=[0] * 70).lie_detector(np.ones((66, 2)))
+
+
 def _small_oracles(name):
     from oracle.pcx_oracle import OracleCPU
     from pyconsensus_amd import Oracle, synthetic

@@ -1,0 +1,41 @@
+"""Throughput of batched rounds above the one-wavefront kernel (csrc/pcx_rounds.cpp):
+B rounds of N x E through pcx_consensus_batched_f64 at several worker-pool sizes.
+
+usage: python tools/bench_rounds.py [B] [N] [E]   (prints one JSON line per pool size)
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+    E = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    import torch
+
+    from pyconsensus_amd import _lib, synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=3)
+    dev = torch.device("cuda", 0)
+    Rt, rt = torch.as_tensor(R, device=dev), torch.as_tensor(rep, device=dev)
+    sct, lot, hit = (torch.as_tensor(a, device=dev) for a in (sc.astype("uint8"), lo, hi))
+    for workers in (1, 4, 8, 16, 32):
+        os.environ["PCX_ROUND_WORKERS"] = str(workers)
+        _lib._ctx.clear()  # fresh context: the pool size is read when it grows
+        consensus_batched(Rt[:workers], rt[:workers], sct[:workers], lot[:workers], hit[:workers])  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        consensus_batched(Rt, rt, sct, lot, hit)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(json.dumps({"rounds": B, "N": N, "E": E, "workers": workers, "seconds": dt,
+                          "rounds_per_s": B / dt}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
