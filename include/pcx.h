@@ -76,7 +76,7 @@ int      pcx_synchronize(pcx_ctx* ctx);
 /* style Monte Carlo, README.rst:52-56).  Each round is the complete            */
 /* Oracle(reports, event_bounds, reputation).consensus() of __init__.py:102-611. */
 /* N <= 64, E <= 32: one round per wavefront, asynchronous on the stream.      */
-/* Larger rounds (E <= 65536; not the clustering algorithms): each round is one */
+/* Larger rounds (E <= 65536, any algorithm): each round is one               */
 /* single-matrix consensus, a pool of worker streams keeps many in flight       */
 /* (PCX_ROUND_WORKERS, default 16); the call is then synchronous.              */
 /* ------------------------------------------------------------------------ */
@@ -115,9 +115,9 @@ enum pcx_algorithm {
     PCX_ALG_BIG_FIVE = 2,          /* eigenvalue-weighted top max_components scores (:373-390) */
     PCX_ALG_FIXED_VARIANCE = 3,    /* components up to variance_threshold (:429-451)           */
     PCX_ALG_COKURTOSIS = 4,        /* caller-supplied scores aux["cokurt"] (:455-457)          */
-    PCX_ALG_KMEANS = 5,            /* cluster sizes of scipy kmeans on whitened wcd (:392-405); batched only */
-    PCX_ALG_HIERARCHICAL = 6,      /* cluster sizes of single-linkage fclusterdata(wcd) (:407-419); batched only */
-    PCX_ALG_CLUSTERFECK = 7,       /* leader clustering of the filled reports (:148-242, :421-424); batched only */
+    PCX_ALG_KMEANS = 5,            /* cluster sizes of scipy kmeans on whitened wcd (:392-405)          */
+    PCX_ALG_HIERARCHICAL = 6,      /* cluster sizes of single-linkage fclusterdata(wcd) (:407-419)     */
+    PCX_ALG_CLUSTERFECK = 7,       /* leader clustering of the filled reports (:148-242, :421-424)     */
 };
 
 typedef struct {
@@ -230,11 +230,18 @@ typedef struct {
     double  catch_tolerance;      /* Oracle(catch_tolerance=0.1)                         */
     double  alpha;                /* Oracle(alpha=0.1)                                   */
     int32_t int_dtype;            /* 1: reports had an integer dtype (truncation, Q3)    */
-    int32_t algorithm;            /* enum pcx_algorithm: PCA, absolute, big-five, fixed-variance, cokurtosis */
+    int32_t algorithm;            /* enum pcx_algorithm (every value; the clustering ones on one rank) */
     int32_t max_components;       /* big-five (Oracle caps it at E, :134-137)            */
     int32_t mem_kind;             /* enum pcx_mem_kind                                   */
     double  variance_threshold;   /* fixed-variance (:448)                               */
     const double* aux_scores;     /* cokurtosis: [n_rows] this rank's aux["cokurt"] (:455-457) */
+    /* clustering algorithms (one rank; ABI >= 7; __init__.py:148-242, 392-424) */
+    double  hierarchy_threshold;  /* "hierarchical": fcluster distance cut, Oracle(hierarchy_threshold=0.5) */
+    double  cluster_threshold;    /* "clusterfeck": leader cut; <= 0: the reference's log10(E)/1.77 rule */
+    int32_t kmeans_k;             /* "k-means": code-book size int(ceil(sqrt(N))) (:396)          */
+    int32_t kmeans_restarts;      /* "k-means": scipy kmeans iter= (20)                           */
+    const int32_t* kmeans_init;   /* "k-means": [restarts][k] HOST rows of the initial code books (the
+                                     reference's rng.choice draws, pyconsensus_amd.batched.kmeans_draws) */
 } pcx_problem;
 
 typedef struct {

@@ -100,7 +100,9 @@ class Problem(C.Structure):
         ("reports", _vp), ("reputation", _vp), ("scaled", _vp), ("lo", _vp), ("hi", _vp),
         ("catch_tolerance", C.c_double), ("alpha", C.c_double),
         ("int_dtype", C.c_int32), ("algorithm", C.c_int32), ("max_components", C.c_int32), ("mem_kind", C.c_int32),
-        ("variance_threshold", C.c_double), ("aux_scores", _vp)]
+        ("variance_threshold", C.c_double), ("aux_scores", _vp),
+        ("hierarchy_threshold", C.c_double), ("cluster_threshold", C.c_double),
+        ("kmeans_k", C.c_int32), ("kmeans_restarts", C.c_int32), ("kmeans_init", _vp)]
 
 
 RESULT_VECTORS = MAT_OUTPUT_AGENTS + MAT_OUTPUT_EVENTS + ["original", "filled", "weighted_mean", "covariance"]

@@ -77,9 +77,6 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     B, N, E = R.shape
     if N < 1 or E < 1:
         raise ValueError("batched rounds need N >= 1 and E >= 1 (got %d x %d)" % (N, E))
-    if (N > MAX_REPORTERS or E > MAX_EVENTS) and algorithm in _abi.CLUSTER_ALGORITHMS:
-        raise NotImplementedError("algorithm %r runs on rounds of at most %d x %d (got %d x %d)"
-                                  % (algorithm, MAX_REPORTERS, MAX_EVENTS, N, E))
     rep = _device.as_device(reputation, t.float64, dev)
     if rep is not None and tuple(rep.shape) != (B, N):
         raise ValueError("reputation must be (B, N)")

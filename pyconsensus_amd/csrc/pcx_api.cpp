@@ -203,16 +203,15 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
         return fail(PCX_EINVAL, "batched: n_reporters must be in [1, 2^31)");
     if (in->n_events < 1 || in->n_events > 65536) return fail(PCX_EINVAL, "batched: n_events must be in [1, 65536]");
     const bool large = in->n_reporters > 64 || in->n_events > 32;  // beyond one wavefront per round
-    if (large && in->algorithm >= PCX_ALG_KMEANS)
-        return fail(PCX_EINVAL, "batched: the clustering algorithms need rounds of at most 64 x 32");
     if (!in->reports) return fail(PCX_EINVAL, "batched: reports is NULL");
     if (in->scaled && (!in->lo || !in->hi)) return fail(PCX_EINVAL, "batched: scaled given without lo/hi");
     if (in->algorithm < PCX_ALG_PCA || in->algorithm > PCX_ALG_CLUSTERFECK)
         return fail(PCX_EINVAL, "batched: algorithm must be an enum pcx_algorithm value (0..7)");
     if (in->algorithm == PCX_ALG_KMEANS &&
-        (!in->kmeans_init || in->kmeans_k < 1 || in->kmeans_k > 8 || in->kmeans_k > in->n_reporters ||
+        (!in->kmeans_init || in->kmeans_k < 1 || in->kmeans_k > (large ? 1024 : 8) || in->kmeans_k > in->n_reporters ||
          in->kmeans_restarts < 1))
-        return fail(PCX_EINVAL, "batched: k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 8), restarts >= 1");
+        return fail(PCX_EINVAL, "batched: k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 8; 1024 above 64 x 32), "
+                                "restarts >= 1");
     if (in->algorithm == PCX_ALG_HIERARCHICAL && std::isnan(in->hierarchy_threshold))
         return fail(PCX_EINVAL, "batched: hierarchy_threshold is NaN");
     if (in->algorithm == PCX_ALG_BIG_FIVE && (in->max_components < 1 || in->max_components > in->n_events))

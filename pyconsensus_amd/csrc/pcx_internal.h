@@ -163,7 +163,7 @@ enum mat_stage_id {
     M_AGENTS, M_MATRICES, M_WCD, M_EIG, M_ZERO_LOADING, M_NC_OUT, M_WMEAN_OUT,
     M_SEL_EXACT, M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_VALUE_FINISH, M_SEL_COMPACT,
     M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH, M_HARD_LIST, M_HARD_GATHER, M_HARD_PREP, M_HARD_SORT, M_HARD_WALK,
-    M_EXCHANGE, M_H2D, M_D2H, M_COV_PLAN, M_COV_I8, M_NSTAGE
+    M_EXCHANGE, M_H2D, M_D2H, M_COV_PLAN, M_COV_I8, M_CLUSTER, M_NSTAGE
 };
 static_assert(M_NSTAGE <= PCX_NSTAGES, "stage table");
 const char* stage_name(int k);
@@ -195,6 +195,36 @@ enum hard_mode { HARD_NONE = 0, HARD_MEAN = 1, HARD_MEDIAN = 2 };
 hipError_t hard_stage(pcx_mat& m, const HardArgs& h, int stage, hipStream_t st, std::string& err);
 
 hipError_t hard_list(pcx_mat& m, int32_t* cols, int32_t* modes, hipStream_t st);
+
+// clustering algorithms on the single-matrix path (one rank): scratch and state
+struct ClusterArgs {
+    int32_t alg;            // PCX_ALG_KMEANS / HIERARCHICAL / CLUSTERFECK
+    double  thr;            // hierarchical distance cut / clusterfeck threshold (default rule applied)
+    int32_t k;              // k-means code-book size
+    int32_t restart;        // k-means: current restart (row of kinit)
+    const double* weights;  // k_cl_mu weights: rep (wpca mean) or wtok (clusterfeck outcomes)
+    double* mu;             // [E] np.ma.average of the filled columns
+    double* sd;             // [E] whiten's column std
+    double* outc;           // [E] clusterfeck outcomes
+    double* X;              // [N][E] wcd (hierarchical), whitened wcd (k-means), filled reports (clusterfeck)
+    double* S;              // [max(N, k)][E] cluster sums
+    double* book;           // [k][E] k-means code book
+    double* best;           // [k][E] best restart's code book
+    double* cs;             // [k] |code|^2
+    double* dist;           // [N] vq distortions / cluster distances
+    double* dm;             // [N] clusterfeck row distances
+    double* dm1;            // [N]
+    double* crep;           // [N] clusterfeck cluster weight sums
+    double* wtok;           // [N] reptokens with zeros -> 1e-5 (:202-204)
+    double* kst;            // [8] k-means state: prev0, prev1, best_d, continue, ncodes, best_n, it
+    int32_t* lab;           // [N] labels / cluster of each row
+    int32_t* cnt;           // [N] members per root / code
+    int32_t* par;           // [N] union-find parents / clusterfeck first member
+    int32_t* kinit;         // [restarts][k] initial code-book rows
+};
+enum cluster_step { CL_WTOK = 0, CL_MU, CL_X_WCD, CL_X_F, CL_WHITEN, CL_HIER, CL_NC_ROOT, CL_NC_LAB, CL_FECK,
+                    KM_INIT, KM_ITER, KM_KEEP, KM_FINAL };
+hipError_t cluster_stage(pcx_mat& m, const ClusterArgs& a, int step, hipStream_t st, std::string& err);
 hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st);
 hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner

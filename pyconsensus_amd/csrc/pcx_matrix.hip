@@ -1755,7 +1755,9 @@ __global__ void __launch_bounds__(BT) k_repu(pcx_mat m) {
     acc2 a, ap;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         double nc = 0.0;
-        if (m.algorithm != 1) {  // "absolute": nc = 0 (Q13)
+        if (m.algorithm >= 5) {  // the clusterings: nc from the cluster sizes / distances
+            nc = m.rowv[RV_N1 * m.n_rows + i];
+        } else if (m.algorithm != 1) {  // "absolute": nc = 0 (Q13)
             const double s = m.rowv[RV_S * m.n_rows + i];
             nc = pick1 ? s + fabs(mn) : s - mx;
         }
@@ -1814,7 +1816,7 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
             const double f = ms ? p.guess : x;
             const double w = wv[u];
             raw.add_prod(w, f);
-            pc += ms ? w : 0.0;
+            pc += w * (ms ? 1.0 : 0.0);  // np.dot(smooth_rep, na_mat): a NaN weight propagates
             b1 += f == 1.0 ? w : 0.0;
             b15 += f == 1.5 ? w : 0.0;
             b2 += f == 2.0 ? w : 0.0;
@@ -3140,6 +3142,497 @@ int grid_rows(int64_t n, int per_block) {
     return (int)g;
 }
 
+// ================================================================== clustering algorithms
+// "k-means" (:392-405), "hierarchical" (:407-419) and "clusterfeck" (:148-242, :421-424) on
+// one rank, any N x E, in the operation order of the batched SPEC (oracle/
+// pcx_oracle_batched.c hier_nc / kmeans_nc / feck_nc, pinned to 525 reference cases), which
+// these kernels generalise from one 64 x 32 round.  Each algorithm turns the filled matrix
+// into the nonconformity vector nc (rowv[RV_N1]); the common tail (:459-611) follows.
+
+// np.ma.average(F, axis=0, weights) (:317, :167): column sums sequential over rows (pairwise
+// when E == 1) over the pairwise total of the weights
+__global__ void __launch_bounds__(BT) k_cl_mu(pcx_mat m, ClusterArgs a, double* out) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (c >= E) return;
+    const ColParam p = col_param(m, c, true);
+    const int64_t N = m.n_rows;
+    const double* w = a.weights;
+    auto F = [&](int64_t i) { return filled(m.reports[i * E + c], p, m.int_dtype); };
+    const double den = pw_sum_dev([&](int64_t i) { return w[i]; }, N);
+    double num;
+    if (E == 1) {
+        num = pw_sum_dev([&](int64_t i) { return F(i) * w[i]; }, N);
+    } else {
+        num = F(0) * w[0];
+        for (int64_t i = 1; i < N; i++) num = num + F(i) * w[i];
+    }
+    out[c] = num / den;
+}
+
+// reptokens with the zeros clusterfeck rewrites (:202-204)
+__global__ void __launch_bounds__(BT) k_cl_wtok(pcx_mat m, ClusterArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT)
+        a.wtok[i] = m.tok[i] == 0.0 ? 0.00001 : m.tok[i];
+}
+
+// X = F - mu (wcd, :322) or X = F
+__global__ void __launch_bounds__(BT) k_cl_x(pcx_mat m, ClusterArgs a, int centre) {
+    const int64_t E = m.n_events, n = m.n_rows * E;
+    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * BT) {
+        const int c = (int)(idx % E);
+        const ColParam p = col_param(m, c, true);
+        const double f = filled(m.reports[idx], p, m.int_dtype);
+        a.X[idx] = centre ? f - a.mu[c] : f;
+    }
+}
+
+// whiten (:395): population std of each wcd column (np.std axis 0: sequential column sums,
+// pairwise when E == 1), zero -> 1
+__global__ void __launch_bounds__(BT) k_cl_sd(pcx_mat m, ClusterArgs a) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    const int64_t E = m.n_events, N = m.n_rows;
+    if (c >= E) return;
+    const double* X = a.X;
+    double s = 0.0;
+    if (E == 1) s = pw_sum_dev([&](int64_t i) { return X[i]; }, N);
+    else
+        for (int64_t i = 0; i < N; i++) s = s + X[i * E + c];
+    const double mean = s / (double)N;
+    double v = 0.0;
+    if (E == 1) {
+        v = pw_sum_dev([&](int64_t i) { return (X[i] - mean) * (X[i] - mean); }, N);
+    } else {
+        for (int64_t i = 0; i < N; i++) {
+            const double d = X[i * E + c] - mean;
+            v = v + d * d;
+        }
+    }
+    double sd = sqrt(v / (double)N);
+    a.sd[c] = sd == 0.0 ? 1.0 : sd;
+}
+
+__global__ void __launch_bounds__(BT) k_cl_div(pcx_mat m, ClusterArgs a) {
+    const int64_t E = m.n_events, n = m.n_rows * E;
+    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * BT)
+        a.X[idx] = a.X[idx] / a.sd[idx % E];
+}
+
+// lock-free union-find: parents point to smaller indices (no cycles), path halving by CAS
+__device__ __forceinline__ int uf_load(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ int uf_find(int* par, int x) {
+    for (;;) {
+        const int q = uf_load(par + x);
+        if (q == x) return x;
+        const int r = uf_load(par + q);
+        if (r != q) atomicCAS(par + x, q, r);
+        x = q;
+    }
+}
+__device__ void uf_unite(int* par, int a, int b) {
+    for (;;) {
+        a = uf_find(par, a);
+        b = uf_find(par, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(par + a, a, b) == a) return;
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_cl_iota(pcx_mat m, ClusterArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        a.par[i] = (int)i;
+        a.cnt[i] = 0;
+    }
+}
+
+// hierarchical (:407-419): scipy fclusterdata(wcd, t, 'distance') with single linkage on
+// euclidean pdist = connected components of {d_ij <= t}; d_ij = sqrt(sum_k (x_ik - x_jk)^2),
+// sequential in k, no fma (scipy's pdist order).  16 x 16 row pairs per block, 32 events per
+// LDS stage (the k order is kept across stages).
+constexpr int CLT = 16, CLK = 32;
+__global__ void __launch_bounds__(CLT * CLT) k_cl_hier(pcx_mat m, ClusterArgs a) {
+    const int I = blockIdx.y, J = blockIdx.x;
+    if (I > J) return;
+    __shared__ double xi[CLT][CLK + 1], xj[CLT][CLK + 1];
+    const int64_t N = m.n_rows, E = m.n_events;
+    const int ti = threadIdx.x / CLT, tj = threadIdx.x % CLT;
+    const int64_t i = (int64_t)I * CLT + ti, j = (int64_t)J * CLT + tj;
+    double d2 = 0.0;
+    for (int64_t k0 = 0; k0 < E; k0 += CLK) {
+        for (int e = threadIdx.x; e < 2 * CLT * CLK; e += CLT * CLT) {
+            const int side = e / (CLT * CLK), r = (e / CLK) % CLT, k = e % CLK;
+            const int64_t row = (int64_t)(side ? J : I) * CLT + r;
+            const double v = (row < N && k0 + k < E) ? a.X[row * E + k0 + k] : 0.0;
+            if (side) xj[r][k] = v;
+            else xi[r][k] = v;
+        }
+        __syncthreads();
+        const int kn = (int)(E - k0 < CLK ? E - k0 : CLK);
+        for (int k = 0; k < kn; k++) {
+            const double df = xi[ti][k] - xj[tj][k];
+            d2 = d2 + df * df;
+        }
+        __syncthreads();
+    }
+    if (i < j && j < N && sqrt(d2) <= a.thr) uf_unite(a.par, (int)i, (int)j);
+}
+
+// members per union-find root
+__global__ void __launch_bounds__(BT) k_cl_roots(pcx_mat m, ClusterArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const int r = uf_find(a.par, (int)i);
+        a.lab[i] = r;
+        atomicAdd(a.cnt + r, 1);
+    }
+}
+
+// nc from the cluster sizes (:398-405, :412-419): (size - min size) / sum, integer sums
+// exact; all clusters the same size give 0 / 0 = NaN like numpy.  size_i = cnt[lab[i]].
+__global__ void __launch_bounds__(1024) k_cl_nc(pcx_mat m, ClusterArgs a) {
+    __shared__ int mn;
+    __shared__ unsigned long long tot;
+    const int64_t N = m.n_rows;
+    if (threadIdx.x == 0) {
+        mn = 0x7fffffff;
+        tot = 0;
+    }
+    __syncthreads();
+    int lmin = 0x7fffffff;
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) lmin = min(lmin, a.cnt[a.lab[i]]);
+    atomicMin(&mn, lmin);
+    __syncthreads();
+    unsigned long long lt = 0;
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) lt += (unsigned long long)(a.cnt[a.lab[i]] - mn);
+    atomicAdd(&tot, lt);
+    __syncthreads();
+    double* nc = m.rowv + RV_N1 * N;
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x)
+        nc[i] = (double)(a.cnt[a.lab[i]] - mn) / (double)tot;
+}
+
+// ---------------------------------------------------------------- clusterfeck
+// block-wide argmin of (d, x) (first minimum) / argmax of (v, x) (first maximum)
+__device__ void cl_argbest(double& v, int& x, bool mx, double* sv, int* sx) {
+    const int t = threadIdx.x;
+    sv[t] = v;
+    sx[t] = x;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s >= 1; s >>= 1) {
+        if (t < s) {
+            const double v2 = sv[t + s];
+            const int x2 = sx[t + s];
+            const bool take = x2 >= 0 && (sx[t] < 0 || (mx ? v2 > sv[t] : v2 < sv[t]) || (v2 == sv[t] && x2 < sx[t]));
+            if (take) {
+                sv[t] = v2;
+                sx[t] = x2;
+            }
+        }
+        __syncthreads();
+    }
+    v = sv[0];
+    x = sx[0];
+    __syncthreads();
+}
+
+// mean vector of cluster x (newMean, :151-157): a singleton's row, else running sums / weight
+__device__ __forceinline__ double feck_mean_k(const ClusterArgs& a, int64_t E, int x, int64_t k) {
+    return a.cnt[x] == 1 ? a.X[(int64_t)a.par[x] * E + k] : a.S[(int64_t)x * E + k] / a.crep[x];
+}
+
+// L2dist (:148-149): sqrt(np.sum((v1 - v2)**2)), numpy pairwise sum
+template <class A, class B>
+__device__ __forceinline__ double feck_l2(A u, B v, int64_t E) {
+    return sqrt(pw_sum_dev([&](int64_t k) { const double d = u(k) - v(k); return d * d; }, E));
+}
+
+// Oracle.cluster (:194-230): rows in order join the nearest cluster (first minimum) when its
+// mean is closer than thr, else found a new cluster (rows with NaN never do); returns the mode
+// (first cluster of largest weight, :162-165)
+__device__ int feck_pass(const pcx_mat& m, const ClusterArgs& a, double thr, double* sv, int* sx, int* nclus) {
+    const int64_t N = m.n_rows, E = m.n_events;
+    if (threadIdx.x == 0) *nclus = 0;
+    __syncthreads();
+    for (int64_t i = 0; i < N; i++) {
+        const int n = *nclus;
+        double bd = 0x1p255;
+        int bx = -1;
+        for (int x = threadIdx.x; x < n; x += blockDim.x) {
+            const double d = feck_l2([&](int64_t k) { return a.X[i * E + k]; },
+                                     [&](int64_t k) { return feck_mean_k(a, E, x, k); }, E);
+            if (d < bd) {
+                bd = d;
+                bx = x;
+            }
+        }
+        cl_argbest(bd, bx, false, sv, sx);
+        if (bx >= 0 && bd < thr) {
+            const double wi = a.wtok[i];
+            for (int64_t k = threadIdx.x; k < E; k += blockDim.x)
+                a.S[(int64_t)bx * E + k] = a.S[(int64_t)bx * E + k] + a.X[i * E + k] * wi;
+            __syncthreads();  // the sums read cnt == 1 rows above: bump the count after them
+            if (threadIdx.x == 0) {
+                a.crep[bx] = a.crep[bx] + wi;
+                a.cnt[bx] += 1;
+                a.lab[i] = bx;
+            }
+        } else {
+            int nan = 0;
+            for (int64_t k = threadIdx.x; k < E; k += blockDim.x) nan |= __builtin_isnan(a.X[i * E + k]) ? 1 : 0;
+            nan = __syncthreads_or(nan);
+            if (!nan) {
+                const double wi = a.wtok[i];
+                for (int64_t k = threadIdx.x; k < E; k += blockDim.x) a.S[(int64_t)n * E + k] = a.X[i * E + k] * wi;
+                if (threadIdx.x == 0) {
+                    a.par[n] = (int)i;
+                    a.cnt[n] = 1;
+                    a.crep[n] = wi;
+                    a.lab[i] = n;
+                    *nclus = n + 1;
+                }
+            } else if (threadIdx.x == 0) {
+                a.lab[i] = -1;
+            }
+        }
+        __syncthreads();
+    }
+    const int n = *nclus;
+    double top = 0.0;
+    int mode = -1;
+    for (int x = threadIdx.x; x < n; x += blockDim.x)
+        if (a.crep[x] > top) {
+            top = a.crep[x];
+            mode = x;
+        }
+    cl_argbest(top, mode, true, sv, sx);
+    return mode;
+}
+
+// per-row distance of its cluster's mean to the mode's mean (:177-183), into dm
+__device__ void feck_rowdist(const pcx_mat& m, const ClusterArgs& a, int mode, int n, double* dm) {
+    const int64_t N = m.n_rows, E = m.n_events;
+    for (int x = threadIdx.x; x < n; x += blockDim.x)
+        a.dist[x] = feck_l2([&](int64_t k) { return feck_mean_k(a, E, mode, k); },
+                            [&](int64_t k) { return feck_mean_k(a, E, x, k); }, E);
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) dm[i] = a.lab[i] >= 0 ? a.dist[a.lab[i]] : 0.0;
+    __syncthreads();
+}
+
+// clusterfeck: outsideCluster(reports_filled, reptokens) (:185-196, :150-183), one workgroup
+__global__ void __launch_bounds__(1024) k_cl_feck(pcx_mat m, ClusterArgs a) {
+    __shared__ double sv[1024];
+    __shared__ int sx[1024];
+    __shared__ int nclus;
+    __shared__ double dsh[2];
+    const int64_t N = m.n_rows, E = m.n_events;
+    const int mode1 = feck_pass(m, a, a.thr, sv, sx, &nclus);
+    if (threadIdx.x == 0)
+        dsh[0] = mode1 < 0 ? __builtin_nan("")
+                           : feck_l2([&](int64_t k) { return feck_mean_k(a, E, mode1, k); },
+                                     [&](int64_t k) { return a.outc[k]; }, E);
+    __syncthreads();
+    const double d1 = dsh[0];
+    if (mode1 >= 0) feck_rowdist(m, a, mode1, nclus, a.dm);
+    if (d1 > 1.07) {  // a far mode re-clusters once with 3 x the threshold (:172-174)
+        const int mode2 = feck_pass(m, a, a.thr * 3.0, sv, sx, &nclus);
+        if (threadIdx.x == 0)
+            dsh[1] = mode2 < 0 ? __builtin_nan("")
+                               : feck_l2([&](int64_t k) { return feck_mean_k(a, E, mode2, k); },
+                                         [&](int64_t k) { return a.outc[k]; }, E);
+        __syncthreads();
+        if (dsh[1] < d1) feck_rowdist(m, a, mode2, nclus, a.dm);
+    }
+    if (threadIdx.x == 0) {  // np.amax (NaN propagates); rv = 1 - dm / (max + 1e-8); normalize
+        double mx = a.dm[0];
+        for (int64_t i = 1; i < N; i++) {
+            const double v = a.dm[i];
+            if (__builtin_isnan(v) || v > mx) mx = __builtin_isnan(mx) ? mx : v;
+        }
+        dsh[0] = mx;
+    }
+    __syncthreads();
+    const double mx = dsh[0];
+    double* rv = a.dist;
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) rv[i] = fabs(1.0 - a.dm[i] / (mx + 0.00000001));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = pw_sum_dev([&](int64_t i) { return rv[i]; }, N);
+        dsh[0] = s;
+        dsh[1] = s == 0.0 ? pw_sum_dev([&](int64_t i) { return rv[i] + 1.0; }, N) : s;
+    }
+    __syncthreads();
+    double* nc = m.rowv + RV_N1 * N;
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) nc[i] = nweight(rv[i], dsh[0], dsh[1]);
+}
+
+// ---------------------------------------------------------------- k-means
+enum km_state { KS_PREV0 = 0, KS_PREV1, KS_BEST, KS_CONT, KS_NCODES, KS_BESTN, KS_IT, KS_FIRST };
+
+// scipy _vq distance^2 (SPEC vq_d2): E < 5 the naive loop; else -2 x.c (one fma chain for
+// E < 32, eight interleaved chains summed as a tree from 32) + |x|^2 + |c|^2
+__device__ __forceinline__ double km_d2(const double* x, const double* c, int64_t E, double xs, double cs) {
+    if (E < 5) {
+        double s = 0.0;
+        for (int64_t k = 0; k < E; k++) {
+            const double d = x[k] - c[k];
+            s = s + d * d;
+        }
+        return s;
+    }
+    double dot;
+    if (E < 32) {
+        dot = 0.0;
+        for (int64_t k = 0; k < E; k++) dot = fma(x[k], c[k], dot);
+    } else {
+        double q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int64_t k = 0; k < E; k++) q[k & 7] = fma(x[k], c[k], q[k & 7]);
+        dot = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+    }
+    return (-2.0 * dot + xs) + cs;
+}
+
+__device__ __forceinline__ double km_sq(const double* x, int64_t E) {
+    double s = 0.0;
+    for (int64_t k = 0; k < E; k++) s = s + x[k] * x[k];
+    return s;
+}
+
+__global__ void __launch_bounds__(BT) k_km_init(pcx_mat m, ClusterArgs a) {
+    const int64_t E = m.n_events, n = (int64_t)a.k * E;
+    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * BT) {
+        const int64_t c = idx / E, k = idx % E;
+        a.book[idx] = a.X[(int64_t)a.kinit[(int64_t)a.restart * a.k + c] * E + k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.kst[KS_PREV0] = __builtin_inf();
+        a.kst[KS_PREV1] = __builtin_inf();
+        a.kst[KS_NCODES] = a.k;
+        a.kst[KS_IT] = 0;
+        a.kst[KS_FIRST] = 1;
+        a.kst[KS_CONT] = 1;
+        if (a.restart == 0) {
+            a.kst[KS_BEST] = __builtin_inf();
+            a.kst[KS_BESTN] = 0;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(BT) k_km_cs(pcx_mat m, ClusterArgs a, const double* book) {
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c < (int)a.kst[KS_NCODES]) a.cs[c] = km_sq(book + (int64_t)c * m.n_events, m.n_events);
+}
+
+// vq (:397-398): nearest code (first minimum) and its distance of every row
+__global__ void __launch_bounds__(BT) k_km_vq(pcx_mat m, ClusterArgs a, const double* book) {
+    const int64_t E = m.n_events;
+    const int nc = (int)a.kst[KS_NCODES];
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const double* x = a.X + i * E;
+        const double xs = km_sq(x, E);
+        double low = __builtin_inf();
+        int l = 0;
+        for (int c = 0; c < nc; c++) {
+            const double d = km_d2(x, book + (int64_t)c * E, E, xs, a.cs[c]);
+            if (d < low) {
+                low = d;
+                l = c;
+            }
+        }
+        a.lab[i] = l;
+        a.dist[i] = low > 0 ? sqrt(low) : 0.0;
+    }
+}
+
+// one Lloyd step after vq (scipy _kmeans): mean distortion (np.mean, pairwise), member sums in
+// row order / counts, empty codes dropped, |avg_prev - avg| > 1e-5 continues
+__global__ void __launch_bounds__(1024) k_km_update(pcx_mat m, ClusterArgs a) {
+    const int64_t N = m.n_rows, E = m.n_events;
+    const int nc = (int)a.kst[KS_NCODES];
+    __shared__ int keep[1024];  // new index of each code (-1: empty); nc <= 1024 (host-checked)
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) a.cnt[c] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) atomicAdd(a.cnt + a.lab[i], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double avg = pw_sum_dev([&](int64_t i) { return a.dist[i]; }, N) / (double)N;
+        if (a.kst[KS_FIRST] != 0) {
+            a.kst[KS_PREV1] = avg;
+            a.kst[KS_FIRST] = 0;
+        } else {
+            a.kst[KS_PREV0] = a.kst[KS_PREV1];
+            a.kst[KS_PREV1] = avg;
+        }
+        int mm = 0;
+        for (int c = 0; c < nc; c++) keep[c] = a.cnt[c] > 0 ? mm++ : -1;
+        a.kst[KS_NCODES] = mm;
+        const double diff = fabs(a.kst[KS_PREV0] - a.kst[KS_PREV1]);
+        const double it = a.kst[KS_IT] + 1;
+        a.kst[KS_IT] = it;
+        a.kst[KS_CONT] = (diff > 1e-5 && it < 4096) ? 1 : 0;  // 4096: the device's guard (SPEC KMEANS_MAXIT)
+    }
+    __syncthreads();
+    for (int64_t idx = threadIdx.x; idx < (int64_t)nc * E; idx += blockDim.x) {
+        const int c = (int)(idx / E);
+        if (keep[c] >= 0) a.book[(int64_t)keep[c] * E + idx % E] = a.S[idx] / (double)a.cnt[c];
+    }
+}
+
+// update_cluster_means: the member sum of (code c, feature k) in row order, one thread each
+__global__ void __launch_bounds__(BT) k_km_sums(pcx_mat m, ClusterArgs a) {
+    const int64_t N = m.n_rows, E = m.n_events;
+    const int64_t n = (int64_t)a.kst[KS_NCODES] * E;
+    for (int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * BT) {
+        const int c = (int)(idx / E);
+        const int64_t k = idx % E;
+        double s = 0.0;
+        for (int64_t i = 0; i < N; i++)
+            if (a.lab[i] == c) s = s + a.X[i * E + k];
+        a.S[idx] = s;
+    }
+}
+
+// best restart by final mean distortion (strictly smaller wins)
+__global__ void __launch_bounds__(1024) k_km_keep(pcx_mat m, ClusterArgs a) {
+    __shared__ int take;
+    const int64_t E = m.n_events;
+    if (threadIdx.x == 0) {
+        take = a.kst[KS_PREV1] < a.kst[KS_BEST];
+        if (take) {
+            a.kst[KS_BEST] = a.kst[KS_PREV1];
+            a.kst[KS_BESTN] = a.kst[KS_NCODES];
+        }
+    }
+    __syncthreads();
+    if (!take) return;
+    const int64_t n = (int64_t)a.kst[KS_NCODES] * E;
+    for (int64_t idx = threadIdx.x; idx < n; idx += blockDim.x) a.best[idx] = a.book[idx];
+}
+
+__global__ void k_km_final_prep(ClusterArgs a) {
+    if (threadIdx.x == 0) a.kst[KS_NCODES] = a.kst[KS_BESTN];
+}
+
+// no restart with a finite distortion (best_n == 0): the reference raises; nc = NaN
+__global__ void __launch_bounds__(BT) k_km_nc_nan(pcx_mat m, ClusterArgs a) {
+    if (a.kst[KS_BESTN] != 0) return;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT)
+        m.rowv[RV_N1 * m.n_rows + i] = __builtin_nan("");
+}
+
+__global__ void __launch_bounds__(BT) k_km_count(pcx_mat m, ClusterArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT)
+        atomicAdd(a.cnt + a.lab[i], 1);
+}
+
+__global__ void __launch_bounds__(BT) k_cl_zero_cnt(pcx_mat m, ClusterArgs a) {
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) a.cnt[i] = 0;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ stage dispatcher
@@ -3150,7 +3643,7 @@ const char* stage_name(int k) {
         "ROWSUMS", "AGENTS", "MATRICES", "WCD", "EIG", "ZERO_LOADING", "NC_OUT", "WMEAN_OUT", "SEL_EXACT",
         "SEL_INIT", "SEL_START", "SEL_ARGMAX", "SEL_VALUE", "SEL_VALUE_FINISH", "SEL_COMPACT", "SEL_HIST",
         "SEL_STEP", "SEL_FINISH", "HARD_LIST", "HARD_GATHER", "HARD_PREP", "HARD_SORT", "HARD_WALK", "EXCHANGE",
-        "H2D", "D2H", "COV_PLAN", "COV_I8"};
+        "H2D", "D2H", "COV_PLAN", "COV_I8", "CLUSTER"};
     return (k >= 0 && k < M_NSTAGE) ? names[k] : "";
 }
 
@@ -3165,6 +3658,67 @@ hipError_t copy2d(double* dst, int64_t dpitch, const double* src, int64_t spitch
     if (width <= 0 || rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_copy2d, dim3(grid_rows(width * rows, BT)), dim3(BT), 0, st, dst, dpitch, src, spitch, width,
                        rows);
+    return hipGetLastError();
+}
+
+hipError_t cluster_stage(pcx_mat& m, const ClusterArgs& a, int step, hipStream_t st, std::string& err) {
+    const int E = (int)m.n_events;
+    const int ceb = (E + BT - 1) / BT;
+    const int rg = grid_rows(m.n_rows, BT);
+    const int eg = grid_rows(m.n_rows * (int64_t)E, BT);
+    switch (step) {
+        case CL_WTOK:
+            hipLaunchKernelGGL(k_cl_wtok, dim3(rg), dim3(BT), 0, st, m, a);
+            break;
+        case CL_MU:  // weights -> a.mu (wpca mean) or a.outc (clusterfeck outcomes): by a.weights
+            hipLaunchKernelGGL(k_cl_mu, dim3(ceb), dim3(BT), 0, st, m, a, a.weights == m.rep ? a.mu : a.outc);
+            break;
+        case CL_X_WCD:
+            hipLaunchKernelGGL(k_cl_x, dim3(eg), dim3(BT), 0, st, m, a, 1);
+            break;
+        case CL_X_F:
+            hipLaunchKernelGGL(k_cl_x, dim3(eg), dim3(BT), 0, st, m, a, 0);
+            break;
+        case CL_WHITEN:
+            hipLaunchKernelGGL(k_cl_sd, dim3(ceb), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_cl_div, dim3(eg), dim3(BT), 0, st, m, a);
+            break;
+        case CL_HIER: {
+            const unsigned nt = (unsigned)((m.n_rows + CLT - 1) / CLT);
+            hipLaunchKernelGGL(k_cl_iota, dim3(rg), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_cl_hier, dim3(nt, nt), dim3(CLT * CLT), 0, st, m, a);
+            hipLaunchKernelGGL(k_cl_roots, dim3(rg), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_cl_nc, dim3(1), dim3(1024), 0, st, m, a);
+            break;
+        }
+        case CL_FECK:
+            hipLaunchKernelGGL(k_cl_feck, dim3(1), dim3(1024), 0, st, m, a);
+            break;
+        case KM_INIT:
+            hipLaunchKernelGGL(k_km_init, dim3(grid_rows((int64_t)a.k * E, BT)), dim3(BT), 0, st, m, a);
+            break;
+        case KM_ITER:
+            hipLaunchKernelGGL(k_km_cs, dim3((a.k + BT - 1) / BT), dim3(BT), 0, st, m, a, (const double*)a.book);
+            hipLaunchKernelGGL(k_km_vq, dim3(rg), dim3(BT), 0, st, m, a, (const double*)a.book);
+            hipLaunchKernelGGL(k_km_sums, dim3(grid_rows((int64_t)a.k * E, BT)), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_km_update, dim3(1), dim3(1024), 0, st, m, a);
+            break;
+        case KM_KEEP:
+            hipLaunchKernelGGL(k_km_keep, dim3(1), dim3(1024), 0, st, m, a);
+            break;
+        case KM_FINAL:
+            hipLaunchKernelGGL(k_km_final_prep, dim3(1), dim3(64), 0, st, a);
+            hipLaunchKernelGGL(k_km_cs, dim3((a.k + BT - 1) / BT), dim3(BT), 0, st, m, a, (const double*)a.best);
+            hipLaunchKernelGGL(k_km_vq, dim3(rg), dim3(BT), 0, st, m, a, (const double*)a.best);
+            hipLaunchKernelGGL(k_cl_zero_cnt, dim3(rg), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_km_count, dim3(rg), dim3(BT), 0, st, m, a);
+            hipLaunchKernelGGL(k_cl_nc, dim3(1), dim3(1024), 0, st, m, a);
+            hipLaunchKernelGGL(k_km_nc_nan, dim3(rg), dim3(BT), 0, st, m, a);
+            break;
+        default:
+            err = "cluster_stage: unknown step";
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

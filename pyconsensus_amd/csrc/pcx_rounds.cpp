@@ -73,6 +73,16 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
         }
         c->pool.push_back(w);
     }
+    std::vector<int32_t> kinit;  // k-means restart rows: device [B][restarts][k] -> host (pcx_problem)
+    const int64_t kper = (int64_t)in->kmeans_restarts * in->kmeans_k;
+    if (in->algorithm == PCX_ALG_KMEANS) {
+        kinit.resize(B * kper);
+        e = hipMemcpy(kinit.data(), in->kmeans_init, B * kper * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            err = std::string("rounds: D2H kmeans_init: ") + hipGetErrorString(e);
+            return PCX_EHIP;
+        }
+    }
     std::vector<double> part(B), avg(B);
     std::vector<int32_t> branch(B), flags(B), iters(B), comps(B);
     std::atomic<int64_t> next{0};
@@ -103,6 +113,11 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             p.mem_kind = PCX_MEM_DEVICE;
             p.variance_threshold = in->variance_threshold;
             p.aux_scores = in->aux_scores ? in->aux_scores + b * N : nullptr;
+            p.hierarchy_threshold = in->hierarchy_threshold;
+            p.cluster_threshold = in->cluster_threshold;
+            p.kmeans_k = in->kmeans_k;
+            p.kmeans_restarts = in->kmeans_restarts;
+            p.kmeans_init = kinit.empty() ? nullptr : kinit.data() + b * kper;
             pcx_result r{};
             r.old_rep = at(out->old_rep, b * N);
             r.this_rep = at(out->this_rep, b * N);

@@ -70,7 +70,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx;
+    } pgg, zd, pmx, clw;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -84,7 +84,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -475,6 +475,97 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
     if (S) R.stage(m, M_SEL_FINISH);
 }
 
+// ------------------------------------------------------------------ clustering algorithms
+// nc of "k-means" (:392-405), "hierarchical" (:407-419) or "clusterfeck" (:148-242,
+// :421-424) into rowv[RV_N1] (pcx_matrix.hip cluster_stage; one rank)
+void cluster_nc(Run& R, pcx_mat& m, pcx_workspace* w, const pcx_problem* p) {
+    const int64_t N = m.n_rows, E = m.n_events;
+    const int alg = m.algorithm;
+    const int64_t K = alg == PCX_ALG_KMEANS ? p->kmeans_k : 0, RS = alg == PCX_ALG_KMEANS ? p->kmeans_restarts : 0;
+    const int64_t nS = alg == PCX_ALG_CLUSTERFECK ? N * E : K * E;
+    auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+    const int64_t dbytes = al(8 * 3 * E) + al(8 * N * E) + al(8 * nS) + 2 * al(8 * K * E) + al(8 * K) + 6 * al(8 * N) +
+                           al(8 * 8);
+    const int64_t ibytes = 3 * al(4 * N) + al(4 * (RS * K + 1));
+    if (!w->grow(w->clw, (size_t)(dbytes + ibytes))) {
+        R.err = "workspace: hipMalloc of the clustering scratch failed";
+        throw Fail{PCX_ENOMEM};
+    }
+    char* b = (char*)w->clw.p;
+    auto take = [&](int64_t bytes) {
+        char* q = b;
+        b += al(bytes);
+        return q;
+    };
+    ClusterArgs a{};
+    a.alg = alg;
+    a.k = (int32_t)K;
+    double* e3 = (double*)take(8 * 3 * E);
+    a.mu = e3;
+    a.sd = e3 + E;
+    a.outc = e3 + 2 * E;
+    a.X = (double*)take(8 * N * E);
+    a.S = (double*)take(8 * nS);
+    a.book = (double*)take(8 * K * E);
+    a.best = (double*)take(8 * K * E);
+    a.cs = (double*)take(8 * K);
+    a.dist = (double*)take(8 * N);
+    a.dm = (double*)take(8 * N);
+    a.dm1 = (double*)take(8 * N);
+    a.crep = (double*)take(8 * N);
+    a.wtok = (double*)take(8 * N);
+    (void)take(8 * N);
+    a.kst = (double*)take(8 * 8);
+    a.lab = (int32_t*)take(4 * N);
+    a.cnt = (int32_t*)take(4 * N);
+    a.par = (int32_t*)take(4 * N);
+    a.kinit = (int32_t*)take(4 * (RS * K + 1));
+    auto step = [&](int s) {
+        std::string e;
+        if (cluster_stage(m, a, s, R.st, e) != hipSuccess) {
+            R.err = e.empty() ? "cluster_stage launch failed" : e;
+            throw Fail{PCX_EHIP};
+        }
+    };
+    R.mark(M_CLUSTER);
+    if (alg == PCX_ALG_CLUSTERFECK) {
+        double thr = p->cluster_threshold;  // the reference's default rule (:187-190, :210-213)
+        if (!(thr > 0.0)) {
+            thr = std::log10((double)E) / 1.77;
+            if (thr == 0.0) thr = 0.3;
+        }
+        a.thr = thr;
+        step(CL_WTOK);
+        a.weights = a.wtok;  // outcomes = np.ma.average(features, axis=0, weights=rep) (:167)
+        step(CL_MU);
+        step(CL_X_F);  // features = reports_filled (:423)
+        R.hip(hipMemsetAsync(a.cnt, 0, 4 * N, R.st), "hipMemset(cluster)");
+        step(CL_FECK);
+    } else {
+        a.weights = m.rep;  // wpca's weighted mean (:317)
+        step(CL_MU);
+        step(CL_X_WCD);
+        if (alg == PCX_ALG_HIERARCHICAL) {
+            a.thr = p->hierarchy_threshold;
+            step(CL_HIER);
+        } else {
+            step(CL_WHITEN);
+            R.hip(hipMemcpyAsync(a.kinit, p->kmeans_init, 4 * RS * K, hipMemcpyHostToDevice, R.st), "H2D kinit");
+            for (int r = 0; r < RS; r++) {
+                a.restart = r;
+                step(KM_INIT);
+                for (;;) {  // Lloyd steps until |avg_prev - avg| <= 1e-5 (scipy _kmeans)
+                    step(KM_ITER);
+                    if (R.read(a.kst + 3) == 0.0) break;  // KS_CONT
+                }
+                step(KM_KEEP);
+            }
+            step(KM_FINAL);
+        }
+    }
+    R.mark(-1);
+}
+
 }  // namespace
 
 void workspace_free(pcx_ctx* c) {
@@ -507,8 +598,28 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         return PCX_EINVAL;
     }
     const int alg = p->algorithm;
-    if (alg < PCX_ALG_PCA || alg > PCX_ALG_COKURTOSIS) {
-        err = "algorithm must be PCA, absolute, big-five, fixed-variance or cokurtosis on the single-matrix path";
+    if (alg < PCX_ALG_PCA || alg > PCX_ALG_CLUSTERFECK) {
+        err = "algorithm must be an enum pcx_algorithm value (0..7)";
+        return PCX_EINVAL;
+    }
+    const bool clustering = alg >= PCX_ALG_KMEANS;
+    if (clustering && (world != 1 || (entry != 0 && entry != 3))) {
+        err = "the clustering algorithms run on one rank, through the consensus / lie_detector entries";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_KMEANS && (!p->kmeans_init || p->kmeans_k < 1 || p->kmeans_k > n_rows ||
+                                  p->kmeans_k > 1024 || p->kmeans_restarts < 1)) {
+        err = "k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 1024), kmeans_restarts >= 1";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_KMEANS)
+        for (int64_t q = 0; q < (int64_t)p->kmeans_k * p->kmeans_restarts; q++)
+            if (p->kmeans_init[q] < 0 || p->kmeans_init[q] >= n_rows) {
+                err = "kmeans_init rows must lie in [0, N)";
+                return PCX_EINVAL;
+            }
+    if (alg == PCX_ALG_HIERARCHICAL && std::isnan(p->hierarchy_threshold)) {
+        err = "hierarchy_threshold is NaN";
         return PCX_EINVAL;
     }
     if (alg == PCX_ALG_COKURTOSIS && !p->aux_scores && entry != 4) {
@@ -701,7 +812,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             R.stage(m, M_MATRICES);
         } else {
             R.stage(m, M_MEAN);
-            const bool wpca = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;
+            const bool wpca = alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE ||
+                              clustering;  // the clusterings call wpca too (:393, :408, :422): the loading
             const bool run_wpca = entry == 2 || (entry != 4 && wpca);
             int64_t flags = 0;
             bool mats_written = false;  // k_wcd writes "original" / "filled" on the way
@@ -776,20 +888,24 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 flags = R.read(m.info + INFO_FLAGS);
                 // big-five / fixed-variance components (:373-390, :429-451); a non-finite
                 // covariance makes the reference's second svd raise (Oracle: LinAlgError)
-                if (entry != 2 && alg != PCX_ALG_PCA && !(flags & PCX_FLAG_SVD_FAIL)) R.stage(m, M_EIG);
+                if (entry != 2 && alg != PCX_ALG_PCA && !clustering && !(flags & PCX_FLAG_SVD_FAIL)) R.stage(m, M_EIG);
             } else {
                 R.stage(m, M_ZERO_LOADING);
             }
             if (entry == 2 && alg != PCX_ALG_PCA) m.algorithm = PCX_ALG_PCA;  // wpca: the first loading's scores
-            R.stage(m, M_SCORES);
+            R.stage(m, M_SCORES);  // also sums the rows' NaN / zero counts (na_row, :549-567)
             R.gather_block(w->skey, 4 * 8);
+            if (clustering) {  // the clusterings' scores stay zeros (:357); nc from the clusters
+                R.hip(hipMemsetAsync(w->rowv, 0, n_rows * 8, R.st), "hipMemset(scores)");
+                cluster_nc(R, m, w, p);
+            }
             if (entry == 2) {
                 R.stage(m, M_WMEAN_OUT);
                 if (cov_out) R.hip(hipMemcpyAsync(cov_out, w->C, E * E * 8, hipMemcpyDeviceToDevice, R.st), "cov");
                 if (ld_out) R.hip(hipMemcpyAsync(ld_out, w->ev + 3 * E, E * 8, hipMemcpyDeviceToDevice, R.st), "ld");
                 if (sc_out) R.hip(hipMemcpyAsync(sc_out, w->rowv, n_rows * 8, hipMemcpyDeviceToDevice, R.st), "scores");
             } else {
-                if (alg != PCX_ALG_ABSOLUTE || entry == 4) {
+                if ((alg != PCX_ALG_ABSOLUTE && !clustering) || entry == 4) {
                     // a8/a9: sign-choice rule (:487-500; the other algorithms: nonconformity, :475-485)
                     R.stage(m, M_NCSUMS);
                     R.gather_slots(w->scal, 1, SS * 2, 2, 6, w);
@@ -838,7 +954,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         R.sync();
         r->participation = sc2[0];
         r->avg_certainty = sc2[1];
-        const bool branchless = (alg == PCX_ALG_ABSOLUTE && entry != 4) || entry == 1 || entry == 2;
+        const bool branchless = (alg == PCX_ALG_ABSOLUTE && entry != 4) || clustering || entry == 1 || entry == 2;
         r->branch = branchless ? PCX_BRANCH_NONE : (int32_t)info[INFO_BRANCH];
         r->pi_iters = (int32_t)info[INFO_PI_ITERS];
         r->flags = (int32_t)info[INFO_FLAGS];

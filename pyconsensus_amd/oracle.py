@@ -34,9 +34,9 @@ class Oracle(object):
     ``"absolute"`` (the reference's unimplemented branch: uniform this_rep,
     :359-362), and the clustering algorithms ``"k-means"`` (:392-405; its restarts draw
     from numpy's global RandomState exactly as the reference's scipy call does),
-    ``"hierarchical"`` (:407-419) and ``"clusterfeck"`` (:148-242, :421-424) for rounds
-    of at most 64 reporters x 32 events (the batched kernel); larger clustering
-    problems raise NotImplementedError (DESIGN.md, scope).
+    ``"hierarchical"`` (:407-419) and ``"clusterfeck"`` (:148-242, :421-424): rounds of at
+    most 64 reporters x 32 events on the batched kernel, larger matrices on the
+    single-matrix path (one GPU).
     """
 
     def __init__(self, reports=None, event_bounds=None, reputation=None,
@@ -217,9 +217,6 @@ class Oracle(object):
                   algorithm=self.algorithm, device=self.device if self.devices is None else self.devices[0],
                   max_components=self.max_components, variance_threshold=self.variance_threshold)
         small = N <= MAX_REPORTERS and E <= MAX_EVENTS
-        if self.algorithm in _abi.CLUSTER_ALGORITHMS and not small:
-            raise NotImplementedError("algorithm %r runs in the batched regime only (N <= %d, E <= %d; got %d x %d)"
-                                      % (self.algorithm, MAX_REPORTERS, MAX_EVENTS, N, E))
         if small:
             out = consensus_batched(self._data[None], None if self._rep_raw is None else self._rep_raw[None],
                                     sc, lo, hi, filled=True, original=True,
@@ -234,9 +231,13 @@ class Oracle(object):
         else:
             from .pipeline import consensus_host
 
+            ckw = {}
+            if self.algorithm in _abi.CLUSTER_ALGORITHMS:  # one GPU (the clusterings do not shard)
+                ckw = dict(hierarchy_threshold=self.hierarchy_threshold)
             g, meta = consensus_host(self._data, self._rep_raw, sc, lo, hi, device_index=self._device_index(),
-                                     aux_scores=aux, devices=self.devices,
-                                     **{k: v for k, v in kw.items() if k != "device"})
+                                     aux_scores=aux,
+                                     devices=None if self.algorithm in _abi.CLUSTER_ALGORITHMS else self.devices,
+                                     **ckw, **{k: v for k, v in kw.items() if k != "device"})
             participation = float(meta["participation"])
             avg_certainty = float(meta["avg_certainty"])
             comps = int(meta["components"])

@@ -199,15 +199,20 @@ def _bounds(scaled, lo, hi, conv):
 
 
 def _problem(n_rows, E, N, r0, P, rep, sc, lo, hi, catch_tolerance, alpha, int_dtype, algorithm, max_components,
-             variance_threshold, aux, mem_kind):
+             variance_threshold, aux, mem_kind, cluster=None):
     alg = _abi.ALGORITHMS.get(algorithm)
-    if alg is None or algorithm in _abi.CLUSTER_ALGORITHMS:
-        raise NotImplementedError("algorithm %r is not on the single-matrix path" % (algorithm,))
+    if alg is None:
+        raise NotImplementedError("algorithm %r is not on the GPU path" % (algorithm,))
     if alg == _abi.ALG_COKURTOSIS and aux is None:
         raise ValueError("cokurtosis needs aux_scores (this rank's rows of aux['cokurt'])")
     mc = int(max_components) if E >= int(max_components) else E  # __init__.py:134-137
+    cl = cluster or {}
+    kinit = cl.get("kmeans_init")  # host int32 [restarts][k], kept alive by the caller
+    k, restarts = (int(kinit.shape[1]), int(kinit.shape[0])) if kinit is not None else (0, 0)
     return _abi.Problem(n_rows, E, N, r0, P, rep, sc, lo, hi, float(catch_tolerance), float(alpha),
-                        int(bool(int_dtype)), alg, mc, mem_kind, float(variance_threshold), aux)
+                        int(bool(int_dtype)), alg, mc, mem_kind, float(variance_threshold), aux,
+                        float(cl.get("hierarchy_threshold", 0.5)), float(cl.get("cluster_threshold", 0.0)), k,
+                        restarts, None if kinit is None else kinit.ctypes.data)
 
 
 def _shape_args(n_rows, comm, n_total, row_offset):
@@ -296,7 +301,8 @@ def _meta(res, algorithm):
 # ---------------------------------------------------------------- host-memory entry points
 def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outputs, catch_tolerance=0.1,
                alpha=0.1, int_dtype=False, algorithm="PCA", max_components=5, variance_threshold=0.9,
-               aux_scores=None, extra=(), devices=None):
+               aux_scores=None, extra=(), devices=None, hierarchy_threshold=0.5, cluster_threshold=None,
+               kmeans_init=None):
     """Call a single-matrix entry point with numpy inputs / outputs (PCX_MEM_HOST: libpcx
     copies in and out).  ``outputs``: {result field: shape}.  ``devices``: a list of device
     ids -- libpcx shards the rows over them (pcx_create_devices), else one GPU."""
@@ -314,9 +320,19 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
 
     sc, lo_, hi_ = (None, None, None) if scaled is None else (ptr(scaled, np.uint8), ptr(lo, np.float64),
                                                               ptr(hi, np.float64))
+    cluster = None
+    if algorithm in _abi.CLUSTER_ALGORITHMS:
+        if algorithm == "k-means" and kmeans_init is None:
+            from .batched import kmeans_draws
+
+            kmeans_init = kmeans_draws(1, n_rows)[0]  # numpy's global RandomState, as scipy draws (:397)
+        kinit = None if kmeans_init is None else np.ascontiguousarray(kmeans_init, dtype=np.int32)
+        keep.append(kinit)
+        cluster = {"hierarchy_threshold": hierarchy_threshold, "kmeans_init": kinit,
+                   "cluster_threshold": 0.0 if cluster_threshold is None else cluster_threshold}
     prob = _problem(n_rows, E, n_rows, 0, R.ctypes.data, ptr(reputation, np.float64), sc, lo_, hi_,
                     catch_tolerance, alpha, int_dtype, algorithm, max_components, variance_threshold,
-                    ptr(aux_scores, np.float64), _abi.MEM_HOST)
+                    ptr(aux_scores, np.float64), _abi.MEM_HOST, cluster)
     res = _abi.Result()
     outs = {}
     for k, shape in outputs.items():

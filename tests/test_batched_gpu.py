@@ -167,10 +167,26 @@ def test_rounds_above_one_wave(gpu_lib, variant):
         assert not bad, (b, bad)
 
 
-def test_rounds_above_one_wave_refuse_clustering(gpu_lib):
+@pytest.mark.parametrize("alg", ["hierarchical", "clusterfeck", "k-means"])
+def test_rounds_above_one_wave_clustering(gpu_lib, alg):
+    """The clustering algorithms in batched rounds above 64 x 32 (the scheduler's single-matrix
+    consensuses): each round against the numpy restatement; k-means draws every round's
+    restarts from numpy's global RandomState in round order, as B sequential reference calls."""
+    from oracle.pcx_oracle import OracleCPU
     from pyconsensus_amd import synthetic
     from pyconsensus_amd.batched import consensus_batched
 
-    R, sc, lo, hi, rep = synthetic.rounds(2, 70, 10, seed=1)
-    with pytest.raises(NotImplementedError):
-        consensus_batched(R, rep, sc, lo, hi, algorithm="hierarchical")
+    B, N, E = 6, 70, 12
+    rng = np.random.default_rng(4)
+    P0 = rng.integers(1, 3, (3, E)).astype(np.float64)
+    R = P0[rng.integers(0, 3, (B, N))]
+    R = np.where(rng.random((B, N, E)) < 0.03, 3.0 - R, R)
+    R[rng.random((B, N, E)) < 0.05] = np.nan
+    rep = rng.integers(1, 100, (B, N)).astype(np.float64)
+    np.random.seed(99)
+    g = _np(consensus_batched(R, rep, algorithm=alg, filled=True))
+    np.random.seed(99)
+    for b in range(B):
+        ref = G.flat_result(OracleCPU(reports=R[b].copy(), reputation=rep[b], algorithm=alg).consensus())
+        bad, _ = P.compare(ref, {k: v[b] for k, v in g.items()})
+        assert not bad, (b, bad)

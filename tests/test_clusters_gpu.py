@@ -6,7 +6,9 @@ k-means (__init__.py:392-405), hierarchical (:407-419), clusterfeck (:148-242, :
 * bit-identical to the C SPEC (oracle/pcx_oracle_batched.c) on seeded synthetic batches of
   several shapes, k-means restarts drawn by the host as the reference's scipy call draws them;
 * the drop-in Oracle: same results as the reference with numpy's global RandomState seeded
-  alike, the clustering result containers, and the batched-only scope.
+  alike, and the clustering result containers;
+* the single-matrix path's clustering kernels (matrices above 64 x 32): every golden case
+  forced through them, and larger clustered matrices against the numpy restatement.
 """
 import numpy as np
 import pytest
@@ -96,9 +98,94 @@ def test_oracle_dropin(gpu_lib):
         assert np.all(np.asarray(res["agents"]["scores"]) == 0.0)
 
 
-def test_oracle_clusters_scope(gpu_lib):
-    from pyconsensus_amd import Oracle
+def _matrix_cluster(R, rep, sc, lo, hi, algorithm, hierarchy_threshold=0.5, kmeans_init=None, int_dtype=False,
+                    catch_tolerance=0.1, alpha=0.1):
+    """The single-matrix path's clustering (pcx_consensus_f64, csrc/pcx_runner.cpp cluster_nc)."""
+    from pyconsensus_amd.pipeline import consensus_host
 
-    R = np.ones((65, 3))
-    with pytest.raises(NotImplementedError):
-        Oracle(reports=R, algorithm="hierarchical").consensus()
+    g, meta = consensus_host(R, rep, sc, lo, hi, algorithm=algorithm, hierarchy_threshold=hierarchy_threshold,
+                             kmeans_init=kmeans_init, int_dtype=int_dtype, catch_tolerance=catch_tolerance,
+                             alpha=alpha)
+    g["participation"] = np.array(meta["participation"])
+    g["avg_certainty"] = np.array(meta["avg_certainty"])
+    g["branch"] = np.array(meta["branch"])
+    return g
+
+
+def test_golden_cases_through_matrix_path(gpu_lib):
+    """Every reference clustering golden forced through the single-matrix path (the kernels
+    that serve matrices above 64 x 32): same results as the reference within the north_star
+    tolerances, discrete outputs exact."""
+    from pyconsensus_amd.batched import kmeans_draws
+
+    bad_cases = {}
+    for name, case in G.clusters().items():
+        N, E = case["in_reports"].shape
+        alg = str(case["in_algorithm"])
+        sc = lo = hi = None
+        if bool(case["in_has_bounds"]):
+            sc, lo, hi = case["in_scaled"], case["in_lo"], case["in_hi"]
+        rep = case["in_reputation"] if bool(case["in_has_rep"]) else None
+        kinit = None
+        if alg == "k-means":
+            kinit = kmeans_draws(1, N, random_state=np.random.RandomState(int(case["in_np_seed"])))[0]
+        ours = _matrix_cluster(case["in_reports"], rep, sc, lo, hi, alg,
+                               hierarchy_threshold=float(case["in_hierarchy_threshold"]), kmeans_init=kinit,
+                               int_dtype=bool(case["in_int_dtype"]), catch_tolerance=float(case["in_catch_tolerance"]),
+                               alpha=float(case["in_alpha"]))
+        bad, _ = P.compare(case, ours)
+        if bad:
+            bad_cases[name] = bad[:2]
+    assert not bad_cases, (len(bad_cases), dict(list(bad_cases.items())[:6]))
+
+
+def _clustered(N, E, seed, protos=4, flip=0.03, na=0.05, scaled_frac=0.0):
+    """Binary reports around a few prototype rows (clusters of equal rows, near rows), plus
+    optional scaled events: a workload where the clusterings are not all singletons."""
+    rng = np.random.default_rng(seed)
+    P0 = rng.integers(1, 3, (protos, E)).astype(np.float64)
+    R = P0[rng.integers(0, protos, N)]
+    R = np.where(rng.random((N, E)) < flip, 3.0 - R, R)
+    sc = rng.random(E) < scaled_frac
+    lo = np.where(sc, -10.0, 1.0)
+    hi = np.where(sc, 30.0, 2.0)
+    R = np.where(sc[None, :], lo + (hi - lo) * rng.uniform(0.05, 1.0, (N, E)), R)
+    R[rng.random((N, E)) < na] = np.nan
+    rep = rng.integers(1, 100, N).astype(np.float64)
+    return R, rep, sc, lo, hi
+
+
+@pytest.mark.parametrize("alg,N,E,scaled", [("hierarchical", 300, 40, 0.0), ("hierarchical", 2000, 24, 0.2),
+                                            ("clusterfeck", 200, 40, 0.0), ("clusterfeck", 1500, 16, 0.2),
+                                            ("k-means", 150, 20, 0.0), ("k-means", 400, 12, 0.2)])
+def test_oracle_clusters_above_one_wave(gpu_lib, alg, N, E, scaled):
+    """The drop-in Oracle on matrices above 64 x 32 (the single-matrix path) against the numpy
+    restatement of the reference (oracle/pcx_oracle.py: scipy's own kmeans / fclusterdata and
+    the restated leader clustering), numpy's global RandomState seeded alike for k-means."""
+    from oracle.pcx_oracle import OracleCPU
+    from pyconsensus_amd import Oracle, synthetic
+
+    R, rep, sc, lo, hi = _clustered(N, E, seed=N + E, scaled_frac=scaled)
+    eb = synthetic.bounds_list(sc, lo, hi)
+    np.random.seed(1234)
+    ref = G.flat_result(OracleCPU(reports=R.copy(), event_bounds=eb, reputation=rep, algorithm=alg).consensus())
+    np.random.seed(1234)
+    o = Oracle(reports=R.copy(), event_bounds=eb, reputation=rep, algorithm=alg)
+    res = o.consensus()
+    assert o.last_info["path"] == "matrix"
+    ours = {P.ABI_NAME[k]: v for k, v in G.flat_result(res).items() if k in P.ABI_NAME}
+    bad, _ = P.compare(ref, ours)
+    assert not bad, bad
+    assert res["convergence"] is True and np.all(np.asarray(res["agents"]["scores"]) == 0.0)
+    nc_spread = np.ptp(np.asarray(res["agents"]["this_rep"], dtype=np.float64))
+    assert np.isfinite(nc_spread)  # not the degenerate all-equal-sizes case
+
+
+def test_oracle_clusters_refuse_sharding(gpu_lib):
+    from pyconsensus_amd import _lib
+    from pyconsensus_amd.pipeline import ThreadComm, ThreadGroup, consensus_matrix
+
+    R = np.ones((100, 3))
+    g = ThreadGroup(2)
+    with pytest.raises(_lib.PcxError, match="one rank"):
+        consensus_matrix(R, None, algorithm="hierarchical", comm=ThreadComm(g, 0), n_total=100, row_offset=0)
