@@ -1160,7 +1160,7 @@ __device__ __forceinline__ dd two_prod(double a, double b) {
 // order (cov_perm) and mirrored (unnormalised).  Pure-grid entries hold the exact integer
 // P_jk: C_jk = c_j c_k T + (c_j Z_k + c_k Z_j) / 2 + P_jk / 4 with this rank's T, Z, P
 // (c = 1 - mu is exact for mu in [1, 2]), evaluated in double-double.
-__global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
+__global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m, double* Cpos) {
     const int64_t E = m.n_events;
     const int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x;
     if (idx >= E * E) return;
@@ -1204,8 +1204,34 @@ __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m) {
         const double ap = 1.0 - m.ev[EV_MU * E + cp];
         s = dd_to_double(dd_add(dd_mul_d(S, ap), dd_mul_d(Q, 0.5)));
     }
-    m.C[cp * E + cq] = s;
-    m.C[cq * E + cp] = s;
+    Cpos[p * E + q] = s;  // position space, lower triangle: coalesced in q
+}
+
+// mirror the position-space lower triangle into the upper one (32 x 32 LDS tiles)
+constexpr int CV_T = 32;
+__global__ void __launch_bounds__(CV_T * 8) k_cov_sym(int64_t E, double* Cpos) {
+    const int64_t I = blockIdx.y, J = blockIdx.x;  // upper tile (I < J) <- lower tile (J, I)
+    if (I > J) return;
+    __shared__ double t[CV_T][CV_T + 1];
+    const int tx = threadIdx.x % CV_T, ty = threadIdx.x / CV_T;
+    for (int r = ty; r < CV_T; r += 8) {  // read rows of the lower tile (J, I): p = J*T + r, q = I*T + tx
+        const int64_t p = J * CV_T + r, q = I * CV_T + tx;
+        t[r][tx] = (p < E && q < E && q <= p) ? Cpos[p * E + q] : 0.0;
+    }
+    __syncthreads();
+    for (int r = ty; r < CV_T; r += 8) {  // write (I*T + r, J*T + tx) = lower (J*T + tx, I*T + r)
+        const int64_t p = I * CV_T + r, q = J * CV_T + tx;
+        if (p < E && q < E && q > p) Cpos[p * E + q] = t[tx][r];
+    }
+}
+
+// event order: C[i][j] = Cpos[pos_i][pos_j] (positions mostly rise with the event index)
+__global__ void __launch_bounds__(BT) k_cov_unperm(pcx_mat m, const double* Cpos) {
+    const int64_t E = m.n_events;
+    const int64_t i = blockIdx.y;
+    const int64_t pi = m.cov_pos[i];
+    for (int64_t j = blockIdx.x * (int64_t)BT + threadIdx.x; j < E; j += (int64_t)gridDim.x * BT)
+        m.C[i * E + j] = Cpos[pi * E + m.cov_pos[j]];
 }
 
 // PCX_M_COV_FINISH: divide by (sum tokens - 1) (:326)
@@ -1670,27 +1696,52 @@ __global__ void __launch_bounds__(BT) k_decide_prep(pcx_mat m) {
     raw2[c] = b;
 }
 
-__global__ void __launch_bounds__(BT) k_ranks(pcx_mat m) {
-    __shared__ double red[BT];
+// counts of smaller / equal values among one chunk of RK_CH events (blockIdx.y), added into
+// cnt[E][6] (integers: any order); k_ranks then forms the average ranks
+constexpr int RK_CH = 64;
+__global__ void __launch_bounds__(BT) k_rank_counts(pcx_mat m, int* cnt) {
+    __shared__ double so[RK_CH], sa[RK_CH], sb[RK_CH];
     const int E = (int)m.n_events;
     const double* old = m.ev + EV_OLD * E;
     const double* n1 = m.ev + EV_D1 * E;
     const double* n2 = m.ev + EV_D2 * E;
+    const int k0 = blockIdx.y * RK_CH;
+    const int kn = E - k0 < RK_CH ? E - k0 : RK_CH;
+    for (int t = threadIdx.x; t < kn; t += BT) {
+        so[t] = old[k0 + t];
+        sa[t] = n1[k0 + t];
+        sb[t] = n2[k0 + t];
+    }
+    __syncthreads();
+    const int c = blockIdx.x * BT + threadIdx.x;
+    if (c >= E) return;
+    int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0, lt2 = 0, eq2 = 0;
+    const double o = old[c], a = n1[c], b = n2[c];
+    for (int t = 0; t < kn; t++) {
+        lt0 += so[t] < o;
+        eq0 += so[t] == o;
+        lt1 += sa[t] < a;
+        eq1 += sa[t] == a;
+        lt2 += sb[t] < b;
+        eq2 += sb[t] == b;
+    }
+    int* q = cnt + (int64_t)c * 6;
+    atomicAdd(q + 0, lt0);
+    atomicAdd(q + 1, eq0);
+    atomicAdd(q + 2, lt1);
+    atomicAdd(q + 3, eq1);
+    atomicAdd(q + 4, lt2);
+    atomicAdd(q + 5, eq2);
+}
+
+__global__ void __launch_bounds__(BT) k_ranks(pcx_mat m, const int* cnt) {
+    __shared__ double red[BT];
+    const int E = (int)m.n_events;
     const int c = blockIdx.x * BT + threadIdx.x;
     double e = 0.0;
     if (c < E) {
-        int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0, lt2 = 0, eq2 = 0;
-        const double o = old[c], a = n1[c], b = n2[c];
-        for (int k = 0; k < E; k++) {
-            const double ok = old[k], ak = n1[k], bk = n2[k];
-            lt0 += ok < o;
-            eq0 += ok == o;
-            lt1 += ak < a;
-            eq1 += ak == a;
-            lt2 += bk < b;
-            eq2 += bk == b;
-        }
-        const double r0 = lt0 + (eq0 + 1) * 0.5, r1 = lt1 + (eq1 + 1) * 0.5, r2 = lt2 + (eq2 + 1) * 0.5;
+        const int* q = cnt + (int64_t)c * 6;
+        const double r0 = q[0] + (q[1] + 1) * 0.5, r1 = q[2] + (q[3] + 1) * 0.5, r2 = q[4] + (q[5] + 1) * 0.5;
         e = fabs(r1 - r0) - fabs(r2 - r0);
     }
     red[threadIdx.x] = e;
@@ -2319,64 +2370,123 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
 // walk the buckets (reduced over ranks): weight mode keeps the bucket where the exact
 // prefix crosses half the total, count mode the one holding rank `target`; a single-key
 // bucket resolves (weight mode: unless the crossing is near a rounding-decided half)
+// one wave per active event: lane l owns buckets PB*l .. PB*l+PB-1.  The exact prefix sums
+// of the bucket counts and weight limbs come from a wave scan (integer limbs: order-free), the
+// first bucket whose prefix crosses the half (weights) / target (counts) by ballot, and that
+// bucket's lane applies the narrowing (a 256-step serial scan per event before).
+constexpr int SEL_PB = NB / WAVE;
+__device__ __forceinline__ uint64_t scan_add_u64(uint64_t v, int lane) {  // inclusive
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const uint64_t u = __shfl_up(v, d, WAVE);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t scan_max_u64(uint64_t v, int lane) {  // inclusive
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const uint64_t u = __shfl_up(v, d, WAVE);
+        if (lane >= d) v = u > v ? u : v;
+    }
+    return v;
+}
+
 __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
-    const int a = blockIdx.x * BT + threadIdx.x;
-    if (a >= n_active) return;
+    const int a = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    if (a >= n_active) return;  // wave-uniform
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     const bool wmode = st[SW_MODE] == 0;
     const L3 tot = ld_l3(st + SW_TOT0);
     const uint64_t n_all = st[SW_COUNT], target = st[SW_TARGET];
-    L3 below = ld_l3(st + SW_BELOW0);
-    uint64_t cbelow = st[SW_CNT_BELOW];
-    uint64_t below_max = st[SW_BELOW_MAX];
-    bool has_below = st[SW_HAS_BELOW] != 0;
+    const L3 below0 = ld_l3(st + SW_BELOW0);
+    const uint64_t cbelow0 = st[SW_CNT_BELOW], below_max0 = st[SW_BELOW_MAX];
+    const bool has_below0 = st[SW_HAS_BELOW] != 0;
     const int64_t o = (int64_t)a * NB;
-    for (int b = 0; b < NB; b++) {
-        const uint64_t n = m.hist_n[o + b];
-        if (n == 0) continue;
+    uint64_t nb[SEL_PB], kmn[SEL_PB], kmx[SEL_PB];
+    L3 hw[SEL_PB];
+    uint64_t sc = 0, sa = 0, sb = 0, sl = 0, smax = 0;  // lane totals (counts, limbs), last key
+#pragma unroll
+    for (int j = 0; j < SEL_PB; j++) {
+        const int b = lane * SEL_PB + j;
+        nb[j] = m.hist_n[o + b];
         const uint64_t* hs = m.hist_w + (o + b) * 3;
-        const L3 hw = wmode ? l3_norm({hs[0], hs[1], hs[2]}) : L3{0, 0, 0};
-        const uint64_t kmin = m.hist_min[o + b], kmax = m.hist_max[o + b];
-        const L3 upto = l3_add(below, hw);
-        const bool cross = wmode ? l3_cmp(l3_twice(upto), tot) > 0 : cbelow + n > target;
-        if (cross) {
-            if (kmin == kmax) {
-                const double xs = dkey_inv(kmin);
-                if (wmode) {
-                    if (near_half(below, tot, n_all) || near_half(upto, tot, n_all)) {
-                        mark_hard(m, s, st);
-                        return;
-                    }
-                    sel_done(st, xs);
-                } else {
-                    double r = xs;
-                    if (st[SW_HALF] == 2) {
-                        r = __builtin_nan("");
-                    } else if (st[SW_HALF] == 1) {
-                        const double pred = target >= cbelow + 1 ? xs : dkey_inv(below_max);
-                        r = (pred + xs) / 2.0;  // sum(bounds) / float(len(bounds))
-                    }
-                    sel_done(st, r);
-                }
-            } else {
-                st[SW_LO] = kmin;
-                st[SW_HI] = kmax;
-                st[SW_SHIFT] = shift_for(kmin, kmax);
-                st[SW_INRANGE] = n;
-                st_l3(st + SW_BELOW0, below);
-                st[SW_CNT_BELOW] = cbelow;
-                st[SW_BELOW_MAX] = below_max;
-                st[SW_HAS_BELOW] = has_below ? 1 : 0;
-            }
-            return;
-        }
-        below = upto;
-        cbelow += n;
-        below_max = kmax;
-        has_below = true;
+        hw[j] = (wmode && nb[j]) ? l3_norm({hs[0], hs[1], hs[2]}) : L3{0, 0, 0};
+        kmn[j] = m.hist_min[o + b];
+        kmx[j] = m.hist_max[o + b];
+        sc += nb[j];
+        sa += hw[j].a;
+        sb += hw[j].b;
+        sl += hw[j].c;
+        if (nb[j]) smax = kmx[j];  // keys rise with the bucket index
     }
-    sel_done(st, __builtin_nan(""));  // no crossing (cannot happen with exact sums)
+    // exclusive prefixes over the lanes below
+    const uint64_t ic = scan_add_u64(sc, lane), ia = scan_add_u64(sa, lane), ib = scan_add_u64(sb, lane),
+                   il = scan_add_u64(sl, lane), imax = scan_max_u64(smax, lane);
+    uint64_t pc = ic - sc, pa = ia - sa, pb = ib - sb, pl = il - sl;
+    uint64_t pmax = __shfl_up(imax, 1, WAVE);
+    if (lane == 0) pmax = 0;
+    int first = SEL_PB;  // this lane's first crossing bucket
+    L3 below{}, upto{};
+    uint64_t cbelow = 0, below_max = 0;
+    bool has_below = false;
+#pragma unroll
+    for (int j = 0; j < SEL_PB; j++) {
+        const L3 bl = l3_norm({below0.a + pa, below0.b + pb, below0.c + pl});
+        const L3 up = l3_norm({bl.a + hw[j].a, bl.b + hw[j].b, bl.c + hw[j].c});
+        const bool cross = nb[j] && (wmode ? l3_cmp(l3_twice(up), tot) > 0 : cbelow0 + pc + nb[j] > target);
+        if (cross && first == SEL_PB) {
+            first = j;
+            below = bl;
+            upto = up;
+            cbelow = cbelow0 + pc;
+            const bool any = pmax != 0 || pc != 0;  // nonempty buckets passed in this pass
+            below_max = any ? pmax : below_max0;
+            has_below = has_below0 || any;
+        }
+        pc += nb[j];
+        pa += hw[j].a;
+        pb += hw[j].b;
+        pl += hw[j].c;
+        if (nb[j]) pmax = kmx[j];
+    }
+    const uint64_t mask = __ballot(first < SEL_PB);
+    if (mask == 0) {  // no crossing (cannot happen with exact sums)
+        if (lane == 0) sel_done(st, __builtin_nan(""));
+        return;
+    }
+    if (lane != __ffsll((long long)mask) - 1) return;
+    const uint64_t n = nb[first], kmin = kmn[first], kmax = kmx[first];
+    if (kmin == kmax) {
+        const double xs = dkey_inv(kmin);
+        if (wmode) {
+            if (near_half(below, tot, n_all) || near_half(upto, tot, n_all)) {
+                mark_hard(m, s, st);
+                return;
+            }
+            sel_done(st, xs);
+        } else {
+            double r = xs;
+            if (st[SW_HALF] == 2) {
+                r = __builtin_nan("");
+            } else if (st[SW_HALF] == 1) {
+                const double pred = target >= cbelow + 1 ? xs : dkey_inv(below_max);
+                r = (pred + xs) / 2.0;  // sum(bounds) / float(len(bounds))
+            }
+            sel_done(st, r);
+        }
+    } else {
+        st[SW_LO] = kmin;
+        st[SW_HI] = kmax;
+        st[SW_SHIFT] = shift_for(kmin, kmax);
+        st[SW_INRANGE] = n;
+        st_l3(st + SW_BELOW0, below);
+        st[SW_CNT_BELOW] = cbelow;
+        st[SW_BELOW_MAX] = below_max;
+        st[SW_HAS_BELOW] = has_below ? 1 : 0;
+    }
 }
 
 // results into guess (phase 1; int dtype truncates, :312) / outcomes (phase 2, :537-538)
@@ -3851,9 +3961,14 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 hipLaunchKernelGGL(k_syrk, dim3(m.cov_fp_tiles * m.fp_ks), dim3(256), SY_LDS_BYTES, st, m);
             break;
         }
-        case M_COV_REDUCE: {
+        case M_COV_REDUCE: {  // position-space lower triangle -> mirrored -> event order (Mw as scratch)
             const int64_t n = (int64_t)E * E;
-            hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m);
+            double* Cpos = m.Mw;
+            hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m, Cpos);
+            const unsigned nt = (unsigned)((E + CV_T - 1) / CV_T);
+            hipLaunchKernelGGL(k_cov_sym, dim3(nt, nt), dim3(CV_T * 8), 0, st, (int64_t)E, Cpos);
+            hipLaunchKernelGGL(k_cov_unperm, dim3((unsigned)((E + BT - 1) / BT), (unsigned)E), dim3(BT), 0, st, m,
+                               (const double*)Cpos);
             break;
         }
         case M_COV_FINISH: {
@@ -3884,7 +3999,12 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_DECIDE:
             hipLaunchKernelGGL(k_decide_prep, dim3(ceb), dim3(BT), 0, st, m);
-            if (m.rank_rule) hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m);
+            if (m.rank_rule) {  // cslab is free after the covariance: int scratch of the rank counts
+                int* cnt = (int*)m.cslab;
+                (void)hipMemsetAsync(cnt, 0, (size_t)E * 6 * sizeof(int), st);
+                hipLaunchKernelGGL(k_rank_counts, dim3(ceb, (E + RK_CH - 1) / RK_CH), dim3(BT), 0, st, m, cnt);
+                hipLaunchKernelGGL(k_ranks, dim3(ceb), dim3(BT), 0, st, m, (const int*)cnt);
+            }
             hipLaunchKernelGGL(k_decide, dim3(1), dim3(1024), 0, st, m);
             break;
         case M_REPU:
@@ -4063,7 +4183,7 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st) {
 
 hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st) {
     if (n_active <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sel_step, dim3((n_active + BT - 1) / BT), dim3(BT), 0, st, m, n_active);
+    hipLaunchKernelGGL(k_sel_step, dim3((n_active + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, n_active);
     return hipGetLastError();
 }
 

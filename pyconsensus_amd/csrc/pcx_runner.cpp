@@ -264,7 +264,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->xsend, (size_t)w->xcap * 8, false},
         {(void**)&w->xrecv, (size_t)(w->xcap * world) * 8, false},
         {(void**)&w->T, (size_t)(S * n_rows) * 8, false},
-        {(void**)&w->cslab, (size_t)(w->cov_kslices * E * E) * 8, false},
+        {(void**)&w->cslab, (size_t)std::max<int64_t>(w->cov_kslices * E * E * 8, 24 * E), false},  // + rank counts
         {(void**)&w->C, (size_t)(E * E) * 8, false},
         {(void**)&w->Mw, (size_t)(2 * E * E + 8 * E + 64) * 8, false},
         {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
