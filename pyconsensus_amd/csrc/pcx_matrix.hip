@@ -427,33 +427,64 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
 }
 
 // reduce part[G][E][k] over G (in order) into cstat[rank][E][base + k]; optional max partials
+// one wave per column: lane l sums the row-chunk partials g = l, l + 64, ... of each dd slot,
+// then a fixed butterfly over the lanes (deterministic); the column extremes likewise, the
+// max-reputation argmax keeping the first row chunk on ties (the sequential order's choice)
+constexpr int CF_MAXK = 8;
 __global__ void __launch_bounds__(BT) k_col_finish(pcx_mat m, int G, int k, int base, int with_max) {
-    const int c = blockIdx.x * BT + threadIdx.x;
+    const int c = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
     const int E = (int)m.n_events;
-    if (c >= E) return;
-    for (int j = 0; j < k; j++) {
-        dd r{0.0, 0.0};
-        for (int g = 0; g < G; g++) r = dd_add(r, ld_dd(m.part + ((int64_t)g * E + c) * 16 + 2 * j));
-        st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + base + j) * 2, r);
+    if (c >= E) return;  // wave-uniform
+    dd r[CF_MAXK];
+#pragma unroll
+    for (int j = 0; j < CF_MAXK; j++) r[j] = dd{0.0, 0.0};
+    for (int g = lane; g < G; g += WAVE) {
+        const double* pp = m.part + ((int64_t)g * E + c) * 16;
+#pragma unroll
+        for (int j = 0; j < CF_MAXK; j++)
+            if (j < k) r[j] = dd_add(r[j], ld_dd(pp + 2 * j));
     }
+#pragma unroll
+    for (int j = 0; j < CF_MAXK; j++)
+        if (j < k) {
+            const dd t = wave_sum_dd(r[j]);
+            if (lane == 0) st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + base + j) * 2, t);
+        }
     if (with_max) {
         double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf(), og = 0.0;
-        for (int g = 0; g < G; g++) {
+        int gi = G;  // chunk of the current maximum
+        for (int g = lane; g < G; g += WAVE) {
             const double* mp = m.mpart + ((int64_t)g * E + c) * CM;
             if (mp[0] > mx) {
                 mx = mp[0];
                 arg = mp[1];
+                gi = g;
             }
             mn_x = fmin(mn_x, mp[2]);
             mx_x = fmax(mx_x, mp[3]);
             og = fmax(og, mp[4]);
         }
-        double* o = m.cmax + ((int64_t)m.rank * E + c) * CM;
-        o[0] = mx;
-        o[1] = arg;
-        o[2] = mn_x;
-        o[3] = mx_x;
-        o[4] = og;
+        for (int d = WAVE / 2; d >= 1; d >>= 1) {
+            const double omx = __shfl_xor(mx, d, WAVE), oarg = __shfl_xor(arg, d, WAVE);
+            const int ogi = __shfl_xor(gi, d, WAVE);
+            if (omx > mx || (omx == mx && ogi < gi)) {
+                mx = omx;
+                arg = oarg;
+                gi = ogi;
+            }
+            mn_x = fmin(mn_x, __shfl_xor(mn_x, d, WAVE));
+            mx_x = fmax(mx_x, __shfl_xor(mx_x, d, WAVE));
+            og = fmax(og, __shfl_xor(og, d, WAVE));
+        }
+        if (lane == 0) {
+            double* o = m.cmax + ((int64_t)m.rank * E + c) * CM;
+            o[0] = mx;
+            o[1] = arg;
+            o[2] = mn_x;
+            o[3] = mx_x;
+            o[4] = og;
+        }
     }
 }
 
@@ -1160,6 +1191,38 @@ __device__ __forceinline__ dd two_prod(double a, double b) {
 // order (cov_perm) and mirrored (unnormalised).  Pure-grid entries hold the exact integer
 // P_jk: C_jk = c_j c_k T + (c_j Z_k + c_k Z_j) / 2 + P_jk / 4 with this rank's T, Z, P
 // (c = 1 - mu is exact for mu in [1, 2]), evaluated in double-double.
+// exact int64 sum of one int32 entry over k-slice slabs (four chains: four loads in flight)
+__device__ __forceinline__ int64_t slab_sum(const int32_t* P, int64_t slab, int ks) {
+    int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int k = 0;
+    for (; k + 4 <= ks; k += 4) {
+        a0 += P[(int64_t)k * slab];
+        a1 += P[(int64_t)(k + 1) * slab];
+        a2 += P[(int64_t)(k + 2) * slab];
+        a3 += P[(int64_t)(k + 3) * slab];
+    }
+    for (; k < ks; k++) a0 += P[(int64_t)k * slab];
+    return (a0 + a1) + (a2 + a3);
+}
+
+// sum tok z_row w_q of the mixed block from its eight digit products, Horner in dd (2^-7)
+__device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t q) {
+    const int64_t gb = (int64_t)m.cov_jb * CT, ldm = 8 * gb;
+    const double sc = ldexp(0x1p-7, -ilogb(m.dscale[q]));  // 2^(e - 7)
+    const int32_t* P = m.Pmx + row * ldm + q;
+    const int64_t slab = m.zq * ldm;
+    dd a{(double)slab_sum(P + 7 * gb, slab, m.ks_mx), 0.0};
+    for (int d = 6; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
+    return dd_mul_d(a, sc);
+}
+
+// the token column's S_q = sum tok w_q of every general position (shared by all grid rows)
+__global__ void __launch_bounds__(BT) k_cov_tokrow(pcx_mat m, double* S) {
+    const int64_t q = blockIdx.x * (int64_t)BT + threadIdx.x;
+    if (q >= (int64_t)m.cov_jb * CT) return;
+    st_dd(S + 2 * q, mixed_comb(m, m.tokpos, q));
+}
+
 __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m, double* Cpos) {
     const int64_t E = m.n_events;
     const int64_t idx = blockIdx.x * (int64_t)BT + threadIdx.x;
@@ -1170,12 +1233,20 @@ __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m, double* Cpos) {
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int64_t cp = m.cov_perm[p], cq = m.cov_perm[q];
     if (q < gb && (!m.cov_mixed || p < gb)) {  // fp64 tiles: the slabs of k_syrk
-        const int64_t ld = m.fp_ld;
-        for (int k = 0; k < m.fp_ks; k++) s += m.cslab[(int64_t)k * ld * ld + p * ld + q];
+        const int64_t ld = m.fp_ld, sl = ld * ld;
+        const double* cs = m.cslab + p * ld + q;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;  // four chains: four loads in flight
+        int k = 0;
+        for (; k + 4 <= m.fp_ks; k += 4) {
+            a0 += cs[(int64_t)k * sl];
+            a1 += cs[(int64_t)(k + 1) * sl];
+            a2 += cs[(int64_t)(k + 2) * sl];
+            a3 += cs[(int64_t)(k + 3) * sl];
+        }
+        for (; k < m.fp_ks; k++) a0 += cs[(int64_t)k * sl];
+        s = (a0 + a1) + (a2 + a3);
     } else if (q >= gb) {  // grid x grid: P from the int8 products
-        int64_t Pi = 0;
-        for (int k = 0; k < m.ks_gg; k++) Pi += m.Pgg[(int64_t)k * m.zq * m.zq + (p - gb) * m.zq + (q - gb)];
-        const double P = (double)Pi;
+        const double P = (double)slab_sum(m.Pgg + (p - gb) * m.zq + (q - gb), m.zq * m.zq, m.ks_gg);
         const double T = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
         const double ap = 1.0 - m.ev[EV_MU * E + cp], aq = 1.0 - m.ev[EV_MU * E + cq];
         const double Zp = 0.5 * (double)m.zsum[cp], Zq = 0.5 * (double)m.zsum[cq];
@@ -1186,21 +1257,7 @@ __global__ void __launch_bounds__(BT) k_cov_reduce(pcx_mat m, double* Cpos) {
     } else if (p >= gb && m.cov_mixed) {
         // general q x grid p: sum tok w_q (c_p + z_p / 2) = c_p S_q + Q_pq / 2, with S_q (the
         // token column) and Q_pq = sum tok z_p w_q from the digit products, Horner in dd
-        const int64_t ldm = (int64_t)8 * gb;
-        const double sc = ldexp(0x1p-7, -ilogb(m.dscale[q]));  // 2^(e - 7)
-        auto comb = [&](int64_t row) {
-            const int32_t* P = m.Pmx + row * ldm + q;
-            const int64_t slab = m.zq * ldm;
-            auto digit = [&](int d) {  // sum over the k-slice slabs
-                int64_t v = 0;
-                for (int k = 0; k < m.ks_mx; k++) v += P[(int64_t)k * slab + (int64_t)d * gb];
-                return (double)v;
-            };
-            dd a{digit(7), 0.0};
-            for (int d = 6; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{digit(d), 0.0});
-            return dd_mul_d(a, sc);
-        };
-        const dd S = comb(m.tokpos), Q = comb(p - gb);
+        const dd S = ld_dd(Cpos + E * E + 2 * q), Q = mixed_comb(m, p - gb, q);  // S: k_cov_tokrow
         const double ap = 1.0 - m.ev[EV_MU * E + cp];
         s = dd_to_double(dd_add(dd_mul_d(S, ap), dd_mul_d(Q, 0.5)));
     }
@@ -1257,8 +1314,10 @@ __global__ void __launch_bounds__(BT) k_pi_check(pcx_mat m) {
         nonfinite |= !__builtin_isfinite(c);
         nonzero |= c != 0.0;
     }
-    if (__any(nonfinite) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&m.info[IN_FLAGS], 2ull);
-    if (__any(nonzero) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&m.info[IN_FLAGS], 8ull);
+    nonfinite = __syncthreads_or(nonfinite);
+    nonzero = __syncthreads_or(nonzero);
+    if (threadIdx.x == 0 && (nonfinite || nonzero))
+        atomicOr((unsigned long long*)&m.info[IN_FLAGS], (nonfinite ? 2ull : 0ull) | (nonzero ? 8ull : 0ull));
 }
 
 // start vector: column of C with the largest diagonal entry (first), normalised
@@ -3881,7 +3940,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_COLSTATS:
             hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
+            hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
             break;
         case M_GUESS:
             hipLaunchKernelGGL(k_guess, dim3(ceb), dim3(BT), 0, st, m);
@@ -3963,7 +4022,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         }
         case M_COV_REDUCE: {  // position-space lower triangle -> mirrored -> event order (Mw as scratch)
             const int64_t n = (int64_t)E * E;
-            double* Cpos = m.Mw;
+            double* Cpos = m.Mw;  // [E][E], then the token row's S [gb] dd
+            if (m.cov_mixed && m.cov_jb > 0)
+                hipLaunchKernelGGL(k_cov_tokrow, dim3((unsigned)((m.cov_jb * CT + BT - 1) / BT)), dim3(BT), 0, st, m,
+                                   Cpos + n);
             hipLaunchKernelGGL(k_cov_reduce, dim3((unsigned)((n + BT - 1) / BT)), dim3(BT), 0, st, m, Cpos);
             const unsigned nt = (unsigned)((E + CV_T - 1) / CV_T);
             hipLaunchKernelGGL(k_cov_sym, dim3(nt, nt), dim3(CV_T * 8), 0, st, (int64_t)E, Cpos);
@@ -3995,7 +4057,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
+            hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
             break;
         case M_DECIDE:
             hipLaunchKernelGGL(k_decide_prep, dim3(ceb), dim3(BT), 0, st, m);
@@ -4017,7 +4079,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_OUTCOMES:
             hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_col_finish, dim3(ceb), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
+            hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
             break;
         case M_EVENTS:
             hipLaunchKernelGGL(k_events, dim3(ceb), dim3(BT), 0, st, m);

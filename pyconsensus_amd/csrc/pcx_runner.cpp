@@ -842,12 +842,27 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
                 // |tok z d| <= 126 * 64 per row) and at least two WGs per CU
                 const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (8 * gb + 255) / 256;
+                // one 128 KB workgroup per CU runs every (tile, k-slice) item for the same time, so
+                // the launch takes ceil(items / CUs) rounds: pick the k in [int32-exact minimum,
+                // 32] with the least rounds per unit of work (no half-empty last round)
+                int ncu = 256;
+                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
                 auto ks_for = [&](int64_t tiles, int64_t max_rows) {
                     tiles = std::max<int64_t>(1, tiles);
-                    int64_t k = std::max<int64_t>((w->wcd_rows + max_rows - 1) / max_rows, (512 + tiles - 1) / tiles);
-                    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(k, nst));
+                    const int64_t kmin = std::max<int64_t>(1, (w->wcd_rows + max_rows - 1) / max_rows);
+                    const int64_t kmax = std::max<int64_t>(kmin, std::min<int64_t>(32, nst));
+                    int64_t best = kmin;
+                    double best_cost = 1e300;
+                    for (int64_t k = kmin; k <= kmax; k++) {
+                        const double cost = (double)((tiles * k + ncu - 1) / ncu) / (double)k;
+                        if (cost < best_cost * (1.0 - 1e-9)) {
+                            best_cost = cost;
+                            best = k;
+                        }
+                    }
+                    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(best, nst));
                 };
-                m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000);
+                m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000);  // lower tiles only do work
                 m.ks_mx = ks_for(tp * tq, 250000);
                 if (np > 0 && !w->grow(w->pgg, (size_t)(m.ks_gg * m.zq * m.zq * 4))) {
                     err = "workspace: hipMalloc of the int8 covariance products failed";
@@ -871,7 +886,18 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     const int64_t want = (16 * 256 + m.cov_fp_tiles - 1) / m.cov_fp_tiles;
                     const int64_t cap = std::min<int64_t>(w->cov_kslices * E * E / (gb * gb),
                                                           std::max<int64_t>(1, w->wcd_rows / (8 * 8)));
-                    m.fp_ks = (int32_t)std::max<int64_t>(1, std::min(want, cap));
+                    // k_syrk holds 3 WGs per CU: the k in [want / 2, 2 want] with whole rounds
+                    const int64_t slots = 3 * (int64_t)ncu, T = m.cov_fp_tiles;
+                    int64_t best = std::max<int64_t>(1, std::min(want, cap));
+                    double best_cost = (double)((T * best + slots - 1) / slots) / (double)best;
+                    for (int64_t k = std::max<int64_t>(1, want / 2); k <= std::min(cap, 2 * want); k++) {
+                        const double cost = (double)((T * k + slots - 1) / slots) / (double)k;
+                        if (cost < best_cost * (1.0 - 1e-9)) {
+                            best_cost = cost;
+                            best = k;
+                        }
+                    }
+                    m.fp_ks = (int32_t)best;
                 }
                 R.stage(m, M_WCD);
                 mats_written = true;
