@@ -1017,7 +1017,14 @@ struct GemmI8 {
 
 constexpr int G_THREADS = 1024;  // 4 x 4 waves of 64 x 64
 
-__global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
+// WAVES = 16: 4 x 4 waves of 64 x 64 (four waves per SIMD); WAVES = 8: 2 x 4 waves of 128 x 64
+// (two per SIMD, 8 A + 4 B fragment reads per 32 MFMAs instead of 4 + 4 per 16: a quarter less
+// LDS read traffic per MFMA).  Same items, slabs and integer results.
+template <int WAVES>
+__global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
+    constexpr int WR = WAVES == 16 ? 4 : 2;  // wave rows (p); 4 wave columns (q)
+    constexpr int TM = GT / WR, AF = TM / 16;
+    constexpr int LPP = 16 / WAVES;  // 1 KB loads per wave per panel per stage (16 KB panels)
     extern __shared__ __attribute__((aligned(16))) char glds[];
     const int ntiles = g.tp * g.tq;
     const int item = xcd_remap(blockIdx.x, gridDim.x);
@@ -1029,21 +1036,24 @@ __global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
     const int64_t s0 = ks * per < nst ? ks * per : nst;
     const int64_t s1 = s0 + per < nst ? s0 + per : nst;  // (an empty slice stores zeros)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int wr = wv >> 2, wc = wv & 3;  // 4 x 4 waves: 64 p x 64 q each
+    const int wr = wv >> 2, wc = wv & 3;
     const int lc = lane & 15, lg = lane >> 4;
-    // this wave moves row group (wv & 3) of each stage, quarter (wv >> 2) of both panels
-    const int mg = wv & 3, mh = wv >> 2;
-    const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
-    const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
     auto issue = [&](int64_t st, int buf) {
-        char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 64) * 16;
-        const int64_t grp = st * 4 + mg;
-        __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16, 0, 0);
-    };
-    v4i acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; a++)
+        for (int j = 0; j < LPP; j++) {  // chunk ch = (row group mg, quarter mh) of both panels
+            const int ch = wv + j * WAVES, mg = ch & 3, mh = ch >> 2;
+            char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 64) * 16;
+            const int64_t grp = st * 4 + mg;
+            const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
+            const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
+            __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16, 0,
+                                             0);
+        }
+    };
+    v4i acc[AF][4];
+#pragma unroll
+    for (int a = 0; a < AF; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
     const int64_t n = s1 - s0;
@@ -1053,31 +1063,31 @@ __global__ void __launch_bounds__(G_THREADS, 1) k_gemm_i8(GemmI8 g) {
     for (int64_t t = 0; t < n; t++) {
         const int buf = (int)(t % G_NBUF);
         if (t + G_NBUF - 2 < n)
-            wait_vmcnt<G_LPW * (G_NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
+            wait_vmcnt<2 * LPP * (G_NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
         else
             wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (t + G_NBUF - 1 < n) issue(s0 + t + G_NBUF - 1, (int)((t + G_NBUF - 1) % G_NBUF));
-        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * 64 + lc;
+        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * TM + lc;
         const v4i* Bs = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL + G_PANEL) + lg * GT + wc * 64 + lc;
-        v4i af[4], bf[4];
+        v4i af[AF], bf[4];
 #pragma unroll
-        for (int a = 0; a < 4; a++) af[a] = As[a * 16];
+        for (int a = 0; a < AF; a++) af[a] = As[a * 16];
 #pragma unroll
         for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
 #pragma unroll
-        for (int a = 0; a < 4; a++)
+        for (int a = 0; a < AF; a++)
 #pragma unroll
             for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
         asm volatile("" ::: "memory");
     }
     // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
-    const int p0 = ip * GT + wr * 64 + 4 * lg, q0 = iq * GT + wc * 64 + lc;
+    const int p0 = ip * GT + wr * TM + 4 * lg, q0 = iq * GT + wc * 64 + lc;
     int32_t* out = g.out + (int64_t)ks * g.slab;
 #pragma unroll
-    for (int a = 0; a < 4; a++)
+    for (int a = 0; a < AF; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++)
 #pragma unroll
@@ -3968,17 +3978,30 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             }
             static std::once_flag g_once;
             static hipError_t g_err = hipSuccess;
+            static int g_waves = 16;  // PCX_GEMM_I8_WAVES=8: 2 x 4 waves of 128 x 64
             std::call_once(g_once, [] {
-                g_err = hipFuncSetAttribute((const void*)k_gemm_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                const char* e = getenv("PCX_GEMM_I8_WAVES");
+                g_waves = (e && atoi(e) == 8) ? 8 : 16;
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)G_LDS_BYTES);
+                if (g_err == hipSuccess)
+                    g_err = hipFuncSetAttribute((const void*)k_gemm_i8<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)G_LDS_BYTES);
             });
             if (g_err != hipSuccess) return g_err;
+            auto gemm = [&](const GemmI8& g) {
+                const dim3 grid((unsigned)(g.tp * g.tq * g.kslices));
+                if (g_waves == 8)
+                    hipLaunchKernelGGL(k_gemm_i8<8>, grid, dim3(8 * 64), G_LDS_BYTES, st, g);
+                else
+                    hipLaunchKernelGGL(k_gemm_i8<16>, grid, dim3(16 * 64), G_LDS_BYTES, st, g);
+            };
             const int64_t rg = m.wcd_rows / 16;
             hipLaunchKernelGGL(k_tokcol, dim3((unsigned)((rg + BT - 1) / BT)), dim3(BT), 0, st, m);
             {  // grid x grid (lower tiles): |tok z z| <= 252 per row
                 GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg};
                 g.tp = g.tq = (np + GT - 1) / GT;
-                hipLaunchKernelGGL(k_gemm_i8, dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(G_THREADS), G_LDS_BYTES, st, g);
+                gemm(g);
             }
             if (m.cov_mixed) {  // grid x general digits: |tok z d| <= 126 * 64 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
@@ -3987,7 +4010,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                          0, 0, 0, m.ks_mx, rg};
                 g.tp = (np + GT - 1) / GT;
                 g.tq = (8 * gb + GT - 1) / GT;
-                hipLaunchKernelGGL(k_gemm_i8, dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(G_THREADS), G_LDS_BYTES, st, g);
+                gemm(g);
             }
             break;
         }
