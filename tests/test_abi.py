@@ -21,7 +21,7 @@ def test_header_declares_entry_points():
     for must in ("pcx_create", "pcx_destroy", "pcx_set_stream", "pcx_last_error",
                  "pcx_consensus_batched_f64", "pcx_abi_version", "pcx_consensus_f64", "pcx_create_rank",
                  "pcx_comm_unique_id", "pcx_interpolate_f64", "pcx_wpca_f64", "pcx_lie_detector_f64",
-                 "pcx_nonconformity_f64"):
+                 "pcx_nonconformity_f64", "pcx_create_devices"):
         assert must in names
 
 
@@ -105,6 +105,11 @@ def test_errors_without_gpu_are_loud():
     with pytest.raises(_lib.PcxError):
         consensus_batched([[[1.0, 2.0]]])
     assert not _lib.lib().pcx_create_grouped(0, None, 0)
+    import ctypes as C
+    ids = (C.c_int * 2)(0, 1)
+    assert not _lib.lib().pcx_create_devices(2, ids)  # the multi-device context needs the GPUs too
+    assert b"no HIP device" in _lib.lib().pcx_last_error()
+    assert not _lib.lib().pcx_create_devices(0, ids)
     from pyconsensus_amd import Oracle
     with pytest.raises(_lib.PcxError):
         Oracle(reports=[[1.0, 2.0]] * 100).consensus()  # the matrix path raises too (no CPU fallback)
