@@ -30,7 +30,9 @@
 
 #include "../include/pcx.h"
 
-#define NMAX 64
+#ifndef NMAX
+#define NMAX 64 /* reporters per round; libpcx_oracle256.so: 256 (the workgroup-per-round kernel's rounds) */
+#endif
 #define EMAX 64
 #define ES (EMAX + 1)
 

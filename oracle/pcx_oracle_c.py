@@ -16,22 +16,29 @@ from pyconsensus_amd.batched import clusterfeck_threshold
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "lib", "libpcx_oracle.so")
+LIB256 = os.path.join(HERE, "lib", "libpcx_oracle256.so")  # NMAX = 256: rounds above 64 reporters
 _lib = None
+_lib256 = None
 
 
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def lib(large=False):
+    global _lib, _lib256
+    if (_lib256 if large else _lib) is None:
+        path = LIB256 if large else LIB
+        if not os.path.exists(path):
             build()
-        _lib = C.CDLL(LIB)
-        _lib.pcxo_consensus_batched_f64.argtypes = [C.POINTER(Batch), C.POINTER(BatchResult), C.c_int]
-        _lib.pcxo_consensus_batched_f64.restype = C.c_int
-    return _lib
+        h = C.CDLL(path)
+        h.pcxo_consensus_batched_f64.argtypes = [C.POINTER(Batch), C.POINTER(BatchResult), C.c_int]
+        h.pcxo_consensus_batched_f64.restype = C.c_int
+        if large:
+            _lib256 = h
+        else:
+            _lib = h
+    return _lib256 if large else _lib
 
 
 def _ptr(a):
@@ -74,7 +81,7 @@ def batched(reports, scaled=None, lo=None, hi=None, reputation=None, catch_toler
         a = np.empty(out_shape(kind, B, N, E), dtype=dt)
         outs[name] = a
         setattr(res, name, a.ctypes.data)
-    rc = lib().pcxo_consensus_batched_f64(C.byref(inp), C.byref(res), int(threads))
+    rc = lib(large=N > 64).pcxo_consensus_batched_f64(C.byref(inp), C.byref(res), int(threads))
     if rc != 0:
         raise ValueError("oracle rejected the batch (rc=%d)" % rc)
     return outs

@@ -11,6 +11,7 @@
 #include <vector>
 #include <cstdlib>
 #include <thread>
+#include <algorithm>
 
 #include "../../include/pcx.h"
 #include "pcx_internal.h"
@@ -176,6 +177,7 @@ void pcx_destroy(pcx_ctx* ctx) {
     for (pcx_ctx* s : ctx->sub) pcx_destroy(s);
     if (ctx->group) pcx::group_destroy(ctx->group);
     pcx::rounds_free(ctx);
+    if (ctx->mscr) (void)hipFree(ctx->mscr);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
     delete ctx->comm;
@@ -222,11 +224,6 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
         return fail(PCX_EINVAL, "batched: cokurtosis needs aux_scores (aux[\"cokurt\"])");
     if (!std::isfinite(in->catch_tolerance) || !std::isfinite(in->alpha))
         return fail(PCX_EINVAL, "batched: catch_tolerance/alpha must be finite");
-    if (large) {  // one single-matrix consensus per round, many rounds in flight (pcx_rounds.cpp)
-        std::string err;
-        const int rc = pcx::run_rounds(ctx, in, out, err);
-        return rc ? fail(rc, "pcx_consensus_batched_f64: " + err) : PCX_OK;
-    }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
     pcx::BatchArgs a{};
@@ -277,6 +274,32 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
     a.components = out->components;
     a.original = out->original;
     a.filled = out->filled;
+    if (large) {
+        if (pcx::medium_fits(a) && !getenv("PCX_NO_MEDIUM")) {
+            // one workgroup per round (pcx_medium.hip), in chunks of bounded scratch
+            const size_t cap = (size_t)2 << 30;
+            const int64_t chunk = pcx::medium_chunk(a, cap);
+            const size_t per = ((a.filled ? 0 : (size_t)a.N * a.E) + (size_t)a.E * a.E) * sizeof(double);
+            const size_t need = per * (size_t)chunk;
+            if (ctx->mscr_bytes < need) {
+                if (ctx->mscr) (void)hipFree(ctx->mscr);
+                ctx->mscr = nullptr;
+                ctx->mscr_bytes = 0;
+                e = hipMalloc(&ctx->mscr, need);
+                if (e != hipSuccess) return hip_fail(e, "hipMalloc(medium scratch)");
+                ctx->mscr_bytes = need;
+            }
+            double* Fscr = (double*)ctx->mscr;
+            double* Cscr = Fscr + (a.filled ? 0 : (size_t)chunk * a.N * a.E);
+            for (int64_t b0 = 0; b0 < a.B && e == hipSuccess; b0 += chunk)
+                e = pcx::launch_medium(a, b0, std::min<int64_t>(chunk, a.B - b0), Fscr, Cscr, ctx->stream);
+            return e == hipSuccess ? PCX_OK : hip_fail(e, "medium_round_kernel launch");
+        }
+        // one single-matrix consensus per round, many rounds in flight (pcx_rounds.cpp)
+        std::string err;
+        const int rc = pcx::run_rounds(ctx, in, out, err);
+        return rc ? fail(rc, "pcx_consensus_batched_f64: " + err) : PCX_OK;
+    }
     const char* st_env = getenv("PCX_STAMPS");
     if (st_env && st_env[0] == '1' && a.B > 0) {  // diagnostic: per-phase clock breakdown
         long long* d = nullptr;

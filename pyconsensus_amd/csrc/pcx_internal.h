@@ -154,6 +154,10 @@ struct BatchArgs {
 
 size_t batched_lds_bytes(int N, int E, int algorithm);
 hipError_t launch_batched(const BatchArgs& a, hipStream_t stream);
+// rounds above one wavefront (N <= 256, E <= 64; PCA / absolute / cokurtosis): one workgroup each
+bool medium_fits(const BatchArgs& a);
+int64_t medium_chunk(const BatchArgs& a, size_t scratch_bytes);
+hipError_t launch_medium(const BatchArgs& a, int64_t b0, int64_t nb, double* Fscr, double* Cscr, hipStream_t st);
 
 // ---------------------------------------------------------------- single-matrix stages
 // Internal stage ids (pcx_stage_name); the runner (pcx_runner.cpp) sequences them.
@@ -270,6 +274,8 @@ struct pcx_ctx {
     int profile = 0;
     double stage_ms[PCX_NSTAGES] = {0};
     int scaled_floor = 0;          // allocate the workspace for at least this many scaled events
+    void* mscr = nullptr;          // per-round scratch of the workgroup-per-round kernel (pcx_medium.hip)
+    size_t mscr_bytes = 0;
     // batched rounds above the one-wave kernel's limits: worker contexts of the round scheduler
     std::vector<pcx_ctx*> pool;
     // pcx_create_devices: one rank context per device, driven by worker threads

@@ -1000,7 +1000,6 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int GT = 256;                              // output tile edge
 constexpr int G_NBUF = 4;                            // LDS ring depth
-constexpr int G_LPW = 2;                             // global_load_lds per wave per stage
 constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one operand's 64-row stage: 16 KB
 constexpr size_t G_LDS_BYTES = G_NBUF * 2 * G_PANEL; // 128 KB
 
@@ -1014,8 +1013,6 @@ struct GemmI8 {
     int np, nq, tp, tq, lower, kslices;
     int64_t rg;  // row groups, a multiple of 4
 };
-
-constexpr int G_THREADS = 1024;  // 4 x 4 waves of 64 x 64
 
 // WAVES = 16: 4 x 4 waves of 64 x 64 (four waves per SIMD); WAVES = 8: 2 x 4 waves of 128 x 64
 // (two per SIMD, 8 A + 4 B fragment reads per 32 MFMAs instead of 4 + 4 per 16: a quarter less

@@ -120,12 +120,74 @@ def test_variants_bitexact_vs_c_oracle(gpu_lib, variant):
         assert np.all(same), (variant, k, int(np.size(same) - np.count_nonzero(same)))
 
 
-@pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "200x24_big-five"])
-def test_rounds_above_one_wave(gpu_lib, variant):
-    """Rounds beyond the one-wavefront kernel (N > 64 or E > 32): the batched entry runs
-    each as a single-matrix consensus on a pool of worker streams (csrc/pcx_rounds.cpp).
-    Every round equals its own pcx_consensus_f64 call bit for bit and the numpy
-    restatement of the reference within the north_star tolerances."""
+def _rounds_kw(variant, B=40, seed=77):
+    from pyconsensus_amd import synthetic
+
+    shape, *rest = variant.split("_")
+    N, E = map(int, shape.split("x"))
+    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=seed)
+    kw = dict(reputation=rep, scaled=sc, lo=lo, hi=hi)
+    if "uniform" in rest:
+        kw["reputation"] = None
+    if "shared" in rest:
+        kw.update(scaled=sc[0], lo=lo[0], hi=hi[0])
+    if "nobounds" in rest:
+        kw.update(scaled=None, lo=None, hi=None)
+    if "int" in rest:
+        R = np.where(np.isnan(R), 0.0, np.trunc(R))
+        kw["int_dtype"] = True
+    for alg in ("big-five", "absolute", "cokurtosis"):
+        if alg in rest:
+            kw["algorithm"] = alg
+    if kw.get("algorithm") == "cokurtosis":
+        kw["aux_scores"] = np.random.default_rng(9).normal(size=(B, N))
+    return R, kw
+
+
+def _round_inputs(kw, b):
+    sc, lo, hi = kw["scaled"], kw["lo"], kw["hi"]
+    if sc is not None and sc.ndim == 2:
+        sc, lo, hi = sc[b], lo[b], hi[b]
+    rep = None if kw["reputation"] is None else kw["reputation"][b]
+    return rep, sc, lo, hi
+
+
+@pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "256x64", "65x33_nobounds", "200x1",
+                                     "120x20_int", "90x36_absolute", "80x40_cokurtosis", "250x60_uniform"])
+def test_medium_rounds_bitexact_vs_spec(gpu_lib, variant):
+    """Rounds above one wavefront up to 256 x 64 (PCA / absolute / cokurtosis): one workgroup per
+    round (csrc/pcx_medium.hip), bit-identical to the C SPEC built for 256 reporters
+    (oracle/pcx_oracle_batched.c, NMAX = 256) on every output, and within the north_star
+    tolerances of the numpy restatement of the reference."""
+    from oracle import pcx_oracle_c as OC
+    from oracle.pcx_oracle import OracleCPU
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, kw = _rounds_kw(variant)
+    g = _np(consensus_batched(R, filled=True, original=True, **kw))
+    c = OC.batched(R, **kw, threads=8)
+    for k, v in g.items():
+        same = (v == c[k]) | (np.isnan(v) & np.isnan(c[k])) if v.dtype.kind == "f" else (v == c[k])
+        assert np.all(same), (variant, k, int(np.size(same) - np.count_nonzero(same)))
+    alg = kw.get("algorithm", "PCA")
+    if kw.get("int_dtype"):
+        return  # an int matrix with a NaN fill makes the reference raise: the SPEC alone pins it
+    for b in range(0, R.shape[0], 7):
+        rep, sc, lo, hi = _round_inputs(kw, b)
+        aux = None if alg != "cokurtosis" else {"cokurt": kw["aux_scores"][b]}
+        Rb = R[b].copy()
+        ref = G.flat_result(OracleCPU(reports=Rb, event_bounds=None if sc is None else synthetic.bounds_list(sc, lo, hi),
+                                      reputation=rep, algorithm=alg, aux=aux).consensus())
+        bad, _ = P.compare(ref, {k: v[b] for k, v in g.items()})
+        assert not bad, (b, bad)
+
+
+@pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "200x24_big-five", "300x20"])
+def test_rounds_scheduler(gpu_lib, variant, monkeypatch):
+    """Rounds the workgroup kernel does not take (big-five, N > 256, or PCX_NO_MEDIUM): each runs
+    as a single-matrix consensus on the worker-stream scheduler (csrc/pcx_rounds.cpp) and equals
+    its own pcx_consensus_f64 call bit for bit, and the numpy restatement within tolerance."""
     import torch
 
     from oracle.pcx_oracle import OracleCPU
@@ -133,37 +195,24 @@ def test_rounds_above_one_wave(gpu_lib, variant):
     from pyconsensus_amd.batched import consensus_batched
     from pyconsensus_amd.pipeline import consensus_matrix
 
-    shape, *rest = variant.split("_")
-    N, E = map(int, shape.split("x"))
-    B = 40
-    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=77)
-    kw = dict(reputation=rep, scaled=sc, lo=lo, hi=hi)
-    if "uniform" in rest:
-        kw["reputation"] = None
-    if "shared" in rest:
-        kw.update(scaled=sc[0], lo=lo[0], hi=hi[0])
-    alg = "big-five" if "big-five" in rest else "PCA"
-    g = _np(consensus_batched(R, filled=True, original=True, algorithm=alg, **kw))
+    monkeypatch.setenv("PCX_NO_MEDIUM", "1")
+    R, kw = _rounds_kw(variant)
+    alg = kw.get("algorithm", "PCA")
+    g = _np(consensus_batched(R, filled=True, original=True, **kw))
     torch.cuda.synchronize()
+    B = R.shape[0]
     for b in [0, 1, B // 2, B - 1]:
-        s_b = kw["scaled"] if kw["scaled"].ndim == 1 else kw["scaled"][b]
-        lo_b = kw["lo"] if kw["lo"].ndim == 1 else kw["lo"][b]
-        hi_b = kw["hi"] if kw["hi"].ndim == 1 else kw["hi"][b]
-        rep_b = None if kw["reputation"] is None else kw["reputation"][b]
-        ev, ag, meta = consensus_matrix(R[b], rep_b, s_b, lo_b, hi_b, algorithm=alg, matrices=True)
+        rep, sc, lo, hi = _round_inputs(kw, b)
+        ev, ag, meta = consensus_matrix(R[b], rep, sc, lo, hi, algorithm=alg, matrices=True)
         one = {k: v.cpu().numpy() for d in (ev, ag) for k, v in d.items()}
         for k, v in one.items():
             np.testing.assert_array_equal(g[k][b], v, err_msg="%s round %d" % (k, b))
         assert int(g["branch"][b]) == meta["branch"] and g["participation"][b] == meta["participation"]
-    for b in range(B):
-        s_b = kw["scaled"] if kw["scaled"].ndim == 1 else kw["scaled"][b]
-        lo_b = kw["lo"] if kw["lo"].ndim == 1 else kw["lo"][b]
-        hi_b = kw["hi"] if kw["hi"].ndim == 1 else kw["hi"][b]
-        rep_b = None if kw["reputation"] is None else kw["reputation"][b]
-        ref = G.flat_result(OracleCPU(reports=R[b].copy(), event_bounds=synthetic.bounds_list(s_b, lo_b, hi_b),
-                                      reputation=rep_b, algorithm=alg).consensus())
-        ours = {k: v[b] for k, v in g.items()}
-        bad, _ = P.compare(ref, ours)
+    for b in range(0, B, 3):
+        rep, sc, lo, hi = _round_inputs(kw, b)
+        ref = G.flat_result(OracleCPU(reports=R[b].copy(), event_bounds=synthetic.bounds_list(sc, lo, hi),
+                                      reputation=rep, algorithm=alg).consensus())
+        bad, _ = P.compare(ref, {k: v[b] for k, v in g.items()})
         assert not bad, (b, bad)
 
 

@@ -1,5 +1,6 @@
-"""Throughput of batched rounds above the one-wavefront kernel (csrc/pcx_rounds.cpp):
-B rounds of N x E through pcx_consensus_batched_f64 at several worker-pool sizes.
+"""Throughput of batched rounds above the one-wavefront kernel: B rounds of N x E through
+pcx_consensus_batched_f64 on the workgroup-per-round kernel (csrc/pcx_medium.hip), then on the
+worker-stream scheduler (csrc/pcx_rounds.cpp, PCX_NO_MEDIUM=1) at several pool sizes.
 
 usage: python tools/bench_rounds.py [B] [N] [E]   (prints one JSON line per pool size)
 """
@@ -24,6 +25,16 @@ def main():
     dev = torch.device("cuda", 0)
     Rt, rt = torch.as_tensor(R, device=dev), torch.as_tensor(rep, device=dev)
     sct, lot, hit = (torch.as_tensor(a, device=dev) for a in (sc.astype("uint8"), lo, hi))
+    for _ in range(2):  # the workgroup-per-round kernel (csrc/pcx_medium.hip), N <= 256, E <= 64
+        consensus_batched(Rt, rt, sct, lot, hit)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        consensus_batched(Rt, rt, sct, lot, hit)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    print(json.dumps({"rounds": B, "N": N, "E": E, "path": "workgroup kernel", "seconds": dt,
+                      "rounds_per_s": B / dt}), flush=True)
+    os.environ["PCX_NO_MEDIUM"] = "1"  # the worker-stream scheduler (csrc/pcx_rounds.cpp)
     for workers in (1, 4, 8, 16, 32):
         os.environ["PCX_ROUND_WORKERS"] = str(workers)
         _lib._ctx.clear()  # fresh context: the pool size is read when it grows
@@ -33,7 +44,7 @@ def main():
         consensus_batched(Rt, rt, sct, lot, hit)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"rounds": B, "N": N, "E": E, "workers": workers, "seconds": dt,
+        print(json.dumps({"rounds": B, "N": N, "E": E, "path": "scheduler", "workers": workers, "seconds": dt,
                           "rounds_per_s": B / dt}), flush=True)
 
 
