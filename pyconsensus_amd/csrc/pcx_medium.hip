@@ -64,16 +64,34 @@ __device__ double mpw(G g, int n) {
     return mpw_leaf(g, 0, n2) + mpw_sub(g, n2, n - n2);
 }
 
-// SPEC tree64 over n <= 64 values (zero padded)
+// the same tree64 on wave 0 (lane = slot): the xor butterfly by shuffles; valid on lane 0
 template <class G>
-__device__ double mtree64(G g, int n) {
-    double t[64], u[64];
-    for (int i = 0; i < 64; i++) t[i] = i < n ? g(i) : 0.0;
-    for (int s = 1; s <= 8; s <<= 1) {
-        for (int i = 0; i < 64; i++) u[i] = t[i] + t[i ^ s];
-        for (int i = 0; i < 64; i++) t[i] = u[i];
+__device__ double wtree64(G g, int n) {
+    const int l = threadIdx.x & 63;
+    double v = l < n ? g(l) : 0.0;
+    for (int s = 1; s <= 8; s <<= 1) v = v + __shfl_xor(v, s, 64);
+    const double t16 = __shfl(v, 16, 64), t32 = __shfl(v, 32, 64), t48 = __shfl(v, 48, 64);
+    return (v + t16) + (t32 + t48);
+}
+
+// block compaction: rows with pred(i) in row order -> out[0..m) = val(i); returns m (all threads)
+template <class P, class V>
+__device__ int bcompact(P pred, V val, int n, double* out, int* wcnt) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int base = 0;
+    for (int i0 = 0; i0 < n; i0 += MT) {
+        const int i = i0 + (int)threadIdx.x;
+        const bool p = i < n && pred(i);
+        const unsigned long long bal = __ballot(p);
+        if (lane == 0) wcnt[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < w; k++) off += wcnt[k];
+        if (p) out[off + __popcll(bal & ((1ull << lane) - 1ull))] = val(i);
+        for (int k = 0; k < MT / 64; k++) base += wcnt[k];
+        __syncthreads();
     }
-    return (t[0] + t[16]) + (t[32] + t[48]);
+    return base;
 }
 
 // SPEC dot2 (compensated dot, index order)
@@ -325,27 +343,23 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         for (int i = 0; i < N; i++)
             if (fl[i * E + j]) F[i * E + j] = g;
     }
+    __shared__ int wcnt[MT / 64];
     for (int j = 0; j < E; j++) {
         if (!scaled(j)) continue;
+        // present values and their reputations in row order (block compaction), then the
+        // sequential present total on one thread and the weights rep / total
+        const int np_ = bcompact([&](int i) { return fl[i * E + j] == 0; }, [&](int i) { return F[i * E + j]; }, N, XA,
+                                 wcnt);
+        bcompact([&](int i) { return fl[i * E + j] == 0; }, [&](int i) { return rep[i]; }, N, WA, wcnt);
         if (tid == 0) {
-            int nmiss = 0, np_ = 0;
             double tot = 0.0;
-            for (int i = 0; i < N; i++) {
-                if (fl[i * E + j]) {
-                    nmiss++;
-                } else {
-                    tot += rep[i];
-                    XA[np_++] = F[i * E + j];
-                }
-            }
-            int m = 0;
-            for (int i = 0; i < N; i++)
-                if (!fl[i * E + j]) WA[m++] = rep[i] / tot;
-            scal[2] = (double)nmiss;
-            scal[3] = (double)np_;
+            for (int q = 0; q < np_; q++) tot += WA[q];
+            scal[2] = tot;
         }
         __syncthreads();
-        const int nmiss = (int)scal[2], np_ = (int)scal[3];
+        for (int q = tid; q < np_; q += MT) WA[q] = WA[q] / scal[2];
+        __syncthreads();
+        const int nmiss = N - np_;
         if (nmiss) {  // block-uniform
             double g = mwmedian(XA, WA, np_, VNp(VN_XS), VNp(VN_WS), sh);
             if (a.int_dtype) g = trunc(g);
@@ -415,7 +429,12 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                 for (int j = 1; j < E; j++)
                     if (C[j * E + j] > C[kd * E + kd]) kd = j;
                 scal[5] = (double)kd;
-                scal[6] = sqrt(mtree64([&](int j) { const double v = C[j * E + kd]; return v * v; }, E));
+            }
+            __syncthreads();
+            if (tid < 64) {
+                const int kd0 = (int)scal[5];
+                const double t = sqrt(wtree64([&](int j) { const double v = C[j * E + kd0]; return v * v; }, E));
+                if (tid == 0) scal[6] = t;
             }
             __syncthreads();
             const int kd = (int)scal[5];
@@ -450,7 +469,10 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                     y[j] = acc;
                 }
                 __syncthreads();
-                if (tid == 0) scal[7] = sqrt(mtree64([&](int j) { return y[j] * y[j]; }, E));
+                if (tid < 64) {
+                    const double t = sqrt(wtree64([&](int j) { return y[j] * y[j]; }, E));
+                    if (tid == 0) scal[7] = t;
+                }
                 __syncthreads();
                 for (int j = tid; j < E; j += MT) y[j] = y[j] / scal[7];
                 __syncthreads();
@@ -651,14 +673,11 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     }
     // --- a14: certainty (:540-546): sum of smooth over the matching rows (pairwise), per event
     double* cert = VEp(VE_CERT);
-    for (int j = 0; j < E; j++) {
-        // compact the matching rows' weights into XA in row order
-        if (tid == 0) {
-            int m = 0;
-            for (int i = 0; i < N; i++)
-                if (F[i * E + j] == adj[j]) XA[m++] = smooth[i];
+    for (int j = 0; j < E; j++) {  // the matching rows' weights in row order (block compaction)
+        const double aj = adj[j];
+        const int m = bcompact([&](int i) { return F[i * E + j] == aj; }, [&](int i) { return smooth[i]; }, N, XA, wcnt);
+        if (tid == 0)
             cert[j] = m ? mpw([&](int q) { return XA[q]; }, m) : (alg == PCX_ALG_PCA ? __builtin_nan("") : 0.0);
-        }
         __syncthreads();
     }
     double* reward = VEp(VE_REWARD);
