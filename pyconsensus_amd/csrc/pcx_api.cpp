@@ -400,7 +400,11 @@ int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, co
         th.emplace_back([&, k, off] {
             rcs[k] = pcx::run_matrix(ctx->sub[k], &ps[k], &rs[k], entry, scores ? scores + off : nullptr, rank_rule,
                                      nc ? nc + off : nullptr, errs[k]);
-            if (rcs[k] && ctx->group) pcx::group_abort(ctx->group);  // release the ranks waiting on this one
+            if (rcs[k]) {  // release the ranks waiting on this one in an exchange
+                if (ctx->group) pcx::group_abort(ctx->group);
+                for (pcx_ctx* o : ctx->sub)
+                    if (o->comm && o != ctx->sub[k]) o->comm->abort();  // RCCL: ncclCommAbort
+            }
         });
     }
     for (auto& t : th) t.join();

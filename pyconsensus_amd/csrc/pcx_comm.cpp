@@ -88,10 +88,19 @@ struct RcclComm : Comm {
     ~RcclComm() override {
         if (comm) ncclCommDestroy(comm);
     }
+    void abort() override {
+        if (comm) ncclCommAbort(comm);
+        comm = nullptr;
+        aborted = true;
+    }
     static ncclDataType_t dt(int d) { return d == PCX_F64 ? ncclFloat64 : ncclUint64; }
     static ncclRedOp_t op_of(int o) { return o == PCX_SUM ? ncclSum : (o == PCX_MIN ? ncclMin : ncclMax); }
     int allreduce(void* buf, int64_t count, int dtype, int op, hipStream_t st, std::string& err) override {
         if (count <= 0) return 0;
+        if (!comm) {
+            err = "RCCL communicator aborted after a failed call: recreate the context";
+            return PCX_ECOMM;
+        }
         ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt(dtype), op_of(op), comm, st);
         if (r != ncclSuccess) {
             err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
@@ -101,6 +110,10 @@ struct RcclComm : Comm {
     }
     int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) override {
         if (bytes <= 0) return 0;
+        if (!comm) {
+            err = "RCCL communicator aborted after a failed call: recreate the context";
+            return PCX_ECOMM;
+        }
         ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, comm, st);
         if (r != ncclSuccess) {
             err = std::string("ncclAllGather: ") + ncclGetErrorString(r);

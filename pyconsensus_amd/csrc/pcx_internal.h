@@ -250,6 +250,10 @@ struct Comm {
     // recv[world][bytes] <- send of every rank; send may alias recv + rank*bytes
     virtual int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) = 0;
     virtual const char* kind() const = 0;
+    // unblock every rank waiting in this communicator after another rank failed (RCCL:
+    // ncclCommAbort); the communicator is unusable afterwards
+    virtual void abort() {}
+    bool aborted = false;
 };
 Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err);
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);

@@ -70,3 +70,25 @@ def test_openblas_gemv_order_model():
         pytest.skip("host OpenBLAS core %s %s differs from the goldens' (SkylakeX 0.3.29)" % (arch, ver))
     bad, tot = PO.check(max_n=40, max_e=12, trials=1)
     assert bad == 0, (bad, tot)
+
+
+@pytest.mark.parametrize("N,E,uniform", [(100, 50, False), (256, 64, False), (30, 40, True), (200, 1, False)])
+def test_spec256_matches_numpy_restatement(N, E, uniform):
+    """The C SPEC built for 256 reporters (oracle/lib/libpcx_oracle256.so: the bitwise target of
+    the workgroup-per-round kernel) against the numpy restatement of the reference, north_star
+    tolerances."""
+    import golden_cases as G
+    import parity as P
+    from oracle import pcx_oracle_c as OC
+    from oracle.pcx_oracle import OracleCPU
+    from pyconsensus_amd import synthetic
+
+    R, sc, lo, hi, rep = synthetic.rounds(4, N, E, seed=N + E)
+    if uniform:
+        rep = None
+    o = OC.batched(R, sc, lo, hi, rep, threads=2)
+    for b in range(R.shape[0]):
+        ref = G.flat_result(OracleCPU(reports=R[b].copy(), event_bounds=synthetic.bounds_list(sc[b], lo[b], hi[b]),
+                                      reputation=None if rep is None else rep[b]).consensus())
+        bad, _ = P.compare(ref, {k: v[b] for k, v in o.items()})
+        assert not bad, (b, bad)
