@@ -76,7 +76,7 @@ int      pcx_synchronize(pcx_ctx* ctx);
 /* style Monte Carlo, README.rst:52-56).  Each round is the complete            */
 /* Oracle(reports, event_bounds, reputation).consensus() of __init__.py:102-611. */
 /* N <= 64, E <= 32: one round per wavefront, asynchronous on the stream.      */
-/* N <= 256, E <= 64 (PCA, absolute, cokurtosis): one 256-thread workgroup per  */
+/* N <= 256, E <= 64 (all but the clusterings): one 256-thread workgroup per    */
 /* round (the same SPEC order), asynchronous.  Any other shape or algorithm     */
 /* (E <= 65536): each round is one single-matrix consensus, a pool of worker    */
 /* streams keeps many in flight (PCX_ROUND_WORKERS, default 16); synchronous.   */

@@ -13,7 +13,8 @@
 // step allows; the reference's sequential sums stay on one thread.  LDS holds the
 // power-iteration matrices, the per-element NA flags and the row / event vectors; the filled
 // matrix and the covariance live in a per-round global scratch (L2-resident).
-// Algorithms: PCA, "absolute", "cokurtosis" (the others take the round scheduler).
+// Algorithms: PCA, "absolute", "big-five", "fixed-variance", "cokurtosis" (the clusterings take
+// the round scheduler).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -259,6 +260,135 @@ __device__ double mwmedian(const double* x, const double* w, int n, double* xs, 
     return r;
 }
 
+// "big-five" / "fixed-variance" (:373-390, :429-451), SPEC component_scores: eigenpairs of C by
+// cyclic two-sided Jacobi with the round-robin pair schedule (every step's pairs disjoint: one
+// thread per pair for the angles, per (pair, index) for the rotations, rows then columns), Sigma
+// descending (ties by index), net_i = sum_c Sigma_c (wcd_i . loading_c) over the components.
+// A = M, V = Tm (LDS, stride ES); returns the fixed-variance count, else -1.
+constexpr int M_JAC_MAXSWEEP = 30;
+constexpr double M_JAC_TOL = 1e-15;
+
+__device__ __forceinline__ void mjac_pair(int i, int r, int n, int& p, int& q) {
+    const int a = i == 0 ? 0 : 1 + (i - 1 + r) % (n - 1);
+    const int b = 1 + (n - 2 - i + r) % (n - 1);
+    p = a < b ? a : b;
+    q = a < b ? b : a;
+}
+
+__device__ int component_scores(const BatchArgs& a, const double* C, double* A, double* V, int ES, const double* F,
+                                const double* mu, double* net, double* sh, double* scal) {
+    const int E = a.E, N = a.N, tid = threadIdx.x;
+    __shared__ double cc[MEV / 2 + 1], ss[MEV / 2 + 1];
+    __shared__ int pp[MEV / 2 + 1], qq[MEV / 2 + 1];
+    __shared__ int order[MEV];
+    __shared__ double sig[MEV];
+    for (int e = tid; e < E * E; e += MT) {
+        const int j = e / E, k = e % E;
+        A[j * ES + k] = C[e];
+        V[j * ES + k] = j == k ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) scal[0] = mpw([&](int j) { return C[j * E + j]; }, E);  // np.trace: add.reduce
+    if (E >= 2) {
+        const int n = E + (E & 1), npair = n / 2;
+        for (int sweep = 0; sweep < M_JAC_MAXSWEEP; sweep++) {
+            double off = 0.0, dg = 0.0;  // max-norms: exact in any order
+            for (int e = tid; e < E * E; e += MT) {
+                const int j = e / E, k = e % E;
+                const double v = fabs(A[j * ES + k]);
+                if (j == k) dg = fmax(dg, v);
+                else off = fmax(off, v);
+            }
+            off = bmax(off, sh);
+            dg = bmax(dg, sh);
+            if (!(off > M_JAC_TOL * dg)) break;  // block-uniform
+            for (int r = 0; r < n - 1; r++) {
+                for (int i = tid; i < npair; i += MT) {
+                    int p, q;
+                    mjac_pair(i, r, n, p, q);
+                    pp[i] = p;
+                    qq[i] = q;
+                    double c = 1.0, sn = 0.0;
+                    if (q < E) {
+                        const double app = A[p * ES + p], aqq = A[q * ES + q], apq = A[p * ES + q];
+                        if (apq != 0.0) {
+                            const double tau = (aqq - app) / (2.0 * apq);
+                            const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                            c = 1.0 / sqrt(1.0 + t * t);
+                            sn = t * c;
+                        }
+                    }
+                    cc[i] = c;
+                    ss[i] = sn;
+                }
+                __syncthreads();
+                for (int e = tid; e < npair * E; e += MT) {  // rows
+                    const int i = e / E, k = e % E;
+                    if (ss[i] == 0.0) continue;
+                    const int p = pp[i], q = qq[i];
+                    const double c = cc[i], sn = ss[i];
+                    const double apk = A[p * ES + k], aqk = A[q * ES + k];
+                    A[p * ES + k] = c * apk - sn * aqk;
+                    A[q * ES + k] = sn * apk + c * aqk;
+                }
+                __syncthreads();
+                for (int e = tid; e < npair * E; e += MT) {  // columns of A and V
+                    const int i = e / E, j = e % E;
+                    if (ss[i] == 0.0) continue;
+                    const int p = pp[i], q = qq[i];
+                    const double c = cc[i], sn = ss[i];
+                    const double ajp = A[j * ES + p], ajq = A[j * ES + q];
+                    A[j * ES + p] = c * ajp - sn * ajq;
+                    A[j * ES + q] = sn * ajp + c * ajq;
+                    const double vjp = V[j * ES + p], vjq = V[j * ES + q];
+                    V[j * ES + p] = c * vjp - sn * vjq;
+                    V[j * ES + q] = sn * vjp + c * vjq;
+                }
+                __syncthreads();
+            }
+        }
+    }
+    for (int j = tid; j < E; j += MT) sig[j] = fabs(A[j * ES + j]);
+    __syncthreads();
+    for (int j = tid; j < E; j += MT) {  // descending Sigma, ties by index
+        int rk = 0;
+        for (int k = 0; k < E; k++) rk += (sig[k] > sig[j]) || (sig[k] == sig[j] && k < j);
+        order[rk] = j;
+    }
+    __syncthreads();
+    const int kmax = a.algorithm == PCX_ALG_BIG_FIVE ? a.max_components : E;
+    if (tid == 0) {  // fixed-variance: cumsum(Sigma / trace) >= threshold stops after that component
+        int used = kmax;
+        if (a.algorithm == PCX_ALG_FIXED_VARIANCE) {
+            double ve = 0.0;
+            for (int c = 0; c < kmax; c++) {
+                ve = ve + sig[order[c]] / scal[0];
+                if (ve >= a.variance_threshold) {
+                    used = c + 1;
+                    break;
+                }
+            }
+        }
+        scal[1] = (double)used;
+    }
+    __syncthreads();
+    const int used = (int)scal[1];
+    for (int i = tid; i < N; i += MT) {
+        double acc = 0.0;
+        for (int c = 0; c < used; c++) {
+            const int idx = order[c];
+            const double sg = sig[idx];
+            const double fl = V[idx] < 0.0 ? -1.0 : 1.0;  // loading *= -1 if loading[0] < 0
+            double d = 0.0;
+            for (int j = 0; j < E; j++) d = fma(F[i * E + j] - mu[j], fl * V[j * ES + idx], d);
+            acc = acc + sg * d;
+        }
+        net[i] = acc;
+    }
+    __syncthreads();
+    return a.algorithm == PCX_ALG_FIXED_VARIANCE ? used : -1;
+}
+
 struct MedLds {  // offsets (doubles) into the dynamic LDS
     int M, T, vN, vE, flags;
 };
@@ -379,7 +509,8 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     for (int j = tid; j < E; j += MT) loading[j] = 0.0;
     for (int i = tid; i < N; i += MT) s[i] = nc[i] = 0.0;
     __syncthreads();
-    if (alg == PCX_ALG_PCA) {
+    int comps = -1;
+    if (alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE) {
         // --- a5: weighted mean (np.ma.average, :317-319)
         double* mu = VEp(VE_MU);
         if (tid == 0) scal[4] = mpw([&](int i) { return rep[i]; }, N);
@@ -525,10 +656,16 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         __syncthreads();
         for (int j = tid; j < E; j += MT) loading[j] = x[j] / scal[9];
         __syncthreads();
-        for (int i = tid; i < N; i += MT) {  // scores (:337)
-            double acc = 0.0;
-            for (int j = 0; j < E; j++) acc = fma(F[i * E + j] - mu[j], loading[j], acc);
-            s[i] = acc;
+        if (alg == PCX_ALG_PCA) {
+            for (int i = tid; i < N; i += MT) {  // scores (:337)
+                double acc = 0.0;
+                for (int j = 0; j < E; j++) acc = fma(F[i * E + j] - mu[j], loading[j], acc);
+                s[i] = acc;
+            }
+        } else if (flags & PCX_FLAG_SVD_FAIL) {  // the reference's second svd raises (:375, :431)
+            for (int i = tid; i < N; i += MT) s[i] = __builtin_nan("");
+        } else {
+            comps = component_scores(a, C, M, Tm, ES, F, mu, s, sh, scal);
         }
     } else if (alg == PCX_ALG_COKURTOSIS) {
         for (int i = tid; i < N; i += MT) s[i] = a.aux_scores[b * N + i];
@@ -758,7 +895,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         if (a.branch) a.branch[b] = branch;
         if (a.flags) a.flags[b] = flags;
         if (a.pi_iters) a.pi_iters[b] = iters;
-        if (a.components) a.components[b] = -1;
+        if (a.components) a.components[b] = comps;
     }
 }
 
@@ -766,7 +903,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
 
 bool medium_fits(const BatchArgs& a) {
     return a.N >= 1 && a.N <= MN && a.E >= 1 && a.E <= MEV &&
-           (a.algorithm == PCX_ALG_PCA || a.algorithm == PCX_ALG_ABSOLUTE || a.algorithm == PCX_ALG_COKURTOSIS);
+           a.algorithm >= PCX_ALG_PCA && a.algorithm <= PCX_ALG_COKURTOSIS;
 }
 
 size_t medium_lds_bytes(int N, int E) {

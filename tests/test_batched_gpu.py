@@ -136,9 +136,12 @@ def _rounds_kw(variant, B=40, seed=77):
     if "int" in rest:
         R = np.where(np.isnan(R), 0.0, np.trunc(R))
         kw["int_dtype"] = True
-    for alg in ("big-five", "absolute", "cokurtosis"):
+    for alg in ("big-five", "fixed-variance", "absolute", "cokurtosis"):
         if alg in rest:
             kw["algorithm"] = alg
+    if kw.get("algorithm") in ("big-five", "fixed-variance"):
+        kw["max_components"] = 5
+        kw["variance_threshold"] = 0.75
     if kw.get("algorithm") == "cokurtosis":
         kw["aux_scores"] = np.random.default_rng(9).normal(size=(B, N))
     return R, kw
@@ -153,9 +156,10 @@ def _round_inputs(kw, b):
 
 
 @pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "256x64", "65x33_nobounds", "200x1",
-                                     "120x20_int", "90x36_absolute", "80x40_cokurtosis", "250x60_uniform"])
+                                     "120x20_int", "90x36_absolute", "80x40_cokurtosis", "250x60_uniform",
+                                     "100x50_big-five", "70x40_fixed-variance", "150x7_big-five"])
 def test_medium_rounds_bitexact_vs_spec(gpu_lib, variant):
-    """Rounds above one wavefront up to 256 x 64 (PCA / absolute / cokurtosis): one workgroup per
+    """Rounds above one wavefront up to 256 x 64 (every non-clustering algorithm): one workgroup per
     round (csrc/pcx_medium.hip), bit-identical to the C SPEC built for 256 reporters
     (oracle/pcx_oracle_batched.c, NMAX = 256) on every output, and within the north_star
     tolerances of the numpy restatement of the reference."""
@@ -178,7 +182,8 @@ def test_medium_rounds_bitexact_vs_spec(gpu_lib, variant):
         aux = None if alg != "cokurtosis" else {"cokurt": kw["aux_scores"][b]}
         Rb = R[b].copy()
         ref = G.flat_result(OracleCPU(reports=Rb, event_bounds=None if sc is None else synthetic.bounds_list(sc, lo, hi),
-                                      reputation=rep, algorithm=alg, aux=aux).consensus())
+                                      reputation=rep, algorithm=alg, aux=aux, max_components=5,
+                                      variance_threshold=kw.get("variance_threshold", 0.9)).consensus())
         bad, _ = P.compare(ref, {k: v[b] for k, v in g.items()})
         assert not bad, (b, bad)
 
