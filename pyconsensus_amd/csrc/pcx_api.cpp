@@ -291,8 +291,35 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
             }
             double* Fscr = (double*)ctx->mscr;
             double* Cscr = Fscr + (a.filled ? 0 : (size_t)chunk * a.N * a.E);
+            const char* mst = getenv("PCX_STAMPS");
+            if (mst && mst[0] == '1') {  // diagnostic: per-phase clock breakdown
+                long long* d = nullptr;
+                if (hipMalloc(&d, a.B * 32 * sizeof(long long)) == hipSuccess) {
+                    (void)hipMemsetAsync(d, 0, a.B * 32 * sizeof(long long), ctx->stream);
+                    a.stamps = d;
+                }
+            }
             for (int64_t b0 = 0; b0 < a.B && e == hipSuccess; b0 += chunk)
                 e = pcx::launch_medium(a, b0, std::min<int64_t>(chunk, a.B - b0), Fscr, Cscr, ctx->stream);
+            if (a.stamps) {  // stamps 0..15 in program order (pcx_medium.hip MSTAMP(k))
+                std::vector<long long> h(a.B * 32);
+                (void)hipMemcpyAsync(h.data(), a.stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost,
+                                     ctx->stream);
+                (void)hipStreamSynchronize(ctx->stream);
+                (void)hipFree(a.stamps);
+                double acc[16] = {0};
+                for (int64_t b = 0; b < a.B; b++)
+                    for (int k = 1, prev = 0; k < 16; k++) {
+                        const long long t1 = h[b * 32 + k], t0 = h[b * 32 + prev];
+                        if (t1 && t0) {
+                            acc[k] += (double)(t1 - t0);
+                            prev = k;
+                        }
+                    }
+                fprintf(stderr, "PCX_STAMPS medium mean cycles per phase:");
+                for (int k = 1; k < 16; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / (double)a.B);
+                fprintf(stderr, "\n");
+            }
             return e == hipSuccess ? PCX_OK : hip_fail(e, "medium_round_kernel launch");
         }
         // one single-matrix consensus per round, many rounds in flight (pcx_rounds.cpp)

@@ -400,6 +400,15 @@ enum { VN_REP = 0, VN_TOK, VN_S, VN_SET1, VN_SET2, VN_NW1, VN_NW2, VN_U, VN_THIS
 enum { VE_MU = 0, VE_OLD, VE_LD, VE_X, VE_Y, VE_SQ, VE_D1, VE_D2, VE_NEW1, VE_NEW2, VE_R0, VE_R1, VE_R2, VE_E1, VE_E2,
        VE_RAW, VE_ADJ, VE_FIN, VE_CERT, VE_REWARD, VE_PC, VE_RELC, VE_COUNT };
 
+// diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
+#define MSTAMP(k)                                                                 \
+    do {                                                                          \
+        if (a.stamps) {                                                           \
+            const long long t_ = (long long)__builtin_amdgcn_s_memtime();         \
+            if (threadIdx.x == 0) a.stamps[b * 32 + (k)] = t_;                    \
+        }                                                                         \
+    } while (0)
+
 __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b0, double* Fscr, double* Cscr) {
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     __shared__ double sh[MT];
@@ -423,6 +432,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     const bool has_bounds = a.scaled != nullptr;
     auto scaled = [&](int j) { return has_bounds && a.scaled[bo + j] != 0; };
     const int alg = a.algorithm;
+    MSTAMP(0);
 
     // --- a1: reputation (:138-146)
     if (tid == 0) scal[0] = a.reputation ? mpw([&](int i) { return a.reputation[b * N + i]; }, N) : 0.0;
@@ -451,6 +461,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         if (a.original) a.original[b * N * E + e] = x;
     }
     __syncthreads();
+    MSTAMP(1);
     // --- a3: interpolate (:284-313): binary columns one thread each; scaled columns one at a
     // time with the whole block (weighted median)
     double* XA = VNp(VN_XA);
@@ -473,6 +484,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         for (int i = 0; i < N; i++)
             if (fl[i * E + j]) F[i * E + j] = g;
     }
+    MSTAMP(2);
     __shared__ int wcnt[MT / 64];
     for (int j = 0; j < E; j++) {
         if (!scaled(j)) continue;
@@ -499,6 +511,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         __syncthreads();
     }
     __syncthreads();
+    MSTAMP(3);
     // old = np.dot(rep, F) (:489)
     for (int j = tid; j < E; j += MT)
         VEp(VE_OLD)[j] = mob_vecmat([&](int i) { return rep[i]; }, [&](int i) { return F[i * E + j]; }, N, E, j);
@@ -509,6 +522,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     for (int j = tid; j < E; j += MT) loading[j] = 0.0;
     for (int i = tid; i < N; i += MT) s[i] = nc[i] = 0.0;
     __syncthreads();
+    MSTAMP(4);
     int comps = -1;
     if (alg == PCX_ALG_PCA || alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE) {
         // --- a5: weighted mean (np.ma.average, :317-319)
@@ -526,6 +540,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             mu[j] = acc / scal[4];
         }
         __syncthreads();
+        MSTAMP(5);
         // --- a6: covariance (:326), lower triangle mirrored
         const double denom = scal[1];
         for (int e = tid; e < E * E; e += MT) {
@@ -538,6 +553,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             C[k * E + j] = c;
         }
         __syncthreads();
+        MSTAMP(6);
         // --- a7: power iteration (SPEC power_iter)
         int finite = 1, nonzero = 0;
         for (int e = tid; e < E * E; e += MT) {
@@ -656,6 +672,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         __syncthreads();
         for (int j = tid; j < E; j += MT) loading[j] = x[j] / scal[9];
         __syncthreads();
+        MSTAMP(7);
         if (alg == PCX_ALG_PCA) {
             for (int i = tid; i < N; i += MT) {  // scores (:337)
                 double acc = 0.0;
@@ -671,6 +688,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         for (int i = tid; i < N; i += MT) s[i] = a.aux_scores[b * N + i];
     }
     __syncthreads();
+    MSTAMP(8);
     if (alg != PCX_ALG_ABSOLUTE) {
         // --- a8/a9: nonconformity_rank (:487-500), tie -> nonconformity (:475-485)
         double* set1 = VNp(VN_SET1);
@@ -763,6 +781,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         for (int i = tid; i < N; i += MT) nc[i] = pick1 ? set1[i] : set2[i];
     }
     __syncthreads();
+    MSTAMP(9);
     // --- a10: reputation update (:460-472)
     double* thisr = VNp(VN_THIS);
     double* smooth = VNp(VN_SMOOTH);
@@ -782,6 +801,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         smooth[i] = a.alpha * t + (1.0 - a.alpha) * rep[i];
     }
     __syncthreads();
+    MSTAMP(10);
     // --- a12/a13: outcomes (:510-538)
     double* raw = VEp(VE_RAW);
     double* adj = VEp(VE_ADJ);
@@ -794,6 +814,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         }
     }
     __syncthreads();
+    MSTAMP(11);
     for (int j = 0; j < E; j++) {
         if (!scaled(j)) continue;
         for (int i = tid; i < N; i += MT) XA[i] = F[i * E + j];
@@ -808,6 +829,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         }
         __syncthreads();
     }
+    MSTAMP(12);
     // --- a14: certainty (:540-546): sum of smooth over the matching rows (pairwise), per event
     double* cert = VEp(VE_CERT);
     for (int j = 0; j < E; j++) {  // the matching rows' weights in row order (block compaction)
@@ -817,6 +839,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             cert[j] = m ? mpw([&](int q) { return XA[q]; }, m) : (alg == PCX_ALG_PCA ? __builtin_nan("") : 0.0);
         __syncthreads();
     }
+    MSTAMP(13);
     double* reward = VEp(VE_REWARD);
     double* pc = VEp(VE_PC);
     double* relc = VEp(VE_RELC);
@@ -834,6 +857,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         if (a.nas_filled) a.nas_filled[b * E + j] = (double)nz;
     }
     __syncthreads();
+    MSTAMP(14);
     double* pr = VNp(VN_SET1);  // reuse
     double* narow = VNp(VN_SET2);
     double* rel = VNp(VN_NW1);
@@ -889,6 +913,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         if (a.participation_columns) a.participation_columns[o] = pc[j];
         if (a.author_bonus) a.author_bonus[o] = relc[j] * pna + reward[j] * (1.0 - pna);
     }
+    MSTAMP(15);
     if (tid == 0) {
         if (a.participation) a.participation[b] = 1.0 - pna;
         if (a.avg_certainty) a.avg_certainty[b] = scal[7];
