@@ -318,7 +318,11 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
                     }
                 fprintf(stderr, "PCX_STAMPS medium mean cycles per phase:");
                 for (int k = 1; k < 16; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / (double)a.B);
-                fprintf(stderr, "\n");
+                double mp[3] = {0, 0, 0};  // wave 0's outcome medians: total+dom, rank, walk
+                for (int64_t b = 0; b < a.B; b++)
+                    for (int k = 0; k < 3; k++) mp[k] += (double)h[b * 32 + 20 + k];
+                fprintf(stderr, " wave0 medians total:%.0f rank:%.0f walk:%.0f\n", mp[0] / (double)a.B,
+                        mp[1] / (double)a.B, mp[2] / (double)a.B);
             }
             return e == hipSuccess ? PCX_OK : hip_fail(e, "medium_round_kernel launch");
         }

@@ -75,24 +75,11 @@ __device__ double wtree64(G g, int n) {
     return (v + t16) + (t32 + t48);
 }
 
-// block compaction: rows with pred(i) in row order -> out[0..m) = val(i); returns m (all threads)
-template <class P, class V>
-__device__ int bcompact(P pred, V val, int n, double* out, int* wcnt) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int base = 0;
-    for (int i0 = 0; i0 < n; i0 += MT) {
-        const int i = i0 + (int)threadIdx.x;
-        const bool p = i < n && pred(i);
-        const unsigned long long bal = __ballot(p);
-        if (lane == 0) wcnt[w] = __popcll(bal);
-        __syncthreads();
-        int off = base;
-        for (int k = 0; k < w; k++) off += wcnt[k];
-        if (p) out[off + __popcll(bal & ((1ull << lane) - 1ull))] = val(i);
-        for (int k = 0; k < MT / 64; k++) base += wcnt[k];
-        __syncthreads();
-    }
-    return base;
+// the same tree64 on a register value per lane (0 beyond n); valid on lane 0
+__device__ double wtree64v(double v) {
+    for (int s = 1; s <= 8; s <<= 1) v = v + __shfl_xor(v, s, 64);
+    const double t16 = __shfl(v, 16, 64), t32 = __shfl(v, 32, 64), t48 = __shfl(v, 48, 64);
+    return (v + t16) + (t32 + t48);
 }
 
 // SPEC dot2 (compensated dot, index order)
@@ -169,33 +156,74 @@ __device__ __forceinline__ double mcatch(double x, double tol) {
 }
 
 // block reductions (max of doubles / first index)
+// (max-norms of non-negative values: exact in any order)
 __device__ double bmax(double v, double* sh) {
-    sh[threadIdx.x] = v;
+    for (int s = 1; s < 64; s <<= 1) v = fmax(v, __shfl_xor(v, s, 64));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int s = MT / 2; s >= 1; s >>= 1) {
-        if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
-        __syncthreads();
-    }
-    const double r = sh[0];
+    double r = sh[0];
+    for (int w = 1; w < MT / 64; w++) r = fmax(r, sh[w]);
     __syncthreads();
     return r;
 }
 
-// weightedstats.weighted_median of n <= 256 (x, w) pairs in LDS (SPEC wmedian), the whole
-// block cooperating on the stable (x, w) ranks; the result on every thread
-__device__ double mwmedian(const double* x, const double* w, int n, double* xs, double* ws, double* sh) {
-    __shared__ double res_s;
-    if (threadIdx.x == 0) {
-        double W = 0.0;
-        for (int i = 0; i < n; i++) W += w[i];
-        const double mid = 0.5 * W;
-        int dom = 0, pos = 0;
-        for (int i = 0; i < n; i++) {
-            dom |= w[i] > mid;
-            pos |= w[i] > 0;
-        }
-        double r = __builtin_nan("");
-        if (dom) {
+// one wave's LDS writes visible to its other lanes (LDS operations of a wave execute in issue
+// order: a compiler-ordering wave barrier, no lgkmcnt drain)
+__device__ __forceinline__ void mwsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// broadcast from a wave-uniform lane (v_readlane into SGPRs)
+__device__ __forceinline__ double mbcast(double v, int src) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// sequential sum g(0) + g(1) + ... in index order (Python's builtin sum), the loads issued
+// eight at a time ahead of the dependent adds
+template <class G>
+__device__ double mseq(G g, int n) {
+    double s = 0.0;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = g(i + q);
+#pragma unroll
+        for (int q = 0; q < 8; q++) s += v[q];
+    }
+    for (; i < n; i++) s += g(i);
+    return s;
+}
+
+// weightedstats.weighted_median (SPEC wmedian) of n <= 256 (x, w) pairs in LDS on ONE wave:
+// lane 0's sequential total and walk (loads batched by eight), the stable (x, w) order by a
+// bitonic network over the lanes in LDS (the SPEC's rank placement when a NaN is present); sb is
+// this wave's sort scratch of PN doubles x, PN doubles w and PN ints (PN = pow2 >= n); the result
+// on every lane of the wave
+__device__ double wv_wmedian(const double* x, const double* w, int n, double* sb, int PN,
+                             long long* prof = nullptr) {
+    const int lane = threadIdx.x & 63;
+    double* xs = sb;
+    double* ws = sb + PN;
+    long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    double W = 0.0;
+    if (lane == 0) W = mseq([&](int i) { return w[i]; }, n);
+    const double mid = 0.5 * mbcast(W, 0);
+    bool dom = false, pos = false, nan_ = false;
+    for (int i = lane; i < n; i += 64) {
+        dom |= w[i] > mid;
+        pos |= w[i] > 0;
+        nan_ |= __builtin_isnan(x[i]) || __builtin_isnan(w[i]);
+    }
+    const bool anydom = __ballot(dom) != 0, anypos = __ballot(pos) != 0;
+    double r = __builtin_nan("");
+    if (anydom) {
+        if (lane == 0) {
             double m = w[0];
             for (int i = 1; i < n; i++)
                 if (w[i] > m) m = w[i];
@@ -204,32 +232,99 @@ __device__ double mwmedian(const double* x, const double* w, int n, double* xs, 
                     r = x[i];
                     break;
                 }
-            sh[0] = 1.0;  // decided
-        } else {
-            sh[0] = pos ? 0.0 : 1.0;
         }
-        sh[1] = mid;
-        res_s = r;
+        return mbcast(r, 0);
     }
-    __syncthreads();
-    const bool decided = sh[0] != 0.0;
-    const double mid = sh[1];
-    __syncthreads();
-    if (decided) return res_s;
-    for (int i = threadIdx.x; i < n; i += MT) {  // stable rank by (x, w)
-        int r = 0;
-        const double xi = x[i], wi = w[i];
-        for (int m = 0; m < n; m++) {
-            const bool lt = (x[m] < xi) || (x[m] == xi && w[m] < wi);
-            const bool eq = (x[m] == xi) && (w[m] == wi);
-            r += (lt || (eq && m < i)) ? 1 : 0;
+    if (!anypos) return r;
+    if (prof) {
+        const long long t = (long long)__builtin_amdgcn_s_memtime();
+        prof[0] += t - t0;
+        t0 = t;
+    }
+    if (__ballot(nan_) == 0) {
+        // the stable (x, w) order is the ascending order of (x, w, index) (x, w compared with
+        // < and ==): a bitonic network over P = pow2 >= n slots in LDS, padding slots last
+        int* id = (int*)(sb + 2 * PN);
+        int P = 2;
+        while (P < n) P <<= 1;
+        for (int i = lane; i < P; i += 64) {
+            const bool v = i < n;
+            xs[i] = v ? x[i] : 0.0;
+            ws[i] = v ? w[i] : 0.0;
+            id[i] = v ? i : -1;
         }
-        xs[r] = xi;
-        ws[r] = wi;
+        mwsync();
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = lane; t < (P >> 1); t += 64) {
+                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i + j;
+                    const int ia = id[i], il = id[l];
+                    const double xa = xs[i], wa = ws[i], xl = xs[l], wl = ws[l];
+                    bool gt;  // (x, w, id) at i after the one at l; padding after everything
+                    if (ia < 0 || il < 0)
+                        gt = ia < 0 && il >= 0;
+                    else
+                        gt = (xl < xa) || (xl == xa && (wl < wa || (wl == wa && il < ia)));
+                    if (gt == ((i & k) == 0)) {
+                        xs[i] = xl;
+                        xs[l] = xa;
+                        ws[i] = wl;
+                        ws[l] = wa;
+                        id[i] = il;
+                        id[l] = ia;
+                    }
+                }
+                mwsync();
+            }
+    } else {
+        // stable rank by (x, w) as the SPEC places it: this lane's elements i = lane + 64 q in
+        // registers, the compared elements m read eight at a time (LDS broadcasts)
+        const int nq = (n + 63) >> 6;
+        double xi[4], wi[4];
+        int rk[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = lane + 64 * q;
+            xi[q] = i < n ? x[i] : 0.0;
+            wi[q] = i < n ? w[i] : 0.0;
+            rk[q] = 0;
+        }
+        auto cmp = [&](double xm, double wm, int m) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (q >= nq) break;  // wave-uniform
+                const bool lt = (xm < xi[q]) || (xm == xi[q] && wm < wi[q]);
+                const bool eq = (xm == xi[q]) && (wm == wi[q]);
+                rk[q] += (lt || (eq && m < lane + 64 * q)) ? 1 : 0;
+            }
+        };
+        int m0 = 0;
+        for (; m0 + 8 <= n; m0 += 8) {
+            double xm[8], wm[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                xm[t] = x[m0 + t];
+                wm[t] = w[m0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) cmp(xm[t], wm[t], m0 + t);
+        }
+        for (; m0 < n; m0++) cmp(x[m0], w[m0], m0);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (lane + 64 * q < n) {
+                xs[rk[q]] = xi[q];
+                ws[rk[q]] = wi[q];
+            }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double cum = 0.0, r;
+    mwsync();
+    if (prof) {
+        const long long t = (long long)__builtin_amdgcn_s_memtime();
+        prof[1] += t - t0;
+        t0 = t;
+    }
+    if (lane == 0) {
+        double cum = 0.0;
         int k = 0;
         bool fail = false;
         while (cum <= mid) {
@@ -237,26 +332,30 @@ __device__ double mwmedian(const double* x, const double* w, int n, double* xs, 
                 fail = true;
                 break;
             }
-            cum += ws[k];
-            k++;
+            const int lim = n - k < 8 ? n - k : 8;
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) v[q] = q < lim ? ws[k + q] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; q++)  // static indices: v stays in registers
+                if (q < lim && cum <= mid) {
+                    cum += v[q];
+                    k++;
+                }
         }
-        if (fail) {
-            r = __builtin_nan("");
-        } else {
+        if (!fail) {
             const double before = cum - ws[k - 1];
             if (fabs(before - mid) < M_DBL_EPS) {
                 if (k >= 2) r = (xs[k - 2] + xs[k - 1]) / 2.0;
                 else if (n == 1) r = xs[0] / 1.0;
-                else r = __builtin_nan("");
             } else {
                 r = xs[k - 1];
             }
         }
-        res_s = r;
     }
-    __syncthreads();
-    const double r = res_s;
-    __syncthreads();
+    r = mbcast(r, 0);
+    mwsync();  // xs / ws free for the wave's next use
+    if (prof) prof[2] += (long long)__builtin_amdgcn_s_memtime() - t0;
     return r;
 }
 
@@ -393,12 +492,26 @@ struct MedLds {  // offsets (doubles) into the dynamic LDS
     int M, T, vN, vE, flags;
 };
 
-// N-vectors (each N doubles): REP, TOK, S, SET1, SET2, NW1, NW2, U, THIS, SMOOTH, XA, WA, XS, WS
-enum { VN_REP = 0, VN_TOK, VN_S, VN_SET1, VN_SET2, VN_NW1, VN_NW2, VN_U, VN_THIS, VN_SMOOTH, VN_XA, VN_WA, VN_XS,
-       VN_WS, VN_COUNT };
+// N-vectors (each N doubles)
+enum { VN_REP = 0, VN_TOK, VN_S, VN_SET1, VN_SET2, VN_NW1, VN_NW2, VN_U, VN_THIS, VN_SMOOTH, VN_XS, VN_COUNT };
 // E-vectors (each E doubles)
 enum { VE_MU = 0, VE_OLD, VE_LD, VE_X, VE_Y, VE_SQ, VE_D1, VE_D2, VE_NEW1, VE_NEW2, VE_R0, VE_R1, VE_R2, VE_E1, VE_E2,
        VE_RAW, VE_ADJ, VE_FIN, VE_CERT, VE_REWARD, VE_PC, VE_RELC, VE_COUNT };
+// doubles of the work region: M and Tm (E x (E+1) each), or per wave two N-vectors (median
+// operands) and the sort scratch (PN doubles x, PN doubles w, PN ints; PN = pow2 >= N)
+__host__ __device__ __forceinline__ int medium_pow2(int N) {
+    int p = 2;
+    while (p < N) p <<= 1;
+    return p;
+}
+__host__ __device__ __forceinline__ int medium_wave_stride(int N) {
+    const int pn = medium_pow2(N);
+    return 2 * N + 2 * pn + pn / 2;
+}
+__host__ __device__ __forceinline__ int medium_work(int N, int E) {
+    const int mt = 2 * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N);
+    return mt > wq ? mt : wq;
+}
 
 // diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
 #define MSTAMP(k)                                                                 \
@@ -418,7 +531,9 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     const int tid = threadIdx.x;
     double* M = mlds;
     double* Tm = M + E * ES;
-    double* vN = Tm + E * ES;
+    // work region: M and Tm in the power iteration / Jacobi, per wave the median operands and
+    // sort scratch in the interpolation, the outcomes and the certainty
+    double* vN = mlds + medium_work(N, E);
     double* vE = vN + VN_COUNT * N;
     uint8_t* fl = (uint8_t*)(vE + VE_COUNT * E);  // [N][E] bit 0 NaN, bit 1 zero
     auto VNp = [&](int k) { return vN + k * N; };
@@ -430,9 +545,24 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     double* C = Cscr + (int64_t)blockIdx.x * E * E;
     const int64_t bo = a.bounds_shared ? 0 : b * E;
     const bool has_bounds = a.scaled != nullptr;
-    auto scaled = [&](int j) { return has_bounds && a.scaled[bo + j] != 0; };
     const int alg = a.algorithm;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int PN = medium_pow2(N);
+    double* wb = mlds + wv * medium_wave_stride(N);  // this wave's median operands and sort scratch
+    __shared__ unsigned long long scmask_s;
+    __shared__ int scl[MEV], nscl_s;
     MSTAMP(0);
+    if (tid < 64) {  // the scaled events: a mask and their list in index order
+        const bool p = has_bounds && tid < E && a.scaled[bo + tid] != 0;
+        const unsigned long long bal = __ballot(p);
+        if (p) scl[__popcll(bal & ((1ull << tid) - 1ull))] = tid;
+        if (tid == 0) {
+            scmask_s = bal;
+            nscl_s = __popcll(bal);
+        }
+    }
+    auto scaled = [&](int j) { return ((scmask_s >> j) & 1ull) != 0; };
+    long long mprof[3] = {0, 0, 0};  // diagnostic (PCX_STAMPS): median total+dom / rank / walk cycles
 
     // --- a1: reputation (:138-146)
     if (tid == 0) scal[0] = a.reputation ? mpw([&](int i) { return a.reputation[b * N + i]; }, N) : 0.0;
@@ -443,11 +573,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         tok[i] = trunc(r * 1e6);
     }
     __syncthreads();
-    if (tid == 0) {
-        double st = 0.0;
-        for (int i = 0; i < N; i++) st += tok[i];
-        scal[1] = st - 1.0;  // denom
-    }
+    if (tid == 0) scal[1] = mseq([&](int i) { return tok[i]; }, N) - 1.0;  // denom
     // --- a2: rescale (:266-269), NA (:278)
     for (int e = tid; e < N * E; e += MT) {
         const int j = e % E;
@@ -464,20 +590,47 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     MSTAMP(1);
     // --- a3: interpolate (:284-313): binary columns one thread each; scaled columns one at a
     // time with the whole block (weighted median)
-    double* XA = VNp(VN_XA);
-    double* WA = VNp(VN_WA);
     for (int j = tid; j < E; j += MT) {
         if (scaled(j)) continue;
+        // sequential sums in row order, the loads issued eight rows ahead
         int nmiss = 0;
         double tot = 0.0;
-        for (int i = 0; i < N; i++) {
+        int i = 0;
+        for (; i + 8 <= N; i += 8) {
+            uint8_t f[8];
+            double r[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                f[q] = fl[(i + q) * E + j];
+                r[q] = rep[i + q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                nmiss += f[q] ? 1 : 0;
+                if (!f[q]) tot += r[q];
+            }
+        }
+        for (; i < N; i++) {
             const bool m = fl[i * E + j] != 0;
             nmiss += m ? 1 : 0;
             if (!m) tot += rep[i];
         }
         if (!nmiss) continue;
         double g = 0.0;
-        for (int i = 0; i < N; i++)
+        for (i = 0; i + 8 <= N; i += 8) {
+            uint8_t f[8];
+            double r[8], x[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                f[q] = fl[(i + q) * E + j];
+                r[q] = rep[i + q];
+                x[q] = F[(i + q) * E + j];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (!f[q]) g += (r[q] / tot) * x[q];
+        }
+        for (; i < N; i++)
             if (!fl[i * E + j]) g += (rep[i] / tot) * F[i * E + j];
         g = mcatch(g, a.catch_tol);
         if (a.int_dtype) g = trunc(g);
@@ -485,30 +638,36 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             if (fl[i * E + j]) F[i * E + j] = g;
     }
     MSTAMP(2);
-    __shared__ int wcnt[MT / 64];
-    for (int j = 0; j < E; j++) {
-        if (!scaled(j)) continue;
-        // present values and their reputations in row order (block compaction), then the
-        // sequential present total on one thread and the weights rep / total
-        const int np_ = bcompact([&](int i) { return fl[i * E + j] == 0; }, [&](int i) { return F[i * E + j]; }, N, XA,
-                                 wcnt);
-        bcompact([&](int i) { return fl[i * E + j] == 0; }, [&](int i) { return rep[i]; }, N, WA, wcnt);
-        if (tid == 0) {
-            double tot = 0.0;
-            for (int q = 0; q < np_; q++) tot += WA[q];
-            scal[2] = tot;
+    const int nscl = nscl_s;
+    for (int c = wv; c < nscl; c += MT / 64) {  // one wave per scaled column
+        const int j = scl[c];
+        // present values and their reputations in row order (wave compaction), then the
+        // sequential present total on lane 0 and the weights rep / total
+        int np_ = 0;
+        for (int i0 = 0; i0 < N; i0 += 64) {
+            const int i = i0 + lane;
+            const bool p = i < N && fl[i * E + j] == 0;
+            const unsigned long long bal = __ballot(p);
+            if (p) {
+                const int o = np_ + __popcll(bal & ((1ull << lane) - 1ull));
+                wb[o] = F[i * E + j];
+                wb[N + o] = rep[i];
+            }
+            np_ += __popcll(bal);
         }
-        __syncthreads();
-        for (int q = tid; q < np_; q += MT) WA[q] = WA[q] / scal[2];
-        __syncthreads();
-        const int nmiss = N - np_;
-        if (nmiss) {  // block-uniform
-            double g = mwmedian(XA, WA, np_, VNp(VN_XS), VNp(VN_WS), sh);
+        mwsync();
+        double tot = 0.0;
+        if (lane == 0) tot = mseq([&](int q) { return wb[N + q]; }, np_);
+        tot = mbcast(tot, 0);
+        for (int q = lane; q < np_; q += 64) wb[N + q] = wb[N + q] / tot;
+        mwsync();
+        if (np_ < N) {  // wave-uniform
+            double g = wv_wmedian(wb, wb + N, np_, wb + 2 * N, PN);
             if (a.int_dtype) g = trunc(g);
-            for (int i = tid; i < N; i += MT)
+            for (int i = lane; i < N; i += 64)
                 if (fl[i * E + j]) F[i * E + j] = g;
         }
-        __syncthreads();
+        mwsync();
     }
     __syncthreads();
     MSTAMP(3);
@@ -541,16 +700,63 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         }
         __syncthreads();
         MSTAMP(5);
-        // --- a6: covariance (:326), lower triangle mirrored
-        const double denom = scal[1];
-        for (int e = tid; e < E * E; e += MT) {
-            const int j = e / E, k = e % E;
-            if (k > j) continue;
-            double acc = 0.0;
-            for (int i = 0; i < N; i++) acc = fma((F[i * E + j] - mu[j]) * tok[i], F[i * E + k] - mu[k], acc);
-            const double c = acc / denom;
-            C[j * E + k] = c;
-            C[k * E + j] = c;
+        // --- a6: covariance (:326), lower triangle mirrored: one 4 x 4 tile (J >= K) per thread,
+        // rows staged through the work region in chunks (A = (F - mu) * tok, D = F - mu), each
+        // entry's fma chain in row order
+        {
+            const double denom = scal[1];
+            const int nT = (E + 3) >> 2, ntiles = nT * (nT + 1) / 2;
+            int tJ = 0, tK = tid;
+            while (tK > tJ) {
+                tK -= tJ + 1;
+                tJ++;
+            }
+            double acc[4][4];
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc[p][q] = 0.0;
+            int CR = medium_work(N, E) / (2 * E);
+            CR = CR > 32 ? 32 : CR;
+            double* Al = mlds;
+            double* Dl = mlds + CR * E;
+            for (int c0 = 0; c0 < N; c0 += CR) {
+                const int cr = N - c0 < CR ? N - c0 : CR;
+                for (int idx = tid; idx < cr * E; idx += MT) {
+                    const int i = c0 + idx / E, j = idx % E;
+                    const double d = F[i * E + j] - mu[j];
+                    Dl[idx] = d;
+                    Al[idx] = d * tok[i];
+                }
+                __syncthreads();
+                if (tid < ntiles)
+                    for (int r = 0; r < cr; r++) {
+                        double av[4], dv[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int j = 4 * tJ + q, k = 4 * tK + q;
+                            av[q] = j < E ? Al[r * E + j] : 0.0;
+                            dv[q] = k < E ? Dl[r * E + k] : 0.0;
+                        }
+#pragma unroll
+                        for (int p = 0; p < 4; p++)
+#pragma unroll
+                            for (int q = 0; q < 4; q++) acc[p][q] = fma(av[p], dv[q], acc[p][q]);
+                    }
+                __syncthreads();
+            }
+            if (tid < ntiles)
+#pragma unroll
+                for (int p = 0; p < 4; p++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int j = 4 * tJ + p, k = 4 * tK + q;
+                        if (j < E && k <= j) {
+                            const double c = acc[p][q] / denom;
+                            C[j * E + k] = c;
+                            C[k * E + j] = c;
+                        }
+                    }
         }
         __syncthreads();
         MSTAMP(6);
@@ -563,7 +769,6 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         finite = __syncthreads_and(finite);
         nonzero = __syncthreads_or(nonzero);
         double* x = VEp(VE_X);
-        double* y = VEp(VE_Y);
         if (!finite) {
             for (int j = tid; j < E; j += MT) x[j] = 1.0;
             flags |= PCX_FLAG_SVD_FAIL;
@@ -608,50 +813,68 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                 }
                 __syncthreads();
             };
-            // y = A x / ||A x|| (tree64 norm), A = M (stride ES) or C (stride E)
-            auto matvec_unit = [&](const double* A, int lda) {
-                for (int j = tid; j < E; j += MT) {
-                    double acc = 0.0;
-                    for (int k = 0; k < E; k++) acc = fma(A[j * lda + k], x[k], acc);
-                    y[j] = acc;
-                }
-                __syncthreads();
-                if (tid < 64) {
-                    const double t = sqrt(wtree64([&](int j) { return y[j] * y[j]; }, E));
-                    if (tid == 0) scal[7] = t;
-                }
-                __syncthreads();
-                for (int j = tid; j < E; j += MT) y[j] = y[j] / scal[7];
-                __syncthreads();
-            };
             int sqn = 0;
             for (; sqn < M_PI_PRESQUARE; sqn++) square();
+            // the power steps between squarings and the polish on wave 0: lane j = row j, x in
+            // registers (x_k broadcast by readlane), tree64 norm and max-norm by shuffles
+            __shared__ int pi_s[3];
+            auto step = [&](const double* A, int lda, double xr) {  // (A x) / ||A x||
+                const int row = lane < E ? lane : 0;
+                double acc = 0.0;
+                for (int k = 0; k < E; k++) acc = fma(A[row * lda + k], mbcast(xr, k), acc);
+                const double yv = lane < E ? acc : 0.0;
+                const double t = mbcast(sqrt(wtree64v(yv * yv)), 0);
+                return yv / t;
+            };
             int since = 0;
             for (;;) {
-                matvec_unit(M, ES);
-                double ld = 0.0;
-                for (int j = tid; j < E; j += MT) ld = fmax(ld, fabs(y[j] - x[j]));
-                const double d = bmax(ld, sh);
-                for (int j = tid; j < E; j += MT) x[j] = y[j];
+                if (wv == 0) {
+                    double xr = lane < E ? x[lane] : 0.0;
+                    int it = iters, sn = since, st = 0;
+                    for (;;) {
+                        const double yn = step(M, ES, xr);
+                        double dl = lane < E ? fabs(yn - xr) : 0.0;
+                        for (int s2 = 1; s2 < 64; s2 <<= 1) dl = fmax(dl, __shfl_xor(dl, s2, 64));
+                        xr = yn;
+                        it++;
+                        sn++;
+                        if (dl <= M_PI_TOL) {
+                            st = 1;
+                            break;
+                        }
+                        if (it >= M_PI_MAXIT) {
+                            st = 2;
+                            break;
+                        }
+                        if (sn >= M_PI_SQUARE_EVERY && sqn < M_PI_MAX_SQUARINGS) break;
+                    }
+                    if (lane < E) x[lane] = xr;
+                    if (lane == 0) {
+                        pi_s[0] = st;
+                        pi_s[1] = it;
+                        pi_s[2] = sn;
+                    }
+                }
                 __syncthreads();
-                iters++;
-                since++;
-                if (d <= M_PI_TOL) break;
-                if (iters >= M_PI_MAXIT) {
+                const int st = pi_s[0];
+                iters = pi_s[1];
+                since = pi_s[2];
+                __syncthreads();
+                if (st == 1) break;
+                if (st == 2) {
                     flags |= PCX_FLAG_PI_MAXIT;
                     break;
                 }
-                if (since >= M_PI_SQUARE_EVERY && sqn < M_PI_MAX_SQUARINGS) {
-                    square();
-                    sqn++;
-                    since = 0;
-                }
+                square();
+                sqn++;
+                since = 0;
             }
-            for (int p = 0; p < M_PI_POLISH; p++) {
-                matvec_unit(C, E);
-                for (int j = tid; j < E; j += MT) x[j] = y[j];
-                __syncthreads();
+            if (wv == 0) {
+                double xr = lane < E ? x[lane] : 0.0;
+                for (int p = 0; p < M_PI_POLISH; p++) xr = step(C, E, xr);
+                if (lane < E) x[lane] = xr;
             }
+            __syncthreads();
             iters += M_PI_POLISH + sqn;  // SPEC: steps + polish + squarings
             if (tid == 0) {  // SPEC sign rule
                 int f = -1, nnz = 0;
@@ -815,30 +1038,39 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     }
     __syncthreads();
     MSTAMP(11);
-    for (int j = 0; j < E; j++) {
-        if (!scaled(j)) continue;
-        for (int i = tid; i < N; i += MT) XA[i] = F[i * E + j];
-        __syncthreads();
-        const double r = mwmedian(XA, smooth, N, VNp(VN_XS), VNp(VN_WS), sh);
-        if (tid == 0) {
+    for (int c = wv; c < nscl; c += MT / 64) {  // one wave per scaled column
+        const int j = scl[c];
+        for (int i = lane; i < N; i += 64) wb[i] = F[i * E + j];
+        mwsync();
+        const double r = wv_wmedian(wb, smooth, N, wb + 2 * N, PN, a.stamps ? mprof : nullptr);
+        if (lane == 0) {
             raw[j] = r;
             adj[j] = r;
             double f = r * (a.hi[bo + j] - a.lo[bo + j]);
             f = f + a.lo[bo + j];
             fin[j] = f;
         }
-        __syncthreads();
     }
+    __syncthreads();
     MSTAMP(12);
     // --- a14: certainty (:540-546): sum of smooth over the matching rows (pairwise), per event
     double* cert = VEp(VE_CERT);
-    for (int j = 0; j < E; j++) {  // the matching rows' weights in row order (block compaction)
+    for (int j = wv; j < E; j += MT / 64) {  // one wave per event: the matching rows' weights in row order
         const double aj = adj[j];
-        const int m = bcompact([&](int i) { return F[i * E + j] == aj; }, [&](int i) { return smooth[i]; }, N, XA, wcnt);
-        if (tid == 0)
-            cert[j] = m ? mpw([&](int q) { return XA[q]; }, m) : (alg == PCX_ALG_PCA ? __builtin_nan("") : 0.0);
-        __syncthreads();
+        int m = 0;
+        for (int i0 = 0; i0 < N; i0 += 64) {
+            const int i = i0 + lane;
+            const bool p = i < N && F[i * E + j] == aj;
+            const unsigned long long bal = __ballot(p);
+            if (p) wb[m + __popcll(bal & ((1ull << lane) - 1ull))] = smooth[i];
+            m += __popcll(bal);
+        }
+        mwsync();
+        if (lane == 0)
+            cert[j] = m ? mpw([&](int q) { return wb[q]; }, m) : (alg == PCX_ALG_PCA ? __builtin_nan("") : 0.0);
+        mwsync();
     }
+    __syncthreads();
     MSTAMP(13);
     double* reward = VEp(VE_REWARD);
     double* pc = VEp(VE_PC);
@@ -914,6 +1146,8 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         if (a.author_bonus) a.author_bonus[o] = relc[j] * pna + reward[j] * (1.0 - pna);
     }
     MSTAMP(15);
+    if (a.stamps && tid == 0)
+        for (int k = 0; k < 3; k++) a.stamps[b * 32 + 20 + k] = mprof[k];
     if (tid == 0) {
         if (a.participation) a.participation[b] = 1.0 - pna;
         if (a.avg_certainty) a.avg_certainty[b] = scal[7];
@@ -932,8 +1166,8 @@ bool medium_fits(const BatchArgs& a) {
 }
 
 size_t medium_lds_bytes(int N, int E) {
-    const size_t ES = (size_t)E + 1;
-    return (2 * E * ES + (size_t)VN_COUNT * N + (size_t)VE_COUNT * E) * sizeof(double) + (size_t)N * E + 16;
+    return ((size_t)medium_work(N, E) + (size_t)VN_COUNT * N + (size_t)VE_COUNT * E) * sizeof(double) +
+           (size_t)N * E + 16;
 }
 
 // rounds in chunks whose scratch (filled matrix unless the caller keeps it, covariance) fits
