@@ -122,6 +122,24 @@ __device__ double mob_vecmat(V v, X F, int N, int E, int j) {
     if (j < (E & ~3)) {
         double y = 0.0;
         int n = 0;
+        for (; n + 8 <= N; n += 8) {  // two blocks of four rows, loads ahead of the adds
+            double f[8], w[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                f[q] = F(n + q);
+                w[q] = v(n + q);
+            }
+            double t0 = f[1] * w[1];
+            t0 = fma(f[0], w[0], t0);
+            t0 = fma(f[2], w[2], t0);
+            t0 = fma(f[3], w[3], t0);
+            double t1 = f[5] * w[5];
+            t1 = fma(f[4], w[4], t1);
+            t1 = fma(f[6], w[6], t1);
+            t1 = fma(f[7], w[7], t1);
+            y = y + t0;
+            y = y + t1;
+        }
         for (; n + 4 <= N; n += 4) {
             double t = F(n + 1) * v(n + 1);
             t = fma(F(n), v(n), t);
@@ -149,10 +167,47 @@ __device__ double mob_vecmat(V v, X F, int N, int E, int j) {
     return t;
 }
 
+// out[j] = np.dot(v, F)[j] for every column (block call, all threads): OpenBLAS's four-row
+// block partials of the columns j < E & ~3 in parallel into tb ((N / 4) x (E & ~3) doubles),
+// then each column's sequential sum of its partials and the row tail; the other columns (and
+// E == 1) by mob_vecmat on their thread.  The caller syncs before reading out.
+template <class V>
+__device__ void bvecmat(V v, const double* F, int N, int E, double* out, double* tb);
+
 __device__ __forceinline__ double mcatch(double x, double tol) {
     if (x < 1.5 - tol) return 1.0;
     if (x > 1.5 + tol) return 2.0;
     return 1.5;
+}
+
+template <class V>
+__device__ void bvecmat(V v, const double* F, int N, int E, double* out, double* tb) {
+    const int E4 = E == 1 ? 0 : (E & ~3), nb = N >> 2;
+    for (int idx = threadIdx.x; idx < nb * E4; idx += MT) {
+        const int j = idx % E4, n = 4 * (idx / E4);
+        double t = F[(n + 1) * E + j] * v(n + 1);
+        t = fma(F[n * E + j], v(n), t);
+        t = fma(F[(n + 2) * E + j], v(n + 2), t);
+        t = fma(F[(n + 3) * E + j], v(n + 3), t);
+        tb[idx] = t;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < E; j += MT) {
+        if (j >= E4) {
+            out[j] = mob_vecmat(v, [&](int i) { return F[i * E + j]; }, N, E, j);
+            continue;
+        }
+        double y = mseq([&](int b) { return tb[b * E4 + j]; }, nb);  // y = y + t, block order
+        int n = 4 * nb;
+        if (n + 2 <= N) {
+            double t = F[(n + 1) * E + j] * v(n + 1);
+            t = fma(F[n * E + j], v(n), t);
+            y = y + t;
+            n += 2;
+        }
+        if (n < N) y = y + F[n * E + j] * v(n);
+        out[j] = y;
+    }
 }
 
 // block reductions (max of doubles / first index)
@@ -498,7 +553,8 @@ enum { VN_REP = 0, VN_TOK, VN_S, VN_SET1, VN_SET2, VN_NW1, VN_NW2, VN_U, VN_THIS
 enum { VE_MU = 0, VE_OLD, VE_LD, VE_X, VE_Y, VE_SQ, VE_D1, VE_D2, VE_NEW1, VE_NEW2, VE_R0, VE_R1, VE_R2, VE_E1, VE_E2,
        VE_RAW, VE_ADJ, VE_FIN, VE_CERT, VE_REWARD, VE_PC, VE_RELC, VE_COUNT };
 // doubles of the work region: M and Tm (E x (E+1) each), or per wave two N-vectors (median
-// operands) and the sort scratch (PN doubles x, PN doubles w, PN ints; PN = pow2 >= N)
+// operands) and the sort scratch (PN doubles x, PN doubles w, PN ints; PN = pow2 >= N), or the
+// vector-matrix block partials, or the covariance's staged rows
 __host__ __device__ __forceinline__ int medium_pow2(int N) {
     int p = 2;
     while (p < N) p <<= 1;
@@ -509,8 +565,9 @@ __host__ __device__ __forceinline__ int medium_wave_stride(int N) {
     return 2 * N + 2 * pn + pn / 2;
 }
 __host__ __device__ __forceinline__ int medium_work(int N, int E) {
-    const int mt = 2 * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N);
-    return mt > wq ? mt : wq;
+    const int mt = 2 * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N), vb = (N >> 2) * (E & ~3);
+    const int m = mt > wq ? mt : wq;
+    return m > vb ? m : vb;  // and bvecmat's block partials
 }
 
 // diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
@@ -672,8 +729,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     __syncthreads();
     MSTAMP(3);
     // old = np.dot(rep, F) (:489)
-    for (int j = tid; j < E; j += MT)
-        VEp(VE_OLD)[j] = mob_vecmat([&](int i) { return rep[i]; }, [&](int i) { return F[i * E + j]; }, N, E, j);
+    bvecmat([&](int i) { return rep[i]; }, F, N, E, VEp(VE_OLD), mlds);
     double* loading = VEp(VE_LD);
     double* s = VNp(VN_S);
     double* nc = VNp(VN_U);  // nc, then u
@@ -793,15 +849,40 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             for (int j = tid; j < E; j += MT) x[j] = C[j * E + kd] / scal[6];
             for (int e = tid; e < E * E; e += MT) M[(e / E) * ES + e % E] = C[e];
             __syncthreads();
-            auto square = [&]() {  // M <- (M M) * 2^-ilogb(max|MM|)
+            auto square = [&]() {  // M <- (M M) * 2^-ilogb(max|MM|): one 4 x 4 tile per thread
                 double lm = 0.0;
-                for (int e = tid; e < E * E; e += MT) {
-                    const int j = e / E, k = e % E;
-                    double acc = 0.0;
-                    for (int l = 0; l < E; l++) acc = fma(M[j * ES + l], M[l * ES + k], acc);
-                    Tm[j * ES + k] = acc;
-                    const double v = fabs(acc);
-                    if (v > lm) lm = v;
+                const int nT = (E + 3) >> 2;
+                for (int t = tid; t < nT * nT; t += MT) {
+                    const int J = t / nT, K = t % nT;
+                    double acc[4][4];
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) acc[p][q] = 0.0;
+                    for (int l = 0; l < E; l++) {
+                        double mr[4], mc[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int j = 4 * J + q, k = 4 * K + q;
+                            mr[q] = j < E ? M[j * ES + l] : 0.0;
+                            mc[q] = k < E ? M[l * ES + k] : 0.0;
+                        }
+#pragma unroll
+                        for (int p = 0; p < 4; p++)
+#pragma unroll
+                            for (int q = 0; q < 4; q++) acc[p][q] = fma(mr[p], mc[q], acc[p][q]);
+                    }
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int j = 4 * J + p, k = 4 * K + q;
+                            if (j < E && k < E) {
+                                Tm[j * ES + k] = acc[p][q];
+                                const double v = fabs(acc[p][q]);
+                                if (v > lm) lm = v;
+                            }
+                        }
                 }
                 const double mx = bmax(lm, sh);
                 const bool pow2 = mx >= M_DBL_MIN && __builtin_isfinite(mx);
@@ -948,11 +1029,12 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         }
         __syncthreads();
         double* old = VEp(VE_OLD);
+        bvecmat([&](int i) { return n1[i]; }, F, N, E, VEp(VE_D1), mlds);
+        __syncthreads();
+        bvecmat([&](int i) { return n2[i]; }, F, N, E, VEp(VE_D2), mlds);
+        __syncthreads();
         for (int j = tid; j < E; j += MT) {
-            const double a1 = mob_vecmat([&](int i) { return n1[i]; }, [&](int i) { return F[i * E + j]; }, N, E, j);
-            const double a2 = mob_vecmat([&](int i) { return n2[i]; }, [&](int i) { return F[i * E + j]; }, N, E, j);
-            VEp(VE_D1)[j] = a1;
-            VEp(VE_D2)[j] = a2;
+            const double a1 = VEp(VE_D1)[j], a2 = VEp(VE_D2)[j];
             const double t = 0.01 * old[j];
             VEp(VE_NEW1)[j] = a1 + t;
             VEp(VE_NEW2)[j] = a2 + t;
@@ -1029,8 +1111,9 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     double* raw = VEp(VE_RAW);
     double* adj = VEp(VE_ADJ);
     double* fin = VEp(VE_FIN);
+    bvecmat([&](int i) { return smooth[i]; }, F, N, E, raw, mlds);
+    __syncthreads();
     for (int j = tid; j < E; j += MT) {
-        raw[j] = mob_vecmat([&](int i) { return smooth[i]; }, [&](int i) { return F[i * E + j]; }, N, E, j);
         if (!scaled(j)) {
             adj[j] = mcatch(raw[j], a.catch_tol);
             fin[j] = adj[j];
