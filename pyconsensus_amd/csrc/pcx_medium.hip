@@ -266,9 +266,8 @@ __device__ double wv_wmedian(const double* x, const double* w, int n, double* sb
     double* xs = sb;
     double* ws = sb + PN;
     long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    double W = 0.0;
-    if (lane == 0) W = mseq([&](int i) { return w[i]; }, n);
-    const double mid = 0.5 * mbcast(W, 0);
+    const double W = mseq([&](int i) { return w[i]; }, n);  // every lane alike (broadcast loads)
+    const double mid = 0.5 * W;
     bool dom = false, pos = false, nan_ = false;
     for (int i = lane; i < n; i += 64) {
         dom |= w[i] > mid;
@@ -378,26 +377,27 @@ __device__ double wv_wmedian(const double* x, const double* w, int n, double* sb
         prof[1] += t - t0;
         t0 = t;
     }
-    if (lane == 0) {
+    {
+        // the walk `while cum <= mid: cum += ws[k]; k += 1` on every lane alike (no divergence):
+        // branch-free steps, eight loads ahead, leaving at the first batch past the crossing
         double cum = 0.0;
         int k = 0;
-        bool fail = false;
-        while (cum <= mid) {
-            if (k == n) {
-                fail = true;
-                break;
-            }
-            const int lim = n - k < 8 ? n - k : 8;
+        bool stop = !(cum <= mid);
+        for (int i = 0; i < n && !stop; i += 8) {
+            const int lim = n - i < 8 ? n - i : 8;
             double v[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) v[q] = q < lim ? ws[k + q] : 0.0;
+            for (int q = 0; q < 8; q++) v[q] = q < lim ? ws[i + q] : 0.0;
 #pragma unroll
-            for (int q = 0; q < 8; q++)  // static indices: v stays in registers
-                if (q < lim && cum <= mid) {
-                    cum += v[q];
-                    k++;
-                }
+            for (int q = 0; q < 8; q++) {
+                const bool go = !stop && q < lim;
+                const double c2 = cum + v[q];
+                cum = go ? c2 : cum;
+                k += go ? 1 : 0;
+                stop = stop || (go && !(cum <= mid));
+            }
         }
+        const bool fail = !stop;  // ran past the end with cum <= mid
         if (!fail) {
             const double before = cum - ws[k - 1];
             if (fabs(before - mid) < M_DBL_EPS) {
@@ -950,9 +950,11 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                 sqn++;
                 since = 0;
             }
+            for (int e = tid; e < E * E; e += MT) Tm[(e / E) * ES + e % E] = C[e];  // C into LDS
+            __syncthreads();
             if (wv == 0) {
                 double xr = lane < E ? x[lane] : 0.0;
-                for (int p = 0; p < M_PI_POLISH; p++) xr = step(C, E, xr);
+                for (int p = 0; p < M_PI_POLISH; p++) xr = step(Tm, ES, xr);
                 if (lane < E) x[lane] = xr;
             }
             __syncthreads();
@@ -1001,10 +1003,19 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
         double* n2 = VNp(VN_NW2);
         if (tid == 0) {  // NaN propagates like np.min / np.max
             double mn = s[0], mx = s[0];
-            for (int i = 1; i < N; i++) {
-                if (__builtin_isnan(s[i]) || s[i] < mn) mn = __builtin_isnan(mn) ? mn : s[i];
-                if (__builtin_isnan(s[i]) || s[i] > mx) mx = __builtin_isnan(mx) ? mx : s[i];
+            auto upd = [&](double v) {
+                if (__builtin_isnan(v) || v < mn) mn = __builtin_isnan(mn) ? mn : v;
+                if (__builtin_isnan(v) || v > mx) mx = __builtin_isnan(mx) ? mx : v;
+            };
+            int i = 1;
+            for (; i + 8 <= N; i += 8) {  // in row order, loads eight ahead
+                double v[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) v[q] = s[i + q];
+#pragma unroll
+                for (int q = 0; q < 8; q++) upd(v[q]);
             }
+            for (; i < N; i++) upd(s[i]);
             scal[10] = mn;
             scal[11] = mx;
         }
