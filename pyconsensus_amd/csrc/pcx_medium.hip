@@ -9,10 +9,13 @@
 // interpolation's sequential means) and the SPEC's fixed orders elsewhere (fma chains of the
 // covariance and scores, the power iteration with Gram squarings, tree64 norms).
 //
-// Work split: one thread per event column, per reporter row or per matrix entry, as each
-// step allows; the reference's sequential sums stay on one thread.  LDS holds the
-// power-iteration matrices, the per-element NA flags and the row / event vectors; the filled
-// matrix and the covariance live in a per-round global scratch (L2-resident).
+// Work split: one thread per event column, per reporter row, per matrix entry or per 4 x 4
+// tile, as each step allows; one wave per weighted median (bitonic (x, w, index) order, the
+// sequential total and walk on every lane alike) and per certainty; the power steps on one
+// wave; the reference's sequential sums in their order, loads issued ahead.  LDS holds a work
+// region (power-iteration matrices / median scratch / staged covariance rows / np.dot block
+// partials), the per-element NA flags and the row / event vectors; the filled matrix and the
+// covariance live in a per-round global scratch (L2-resident).  DESIGN.md 5.3.
 // Algorithms: PCA, "absolute", "big-five", "fixed-variance", "cokurtosis" (the clusterings take
 // the round scheduler).
 #include <hip/hip_runtime.h>
