@@ -555,7 +555,7 @@ enum { VN_REP = 0, VN_TOK, VN_S, VN_SET1, VN_SET2, VN_NW1, VN_NW2, VN_U, VN_THIS
 // E-vectors (each E doubles)
 enum { VE_MU = 0, VE_OLD, VE_LD, VE_X, VE_Y, VE_SQ, VE_D1, VE_D2, VE_NEW1, VE_NEW2, VE_R0, VE_R1, VE_R2, VE_E1, VE_E2,
        VE_RAW, VE_ADJ, VE_FIN, VE_CERT, VE_REWARD, VE_PC, VE_RELC, VE_COUNT };
-// doubles of the work region: M and Tm (E x (E+1) each), or per wave two N-vectors (median
+// doubles of the work region: M (E x (E+1); and Tm for the Jacobi algorithms), or per wave two N-vectors (median
 // operands) and the sort scratch (PN doubles x, PN doubles w, PN ints; PN = pow2 >= N), or the
 // vector-matrix block partials, or the covariance's staged rows
 __host__ __device__ __forceinline__ int medium_pow2(int N) {
@@ -567,8 +567,9 @@ __host__ __device__ __forceinline__ int medium_wave_stride(int N) {
     const int pn = medium_pow2(N);
     return 2 * N + 2 * pn + pn / 2;
 }
-__host__ __device__ __forceinline__ int medium_work(int N, int E) {
-    const int mt = 2 * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N), vb = (N >> 2) * (E & ~3);
+__host__ __device__ __forceinline__ int medium_work(int N, int E, int alg) {
+    const bool jac = alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;  // Tm: the eigenvectors
+    const int mt = (jac ? 2 : 1) * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N), vb = (N >> 2) * (E & ~3);
     const int m = mt > wq ? mt : wq;
     return m > vb ? m : vb;  // and bvecmat's block partials
 }
@@ -582,7 +583,7 @@ __host__ __device__ __forceinline__ int medium_work(int N, int E) {
         }                                                                         \
     } while (0)
 
-__global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b0, double* Fscr, double* Cscr) {
+__global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_t b0, double* Fscr, double* Cscr) {
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     __shared__ double sh[MT];
     __shared__ double scal[16];
@@ -593,7 +594,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
     double* Tm = M + E * ES;
     // work region: M and Tm in the power iteration / Jacobi, per wave the median operands and
     // sort scratch in the interpolation, the outcomes and the certainty
-    double* vN = mlds + medium_work(N, E);
+    double* vN = mlds + medium_work(N, E, a.algorithm);
     double* vE = vN + VN_COUNT * N;
     uint8_t* fl = (uint8_t*)(vE + VE_COUNT * E);  // [N][E] bit 0 NaN, bit 1 zero
     auto VNp = [&](int k) { return vN + k * N; };
@@ -775,7 +776,7 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             for (int p = 0; p < 4; p++)
 #pragma unroll
                 for (int q = 0; q < 4; q++) acc[p][q] = 0.0;
-            int CR = medium_work(N, E) / (2 * E);
+            int CR = medium_work(N, E, a.algorithm) / (2 * E);
             CR = CR > 32 ? 32 : CR;
             double* Al = mlds;
             double* Dl = mlds + CR * E;
@@ -853,15 +854,17 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
             for (int e = tid; e < E * E; e += MT) M[(e / E) * ES + e % E] = C[e];
             __syncthreads();
             auto square = [&]() {  // M <- (M M) * 2^-ilogb(max|MM|): one 4 x 4 tile per thread
+                // (E <= 64: at most 16 x 16 tiles, one per thread; the product stays in registers
+                // across the block max, then overwrites M)
                 double lm = 0.0;
-                const int nT = (E + 3) >> 2;
-                for (int t = tid; t < nT * nT; t += MT) {
-                    const int J = t / nT, K = t % nT;
-                    double acc[4][4];
+                const int nT = (E + 3) >> 2, J = tid / nT, K = tid % nT;
+                const bool own = tid < nT * nT;
+                double acc[4][4];
 #pragma unroll
-                    for (int p = 0; p < 4; p++)
+                for (int p = 0; p < 4; p++)
 #pragma unroll
-                        for (int q = 0; q < 4; q++) acc[p][q] = 0.0;
+                    for (int q = 0; q < 4; q++) acc[p][q] = 0.0;
+                if (own) {
                     for (int l = 0; l < E; l++) {
                         double mr[4], mc[4];
 #pragma unroll
@@ -879,22 +882,22 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                     for (int p = 0; p < 4; p++)
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
-                            const int j = 4 * J + p, k = 4 * K + q;
-                            if (j < E && k < E) {
-                                Tm[j * ES + k] = acc[p][q];
-                                const double v = fabs(acc[p][q]);
-                                if (v > lm) lm = v;
-                            }
+                            const double v = fabs(acc[p][q]);
+                            if (4 * J + p < E && 4 * K + q < E && v > lm) lm = v;
                         }
                 }
-                const double mx = bmax(lm, sh);
+                const double mx = bmax(lm, sh);  // (its barriers: every read of M is done)
                 const bool pow2 = mx >= M_DBL_MIN && __builtin_isfinite(mx);
                 const double sc = pow2 ? ldexp(1.0, -ilogb(mx)) : 1.0;
-                for (int e = tid; e < E * E; e += MT) {
-                    const int j = e / E, k = e % E;
-                    const double t = Tm[j * ES + k];
-                    M[j * ES + k] = pow2 ? t * sc : (mx > 0.0 ? t / mx : t);
-                }
+                if (own)
+#pragma unroll
+                    for (int p = 0; p < 4; p++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int j = 4 * J + p, k = 4 * K + q;
+                            const double t = acc[p][q];
+                            if (j < E && k < E) M[j * ES + k] = pow2 ? t * sc : (mx > 0.0 ? t / mx : t);
+                        }
                 __syncthreads();
             };
             int sqn = 0;
@@ -953,11 +956,11 @@ __global__ void __launch_bounds__(MT) medium_round_kernel(BatchArgs a, int64_t b
                 sqn++;
                 since = 0;
             }
-            for (int e = tid; e < E * E; e += MT) Tm[(e / E) * ES + e % E] = C[e];  // C into LDS
+            for (int e = tid; e < E * E; e += MT) M[(e / E) * ES + e % E] = C[e];  // C into LDS
             __syncthreads();
             if (wv == 0) {
                 double xr = lane < E ? x[lane] : 0.0;
-                for (int p = 0; p < M_PI_POLISH; p++) xr = step(Tm, ES, xr);
+                for (int p = 0; p < M_PI_POLISH; p++) xr = step(M, ES, xr);
                 if (lane < E) x[lane] = xr;
             }
             __syncthreads();
@@ -1262,8 +1265,8 @@ bool medium_fits(const BatchArgs& a) {
            a.algorithm >= PCX_ALG_PCA && a.algorithm <= PCX_ALG_COKURTOSIS;
 }
 
-size_t medium_lds_bytes(int N, int E) {
-    return ((size_t)medium_work(N, E) + (size_t)VN_COUNT * N + (size_t)VE_COUNT * E) * sizeof(double) +
+size_t medium_lds_bytes(int N, int E, int alg) {
+    return ((size_t)medium_work(N, E, alg) + (size_t)VN_COUNT * N + (size_t)VE_COUNT * E) * sizeof(double) +
            (size_t)N * E + 16;
 }
 
@@ -1277,7 +1280,7 @@ int64_t medium_chunk(const BatchArgs& a, size_t scratch_bytes) {
 
 hipError_t launch_medium(const BatchArgs& a, int64_t b0, int64_t nb, double* Fscr, double* Cscr, hipStream_t st) {
     if (nb <= 0) return hipSuccess;
-    const size_t lds = medium_lds_bytes(a.N, a.E);
+    const size_t lds = medium_lds_bytes(a.N, a.E, a.algorithm);
     // (dynamic LDS above 64 KB needs no attribute on gfx950: the launch checks it against 160 KB)
     (void)hipGetLastError();  // report launch errors only
     hipLaunchKernelGGL(medium_round_kernel, dim3((unsigned)nb), dim3(MT), lds, st, a, b0, Fscr, Cscr);

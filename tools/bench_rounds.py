@@ -2,7 +2,8 @@
 pcx_consensus_batched_f64 on the workgroup-per-round kernel (csrc/pcx_medium.hip), then on the
 worker-stream scheduler (csrc/pcx_rounds.cpp, PCX_NO_MEDIUM=1) at several pool sizes.
 
-usage: python tools/bench_rounds.py [B] [N] [E]   (prints one JSON line per pool size)
+usage: python tools/bench_rounds.py [B] [N] [E] [wg]   (one JSON line per path / pool size; "wg":
+the workgroup kernel only)
 """
 import json
 import os
@@ -34,6 +35,8 @@ def main():
         dt = time.perf_counter() - t0
     print(json.dumps({"rounds": B, "N": N, "E": E, "path": "workgroup kernel", "seconds": dt,
                       "rounds_per_s": B / dt}), flush=True)
+    if len(sys.argv) > 4 and sys.argv[4] == "wg":
+        return
     os.environ["PCX_NO_MEDIUM"] = "1"  # the worker-stream scheduler (csrc/pcx_rounds.cpp)
     for workers in (1, 4, 8, 16, 32):
         os.environ["PCX_ROUND_WORKERS"] = str(workers)
