@@ -321,8 +321,16 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
                 double mp[3] = {0, 0, 0};  // wave 0's outcome medians: total+dom, rank, walk
                 for (int64_t b = 0; b < a.B; b++)
                     for (int k = 0; k < 3; k++) mp[k] += (double)h[b * 32 + 20 + k];
-                fprintf(stderr, " wave0 medians total:%.0f rank:%.0f walk:%.0f\n", mp[0] / (double)a.B,
+                fprintf(stderr, " wave0 medians total:%.0f rank:%.0f walk:%.0f", mp[0] / (double)a.B,
                         mp[1] / (double)a.B, mp[2] / (double)a.B);
+                double sub[4] = {0, 0, 0, 0};  // the nonconformity phase's steps (stamps 24-27 after 8)
+                for (int64_t b = 0; b < a.B; b++)
+                    for (int k = 0; k < 4; k++) {
+                        const long long t1 = h[b * 32 + 24 + k], t0 = h[b * 32 + (k ? 23 + k : 8)];
+                        if (t1 && t0) sub[k] += (double)(t1 - t0);
+                    }
+                fprintf(stderr, " nc: minmax+norm:%.0f n12:%.0f dots:%.0f ranks:%.0f\n", sub[0] / (double)a.B,
+                        sub[1] / (double)a.B, sub[2] / (double)a.B, sub[3] / (double)a.B);
             }
             return e == hipSuccess ? PCX_OK : hip_fail(e, "medium_round_kernel launch");
         }

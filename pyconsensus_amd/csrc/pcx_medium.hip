@@ -89,8 +89,7 @@ __device__ double wtree64v(double v) {
 template <class A, class B>
 __device__ double mdot2(A a, B b, int n) {
     double s = 0.0, c = 0.0;
-    for (int i = 0; i < n; i++) {
-        const double x = a(i), y = b(i);
+    auto step = [&](double x, double y) {
         const double p = x * y;
         const double pe = fma(x, y, -p);
         const double t = s + p;
@@ -98,7 +97,19 @@ __device__ double mdot2(A a, B b, int n) {
         const double se = (s - (t - z)) + (p - z);
         s = t;
         c = c + (pe + se);
+    };
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {  // in index order, loads eight ahead
+        double xa[8], ya[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            xa[q] = a(i + q);
+            ya[q] = b(i + q);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) step(xa[q], ya[q]);
     }
+    for (; i < n; i++) step(a(i), b(i));
     return s + c;
 }
 
@@ -173,7 +184,8 @@ __device__ double mob_vecmat(V v, X F, int N, int E, int j) {
 // out[j] = np.dot(v, F)[j] for every column (block call, all threads): OpenBLAS's four-row
 // block partials of the columns j < E & ~3 in parallel into tb ((N / 4) x (E & ~3) doubles),
 // then each column's sequential sum of its partials and the row tail; the other columns (and
-// E == 1) by mob_vecmat on their thread.  The caller syncs before reading out.
+// E == 1) by mob_vecmat on their thread over a copy staged in LDS after the partials
+// ((E - E & ~3) x N doubles).  The caller syncs before reading out.
 template <class V>
 __device__ void bvecmat(V v, const double* F, int N, int E, double* out, double* tb);
 
@@ -185,19 +197,37 @@ __device__ __forceinline__ double mcatch(double x, double tol) {
 
 template <class V>
 __device__ void bvecmat(V v, const double* F, int N, int E, double* out, double* tb) {
-    const int E4 = E == 1 ? 0 : (E & ~3), nb = N >> 2;
-    for (int idx = threadIdx.x; idx < nb * E4; idx += MT) {
-        const int j = idx % E4, n = 4 * (idx / E4);
-        double t = F[(n + 1) * E + j] * v(n + 1);
-        t = fma(F[n * E + j], v(n), t);
-        t = fma(F[(n + 2) * E + j], v(n + 2), t);
-        t = fma(F[(n + 3) * E + j], v(n + 3), t);
-        tb[idx] = t;
+    const int E4 = E == 1 ? 0 : (E & ~3), nb = N >> 2, ni = nb * E4;
+    for (int i0 = threadIdx.x; i0 < ni; i0 += 4 * MT) {  // four blocks' loads per round trip
+        double f[4][4], w[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int idx = i0 + u * MT;
+            const int j = idx % E4, n = 4 * (idx / E4);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                f[u][r] = idx < ni ? F[(n + r) * E + j] : 0.0;
+                w[u][r] = idx < ni ? v(n + r) : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int idx = i0 + u * MT;
+            double t = f[u][1] * w[u][1];
+            t = fma(f[u][0], w[u][0], t);
+            t = fma(f[u][2], w[u][2], t);
+            t = fma(f[u][3], w[u][3], t);
+            if (idx < ni) tb[idx] = t;
+        }
     }
+    double* tl = tb + ni;  // the columns past E & ~3 staged from F (their chains read LDS)
+    const int nt = (E - E4) * N;
+    for (int idx = threadIdx.x; idx < nt; idx += MT) tl[idx] = F[(idx % N) * E + E4 + idx / N];
     __syncthreads();
     for (int j = threadIdx.x; j < E; j += MT) {
         if (j >= E4) {
-            out[j] = mob_vecmat(v, [&](int i) { return F[i * E + j]; }, N, E, j);
+            const double* col = tl + (j - E4) * N;
+            out[j] = mob_vecmat(v, [&](int i) { return col[i]; }, N, E, j);
             continue;
         }
         double y = mseq([&](int b) { return tb[b * E4 + j]; }, nb);  // y = y + t, block order
@@ -569,7 +599,9 @@ __host__ __device__ __forceinline__ int medium_wave_stride(int N) {
 }
 __host__ __device__ __forceinline__ int medium_work(int N, int E, int alg) {
     const bool jac = alg == PCX_ALG_BIG_FIVE || alg == PCX_ALG_FIXED_VARIANCE;  // Tm: the eigenvectors
-    const int mt = (jac ? 2 : 1) * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N), vb = (N >> 2) * (E & ~3);
+    const int E4 = E == 1 ? 0 : (E & ~3);
+    const int mt = (jac ? 2 : 1) * E * (E + 1), wq = (MT / 64) * medium_wave_stride(N),
+              vb = (N >> 2) * E4 + (E - E4) * N;
     const int m = mt > wq ? mt : wq;
     return m > vb ? m : vb;  // and bvecmat's block partials
 }
@@ -636,67 +668,99 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     __syncthreads();
     if (tid == 0) scal[1] = mseq([&](int i) { return tok[i]; }, N) - 1.0;  // denom
     // --- a2: rescale (:266-269), NA (:278)
-    for (int e = tid; e < N * E; e += MT) {
-        const int j = e % E;
-        double x = Rin[e];
-        if (scaled(j)) {
-            x = (x - a.lo[bo + j]) / (a.hi[bo + j] - a.lo[bo + j]);
-            if (a.int_dtype) x = trunc(x);
+    for (int e0 = tid; e0 < N * E; e0 += 8 * MT) {  // eight reports' loads ahead of the stores
+        double xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = e0 + u * MT;
+            xv[u] = e < N * E ? Rin[e] : 0.0;
         }
-        F[e] = x;
-        fl[e] = (uint8_t)((__builtin_isnan(x) ? 1 : 0) | (x == 0.0 ? 2 : 0));
-        if (a.original) a.original[b * N * E + e] = x;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = e0 + u * MT;
+            if (e >= N * E) break;
+            const int j = e % E;
+            double x = xv[u];
+            if (scaled(j)) {
+                x = (x - a.lo[bo + j]) / (a.hi[bo + j] - a.lo[bo + j]);
+                if (a.int_dtype) x = trunc(x);
+            }
+            F[e] = x;
+            fl[e] = (uint8_t)((__builtin_isnan(x) ? 1 : 0) | (x == 0.0 ? 2 : 0));
+            if (a.original) a.original[b * N * E + e] = x;
+        }
     }
     __syncthreads();
     MSTAMP(1);
     // --- a3: interpolate (:284-313): binary columns one thread each; scaled columns one at a
     // time with the whole block (weighted median)
-    for (int j = tid; j < E; j += MT) {
-        if (scaled(j)) continue;
-        // sequential sums in row order, the loads issued eight rows ahead
+    {
+        // one thread per binary column (E <= 64): the present total from the LDS flags, then the
+        // weighted mean over the present rows in row order, the filled matrix staged through the
+        // work region in row chunks (one round trip per chunk, not per eight rows)
+        const int j = tid;
+        const bool act = j < E && !scaled(j);
         int nmiss = 0;
         double tot = 0.0;
-        int i = 0;
-        for (; i + 8 <= N; i += 8) {
-            uint8_t f[8];
-            double r[8];
+        if (act) {
+            int i = 0;
+            for (; i + 8 <= N; i += 8) {
+                uint8_t f[8];
+                double r[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                f[q] = fl[(i + q) * E + j];
-                r[q] = rep[i + q];
+                for (int q = 0; q < 8; q++) {
+                    f[q] = fl[(i + q) * E + j];
+                    r[q] = rep[i + q];
+                }
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    nmiss += f[q] ? 1 : 0;
+                    if (!f[q]) tot += r[q];
+                }
             }
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                nmiss += f[q] ? 1 : 0;
-                if (!f[q]) tot += r[q];
+            for (; i < N; i++) {
+                const bool m = fl[i * E + j] != 0;
+                nmiss += m ? 1 : 0;
+                if (!m) tot += rep[i];
             }
         }
-        for (; i < N; i++) {
-            const bool m = fl[i * E + j] != 0;
-            nmiss += m ? 1 : 0;
-            if (!m) tot += rep[i];
-        }
-        if (!nmiss) continue;
+        const bool need = act && nmiss > 0;
         double g = 0.0;
-        for (i = 0; i + 8 <= N; i += 8) {
-            uint8_t f[8];
-            double r[8], x[8];
+        if (__syncthreads_or(need)) {
+            int CR = medium_work(N, E, a.algorithm) / E;
+            CR = CR > 64 ? 64 : CR;
+            double* st = mlds;
+            for (int c0 = 0; c0 < N; c0 += CR) {
+                const int cr = N - c0 < CR ? N - c0 : CR;
+                for (int idx = tid; idx < cr * E; idx += MT) st[idx] = F[c0 * E + idx];
+                __syncthreads();
+                if (need) {
+                    int r = 0;
+                    for (; r + 8 <= cr; r += 8) {
+                        uint8_t f[8];
+                        double w8[8], x[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                f[q] = fl[(i + q) * E + j];
-                r[q] = rep[i + q];
-                x[q] = F[(i + q) * E + j];
+                        for (int q = 0; q < 8; q++) {
+                            f[q] = fl[(c0 + r + q) * E + j];
+                            w8[q] = rep[c0 + r + q];
+                            x[q] = st[(r + q) * E + j];
+                        }
+#pragma unroll
+                        for (int q = 0; q < 8; q++)
+                            if (!f[q]) g += (w8[q] / tot) * x[q];
+                    }
+                    for (; r < cr; r++)
+                        if (!fl[(c0 + r) * E + j]) g += (rep[c0 + r] / tot) * st[r * E + j];
+                }
+                __syncthreads();
             }
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (!f[q]) g += (r[q] / tot) * x[q];
         }
-        for (; i < N; i++)
-            if (!fl[i * E + j]) g += (rep[i] / tot) * F[i * E + j];
-        g = mcatch(g, a.catch_tol);
-        if (a.int_dtype) g = trunc(g);
-        for (int i = 0; i < N; i++)
-            if (fl[i * E + j]) F[i * E + j] = g;
+        if (need) {
+            g = mcatch(g, a.catch_tol);
+            if (a.int_dtype) g = trunc(g);
+            for (int i = 0; i < N; i++)
+                if (fl[i * E + j]) F[i * E + j] = g;
+        }
     }
     MSTAMP(2);
     const int nscl = nscl_s;
@@ -1031,21 +1095,24 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             set2[i] = s[i] - scal[11];
         }
         __syncthreads();
-        if (tid == 0) {  // normalize (:244-249)
+        if (tid == 0) {  // normalize (:244-249); the two sets on two waves
             double S1 = mpw([&](int i) { return fabs(set1[i]); }, N);
             scal[12] = S1;
             scal[13] = S1 == 0 ? mpw([&](int i) { return fabs(set1[i]) + 1.0; }, N) : S1;
+        } else if (tid == 64) {
             double S2 = mpw([&](int i) { return fabs(set2[i]); }, N);
             scal[14] = S2;
             scal[15] = S2 == 0 ? mpw([&](int i) { return fabs(set2[i]) + 1.0; }, N) : S2;
         }
         __syncthreads();
+        MSTAMP(24);
         for (int i = tid; i < N; i += MT) {
             n1[i] = scal[12] == 0 ? (fabs(set1[i]) + 1.0) / scal[13] : fabs(set1[i]) / scal[13];
             n2[i] = scal[14] == 0 ? (fabs(set2[i]) + 1.0) / scal[15] : fabs(set2[i]) / scal[15];
         }
         __syncthreads();
         double* old = VEp(VE_OLD);
+        MSTAMP(25);
         bvecmat([&](int i) { return n1[i]; }, F, N, E, VEp(VE_D1), mlds);
         __syncthreads();
         bvecmat([&](int i) { return n2[i]; }, F, N, E, VEp(VE_D2), mlds);
@@ -1057,20 +1124,35 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             VEp(VE_NEW2)[j] = a2 + t;
         }
         __syncthreads();
+        MSTAMP(26);
         double ref = 0.0;
         if (alg == PCX_ALG_PCA) {
             double* nw1 = VEp(VE_NEW1);
             double* nw2 = VEp(VE_NEW2);
             for (int j = tid; j < E; j += MT) {
                 int lt0 = 0, eq0 = 0, lt1 = 0, eq1 = 0, lt2 = 0, eq2 = 0;
-                for (int k = 0; k < E; k++) {
-                    lt0 += old[k] < old[j];
-                    eq0 += old[k] == old[j];
-                    lt1 += nw1[k] < nw1[j];
-                    eq1 += nw1[k] == nw1[j];
-                    lt2 += nw2[k] < nw2[j];
-                    eq2 += nw2[k] == nw2[j];
+                const double o = old[j], v1 = nw1[j], v2 = nw2[j];
+                auto cnt = [&](double a0, double a1, double a2) {
+                    lt0 += a0 < o;
+                    eq0 += a0 == o;
+                    lt1 += a1 < v1;
+                    eq1 += a1 == v1;
+                    lt2 += a2 < v2;
+                    eq2 += a2 == v2;
+                };
+                int k = 0;
+                for (; k + 8 <= E; k += 8) {  // broadcast loads eight ahead
+                    double b0[8], b1[8], b2[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        b0[q] = old[k + q];
+                        b1[q] = nw1[k + q];
+                        b2[q] = nw2[k + q];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; q++) cnt(b0[q], b1[q], b2[q]);
                 }
+                for (; k < E; k++) cnt(old[k], nw1[k], nw2[k]);
                 const double r0 = (double)lt0 + (double)(eq0 + 1) * 0.5;
                 const double r1 = (double)lt1 + (double)(eq1 + 1) * 0.5;
                 const double r2 = (double)lt2 + (double)(eq2 + 1) * 0.5;
@@ -1084,6 +1166,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             ref = scal[2];
             __syncthreads();
         }
+        MSTAMP(27);
         int pick1;
         if (ref == 0) {
             if (tid == 0) {
@@ -1175,7 +1258,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     double* reward = VEp(VE_REWARD);
     double* pc = VEp(VE_PC);
     double* relc = VEp(VE_RELC);
-    if (tid == 0) {
+    if (tid == 64) {  // (wave 1: wave 0 runs the participation columns meanwhile)
         const double S = mpw([&](int j) { return fabs(cert[j]); }, E);
         const double Sp = S == 0 ? mpw([&](int j) { return fabs(cert[j]) + 1.0; }, E) : S;
         for (int j = 0; j < E; j++) reward[j] = S == 0 ? (fabs(cert[j]) + 1.0) / Sp : fabs(cert[j]) / Sp;
@@ -1207,13 +1290,15 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
         a2v[i] = rmask[i] != 0.0 ? 0.0 : fabs(pr[i]);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0) {  // the three totals on three waves
         scal[8] = 1.0 - mpw([&](int j) { return pc[j]; }, E) / (double)E;  // pna
+    } else if (tid == 64) {
         double S = mpw([&](int i) { return a2v[i]; }, N);
         const bool bump = S == 0;
         if (bump) S = mpw([&](int i) { return rmask[i] != 0.0 ? 0.0 : fabs(pr[i]) + 1.0; }, N);
         scal[9] = S;
         scal[10] = bump ? 1.0 : 0.0;
+    } else if (tid == 128) {
         const double P = mpw([&](int j) { return fabs(pc[j]); }, E);
         const double Pp = P == 0 ? mpw([&](int j) { return fabs(pc[j]) + 1.0; }, E) : P;
         for (int j = 0; j < E; j++) relc[j] = P == 0 ? (fabs(pc[j]) + 1.0) / Pp : fabs(pc[j]) / Pp;
