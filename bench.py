@@ -162,6 +162,30 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
                     "reputation=None"}
 
 
+def bench_medium(dev, B=16384, N=100, E=50, steps=3):
+    """Batched rounds above one wavefront: B rounds of 100 x 50 (SURVEY.md 8(d) generator) on the
+    workgroup-per-round kernel (csrc/pcx_medium.hip, DESIGN.md 5.3), every output written;
+    inputs resident on the device, best of `steps` timed calls."""
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=3)
+    args = [torch.as_tensor(x, device=dev) for x in (R, rep, sc.astype("uint8"), lo, hi)]
+    consensus_batched(*args)
+    torch.cuda.synchronize(dev)
+    best = float("inf")
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        consensus_batched(*args)
+        torch.cuda.synchronize(dev)
+        best = min(best, time.perf_counter() - t0)
+    return {"metric": "oracle rounds/sec (batched %dx%d, one workgroup per round)" % (N, E), "rounds": B,
+            "rounds_per_s": B / best, "ms": best * 1e3,
+            "data": "synthetic (SURVEY.md 8(d) generator, seed 3), every output written"}
+
+
 def bench_c4(dev, steps=3, oracle=True):
     """Config C4: one 100k x 1k matrix (seed 2, integer reputations),
     device-resident consensus latency; the host->device copy of the reports timed apart; the
@@ -383,7 +407,15 @@ def main():
             c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
             c4 = {"metric": "100k x 1k consensus latency", "error": repr(e)[:400]}
+    medium = None
+    if args.c4 and world == 1:
+        try:
+            medium = bench_medium(dev)
+        except Exception as e:  # noqa: BLE001
+            medium = {"metric": "oracle rounds/sec (batched 100x50)", "error": repr(e)[:400]}
     if rank == 0:
+        if medium is not None:
+            line["medium"] = medium
         if c5 is not None:
             line["c5"] = c5
         if c4 is not None:
