@@ -329,8 +329,15 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
                         const long long t1 = h[b * 32 + 24 + k], t0 = h[b * 32 + (k ? 23 + k : 8)];
                         if (t1 && t0) sub[k] += (double)(t1 - t0);
                     }
-                fprintf(stderr, " nc: minmax+norm:%.0f n12:%.0f dots:%.0f ranks:%.0f\n", sub[0] / (double)a.B,
+                fprintf(stderr, " nc: minmax+norm:%.0f n12:%.0f dots:%.0f ranks:%.0f", sub[0] / (double)a.B,
                         sub[1] / (double)a.B, sub[2] / (double)a.B, sub[3] / (double)a.B);
+                double pw[2] = {0, 0};  // power iteration: presquares (6 -> 28), steps (28 -> 29)
+                for (int64_t b = 0; b < a.B; b++) {
+                    const long long* hb = &h[b * 32];
+                    if (hb[28] && hb[6]) pw[0] += (double)(hb[28] - hb[6]);
+                    if (hb[29] && hb[28]) pw[1] += (double)(hb[29] - hb[28]);
+                }
+                fprintf(stderr, " pi: presq:%.0f steps:%.0f\n", pw[0] / (double)a.B, pw[1] / (double)a.B);
             }
             return e == hipSuccess ? PCX_OK : hip_fail(e, "medium_round_kernel launch");
         }

@@ -966,6 +966,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             };
             int sqn = 0;
             for (; sqn < M_PI_PRESQUARE; sqn++) square();
+            MSTAMP(28);
             // the power steps between squarings and the polish on wave 0: lane j = row j, x in
             // registers (x_k broadcast by readlane), tree64 norm and max-norm by shuffles
             __shared__ int pi_s[3];
@@ -1020,6 +1021,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                 sqn++;
                 since = 0;
             }
+            MSTAMP(29);
             for (int e = tid; e < E * E; e += MT) M[(e / E) * ES + e % E] = C[e];  // C into LDS
             __syncthreads();
             if (wv == 0) {
