@@ -628,7 +628,9 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     // sort scratch in the interpolation, the outcomes and the certainty
     double* vN = mlds + medium_work(N, E, a.algorithm);
     double* vE = vN + VN_COUNT * N;
-    uint8_t* fl = (uint8_t*)(vE + VE_COUNT * E);  // [N][E] bit 0 NaN, bit 1 zero
+    // NA flags [N][E], two bits per element (bit 0 NaN, bit 1 zero), sixteen to a word
+    uint32_t* flw = (uint32_t*)(vE + VE_COUNT * E);
+    auto FL = [&](int e) -> uint32_t { return (flw[e >> 4] >> ((e & 15) << 1)) & 3u; };
     auto VNp = [&](int k) { return vN + k * N; };
     auto VEp = [&](int k) { return vE + k * E; };
     double* rep = VNp(VN_REP);
@@ -657,6 +659,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     auto scaled = [&](int j) { return ((scmask_s >> j) & 1ull) != 0; };
     long long mprof[3] = {0, 0, 0};  // diagnostic (PCX_STAMPS): median total+dom / rank / walk cycles
 
+    for (int w = tid; w < (N * E + 15) >> 4; w += MT) flw[w] = 0u;  // (ordered by the barrier below)
     // --- a1: reputation (:138-146)
     if (tid == 0) scal[0] = a.reputation ? mpw([&](int i) { return a.reputation[b * N + i]; }, N) : 0.0;
     __syncthreads();
@@ -686,7 +689,8 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                 if (a.int_dtype) x = trunc(x);
             }
             F[e] = x;
-            fl[e] = (uint8_t)((__builtin_isnan(x) ? 1 : 0) | (x == 0.0 ? 2 : 0));
+            const uint32_t bits = (__builtin_isnan(x) ? 1u : 0u) | (x == 0.0 ? 2u : 0u);
+            if (bits) atomicOr(&flw[e >> 4], bits << ((e & 15) << 1));
             if (a.original) a.original[b * N * E + e] = x;
         }
     }
@@ -709,7 +713,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                 double r[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
-                    f[q] = fl[(i + q) * E + j];
+                    f[q] = FL((i + q) * E + j);
                     r[q] = rep[i + q];
                 }
 #pragma unroll
@@ -719,7 +723,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                 }
             }
             for (; i < N; i++) {
-                const bool m = fl[i * E + j] != 0;
+                const bool m = FL(i * E + j) != 0;
                 nmiss += m ? 1 : 0;
                 if (!m) tot += rep[i];
             }
@@ -741,7 +745,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                         double w8[8], x[8];
 #pragma unroll
                         for (int q = 0; q < 8; q++) {
-                            f[q] = fl[(c0 + r + q) * E + j];
+                            f[q] = FL((c0 + r + q) * E + j);
                             w8[q] = rep[c0 + r + q];
                             x[q] = st[(r + q) * E + j];
                         }
@@ -750,7 +754,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                             if (!f[q]) g += (w8[q] / tot) * x[q];
                     }
                     for (; r < cr; r++)
-                        if (!fl[(c0 + r) * E + j]) g += (rep[c0 + r] / tot) * st[r * E + j];
+                        if (!FL((c0 + r) * E + j)) g += (rep[c0 + r] / tot) * st[r * E + j];
                 }
                 __syncthreads();
             }
@@ -759,7 +763,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             g = mcatch(g, a.catch_tol);
             if (a.int_dtype) g = trunc(g);
             for (int i = 0; i < N; i++)
-                if (fl[i * E + j]) F[i * E + j] = g;
+                if (FL(i * E + j)) F[i * E + j] = g;
         }
     }
     MSTAMP(2);
@@ -771,7 +775,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
         int np_ = 0;
         for (int i0 = 0; i0 < N; i0 += 64) {
             const int i = i0 + lane;
-            const bool p = i < N && fl[i * E + j] == 0;
+            const bool p = i < N && FL(i * E + j) == 0;
             const unsigned long long bal = __ballot(p);
             if (p) {
                 const int o = np_ + __popcll(bal & ((1ull << lane) - 1ull));
@@ -790,7 +794,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
             double g = wv_wmedian(wb, wb + N, np_, wb + 2 * N, PN);
             if (a.int_dtype) g = trunc(g);
             for (int i = lane; i < N; i += 64)
-                if (fl[i * E + j]) F[i * E + j] = g;
+                if (FL(i * E + j)) F[i * E + j] = g;
         }
         mwsync();
     }
@@ -1268,9 +1272,9 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     }
     // --- a15: participation and bonuses (:549-581)
     for (int j = tid; j < E; j += MT) {
-        pc[j] = 1.0 - mdot2([&](int i) { return smooth[i]; }, [&](int i) { return fl[i * E + j] ? 1.0 : 0.0; }, N);
+        pc[j] = 1.0 - mdot2([&](int i) { return smooth[i]; }, [&](int i) { return FL(i * E + j) ? 1.0 : 0.0; }, N);
         int nz = 0;
-        for (int i = 0; i < N; i++) nz += (fl[i * E + j] & 2) ? 1 : 0;
+        for (int i = 0; i < N; i++) nz += (FL(i * E + j) & 2) ? 1 : 0;
         if (a.nas_filled) a.nas_filled[b * E + j] = (double)nz;
     }
     __syncthreads();
@@ -1283,8 +1287,8 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     for (int i = tid; i < N; i += MT) {
         int nz = 0, nn = 0;
         for (int j = 0; j < E; j++) {
-            nz += (fl[i * E + j] & 2) ? 1 : 0;
-            nn += (fl[i * E + j] & 1) ? 1 : 0;
+            nz += (FL(i * E + j) & 2) ? 1 : 0;
+            nn += (FL(i * E + j) & 1) ? 1 : 0;
         }
         narow[i] = (double)nz;
         pr[i] = 1.0 - narow[i] / (double)E;
@@ -1354,7 +1358,7 @@ bool medium_fits(const BatchArgs& a) {
 
 size_t medium_lds_bytes(int N, int E, int alg) {
     return ((size_t)medium_work(N, E, alg) + (size_t)VN_COUNT * N + (size_t)VE_COUNT * E) * sizeof(double) +
-           (size_t)N * E + 16;
+           (size_t)((N * E + 15) >> 4) * 4 + 16;
 }
 
 // rounds in chunks whose scratch (filled matrix unless the caller keeps it, covariance) fits
