@@ -188,6 +188,25 @@ def test_medium_rounds_bitexact_vs_spec(gpu_lib, variant):
         assert not bad, (b, bad)
 
 
+@pytest.mark.parametrize("variant", ["1x40", "2x33", "3x64_uniform", "7x50_nobounds", "9x35_absolute",
+                                     "33x64_shared", "64x33_int", "65x2", "129x3", "255x63", "256x1_uniform",
+                                     "5x40_big-five", "40x34_fixed-variance"])
+def test_medium_rounds_edge_shapes_vs_spec(gpu_lib, variant):
+    """The workgroup-per-round kernel at its edges: tiny reporter counts (one-row rounds, a
+    bitonic network of two slots), E just above the one-wave limit, E = 1-3 (np.dot's ddot / dgemv
+    tail orders), N just above 64 / 128 and just below 256: bit-identical to the 256-reporter SPEC
+    on every output (the SPEC alone pins these; the numpy restatement is covered above)."""
+    from oracle import pcx_oracle_c as OC
+    from pyconsensus_amd.batched import consensus_batched
+
+    R, kw = _rounds_kw(variant, B=24, seed=5)
+    g = _np(consensus_batched(R, filled=True, original=True, **kw))
+    c = OC.batched(R, **kw, threads=8)
+    for k, v in g.items():
+        same = (v == c[k]) | (np.isnan(v) & np.isnan(c[k])) if v.dtype.kind == "f" else (v == c[k])
+        assert np.all(same), (variant, k, int(np.size(same) - np.count_nonzero(same)))
+
+
 @pytest.mark.parametrize("variant", ["100x50", "30x40_uniform_shared", "200x24_big-five", "300x20"])
 def test_rounds_scheduler(gpu_lib, variant, monkeypatch):
     """Rounds the workgroup kernel does not take (big-five, N > 256, or PCX_NO_MEDIUM): each runs
