@@ -105,13 +105,16 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
         raise ValueError("C5 needs a GPU count dividing 8")
     R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, shards=shards, device=dev)
     comm = Comm.from_env(dev.index)  # RCCL inside libpcx for the nccl backend
+    _C5_STATE["comm"], _C5_STATE["dev"] = comm, dev.index
 
     def run(profile=None):
         return consensus_matrix(R, None, sc, lo, hi, comm=comm, n_total=N, row_offset=off, device=dev,
                                 profile=profile, matrices=True)
 
+    _C5_STATE["phase"] = "warmup"
     for _ in range(warmup):
         run()
+    _C5_STATE["phase"] = "timed steps"
     times, prof = [], {}
     ev = ag = None
     for _ in range(steps):
@@ -246,6 +249,23 @@ def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
 
 
 C5_TIMEOUT_S = 300          # multi-rank C5 watchdog (bench main)
+C5_WATCHDOG_EXIT = 3        # exit status of a rank whose C5 stalled
+_C5_STATE = {"comm": None, "dev": None, "phase": "setup"}
+
+
+def c5_stall_report(rank):
+    """One line naming the rank and the libpcx stage its C5 call is in (pcx_ctx_progress)."""
+    where = _C5_STATE["phase"]
+    comm = _C5_STATE["comm"]
+    if comm is not None:
+        try:
+            from pyconsensus_amd.pipeline import progress
+
+            stage, waiting = progress(comm, _C5_STATE["dev"])
+            where += ", libpcx stage %s%s" % (stage or "(none yet)", " (host waiting on the stream)" if waiting else "")
+        except Exception as e:  # noqa: BLE001
+            where += ", progress unavailable: %r" % (e,)
+    return "rank %d stalled in C5 %s" % (rank, where)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA, 2x the bf16 rate (MI355X_MICROARCH.md, Matrix cores)
 VALU_ISSUE_CYCLES = 4      # a wave64 VALU instruction holds its SIMD 4 cycles
 SIMDS, CLOCK_GHZ = 1024, 2.4
@@ -381,17 +401,20 @@ def main():
     if args.c5_steps > 0:
         # a failure here is recorded in the line; the C3 headline above stands.  With several
         # ranks a watchdog also guards against a stuck collective: after C5_TIMEOUT_S every rank
-        # exits, rank 0 first printing the C3 line with the C5 entry marked.
+        # names the stage it is stuck in on stderr and exits with status C5_WATCHDOG_EXIT (the
+        # run FAILS), rank 0 first printing the C3 line with the C5 entry marked as stalled.
         watchdog = None
         if world > 1:
             import threading
 
             def on_timeout():
+                msg = c5_stall_report(rank)
+                print("bench.py watchdog: %s after %d s" % (msg, C5_TIMEOUT_S), file=sys.stderr, flush=True)
                 if rank == 0:
                     line["c5"] = {"metric": "1M x 4k consensus latency", "n_gpus": world,
-                                  "error": "timed out after %d s" % C5_TIMEOUT_S}
+                                  "error": "watchdog: %s after %d s" % (msg, C5_TIMEOUT_S)}
                     print(json.dumps(line), flush=True)
-                os._exit(0)
+                os._exit(C5_WATCHDOG_EXIT)
 
             watchdog = threading.Timer(C5_TIMEOUT_S, on_timeout)
             watchdog.daemon = True

@@ -300,6 +300,12 @@ int pcx_nonconformity_f64(pcx_ctx* ctx, const pcx_problem* p, const double* scor
 int         pcx_profile_enable(pcx_ctx* ctx, int on);
 int         pcx_profile_read(pcx_ctx* ctx, double* ms /* [PCX_NSTAGES] */);
 const char* pcx_stage_name(int k);
+/* Progress of the single-matrix call running on `ctx` (safe to call from another
+ * thread while it runs): *stage = the last stage enqueued (pcx_stage_name; -1 before
+ * the first), *host_waiting = 1 while the host blocks on the context's stream (a
+ * collective waiting for a peer shows as a wait after M_EXCHANGE or a later stage).
+ * A multi-device context reports device 0's worker. */
+int pcx_ctx_progress(const pcx_ctx* ctx, int* stage, int* host_waiting);
 
 /* Sequential float sums of a constant (weightedstats' builtin-sum walk over equal
  * weights, __init__.py:287-303, :519-523): S(k) = 0 + c + c + ... (k terms, each

@@ -57,6 +57,7 @@ def _declare(lib):
         ("pcx_profile_enable", i32, [vp, i32]),
         ("pcx_profile_read", i32, [vp, C.POINTER(C.c_double)]),
         ("pcx_stage_name", C.c_char_p, [i32]),
+        ("pcx_ctx_progress", i32, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         ("pcx_seqsum_const", C.c_double, [C.c_double, i64]),
         ("pcx_seqsum_first_above", i64, [C.c_double, C.c_double, i64]),
     ]:
@@ -80,6 +81,9 @@ def lib():
                 raise PcxError("libpcx ABI version %d, expected %d" % (v, _abi.ABI_VERSION))
             _lib = h
     return _lib
+
+
+PCX_ECOMM = -4  # include/pcx.h enum pcx_status
 
 
 def check(rc):
@@ -113,6 +117,15 @@ def devices_context(device_ids):
         h = new_context(lib().pcx_create_devices(len(ids), arr), "pcx_create_devices(%s)" % (ids,))
         _ctx[key] = h
     return h
+
+
+def drop_devices_context(device_ids):
+    """Destroy and forget this thread's cached multi-device context of ``device_ids`` (after
+    PCX_ECOMM its RCCL communicators are aborted; the next call creates a fresh one)."""
+    key = (threading.get_ident(), tuple(int(d) for d in device_ids))
+    h = _ctx.pop(key, None)
+    if h is not None:
+        lib().pcx_destroy(h)
 
 
 def bind_stream(device_index, stream_handle, ctx=None):

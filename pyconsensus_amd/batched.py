@@ -66,8 +66,12 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     cluster_threshold: clusterfeck's cut (default: the reference's log10(E)/1.77 rule)
 
     Returns a dict of torch tensors on the device, named like the ABI fields
-    (``smooth_rep``, ``outcomes_final``, ...).  Asynchronous on torch's current stream
-    for rounds up to 64 x 32; larger rounds return when every output is written.
+    (``smooth_rep``, ``outcomes_final``, ...).  Three regimes:
+    rounds up to 64 x 32 (one wave per round) and up to 256 x 64 (one workgroup per round,
+    any non-clustering algorithm) are ONE kernel launch, asynchronous on torch's current
+    stream -- synchronise before reading the outputs on the host; the round scheduler (the
+    clusterings above 64 x 32, or rounds above 256 x 64) returns only once every output is
+    written.
     """
     t = _device.require_gpu()
     dev = t.device(device) if device is not None else t.device("cuda", t.cuda.current_device())

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <atomic>
 #include <thread>
 #include <algorithm>
 
@@ -400,6 +401,9 @@ int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, co
         err = "bad shape (fewer rows than devices) or missing reports";
         return PCX_EINVAL;
     }
+    // the rank-independent checks once, here: a bad argument fails before any worker starts,
+    // so it never takes the abort path below (which leaves an RCCL context unusable)
+    if (const int rc = pcx::check_problem(p, n, entry, err)) return rc;
     std::vector<pcx_problem> ps(n, *p);
     std::vector<pcx_result> rs(n);
     std::vector<std::string> errs(n);
@@ -441,15 +445,18 @@ int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, co
         }
     }
     std::vector<std::thread> th;
+    std::atomic<bool> aborting{false};
     for (int k = 0; k < n; k++) {
         const int64_t off = ps[k].row_offset;
         th.emplace_back([&, k, off] {
             rcs[k] = pcx::run_matrix(ctx->sub[k], &ps[k], &rs[k], entry, scores ? scores + off : nullptr, rank_rule,
                                      nc ? nc + off : nullptr, errs[k]);
-            if (rcs[k]) {  // release the ranks waiting on this one in an exchange
+            // release the ranks waiting on this one in an exchange: the first failing worker
+            // aborts every other rank's communicator (RCCL: ncclCommAbort), later ones do nothing
+            if (rcs[k] && !aborting.exchange(true)) {
                 if (ctx->group) pcx::group_abort(ctx->group);
                 for (pcx_ctx* o : ctx->sub)
-                    if (o->comm && o != ctx->sub[k]) o->comm->abort();  // RCCL: ncclCommAbort
+                    if (o->comm && o != ctx->sub[k]) o->comm->abort();
             }
         });
     }
@@ -530,6 +537,14 @@ int pcx_profile_read(pcx_ctx* ctx, double* ms) {
 }
 
 const char* pcx_stage_name(int k) { return pcx::stage_name(k); }
+
+int pcx_ctx_progress(const pcx_ctx* ctx, int* stage, int* host_waiting) {
+    if (!ctx || !stage || !host_waiting) return fail(PCX_EINVAL, "pcx_ctx_progress: null argument");
+    const pcx_ctx* src = ctx->sub.empty() ? ctx : ctx->sub[0];
+    *stage = src->progress_stage.load(std::memory_order_relaxed);
+    *host_waiting = src->progress_wait.load(std::memory_order_relaxed);
+    return PCX_OK;
+}
 
 double pcx_seqsum_const(double c, int64_t k) { return pcx::seqsum_const(c, k); }
 

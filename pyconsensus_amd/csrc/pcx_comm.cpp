@@ -84,24 +84,28 @@ int hip_err(hipError_t e, const char* what, std::string& err) {
 
 // ------------------------------------------------------------------ RCCL
 struct RcclComm : Comm {
-    ncclComm_t comm = nullptr;
+    // the handle is swapped out atomically by abort(): ncclCommAbort runs exactly once even
+    // when several failing worker threads abort the same communicator, and an exchange that
+    // starts after the abort sees nullptr and fails instead of using a freed communicator
+    std::atomic<ncclComm_t> comm{nullptr};
     ~RcclComm() override {
-        if (comm) ncclCommDestroy(comm);
+        if (ncclComm_t c = comm.exchange(nullptr)) ncclCommDestroy(c);
     }
     void abort() override {
-        if (comm) ncclCommAbort(comm);
-        comm = nullptr;
         aborted = true;
+        if (ncclComm_t c = comm.exchange(nullptr)) ncclCommAbort(c);
     }
     static ncclDataType_t dt(int d) { return d == PCX_F64 ? ncclFloat64 : ncclUint64; }
     static ncclRedOp_t op_of(int o) { return o == PCX_SUM ? ncclSum : (o == PCX_MIN ? ncclMin : ncclMax); }
+    static int gone(std::string& err) {
+        err = "RCCL communicator aborted after a failed call: recreate the context";
+        return PCX_ECOMM;
+    }
     int allreduce(void* buf, int64_t count, int dtype, int op, hipStream_t st, std::string& err) override {
         if (count <= 0) return 0;
-        if (!comm) {
-            err = "RCCL communicator aborted after a failed call: recreate the context";
-            return PCX_ECOMM;
-        }
-        ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt(dtype), op_of(op), comm, st);
+        ncclComm_t c = comm.load();
+        if (!c || aborted) return gone(err);
+        ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt(dtype), op_of(op), c, st);
         if (r != ncclSuccess) {
             err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
             return PCX_ECOMM;
@@ -110,11 +114,9 @@ struct RcclComm : Comm {
     }
     int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) override {
         if (bytes <= 0) return 0;
-        if (!comm) {
-            err = "RCCL communicator aborted after a failed call: recreate the context";
-            return PCX_ECOMM;
-        }
-        ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, comm, st);
+        ncclComm_t c = comm.load();
+        if (!c || aborted) return gone(err);
+        ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c, st);
         if (r != ncclSuccess) {
             err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
             return PCX_ECOMM;
@@ -228,13 +230,14 @@ Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::str
     if (!c) return nullptr;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+    ncclComm_t h = nullptr;
+    ncclResult_t r = ncclCommInitRank(&h, world, uid, rank);
     if (r != ncclSuccess) {
         err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
-        c->comm = nullptr;
         delete c;
         return nullptr;
     }
+    c->comm = h;
     c->world = world;
     c->rank = rank;
     return c;

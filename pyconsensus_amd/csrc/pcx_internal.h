@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -251,9 +252,10 @@ struct Comm {
     virtual int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) = 0;
     virtual const char* kind() const = 0;
     // unblock every rank waiting in this communicator after another rank failed (RCCL:
-    // ncclCommAbort); the communicator is unusable afterwards
+    // ncclCommAbort, exactly once whatever the number of callers); the communicator is
+    // unusable afterwards and every later exchange returns PCX_ECOMM
     virtual void abort() {}
-    bool aborted = false;
+    std::atomic<bool> aborted{false};
 };
 Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err);
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);
@@ -285,6 +287,10 @@ struct pcx_ctx {
     // pcx_create_devices: one rank context per device, driven by worker threads
     std::vector<pcx_ctx*> sub;
     pcx_group* group = nullptr;    // host exchange of `sub` when a device id repeats
+    // progress of the running single-matrix call, readable from another thread
+    // (pcx_ctx_progress: a watchdog names the stage a stuck call is in)
+    std::atomic<int> progress_stage{-1};
+    std::atomic<int> progress_wait{0};   // 1 while the host blocks on the stream
 };
 
 namespace pcx {
@@ -292,6 +298,9 @@ void workspace_free(pcx_ctx* c);
 // entry: 0 consensus, 1 interpolate, 2 wpca, 3 lie_detector, 4 nonconformity
 int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const double* scores_in, int rank_rule,
                double* nc_out, std::string& err);
+// the rank-independent argument checks of run_matrix (algorithm, clustering vs world,
+// k-means draws, thresholds, aux scores, mem_kind); 0 = ok
+int check_problem(const pcx_problem* p, int world, int entry, std::string& err);
 // batched rounds of any N x E (pcx_rounds.cpp): each round one single-matrix consensus on a
 // pool of worker contexts with their own streams; synchronous
 int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::string& err);

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -56,6 +57,23 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
         err = std::string("rounds: ") + hipGetErrorString(e);
         return PCX_EHIP;
     }
+    // workspaces are sized for the most scaled events any round of this batch has (the
+    // selection buffers scale with it), not for E
+    int max_scaled = 0;
+    if (in->scaled) {
+        const int64_t rows = in->bounds_shared ? 1 : B;
+        std::vector<uint8_t> sc(rows * E);
+        e = hipMemcpy(sc.data(), in->scaled, rows * E, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            err = std::string("rounds: D2H scaled: ") + hipGetErrorString(e);
+            return PCX_EHIP;
+        }
+        for (int64_t b = 0; b < rows; b++) {
+            int n = 0;
+            for (int64_t j = 0; j < E; j++) n += sc[b * E + j] != 0;
+            max_scaled = std::max(max_scaled, n);
+        }
+    }
     const int K = (int)std::min<int64_t>(pool_size(), B);
     while ((int)c->pool.size() < K) {
         pcx_ctx* w = new (std::nothrow) pcx_ctx;
@@ -64,7 +82,6 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             return PCX_ENOMEM;
         }
         w->device = c->device;
-        w->scaled_floor = (int)E;  // one workspace serves every round's bounds
         e = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking);
         if (e != hipSuccess) {
             delete w;
@@ -83,17 +100,19 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             return PCX_EHIP;
         }
     }
+    for (pcx_ctx* w : c->pool) w->scaled_floor = max_scaled;  // one workspace serves every round's bounds
     std::vector<double> part(B), avg(B);
     std::vector<int32_t> branch(B), flags(B), iters(B), comps(B);
     std::atomic<int64_t> next{0};
     std::atomic<int> failed{0};
     std::vector<std::string> errs(K);
     std::vector<int> rcs(K, 0);
-    auto worker = [&](int k) {
-        pcx_ctx* w = c->pool[k];
-        for (;;) {
-            const int64_t b = next.fetch_add(1);
-            if (b >= B || failed.load()) return;
+    // a worker whose workspace does not fit (PCX_ENOMEM) leaves the pool and hands its round
+    // back: fewer rounds run in flight instead of the batch failing
+    std::mutex retry_mu;
+    std::vector<int64_t> retry;
+    std::atomic<int> alive{K};
+    auto one = [&](pcx_ctx* w, int64_t b, std::string& werr) -> int {
             pcx_problem p{};
             p.n_rows = N;
             p.n_events = E;
@@ -138,19 +157,35 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             r.author_bonus = at(out->author_bonus, b * E);
             r.original = at(out->original, b * N * E);
             r.filled = at(out->filled, b * N * E);
-            const int rc = run_matrix(w, &p, &r, 0, nullptr, 0, nullptr, errs[k]);
-            if (rc) {
-                rcs[k] = rc;
-                errs[k] = "round " + std::to_string(b) + ": " + errs[k];
-                failed.store(1);
-                return;
-            }
+            const int rc = run_matrix(w, &p, &r, 0, nullptr, 0, nullptr, werr);
+            if (rc) return rc;
             part[b] = r.participation;
             avg[b] = r.avg_certainty;
             branch[b] = r.branch;
             flags[b] = r.flags;
             iters[b] = r.pi_iters;
             comps[b] = r.components;
+            return 0;
+    };
+    auto worker = [&](int k) {
+        pcx_ctx* w = c->pool[k];
+        for (;;) {
+            const int64_t b = next.fetch_add(1);
+            if (b >= B || failed.load()) return;
+            const int rc = one(w, b, errs[k]);
+            if (rc == PCX_ENOMEM && alive.fetch_sub(1) > 1) {
+                workspace_free(w);
+                std::lock_guard<std::mutex> lk(retry_mu);
+                retry.push_back(b);
+                errs[k].clear();
+                return;
+            }
+            if (rc) {
+                rcs[k] = rc;
+                errs[k] = "round " + std::to_string(b) + ": " + errs[k];
+                failed.store(1);
+                return;
+            }
         }
     };
     std::vector<std::thread> th;
@@ -161,6 +196,20 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             err = errs[k];
             return rcs[k];
         }
+    // the handed-back rounds, one at a time on a context whose workspace is resident
+    for (int64_t b : retry) {
+        pcx_ctx* w = c->pool[0];
+        for (pcx_ctx* q : c->pool)
+            if (q->ws) {
+                w = q;
+                break;
+            }
+        std::string werr;
+        if (const int rc = one(w, b, werr)) {
+            err = "round " + std::to_string(b) + ": " + werr;
+            return rc;
+        }
+    }
     (void)hipSetDevice(c->device);
     auto put = [&](void* dst, const void* src, size_t bytes) {
         if (dst && e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);

@@ -121,6 +121,7 @@ struct Run {
     }
     // profiling marks (HIP events on the context's stream)
     void mark(int stage) {
+        if (stage >= 0) c->progress_stage.store(stage, std::memory_order_relaxed);
         if (!c->profile) return;
         hipEvent_t e;
         hip(hipEventCreate(&e), "hipEventCreate");
@@ -133,7 +134,11 @@ struct Run {
         check_err(mat_stage(m, s, st, err), stage_name(s));
         mark(-1);
     }
-    void sync() { hip(hipStreamSynchronize(st), "hipStreamSynchronize"); }
+    void sync() {
+        c->progress_wait.store(1, std::memory_order_relaxed);
+        hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+        c->progress_wait.store(0, std::memory_order_relaxed);
+    }
     template <class T>
     T read(const T* dev) {
         T v;
@@ -573,6 +578,53 @@ void workspace_free(pcx_ctx* c) {
     c->ws = nullptr;
 }
 
+// The checks that do not depend on the rank: run once per call, before any worker of a
+// multi-device context starts (so invalid input never reaches the abort path).
+int check_problem(const pcx_problem* p, int world, int entry, std::string& err) {
+    if (p->scaled && (!p->lo || !p->hi)) {
+        err = "scaled given without lo / hi";
+        return PCX_EINVAL;
+    }
+    const int alg = p->algorithm;
+    if (alg < PCX_ALG_PCA || alg > PCX_ALG_CLUSTERFECK) {
+        err = "algorithm must be an enum pcx_algorithm value (0..7)";
+        return PCX_EINVAL;
+    }
+    const bool clustering = alg >= PCX_ALG_KMEANS;
+    if (clustering && (world != 1 || (entry != 0 && entry != 3))) {
+        err = "the clustering algorithms run on one rank, through the consensus / lie_detector entries";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_KMEANS && (!p->kmeans_init || p->kmeans_k < 1 || p->kmeans_k > p->n_total ||
+                                  p->kmeans_k > 1024 || p->kmeans_restarts < 1)) {
+        err = "k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 1024), kmeans_restarts >= 1";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_KMEANS)
+        for (int64_t q = 0; q < (int64_t)p->kmeans_k * p->kmeans_restarts; q++)
+            if (p->kmeans_init[q] < 0 || p->kmeans_init[q] >= p->n_total) {
+                err = "kmeans_init rows must lie in [0, N)";
+                return PCX_EINVAL;
+            }
+    if (alg == PCX_ALG_HIERARCHICAL && std::isnan(p->hierarchy_threshold)) {
+        err = "hierarchy_threshold is NaN";
+        return PCX_EINVAL;
+    }
+    if (alg == PCX_ALG_COKURTOSIS && !p->aux_scores && entry != 4) {
+        err = "cokurtosis needs aux_scores";
+        return PCX_EINVAL;
+    }
+    if (!std::isfinite(p->catch_tolerance) || !std::isfinite(p->alpha)) {
+        err = "catch_tolerance / alpha must be finite";
+        return PCX_EINVAL;
+    }
+    if (p->mem_kind != PCX_MEM_DEVICE && p->mem_kind != PCX_MEM_HOST) {
+        err = "mem_kind must be PCX_MEM_DEVICE or PCX_MEM_HOST";
+        return PCX_EINVAL;
+    }
+    return 0;
+}
+
 int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const double* scores_in, int rank_rule,
                double* nc_out, std::string& err) {
     if (!p || !r) {
@@ -593,53 +645,17 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         err = "row_offset / n_total inconsistent with n_rows and the context's world";
         return PCX_EINVAL;
     }
-    if (p->scaled && (!p->lo || !p->hi)) {
-        err = "scaled given without lo / hi";
-        return PCX_EINVAL;
-    }
+    if (const int rc = check_problem(p, world, entry, err)) return rc;
     const int alg = p->algorithm;
-    if (alg < PCX_ALG_PCA || alg > PCX_ALG_CLUSTERFECK) {
-        err = "algorithm must be an enum pcx_algorithm value (0..7)";
-        return PCX_EINVAL;
-    }
     const bool clustering = alg >= PCX_ALG_KMEANS;
-    if (clustering && (world != 1 || (entry != 0 && entry != 3))) {
-        err = "the clustering algorithms run on one rank, through the consensus / lie_detector entries";
-        return PCX_EINVAL;
-    }
-    if (alg == PCX_ALG_KMEANS && (!p->kmeans_init || p->kmeans_k < 1 || p->kmeans_k > n_rows ||
-                                  p->kmeans_k > 1024 || p->kmeans_restarts < 1)) {
-        err = "k-means needs kmeans_init and 1 <= kmeans_k <= min(N, 1024), kmeans_restarts >= 1";
-        return PCX_EINVAL;
-    }
-    if (alg == PCX_ALG_KMEANS)
-        for (int64_t q = 0; q < (int64_t)p->kmeans_k * p->kmeans_restarts; q++)
-            if (p->kmeans_init[q] < 0 || p->kmeans_init[q] >= n_rows) {
-                err = "kmeans_init rows must lie in [0, N)";
-                return PCX_EINVAL;
-            }
-    if (alg == PCX_ALG_HIERARCHICAL && std::isnan(p->hierarchy_threshold)) {
-        err = "hierarchy_threshold is NaN";
-        return PCX_EINVAL;
-    }
-    if (alg == PCX_ALG_COKURTOSIS && !p->aux_scores && entry != 4) {
-        err = "cokurtosis needs aux_scores";
-        return PCX_EINVAL;
-    }
-    if (!std::isfinite(p->catch_tolerance) || !std::isfinite(p->alpha)) {
-        err = "catch_tolerance / alpha must be finite";
-        return PCX_EINVAL;
-    }
-    if (p->mem_kind != PCX_MEM_DEVICE && p->mem_kind != PCX_MEM_HOST) {
-        err = "mem_kind must be PCX_MEM_DEVICE or PCX_MEM_HOST";
-        return PCX_EINVAL;
-    }
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) {
         err = std::string("hipSetDevice: ") + hipGetErrorString(he);
         return PCX_EHIP;
     }
     Run R{c, c->stream, err, c->comm, world, rank, {}, {}};
+    c->progress_stage.store(-1, std::memory_order_relaxed);
+    c->progress_wait.store(0, std::memory_order_relaxed);
     const bool host = p->mem_kind == PCX_MEM_HOST;
     const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
     try {

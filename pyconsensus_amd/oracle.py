@@ -164,9 +164,18 @@ class Oracle(object):
         aux = None
         if self.algorithm == "cokurtosis":
             aux = np.asarray(self.aux["cokurt"], dtype=np.float64).ravel()
-        outs, meta = lie_detector_host(F, self._rep_raw, device_index=self._device_index(), aux_scores=aux,
-                                       **self._kw())
+        kw = self._kw()
+        if self.algorithm in _abi.CLUSTER_ALGORITHMS:
+            # nc from the clusters (:392-424) on one GPU: the clusterings do not shard
+            if self.devices is not None and len(set(self.devices)) > 1:
+                raise NotImplementedError("the clustering algorithms run on one GPU; got devices=%r" % self.devices)
+            kw.update(algorithm=self.algorithm, devices=None, hierarchy_threshold=self.hierarchy_threshold)
+        elif self.algorithm not in _abi.ALGORITHMS:
+            raise NotImplementedError("algorithm %r is not on the GPU path" % (self.algorithm,))
+        outs, meta = lie_detector_host(F, self._rep_raw, device_index=self._device_index(), aux_scores=aux, **kw)
         self.convergence = self.algorithm != "absolute"
+        if self.algorithm == "clusterfeck":  # cluster() rewrites zero tokens in the caller's list (:202-204)
+            self.reptokens = [0.00001 if t == 0 else t for t in self.reptokens]
         self.last_info = {"branch": meta["branch"], "path": "matrix"}
         ma = np.ma.masked_array if self.algorithm == "PCA" else np.asarray
         return {"first_loading": np.ma.masked_array(outs["adj_first_loadings"]),

@@ -173,6 +173,15 @@ class CallbackComm(_OwnedCtx):
         return self._ctx
 
 
+def progress(comm, device_index):
+    """Where the single-matrix call running on ``comm``'s context is (callable from another
+    thread while it runs): ``(stage name or None, host_waiting)`` (pcx_ctx_progress)."""
+    st, wt = C.c_int(-1), C.c_int(0)
+    _lib.check(_lib.lib().pcx_ctx_progress(comm.context(device_index), C.byref(st), C.byref(wt)))
+    name = _lib.lib().pcx_stage_name(st.value).decode() if st.value >= 0 else None
+    return name, bool(wt.value)
+
+
 def shard_rows(N, world, rank):
     """Contiguous row block of ``rank``: (offset, count); remainder rows go to the first ranks."""
     base, rem = divmod(int(N), int(world))
@@ -339,7 +348,12 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
         outs[k] = np.empty(shape, dtype=np.float64)
         setattr(res, k, outs[k].ctypes.data)
     h = _lib.context(device_index) if devices is None else _lib.devices_context(devices)
-    _lib.check(getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res)))
+    rc = getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res))
+    if rc == _lib.PCX_ECOMM and devices is not None:  # the failed call aborted the context's communicators
+        err = _lib.PcxError("libpcx error %d: %s" % (rc, _lib.lib().pcx_last_error().decode(errors="replace")))
+        _lib.drop_devices_context(devices)
+        raise err
+    _lib.check(rc)
     return outs, _meta(res, algorithm)
 
 

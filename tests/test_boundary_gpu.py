@@ -138,6 +138,26 @@ def test_oracle_devices_matches_one_gpu(gpu_lib):
         Oracle(reports=np.ones((66, 2)), devices=[0] * 70).lie_detector(np.ones((66, 2)))
 
 
+def test_devices_context_survives_a_failed_call(gpu_lib):
+    """A bad argument on a multi-device context (non-finite catch_tolerance, cokurtosis
+    without aux scores) fails before any worker starts -- no abort of the context's
+    exchange -- and the next call on the same cached context succeeds with the one-device
+    result."""
+    from pyconsensus_amd import _lib, synthetic
+    from pyconsensus_amd.pipeline import consensus_host
+
+    R, sc, lo, hi, rep = synthetic.matrix(500, 40, seed=21)
+    with pytest.raises(_lib.PcxError, match="catch_tolerance"):
+        consensus_host(R, rep, sc, lo, hi, devices=[0, 0], catch_tolerance=float("nan"))
+    with pytest.raises(_lib.PcxError, match="aux_scores"):
+        consensus_host(R, rep, sc, lo, hi, devices=[0, 0], algorithm="cokurtosis")
+    two, m2 = consensus_host(R, rep, sc, lo, hi, devices=[0, 0])
+    one, m1 = consensus_host(R, rep, sc, lo, hi)
+    assert m2["branch"] == m1["branch"]
+    np.testing.assert_array_equal(two["outcomes_final"], one["outcomes_final"])
+    np.testing.assert_allclose(two["smooth_rep"], one["smooth_rep"], rtol=1e-9, atol=1e-12)
+
+
 def _small_oracles(name):
     from oracle.pcx_oracle import OracleCPU
     from pyconsensus_amd import Oracle, synthetic

@@ -189,3 +189,32 @@ def test_oracle_clusters_refuse_sharding(gpu_lib):
     g = ThreadGroup(2)
     with pytest.raises(_lib.PcxError, match="one rank"):
         consensus_matrix(R, None, algorithm="hierarchical", comm=ThreadComm(g, 0), n_total=100, row_offset=0)
+
+
+@pytest.mark.parametrize("name", ["readme@k-means", "readme@hierarchical", "readme@clusterfeck", "t3@k-means",
+                                  "s007@k-means", "s010@clusterfeck", "s011@hierarchical"])
+def test_lie_detector_stage_with_clustering(gpu_lib, name):
+    """Oracle(algorithm=<clustering>).lie_detector(filled) (__init__.py:392-424): nc from the
+    clusters, scores left at zeros (:357), this_rep / smooth_rep as in the reference golden
+    (the golden's own filled matrix as input; numpy's global RandomState seeded alike)."""
+    from pyconsensus_amd import Oracle
+
+    case = G.clusters()[name]
+    kw = G.oracle_args(case)
+    kw.update(G.cluster_kwargs(case))
+    o = Oracle(**kw)
+    np.random.seed(int(case["in_np_seed"]))
+    out = o.lie_detector(np.array(case["filled"], dtype=np.float64))
+    assert np.all(np.asarray(out["scores"]) == 0.0)
+    assert not isinstance(out["this_rep"], np.ma.MaskedArray)
+    for k in ("this_rep", "smooth_rep"):
+        np.testing.assert_allclose(np.asarray(out[k], dtype=np.float64), case["agents." + k], rtol=1e-9, atol=1e-12,
+                                   err_msg="%s %s" % (name, k))
+    assert o.convergence is True
+
+
+def test_lie_detector_clustering_refuses_several_devices(gpu_lib):
+    from pyconsensus_amd import Oracle
+
+    with pytest.raises(NotImplementedError, match="one GPU"):
+        Oracle(reports=np.ones((80, 40)), algorithm="hierarchical", devices=[0, 1]).lie_detector(np.ones((80, 40)))
