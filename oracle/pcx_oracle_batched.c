@@ -222,8 +222,14 @@ static double wmedian(const double* x, const double* w, int n) {
     return xs[k - 1];
 }
 
-static void rank_avg(const double* v, int n, double* r) {  /* scipy.stats.rankdata 'average' */
+/* scipy.stats.rankdata 'average'; a NaN ranks NaN, so the rule's sums are NaN when any value
+ * is (rankdata's nan_policy='propagate' makes every rank NaN: the same sums) */
+static void rank_avg(const double* v, int n, double* r) {
     for (int j = 0; j < n; j++) {
+        if (isnan(v[j])) {
+            r[j] = NAN;
+            continue;
+        }
         int lt = 0, eq = 0;
         for (int k = 0; k < n; k++) {
             lt += v[k] < v[j];

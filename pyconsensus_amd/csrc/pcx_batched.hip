@@ -525,6 +525,7 @@ __device__ __forceinline__ double rank_avg(const double* v, int E) {
             eq += y == x;
         }
         r = (double)lt + (double)(eq + 1) * 0.5;
+        if (__builtin_isnan(x)) r = __builtin_nan("");  // rankdata propagates NaN: the rule's sums go NaN
     }
     return r;
 }

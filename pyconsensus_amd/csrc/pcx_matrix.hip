@@ -1809,6 +1809,12 @@ __global__ void __launch_bounds__(BT) k_ranks(pcx_mat m, const int* cnt) {
         const int* q = cnt + (int64_t)c * 6;
         const double r0 = q[0] + (q[1] + 1) * 0.5, r1 = q[2] + (q[3] + 1) * 0.5, r2 = q[4] + (q[5] + 1) * 0.5;
         e = fabs(r1 - r0) - fabs(r2 - r0);
+        // rankdata propagates NaN (every rank NaN): any NaN value makes the rule's sum NaN,
+        // which the decision reads as "not < 0" (set2), as the reference does
+        const double* ev = m.ev;
+        if (__builtin_isnan(ev[EV_OLD * E + c]) || __builtin_isnan(ev[EV_D1 * E + c]) ||
+            __builtin_isnan(ev[EV_D2 * E + c]))
+            e = __builtin_nan("");
     }
     red[threadIdx.x] = e;
     __syncthreads();

@@ -1162,8 +1162,10 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
                 const double r0 = (double)lt0 + (double)(eq0 + 1) * 0.5;
                 const double r1 = (double)lt1 + (double)(eq1 + 1) * 0.5;
                 const double r2 = (double)lt2 + (double)(eq2 + 1) * 0.5;
-                VEp(VE_E1)[j] = fabs(r1 - r0);
-                VEp(VE_E2)[j] = fabs(r2 - r0);
+                // rankdata propagates NaN (every rank NaN): a NaN value makes the rule's sums NaN
+                const bool nan = __builtin_isnan(o) || __builtin_isnan(v1) || __builtin_isnan(v2);
+                VEp(VE_E1)[j] = nan ? __builtin_nan("") : fabs(r1 - r0);
+                VEp(VE_E2)[j] = nan ? __builtin_nan("") : fabs(r2 - r0);
             }
             __syncthreads();
             if (tid == 0)

@@ -77,7 +77,10 @@ def _big_case(name):
     C4: BASELINE config C4 exactly as SURVEY.md 8(d) specifies it -- 100k x 1k, integer
     reputations U[1, 99], seed 2 -- so exact-half weighted-median prefixes occur and must be
     resolved the reference's way.  C5r: the C5 recipe (GPU generator, seed 3, eight shards,
-    reputation=None: every interpolation weight of a column is the same double) at 250k x 1024."""
+    reputation=None: every interpolation weight of a column is the same double) at 250k x 1024.
+    C5r_1M: the same recipe at C5's own row count, 1M x 1024 -- there every token is
+    int(1e-6 * 1e6) = 1 (__init__.py:146) and every median is a 1M-row equal-weight walk
+    (:303, :520-523); the restatement needs ~60 GB of host memory and a few minutes."""
     if name in _REF:
         return _REF[name]
     from oracle.pcx_oracle import OracleCPU
@@ -85,10 +88,11 @@ def _big_case(name):
 
     if name == "C4":
         R, sc, lo, hi, rep = synthetic.matrix(100_000, 1000, seed=2)
-    elif name == "C5r":
+    elif name in ("C5r", "C5r_1M"):
         import torch
 
-        Rd, scd, lod, hid, _ = synthetic.matrix_device(250_000, 1024, seed=3, n_shards=8, device="cuda:0")
+        N = 250_000 if name == "C5r" else 1_000_000
+        Rd, scd, lod, hid, _ = synthetic.matrix_device(N, 1024, seed=3, n_shards=8, device="cuda:0")
         R, sc, lo, hi, rep = Rd.cpu().numpy(), scd.cpu().numpy().astype(bool), lod.cpu().numpy(), hid.cpu().numpy(), None
         del Rd
         torch.cuda.empty_cache()
@@ -99,6 +103,21 @@ def _big_case(name):
     ref = G.flat_result(OracleCPU(reports=R, event_bounds=b, reputation=rep).consensus())
     _REF[name] = (R, sc, lo, hi, rep, ref)
     return _REF[name]
+
+
+def _record(name, world, info):
+    """Keep the large cases' selection statistics (n_hard, sel_passes) beside the run's logs."""
+    import json
+    import os
+
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "large_cases.jsonl"), "a") as f:
+            f.write(json.dumps({"case": name, "world": world, "n_hard": info.get("n_hard"),
+                                "sel_passes": info.get("sel_passes"), "branch": info.get("branch")}) + "\n")
+    except OSError:
+        pass
 
 
 def _flat_gpu(ev, ag, meta):
@@ -151,8 +170,10 @@ def _abi_events():
     return _abi.MAT_OUTPUT_EVENTS
 
 
-@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), "C4", "C5r"],
-                         ids=["3000x150", "20000x400", "C4_100k_x_1k_intrep", "C5recipe_250k_x_1024_repNone"])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), "C4", "C5r", "C5r_1M"],
+                         ids=["3000x150", "20000x400", "C4_100k_x_1k_intrep", "C5recipe_250k_x_1024_repNone",
+                              "C5r_1M_x_1024_repNone"])
 @pytest.mark.parametrize("world", [1, 2])
 def test_matrix_vs_numpy_oracle(gpu_lib, case, world):
     """Against the numpy restatement run on the box, no exemption: binary outcomes and the
@@ -171,6 +192,10 @@ def test_matrix_vs_numpy_oracle(gpu_lib, case, world):
     print(case, world, {k: info[k] for k in ("n_hard", "sel_passes") if k in info})
     bad, sign = P.compare(ref, ours)
     assert not bad, bad
+    if case == "C5r_1M":
+        if world == 1:  # the drop-in's tokens: int(1e-6 * 1e6) = 1 for every reporter (:146)
+            assert set(o.reptokens) == {1}
+        _record("C5r_1M", world, info)
 
 
 def test_virtual_shards_match_single(gpu_lib):
