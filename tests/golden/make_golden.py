@@ -15,7 +15,7 @@ applies the harness of SURVEY.md Appendix A in memory:
    dependency, ``requirements.txt:2``), restating the published pure-Python
    ``weighted_median``.
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [algos | clusters | medium]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -635,6 +635,43 @@ def clusters_main(ref):
     print("clusters: %d cases" % len(cases))
 
 
+def medium_main(ref):
+    """Rounds of 100 x 50, 250 x 60 and 256 x 64 (the workgroup-per-round kernel's shapes,
+    csrc/pcx_medium.hip), 40 each, PCA, from the reference itself.  Only OUTPUTS are stored
+    (plus a checksum of the regenerated inputs): the reports come from medium_inputs(), and
+    the filled matrix is stored as its per-column fill value (every missing cell of a column
+    takes the same guess, :310-312), which with the inputs gives it back exactly."""
+    import hashlib
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from golden_cases import MEDIUM_SHAPES, medium_inputs
+
+    out = {}
+    for N, E in MEDIUM_SHAPES:
+        R, sc, lo, hi, rep, uniform = medium_inputs(N, E)
+        from pyconsensus_amd import synthetic
+
+        for b in range(R.shape[0]):
+            d = run_case(ref, R[b], synthetic.bounds_list(sc[b], lo[b], hi[b]), None if uniform[b] else rep[b])
+            X, F = d.pop("original"), d.pop("filled")
+            miss = np.isnan(X) | (X == 0.0)
+            fill = np.full(E, np.nan)
+            for j in np.nonzero(miss.any(axis=0))[0]:
+                vals = F[miss[:, j], j]
+                assert np.all((vals == vals[0]) | (np.isnan(vals) & np.isnan(vals[0])))
+                fill[j] = vals[0]
+            d["fill_value"] = fill
+            d["in_sha256"] = np.array(hashlib.sha256(np.ascontiguousarray(d.pop("in_reports")).tobytes()).hexdigest())
+            for k in [k for k in d if k.startswith("in_") and k not in ("in_sha256", "in_has_rep", "in_has_bounds",
+                                                                        "in_catch_tolerance", "in_alpha",
+                                                                        "in_int_dtype", "in_algorithm")]:
+                del d[k]  # regenerated with the reports
+            for k, v in d.items():
+                out["w%dx%d_%02d/%s" % (N, E, b, k)] = v
+        print("medium %dx%d: %d rounds" % (N, E, R.shape[0]))
+    np.savez_compressed(os.path.join(HERE, "medium.npz"), **out)
+
+
 def split_keys(flat):
     res = {}
     for k, v in flat.items():
@@ -648,5 +685,7 @@ if __name__ == "__main__":
         algos_main(load_reference())
     elif len(sys.argv) > 1 and sys.argv[1] == "clusters":
         clusters_main(load_reference())
+    elif len(sys.argv) > 1 and sys.argv[1] == "medium":
+        medium_main(load_reference())
     else:
         main()

@@ -106,3 +106,50 @@ def cluster_kwargs(case):
     """Extra constructor kwargs of a clusters.npz case (k-means also needs numpy's global
     RandomState seeded with case['in_np_seed'] before the call)."""
     return {"hierarchy_threshold": float(case["in_hierarchy_threshold"])}
+
+
+# --- the workgroup-per-round golden set (make_golden.py medium_main) -------------------
+MEDIUM_SHAPES = ((100, 50), (250, 60), (256, 64))
+MEDIUM_ROUNDS = 40
+
+
+def medium_inputs(N, E):
+    """The seeded inputs of the medium golden set (synthetic.rounds: numpy's default_rng,
+    identical on any host); every third round with reputation=None."""
+    from pyconsensus_amd import synthetic
+
+    R, sc, lo, hi, rep = synthetic.rounds(MEDIUM_ROUNDS, N, E, seed=5000 + N + E)
+    uniform = np.arange(MEDIUM_ROUNDS) % 3 == 2
+    return R, sc, lo, hi, rep, uniform
+
+
+def medium():
+    """{shape: [case, ...]} of medium.npz with the inputs regenerated (checked against the
+    stored sha256) and the original / filled matrices rebuilt exactly: original = the
+    reference's rescale (:266-269), filled = original with every missing cell of a column
+    set to that column's stored fill value (:310-312)."""
+    import hashlib
+
+    flat = split_cases(load("medium.npz"))
+    out = {}
+    for N, E in MEDIUM_SHAPES:
+        R, sc, lo, hi, rep, uniform = medium_inputs(N, E)
+        cases = []
+        for b in range(R.shape[0]):
+            c = dict(flat["w%dx%d_%02d" % (N, E, b)])
+            X = np.array(R[b], dtype=np.float64)
+            assert hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest() == str(c["in_sha256"])
+            c["in_reports"] = X.copy()
+            c["in_scaled"], c["in_lo"], c["in_hi"] = sc[b].astype(bool), lo[b], hi[b]
+            if not uniform[b]:
+                c["in_reputation"] = rep[b]
+            for j in np.nonzero(sc[b])[0]:
+                X[:, j] = (X[:, j] - lo[b][j]) / float(hi[b][j] - lo[b][j])
+            miss = np.isnan(X) | (X == 0.0)
+            F = X.copy()
+            for j in np.nonzero(miss.any(axis=0))[0]:
+                F[miss[:, j], j] = c["fill_value"][j]
+            c["original"], c["filled"] = X, F
+            cases.append(c)
+        out[(N, E)] = cases
+    return out

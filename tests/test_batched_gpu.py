@@ -188,6 +188,32 @@ def test_medium_rounds_bitexact_vs_spec(gpu_lib, variant):
         assert not bad, (b, bad)
 
 
+@pytest.mark.parametrize("shape", [(100, 50), (250, 60), (256, 64)], ids=["100x50", "250x60", "256x64"])
+def test_medium_rounds_vs_reference_goldens(gpu_lib, shape):
+    """The workgroup-per-round kernel on rounds the REFERENCE computed (tests/golden/medium.npz:
+    40 rounds each of 100 x 50, 250 x 60, 256 x 64, a third with reputation=None): every output
+    within the north_star tolerances, fills and outcomes exact, branch codes equal."""
+    import torch
+    from pyconsensus_amd.batched import consensus_batched
+
+    cases = G.medium()[shape]
+    observed, ran = {}, []
+    for uniform in (False, True):
+        idx = [i for i, c in enumerate(cases) if ("in_reputation" not in c) == uniform]
+        st = lambda k: np.stack([cases[i][k] for i in idx])
+        g = _np(consensus_batched(st("in_reports"), None if uniform else st("in_reputation"), st("in_scaled"),
+                                  st("in_lo"), st("in_hi"), filled=True, original=True))
+        torch.cuda.synchronize()
+        for t, i in enumerate(idx):
+            name = "w%dx%d_%02d" % (shape[0], shape[1], i)
+            ran.append(name)
+            kind, _ = P.mismatch_kind(cases[i], {k: v[t] for k, v in g.items()})
+            if kind:
+                observed[name] = kind
+    assert len(ran) == len(cases)
+    P.assert_known("exact", observed, ran)
+
+
 @pytest.mark.parametrize("variant", ["1x40", "2x33", "3x64_uniform", "7x50_nobounds", "9x35_absolute",
                                      "33x64_shared", "64x33_int", "65x2", "129x3", "255x63", "256x1_uniform",
                                      "5x40_big-five", "40x34_fixed-variance"])

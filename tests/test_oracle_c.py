@@ -99,3 +99,33 @@ def test_spec256_matches_numpy_restatement(N, E, uniform):
                                       reputation=None if rep is None else rep[b]).consensus())
         bad, _ = P.compare(ref, {k: v[b] for k, v in o.items()})
         assert not bad, (b, bad)
+
+
+def _medium_batch(cases, uniform):
+    idx = [i for i, c in enumerate(cases) if ("in_reputation" not in c) == uniform]
+    st = lambda k: np.stack([cases[i][k] for i in idx])
+    rep = None if uniform else st("in_reputation")
+    return idx, st("in_reports"), st("in_scaled"), st("in_lo"), st("in_hi"), rep
+
+
+@pytest.mark.parametrize("shape", [(100, 50), (250, 60), (256, 64)], ids=["100x50", "250x60", "256x64"])
+def test_spec256_vs_reference_medium_goldens(shape):
+    """The 256-reporter SPEC (the workgroup-per-round kernel's bitwise target) against rounds the
+    REFERENCE computed at 100 x 50, 250 x 60 and 256 x 64 (tests/golden/medium.npz; at the two
+    larger shapes N*E >= 9216, where the reference's dgemv is multi-threaded): no mismatch,
+    branch codes included."""
+    import golden_cases as G
+
+    cases = G.medium()[shape]
+    observed, ran = {}, []
+    for uniform in (False, True):
+        idx, R, sc, lo, hi, rep = _medium_batch(cases, uniform)
+        o = OC.batched(R, sc, lo, hi, rep, threads=8)
+        for t, i in enumerate(idx):
+            name = "w%dx%d_%02d" % (shape[0], shape[1], i)
+            ran.append(name)
+            kind, _ = P.mismatch_kind(cases[i], {k: v[t] for k, v in o.items()})
+            if kind:
+                observed[name] = kind
+    assert len(ran) == len(cases)
+    P.assert_known("exact", observed, ran)

@@ -49,6 +49,14 @@ def test_c2():
     _check(case, OracleCPU(**G.oracle_args(case)).consensus())
 
 
+@pytest.mark.parametrize("shape", G.MEDIUM_SHAPES, ids=["%dx%d" % s for s in G.MEDIUM_SHAPES])
+def test_medium_shapes(shape):
+    """Rounds of the workgroup-per-round shapes, 40 each (medium.npz, reference-generated):
+    at 250 x 60 and 256 x 64 (N*E >= 9216) the reference's np.dot is multi-threaded OpenBLAS."""
+    for case in G.medium()[shape]:
+        _check(case, OracleCPU(**G.oracle_args(case)).consensus())
+
+
 def test_weighted_median_branches():
     # dominant weight
     assert weighted_median([5.0, 1.0, 3.0], [0.1, 0.7, 0.2]) == 1.0
