@@ -2373,7 +2373,11 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const bool gin = gties && gk >= lo && gk <= hi;
     const uint64_t ties_all = gin ? (uint64_t)m.ev[EV_MISS * m.n_events + m.scaled_cols[s]] : 0;  // all ranks
     const uint64_t need = st[SW_INRANGE] > ties_all ? st[SW_INRANGE] - ties_all : 0;
-    const bool gather = !from_buf && m.cbuf && st[SW_INRANGE] > 0 && need <= (uint64_t)m.ccap;
+    // gather only once the range has narrowed: later passes then read 16 B per in-range element
+    // instead of the column, which pays when the range holds a small part of it (a shard whose
+    // whole column fits cbuf would otherwise gather everything and re-read it per pass)
+    const bool gather = !from_buf && m.cbuf && st[SW_INRANGE] > 0 && need <= (uint64_t)m.ccap &&
+                        8 * need <= st[SW_COUNT];
     uint64_t* cb = m.cbuf ? m.cbuf + (int64_t)s * m.ccap * 2 : nullptr;
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh);

@@ -139,8 +139,8 @@ def test_oracle_devices_matches_one_gpu(gpu_lib):
 
 
 def test_devices_context_survives_a_failed_call(gpu_lib):
-    """A bad argument on a multi-device context (non-finite catch_tolerance, cokurtosis
-    without aux scores) fails before any worker starts -- no abort of the context's
+    """A bad argument on a multi-device context (non-finite catch_tolerance, a clustering
+    algorithm on several ranks) fails before any worker starts -- no abort of the context's
     exchange -- and the next call on the same cached context succeeds with the one-device
     result."""
     from pyconsensus_amd import _lib, synthetic
@@ -149,8 +149,8 @@ def test_devices_context_survives_a_failed_call(gpu_lib):
     R, sc, lo, hi, rep = synthetic.matrix(500, 40, seed=21)
     with pytest.raises(_lib.PcxError, match="catch_tolerance"):
         consensus_host(R, rep, sc, lo, hi, devices=[0, 0], catch_tolerance=float("nan"))
-    with pytest.raises(_lib.PcxError, match="aux_scores"):
-        consensus_host(R, rep, sc, lo, hi, devices=[0, 0], algorithm="cokurtosis")
+    with pytest.raises(_lib.PcxError, match="one rank"):
+        consensus_host(R, rep, sc, lo, hi, devices=[0, 0], algorithm="hierarchical")
     two, m2 = consensus_host(R, rep, sc, lo, hi, devices=[0, 0])
     one, m1 = consensus_host(R, rep, sc, lo, hi)
     assert m2["branch"] == m1["branch"]
