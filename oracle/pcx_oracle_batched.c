@@ -42,7 +42,7 @@
 #define PI_PRESQUARE 3
 #define PI_SQUARE_EVERY 32
 #define PI_MAX_SQUARINGS 8
-#define PI_POLISH 4
+#define PI_POLISH 2
 
 /* numpy pairwise summation (umath loops_utils pairwise_sum, PW_BLOCKSIZE 128),
  * as np.add.reduce uses it for a contiguous 1-D array of <= 8192 elements. */

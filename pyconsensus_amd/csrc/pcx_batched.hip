@@ -38,7 +38,7 @@ constexpr int PI_MAXIT = 256;
 constexpr int PI_PRESQUARE = 3;
 constexpr int PI_SQUARE_EVERY = 32;
 constexpr int PI_MAX_SQUARINGS = 8;
-constexpr int PI_POLISH = 4;
+constexpr int PI_POLISH = 2;
 constexpr double DBL_MIN_ = 2.2250738585072014e-308;
 constexpr double DBL_EPS = 2.220446049250313080847e-16;
 
@@ -511,6 +511,27 @@ __device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel
     return ox[k - 1];
 }
 
+
+// the N x E round in LDS (row pitch ES) -> dst [N][E] row-major, lane-contiguous: each store
+// instruction covers 64 consecutive elements (16-byte pairs when N * E is even and the
+// shape is compiled in)
+__device__ __forceinline__ void round_to_global(double* dst, const double* F, int N, int E, int ES, int NT, int ET) {
+    const int l = lane_id();
+    if (NT > 0 && ET > 0 && (NT * ET) % 2 == 0 && ((uintptr_t)dst & 15) == 0) {
+        const int tot2 = NT * ET / 2;
+        for (int q = l; q < tot2; q += W) {
+            const int idx = 2 * q;
+            const int i0 = idx / ET, j0 = idx - i0 * ET;
+            const int i1 = (idx + 1) / ET, j1 = idx + 1 - i1 * ET;
+            reinterpret_cast<double2*>(dst)[q] = double2{F[i0 * ES + j0], F[i1 * ES + j1]};
+        }
+    } else {
+        for (int idx = l; idx < N * E; idx += W) {
+            const int i = idx / E, j = idx - i * E;
+            dst[idx] = F[i * ES + j];
+        }
+    }
+}
 
 // scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
 __device__ __forceinline__ double rank_avg(const double* v, int E) {
@@ -1243,7 +1264,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                 if (a.int_dtype) x = trunc(x);
                 S.F[l * ES + j] = x;
             }
+#ifdef PCX_X_COLWRITES
             if (a.original) a.original[(b * N + l) * E + j] = x;
+#endif
         }
         const uint64_t nm = ballot(row && __builtin_isnan(x));
         const uint64_t zm = ballot(row && x == 0.0);
@@ -1253,6 +1276,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         }
     }
     wsync();
+#ifndef PCX_X_COLWRITES
+    // result["original"] (the rescaled reports), from LDS in row-major order: every store
+    // instruction writes 64 consecutive doubles (whole lines), not one column's 50 strided ones
+    if (a.original) round_to_global(a.original + b * (int64_t)N * E, S.F, N, E, ES, NT, ET);
+#endif
 
     STAMP(2);
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
@@ -1354,8 +1382,12 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         }
     }
     wsync();
+#ifdef PCX_X_COLWRITES
     if (a.filled && row)
         for (int j = 0; j < E; j++) a.filled[(b * N + l) * E + j] = S.F[l * ES + j];
+#else
+    if (a.filled) round_to_global(a.filled + b * (int64_t)N * E, S.F, N, E, ES, NT, ET);
+#endif
 
     STAMP(3);
     // ---- old = rep . F (np.dot) -------------------------------------------

@@ -25,6 +25,9 @@ typedef struct {
     double  catch_tolerance, alpha;
     int32_t n_scaled;             /* number of scaled events                      */
     int32_t sel_phase;            /* 1: interpolation medians, 2: outcome medians */
+    int32_t sel_first;            /* the selection's first histogram pass: over the column's whole key
+                                     range (known from M_COLSTATS / the fill), also collecting the
+                                     totals, weight extremes and fill-row sums (no separate init pass) */
     int32_t col_blocks;           /* row chunks of the column passes (G)          */
     int32_t cov_tiles, cov_kslices;
     int32_t no_fill;              /* reports are already filled (stage entries): no NA fill */

@@ -2101,83 +2101,47 @@ __global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
     if (m.sel_phase == 2 || need) m.hard[c] = HARD_NONE;
 }
 
-// PCX selection init: this rank's exact total weight (limbs), count, key range, min / max weight
-__global__ void __launch_bounds__(BT) k_sel_init(pcx_mat m) {
-    const int s = blockIdx.x;
-    uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    if (st[SW_STATUS] != 1) return;
-    __shared__ unsigned long long la, lb, lc, kmin, kmax, cnt, wminb, wmaxb, ga_s, gb_s, gc_s, gn_s;
-    if (threadIdx.x == 0) {
-        la = lb = lc = cnt = 0;
-        ga_s = gb_s = gc_s = gn_s = 0;
-        kmin = ~0ull;
-        kmax = 0;
-        wminb = ~0ull;
-        wmaxb = 0;  // weights are >= 0 and order like their bit patterns
-    }
-    __syncthreads();
-    uint64_t a = 0, b = 0, c = 0, mn = ~0ull, mx = 0, n = 0, wlo = ~0ull, whi = 0;
-    uint64_t ga = 0, gb = 0, gc = 0, gn = 0;
-    rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
-                             [&](int64_t, XW v) {
-                                 double x, w;
-                                 if (!sel_decode(m, s, v, x, w)) return;
-                                 const limbs3 L = to_limbs(w);
-                                 a += L.l0;
-                                 b += L.l1;
-                                 c += L.l2;
-                                 if (m.sel_phase == 2 && __builtin_isnan(v.x)) {
-                                     ga += L.l0;
-                                     gb += L.l1;
-                                     gc += L.l2;
-                                     gn++;
-                                 }
-                                 const uint64_t k = dkey(x);
-                                 mn = k < mn ? k : mn;
-                                 mx = k > mx ? k : mx;
-                                 const uint64_t wb = (uint64_t)__double_as_longlong(w);
-                                 wlo = wb < wlo ? wb : wlo;
-                                 whi = wb > whi ? wb : whi;
-                                 n++;
-                             });
-    atomicAdd(&la, (unsigned long long)a);
-    atomicAdd(&lb, (unsigned long long)b);
-    atomicAdd(&lc, (unsigned long long)c);
-    atomicAdd(&cnt, (unsigned long long)n);
-    atomicMin(&kmin, (unsigned long long)mn);
-    atomicMax(&kmax, (unsigned long long)mx);
-    atomicMin(&wminb, (unsigned long long)wlo);
-    atomicMax(&wmaxb, (unsigned long long)whi);
-    if (gn) {
-        atomicAdd(&ga_s, (unsigned long long)ga);
-        atomicAdd(&gb_s, (unsigned long long)gb);
-        atomicAdd(&gc_s, (unsigned long long)gc);
-        atomicAdd(&gn_s, (unsigned long long)gn);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        st[SW_GN] = gn_s;  // this rank's only: added to its own histograms
-        st[SW_GW0] = ga_s;
-        st[SW_GW1] = gb_s;
-        st[SW_GW2] = gc_s;
-        // limbs stay unnormalised here (carries are exact under the cross-rank SUM)
-        m.sel_isum[s * 4 + 0] = la;
-        m.sel_isum[s * 4 + 1] = lb;
-        m.sel_isum[s * 4 + 2] = lc;
-        m.sel_isum[s * 4 + 3] = cnt;
-        m.sel_imin[s * 2 + 0] = kmin;
-        m.sel_imin[s * 2 + 1] = wminb;
-        m.sel_imax[s * 2 + 0] = kmax;
-        m.sel_imax[s * 2 + 1] = wmaxb;
-    }
-}
-
 __device__ __forceinline__ int shift_for(uint64_t lo, uint64_t hi) {
     const uint64_t d = hi - lo;
     if (d == 0) return 0;
     const int bits = 64 - __clzll(d);
     return bits > 8 ? bits - 8 : 0;
 }
+
+// PCX selection init: the key range of every needed event without reading the column --
+// phase 1: the present values' extremes (M_COLSTATS, all ranks); phase 2: those and the fill
+// value (every missing row takes it, :310-312).  The first histogram pass (sel_first) then
+// covers that range and also collects what the reference's walk needs first: the exact total
+// weight, the count, the weight extremes and the filled rows' sums.  reputation=None in
+// phase 1: every weight is the same double, so that pass counts only (count mode).
+__global__ void __launch_bounds__(BT) k_sel_range(pcx_mat m) {
+    const int s = blockIdx.x * BT + threadIdx.x;
+    if (s >= m.n_scaled) return;
+    uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[SW_STATUS] != 1) return;
+    const int E = (int)m.n_events;
+    const int c = m.scaled_cols[s];
+    double mn = m.ev[EV_MINX * E + c], mx = m.ev[EV_MAXX * E + c];
+    if (m.sel_phase == 2 && m.ev[EV_MISS * E + c] > 0) {
+        const double g = m.ev[EV_GUESS * E + c];
+        if (!__builtin_isnan(g)) {
+            mn = fmin(mn, g);
+            mx = fmax(mx, g);
+        }
+    }
+    uint64_t lo = 1, hi = 0;  // no element: an empty range
+    if (mn <= mx) {
+        lo = dkey(mn);
+        hi = dkey(mx);
+    }
+    st[SW_LO] = lo;
+    st[SW_HI] = hi;
+    st[SW_SHIFT] = lo <= hi ? shift_for(lo, hi) : 0;
+    st[SW_INRANGE] = 0;  // (with SW_COUNT = 0: the first pass never compacts)
+    st[SW_COUNT] = 0;
+    st[SW_MODE] = (m.sel_phase == 1 && !m.rep_raw) ? 1 : 0;
+}
+
 
 __device__ __forceinline__ void mark_hard(const pcx_mat& m, int s, uint64_t* st) {
     st[SW_STATUS] = 3;
@@ -2187,15 +2151,37 @@ __device__ __forceinline__ void mark_hard(const pcx_mat& m, int s, uint64_t* st)
 // start: totals of all ranks (already reduced); empty / no positive weight -> None (NaN);
 // equal weights -> the reference's walk by pcx_seqsum.h, then a count selection; else the
 // dominant-weight test (:any(w > midpoint)) and the exact weight selection
+// The totals come from the first pass's histogram (all ranks, reduced): exact integer sums of
+// its bucket counts and weight limbs, the extreme keys of its buckets; one thread per event of
+// that pass (active index a), whose histogram row k_sel_step then narrows in the same pass.
 __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
-    const int s = blockIdx.x * BT + threadIdx.x;
-    if (s >= m.n_scaled) return;
+    const int a = blockIdx.x * BT + threadIdx.x;
+    if (a >= (int)m.info[IN_SEL_ACTIVE]) return;
+    const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     if (st[SW_STATUS] != 1) return;
-    const L3 tot = l3_norm({m.sel_isum[s * 4], m.sel_isum[s * 4 + 1], m.sel_isum[s * 4 + 2]});
-    const uint64_t n = m.sel_isum[s * 4 + 3];
-    const uint64_t kmin = m.sel_imin[s * 2], kmax = m.sel_imax[s * 2];
+    const bool wsum = st[SW_MODE] == 0;  // the first pass summed weight limbs
+    const int64_t o = (int64_t)a * NB;
+    uint64_t ta = 0, tb = 0, tc = 0, n = 0, kmin = ~0ull, kmax = 0;
+    for (int b = 0; b < NB; b++) {
+        const uint64_t c = m.hist_n[o + b];
+        if (!c) continue;
+        n += c;
+        if (wsum) {
+            ta += m.hist_w[(o + b) * 3 + 0];
+            tb += m.hist_w[(o + b) * 3 + 1];
+            tc += m.hist_w[(o + b) * 3 + 2];
+        }
+        kmin = m.hist_min[o + b] < kmin ? m.hist_min[o + b] : kmin;
+        kmax = m.hist_max[o + b] > kmax ? m.hist_max[o + b] : kmax;
+    }
     const uint64_t wminb = m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
+    // count mode known up front (equal weights): the total only needs to be nonzero
+    const L3 tot = wsum ? l3_norm({ta, tb, tc}) : L3{n && wmaxb ? 1ull : 0ull, 0, 0};
+    if (!wsum && wminb != wmaxb) {  // (cannot happen: reputation=None gives one weight) exact replay
+        mark_hard(m, s, st);
+        return;
+    }
     st_l3(st + SW_TOT0, tot);
     st_l3(st + SW_BELOW0, {0, 0, 0});
     st[SW_BELOW_MAX] = 0;
@@ -2203,9 +2189,7 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
     st[SW_CNT_BELOW] = 0;
     st[SW_WMAX] = wmaxb;
     st[SW_COUNT] = n;
-    st[SW_LO] = kmin;
-    st[SW_HI] = kmax;
-    st[SW_SHIFT] = shift_for(kmin, kmax);
+    // SW_LO / SW_HI / SW_SHIFT stay the first pass's (k_sel_step narrows that histogram)
     st[SW_INRANGE] = n;
     if (n == 0 || !(tot.a | tot.b | tot.c)) {  // weighted_median returns None -> NaN
         sel_done(st, __builtin_nan(""));
@@ -2352,17 +2336,28 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
 // sums / minima / maxima, so the compacted order does not matter).
 __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
+    if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB];
-    __shared__ unsigned long long gcount;
+    __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
         hmin[b] = ~0ull;
         hmax[b] = 0;
     }
-    if (threadIdx.x == 0) gcount = 0;
+    if (threadIdx.x == 0) {
+        gcount = 0;
+        f_wlo = ~0ull;
+        f_whi = 0;
+        f_ga = f_gb = f_gc = f_gn = 0;
+    }
     __syncthreads();
+    // first pass (sel_first): the weight extremes of every element, and in phase 2 the filled
+    // rows (all at the fill value) summed apart and binned once at the end
+    const bool first = m.sel_first != 0;
+    const bool gfirst = first && m.sel_phase == 2;
+    uint64_t wlo = ~0ull, whi = 0, ga = 0, gb = 0, gc = 0, gn = 0;
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
     const int sh = (int)st[SW_SHIFT];
     const bool wmode = st[SW_MODE] == 0;
@@ -2404,6 +2399,21 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             double x, w;
             if (gties && __builtin_isnan(v.x)) return;  // a filled row
             if (!sel_decode(m, s, v, x, w)) return;
+            if (first) {
+                const uint64_t wb = (uint64_t)__double_as_longlong(w);  // weights >= 0 order like their bits
+                wlo = wb < wlo ? wb : wlo;
+                whi = wb > whi ? wb : whi;
+                if (gfirst && __builtin_isnan(v.x)) {  // a filled row: summed here, binned once below
+                    if (wmode) {
+                        const limbs3 L = to_limbs(w);
+                        ga += L.l0;
+                        gb += L.l1;
+                        gc += L.l2;
+                    }
+                    gn++;
+                    return;
+                }
+            }
             const uint64_t k = dkey(x);
             if (k < lo || k > hi) return;
             bin(k, w);
@@ -2413,6 +2423,37 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
                 cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
             }
         });
+    }
+    if (first) {
+        atomicMin(&f_wlo, (unsigned long long)wlo);
+        atomicMax(&f_whi, (unsigned long long)whi);
+        if (gn) {
+            atomicAdd(&f_ga, (unsigned long long)ga);
+            atomicAdd(&f_gb, (unsigned long long)gb);
+            atomicAdd(&f_gc, (unsigned long long)gc);
+            atomicAdd(&f_gn, (unsigned long long)gn);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            m.sel_imin[s * 2 + 1] = f_wlo;  // all ranks: MIN / MAX before k_sel_start
+            m.sel_imax[s * 2 + 1] = f_whi;
+            if (f_gn) {  // this rank's filled rows, all at the fill value (inside [lo, hi])
+                st[SW_GN] = f_gn;
+                st[SW_GW0] = f_ga;
+                st[SW_GW1] = f_gb;
+                st[SW_GW2] = f_gc;
+                const uint64_t fk = dkey(m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]]);
+                const int b = (int)((fk - lo) >> sh);
+                if (wmode) {
+                    atomicAdd(&ha[b], f_ga);
+                    atomicAdd(&hb[b], f_gb);
+                    atomicAdd(&hc[b], f_gc);
+                }
+                atomicAdd(&hn[b], f_gn);
+                atomicMin(&hmin[b], (unsigned long long)fk);
+                atomicMax(&hmax[b], (unsigned long long)fk);
+            }
+        }
     }
     if (gin && threadIdx.x == 0) {
         const int b = (int)((gk - lo) >> sh);
@@ -2471,9 +2512,10 @@ __device__ __forceinline__ uint64_t scan_max_u64(uint64_t v, int lane) {  // inc
 __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
     const int a = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
     const int lane = threadIdx.x % WAVE;
-    if (a >= n_active) return;  // wave-uniform
+    if (a >= n_active || a >= (int)m.info[IN_SEL_ACTIVE]) return;  // wave-uniform
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[SW_STATUS] != 1) return;  // the first pass's start may have finished it
     const bool wmode = st[SW_MODE] == 0;
     const L3 tot = ld_l3(st + SW_TOT0);
     const uint64_t n_all = st[SW_COUNT], target = st[SW_TARGET];
@@ -4133,10 +4175,11 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_WMEAN_OUT:
             hipLaunchKernelGGL(k_wmean_out, dim3(ceb), dim3(BT), 0, st, m);
             break;
-        case M_SEL_INIT:
+        case M_SEL_INIT:  // status, key range and the active list of the first histogram pass
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_sel_setup, dim3(sg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_sel_init, dim3(m.n_scaled), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_range, dim3(sg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_compact, dim3(1), dim3(1024), 0, st, m);
             break;
         case M_SEL_EXACT:
             if (m.n_scaled == 0) break;

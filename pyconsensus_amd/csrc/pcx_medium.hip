@@ -31,7 +31,7 @@ constexpr int MN = 256;  // max reporters
 constexpr int MEV = 64;  // max events
 constexpr double M_PI_TOL = 1e-14;
 constexpr int M_PI_MAXIT = 256, M_PI_PRESQUARE = 3, M_PI_SQUARE_EVERY = 32, M_PI_MAX_SQUARINGS = 8,
-              M_PI_POLISH = 4;
+              M_PI_POLISH = 2;
 constexpr double M_DBL_EPS = 2.220446049250313080847e-16;
 constexpr double M_DBL_MIN = 2.2250738585072014e-308;
 

@@ -433,11 +433,26 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         // small matrices: replay the reference's float walk directly
         if (S) R.stage(m, M_SEL_EXACT);
     } else if (S) {
+        // first pass, with no host read before it: the key range of every needed event is
+        // known (M_COLSTATS, the fill), so one histogram pass over the whole range also collects
+        // the totals the walk starts from; launched for all S events (those not needed exit),
+        // its collectives sized for S.  Counting only for reputation=None interpolation medians.
         R.stage(m, M_SEL_INIT);
-        R.allreduce(w->sel_isum, (int64_t)S * 4, PCX_U64, PCX_SUM);
+        m.sel_first = 1;
+        R.mark(M_SEL_HIST);
+        R.check_err(sel_hist(m, S, R.st), "k_sel_hist");
+        R.mark(-1);
+        m.sel_first = 0;
+        if (!(phase == 1 && !m.rep_raw)) R.allreduce(w->hist_w, (int64_t)S * SEL_NB * 3, PCX_U64, PCX_SUM);
+        R.allreduce(w->hist_n, (int64_t)S * SEL_NB, PCX_U64, PCX_SUM);
+        R.allreduce(w->hist_min, (int64_t)S * SEL_NB, PCX_U64, PCX_MIN);
+        R.allreduce(w->hist_max, (int64_t)S * SEL_NB, PCX_U64, PCX_MAX);
         R.allreduce(w->sel_imin, (int64_t)S * 2, PCX_U64, PCX_MIN);
         R.allreduce(w->sel_imax, (int64_t)S * 2, PCX_U64, PCX_MAX);
         R.stage(m, M_SEL_START);
+        R.mark(M_SEL_STEP);
+        R.check_err(sel_step(m, S, R.st), "k_sel_step");
+        R.mark(-1);
         R.stage(m, M_SEL_COMPACT);
         int64_t inf5[5];  // active, argmax, (pick1), (hard), weight-mode active
         R.hip(hipMemcpyAsync(inf5, m.info + INFO_SEL_ACTIVE, sizeof(inf5), hipMemcpyDeviceToHost, R.st), "D2H");
@@ -450,7 +465,7 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
             R.allreduce(w->sel_arg + S, S, PCX_U64, PCX_MAX);
             R.stage(m, M_SEL_VALUE_FINISH);
         }
-        int passes = 0;
+        int passes = 1;
         while (active > 0) {
             if (passes == MAX_SEL_PASSES) {
                 R.err = "weighted selection did not converge";
