@@ -52,7 +52,7 @@ constexpr int CM = 8;            // doubles per column in mpart / cmax
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
                EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
-enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK };
+enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
                  IN_COV_GENERAL, IN_COV_MIXED };
 
@@ -295,6 +295,7 @@ __global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
     __shared__ dd lds[8];
     acc2 at, ar;
     double big = 0.0;  // tokens outside [0, 63]: the int8 covariance path needs tok * z <= 126
+    double tmax = 0.0;  // the largest token (scales the mixed block's digits of tok w)
     const double tot = m.rep_raw ? m.pvec[0] : 0.0;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         const double r = m.rep_raw ? m.rep_raw[m.row_offset + i] / tot : 1.0 / (double)m.n_total;
@@ -304,15 +305,36 @@ __global__ void __launch_bounds__(BT) k_rep_local(pcx_mat m) {
         at.add(t);
         ar.add(r);
         big += (t >= 0.0 && t <= 63.0) ? 0.0 : 1.0;
+        tmax = fmax(tmax, t);
     }
     dd st = block_sum_dd<BT>(at.get(), lds);
     dd sr = block_sum_dd<BT>(ar.get(), lds);
     dd sb = block_sum_dd<BT>(dd{big, 0.0}, lds);
+    __shared__ double tm[BT / WAVE];
+    for (int o = WAVE / 2; o >= 1; o >>= 1) tmax = fmax(tmax, __shfl_xor(tmax, o, WAVE));
+    if (threadIdx.x % WAVE == 0) tm[threadIdx.x / WAVE] = tmax;
+    __syncthreads();
     if (threadIdx.x == 0) {
+        for (int k = 1; k < BT / WAVE; k++) tmax = fmax(tmax, tm[k]);
         st_dd(m.spart + blockIdx.x * 8 + 0, st);
         st_dd(m.spart + blockIdx.x * 8 + 2, sr);
         st_dd(m.spart + blockIdx.x * 8 + 4, sb);
+        st_dd(m.spart + blockIdx.x * 8 + 6, dd{tmax, 0.0});
     }
+}
+
+// the largest block value of spart slot `src` (hi parts) -> scal[rank][slot] (one block)
+__global__ void __launch_bounds__(BT) k_spart_max(pcx_mat m, int nblk, int slot, int src) {
+    __shared__ double red[BT];
+    double v = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += BT) v = fmax(v, m.spart[b * 8 + 2 * src]);
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int st = BT / 2; st >= 1; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) st_dd(m.scal + ((int64_t)m.rank * SS + slot) * 2, dd{red[0], 0.0});
 }
 
 // reduce spart[nblk][4 dd] slots src0 .. src0+k into scal[rank][slot0 .. slot0+k): one
@@ -618,6 +640,12 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
 }
 
 // ---------------------------------------------------------------- covariance operands
+// z in {0, 1, 2} of 16 rows packed into one uint32 (k_gemm_i8 BPACK): row r at bit
+// 8 (r % 4) + 2 (r / 4); zpack_bit(r) is the bit of value 1
+__device__ __forceinline__ uint32_t zpack_bit(int r) { return 1u << (8 * (r & 3) + 2 * (r >> 2)); }
+__device__ __forceinline__ uint32_t zpack_get(uint32_t P, int r) { return (P >> (8 * (r & 3) + 2 * (r >> 2))) & 3u; }
+__device__ __forceinline__ uint32_t* zb_packed(const pcx_mat& m) { return reinterpret_cast<uint32_t*>(m.zB); }
+
 // PCX_M_COV_PLAN: the wcd column order.  A "grid" event is binary with every filled value
 // in {1, 1.5, 2} (present reports on the grid -- k_colstats -- and a fill, if any, on it),
 // while every token lies in [0, 63] (so tok * z fits int8).  General events take the
@@ -691,6 +719,8 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
     const int G = base[0];
     const int gb = (G + CT - 1) / CT * CT;
     int bad = 0;
+    double maxtok = 0.0;  // the largest token over all ranks (scal slot SC_MAXTOK, an integer)
+    for (int w = 0; w < m.world; w++) maxtok = fmax(maxtok, m.scal[((int64_t)w * SS + SC_MAXTOK) * 2]);
     if (!big && gb > 0 && gb < E) {
         for (int q = tid; q < gb; q += 1024) {
             const int c = m.cov_perm[q];
@@ -706,7 +736,9 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
             }
             if (m.ev[EV_MISS * E + c] > 0.0) bnd = fmax(bnd, fabs(m.ev[EV_GUESS * E + c] - mu));
             if (!__builtin_isfinite(bnd) || __builtin_isnan(mu)) bad = 1;
-            // |w| <= bnd < 2^(ilogb + 1): |w| 2^-e <= 1/2 with e = ilogb + 2 (first digit |d| <= 64)
+            // the digits are of tok w: |tok w| <= maxtok bnd < 2^(ilogb + 1), so |tok w| 2^-e <= 1/2
+            // with e = ilogb + 2 (first digit |d| <= 64)
+            bnd *= maxtok;
             m.dscale[q] = bnd > 0.0 && __builtin_isfinite(bnd) ? ldexp(1.0, -(ilogb(bnd) + 2)) : 1.0;
         }
     }
@@ -758,7 +790,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int64_t g0 = r0; g0 < r1; g0 += 64) {
         const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;  // a multiple of 16 (wcd_rows % 16 == 0)
         for (int q0 = 0; q0 < gn; q0 += 16) {
-            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
                 double rv[4][2];
@@ -790,7 +822,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                             if (zc[k]) {
                                 const int z = (int)((f - 1.0) * 2.0);
                                 za[k][h] |= (uint32_t)(uint8_t)(int8_t)(tk * z) << (8 * u);
-                                zb[k][h] |= (uint32_t)z << (8 * u);
+                                zb[k] |= (uint32_t)z * zpack_bit(4 * h + u);
                                 zs[k] += tk * z;
                             }
                         }
@@ -825,9 +857,9 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
 #pragma unroll
             for (int k = 0; k < 2; k++)
                 if (zc[k]) {
-                    const int64_t o = (grp * m.zq + (pos[k] - gb)) * 16;
-                    *(uint4*)(m.zA + o) = uint4{za[k][0], za[k][1], za[k][2], za[k][3]};
-                    *(uint4*)(m.zB + o) = uint4{zb[k][0], zb[k][1], zb[k][2], zb[k][3]};
+                    const int64_t o = grp * m.zq + (pos[k] - gb);
+                    *(uint4*)(m.zA + o * 16) = uint4{za[k][0], za[k][1], za[k][2], za[k][3]};
+                    zb_packed(m)[o] = zb[k];
                 }
         }
         __syncthreads();
@@ -989,39 +1021,54 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
             }
 }
 
-// PCX_M_COV_I8: exact integer products on int8 MFMA (v_mfma_i32_16x16x64_i8).  Operands are
-// [row / 16][position][16] int8 blocks, so one 16-byte load is one lane's MFMA fragment (16
-// rows of one position).  256 x 256 output tiles, 16 waves of 64 x 64 (16 int32
-// accumulators each, four waves per SIMD); 64-row stages of both 16 KB panels go to LDS by global_load_lds in a
-// four-stage ring (three stages in flight under the MFMAs -- the loads' latency is several
-// stages long -- one barrier per stage, counted vmcnt); each k-slice's int32 tile is stored
-// to its own slab (k_cov_reduce sums the slabs in int64).  Tiles run k-slice major and
-// XCD-grouped, so the WGs resident at once stream the same rows through L2.
+// PCX_M_COV_I8: exact integer products on int8 MFMA (v_mfma_i32_16x16x64_i8).  The A operand
+// is [row / 16][position][16] int8 blocks, so one 16-byte load is one lane's MFMA fragment (16
+// rows of one position).  The B operand is either the same (BPACK = false) or z in {0, 1, 2}
+// packed 2 bits per value (BPACK): [row / 16][position] uint32, row r of the 16 at bit
+// 8 (r % 4) + 2 (r / 4), so dword k of the fragment (rows 4k .. 4k+3, one per byte) is
+// (P >> 2k) & 0x03030303 -- a quarter of the bytes through L2 and LDS, unpacked by two VALU
+// ops per dword beside the MFMAs.  The kernel streams 64-row stages of both panels from L2
+// into LDS (global_load_lds) and is bound by that stream: at 256 x 256 tiles (the largest the
+// register file holds) a 16 KB + 16 KB stage feeds 1,024 MFMA cycles per SIMD, more than L2
+// delivers per CU; a packed B panel cuts the stage to 20 KB.  256 x 256 output tiles, 16 waves
+// of 64 x 64 (16 int32 accumulators each, four waves per SIMD); a G_NBUF-stage ring (one
+// barrier per stage, counted vmcnt); each k-slice's int32 tile is stored to its own slab
+// (k_cov_reduce sums the slabs in int64), transposed (out[q][p]) when trans is set.  Tiles run
+// k-slice major and XCD-grouped, so the WGs resident at once stream the same rows through L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int GT = 256;                              // output tile edge
-constexpr int G_NBUF = 4;                            // LDS ring depth
-constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one operand's 64-row stage: 16 KB
-constexpr size_t G_LDS_BYTES = G_NBUF * 2 * G_PANEL; // 128 KB
+constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one int8 operand's 64-row stage: 16 KB
+constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
+template <bool BPACK>
+struct GRing {
+    static constexpr int NBUF = BPACK ? 6 : 4;       // LDS ring depth
+    static constexpr size_t STAGE = G_PANEL + (BPACK ? G_PANEL_PK : G_PANEL);
+    static constexpr size_t BYTES = NBUF * STAGE;    // 120 KB / 128 KB
+};
 
 struct GemmI8 {
     const int8_t* A;
     int64_t lda;  // positions per row group
     const int8_t* B;
     int64_t ldb;
-    int32_t* out;  // [kslices][slab]: row p at p * ldo
+    int32_t* out;  // [kslices][slab]: row p at p * ldo (trans: row q at q * ldo)
     int64_t ldo, slab;
     int np, nq, tp, tq, lower, kslices;
     int64_t rg;  // row groups, a multiple of 4
+    int trans;
 };
 
 // WAVES = 16: 4 x 4 waves of 64 x 64 (four waves per SIMD); WAVES = 8: 2 x 4 waves of 128 x 64
 // (two per SIMD, 8 A + 4 B fragment reads per 32 MFMAs instead of 4 + 4 per 16: a quarter less
 // LDS read traffic per MFMA).  Same items, slabs and integer results.
-template <int WAVES>
+template <int WAVES, bool BPACK>
 __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
+    static_assert(!BPACK || WAVES == 16, "packed B: one dword load per wave per stage");
+    using RG = GRing<BPACK>;
     constexpr int WR = WAVES == 16 ? 4 : 2;  // wave rows (p); 4 wave columns (q)
     constexpr int TM = GT / WR, AF = TM / 16;
-    constexpr int LPP = 16 / WAVES;  // 1 KB loads per wave per panel per stage (16 KB panels)
+    constexpr int LPP = 16 / WAVES;  // 1 KB loads per wave per int8 panel per stage (16 KB panels)
+    constexpr int LOADS = LPP + (BPACK ? 1 : LPP);  // vector-memory ops per wave per stage
     extern __shared__ __attribute__((aligned(16))) char glds[];
     const int ntiles = g.tp * g.tq;
     const int item = xcd_remap(blockIdx.x, gridDim.x);
@@ -1036,16 +1083,26 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
     const int wr = wv >> 2, wc = wv & 3;
     const int lc = lane & 15, lg = lane >> 4;
     auto issue = [&](int64_t st, int buf) {
+        char* sbase = glds + (size_t)buf * RG::STAGE;
 #pragma unroll
-        for (int j = 0; j < LPP; j++) {  // chunk ch = (row group mg, quarter mh) of both panels
+        for (int j = 0; j < LPP; j++) {  // chunk ch = (row group mg, quarter mh) of the int8 panels
             const int ch = wv + j * WAVES, mg = ch & 3, mh = ch >> 2;
-            char* base = glds + (size_t)buf * 2 * G_PANEL + ((size_t)mg * GT + mh * 64) * 16;
+            char* base = sbase + ((size_t)mg * GT + mh * 64) * 16;
             const int64_t grp = st * 4 + mg;
             const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
-            const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
             __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16, 0,
-                                             0);
+            if constexpr (!BPACK) {
+                const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
+                __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16,
+                                                 0, 0);
+            }
+        }
+        if constexpr (BPACK) {  // packed panel [mg][256 positions] uint32: 256 B per wave
+            const int mg = wv & 3, mh = wv >> 2;
+            const uint32_t* Bb = reinterpret_cast<const uint32_t*>(g.B) + (st * 4 + mg) * g.ldb + (int64_t)iq * GT +
+                                 mh * 64 + lane;
+            __builtin_amdgcn_global_load_lds((const void*)Bb,
+                                             (lds_ptr_t)(sbase + G_PANEL + ((size_t)mg * GT + mh * 64) * 4), 4, 0, 0);
         }
     };
     v4i acc[AF][4];
@@ -1055,25 +1112,36 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
         for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
     const int64_t n = s1 - s0;
 #pragma unroll
-    for (int k = 0; k < G_NBUF - 1; k++)
+    for (int k = 0; k < RG::NBUF - 1; k++)
         if (k < n) issue(s0 + k, k);
     for (int64_t t = 0; t < n; t++) {
-        const int buf = (int)(t % G_NBUF);
-        if (t + G_NBUF - 2 < n)
-            wait_vmcnt<2 * LPP * (G_NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
+        const int buf = (int)(t % RG::NBUF);
+        if (t + RG::NBUF - 2 < n)
+            wait_vmcnt<LOADS * (RG::NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
         else
             wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + G_NBUF - 1 < n) issue(s0 + t + G_NBUF - 1, (int)((t + G_NBUF - 1) % G_NBUF));
-        const v4i* As = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL) + lg * GT + wr * TM + lc;
-        const v4i* Bs = (const v4i*)(glds + (size_t)buf * 2 * G_PANEL + G_PANEL) + lg * GT + wc * 64 + lc;
+        if (t + RG::NBUF - 1 < n) issue(s0 + t + RG::NBUF - 1, (int)((t + RG::NBUF - 1) % RG::NBUF));
+        const char* sb = glds + (size_t)buf * RG::STAGE;
+        const v4i* As = (const v4i*)sb + lg * GT + wr * TM + lc;
         v4i af[AF], bf[4];
 #pragma unroll
         for (int a = 0; a < AF; a++) af[a] = As[a * 16];
+        if constexpr (BPACK) {
+            const uint32_t* Bs = (const uint32_t*)(sb + G_PANEL) + lg * GT + wc * 64 + lc;
+            constexpr uint32_t M2 = 0x03030303u;
 #pragma unroll
-        for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
+            for (int b = 0; b < 4; b++) {
+                const uint32_t P = Bs[b * 16];
+                bf[b] = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
+            }
+        } else {
+            const v4i* Bs = (const v4i*)(sb + G_PANEL) + lg * GT + wc * 64 + lc;
+#pragma unroll
+            for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
+        }
 #pragma unroll
         for (int a = 0; a < AF; a++)
 #pragma unroll
@@ -1086,34 +1154,46 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
 #pragma unroll
     for (int a = 0; a < AF; a++)
 #pragma unroll
-        for (int b = 0; b < 4; b++)
+        for (int b = 0; b < 4; b++) {
+            const int pa = p0 + a * 16, q = q0 + b * 16;
+            if (g.trans) {  // out[q][p .. p + 3]: one 16-byte store per lane
+                if (q < g.nq && pa + 3 < g.np && (g.ldo & 3) == 0) {
+                    *(v4i*)(out + (int64_t)q * g.ldo + pa) = acc[a][b];
+                } else {
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int p = p0 + a * 16 + r, q = q0 + b * 16;
-                if (p < g.np && q < g.nq && (!g.lower || q <= p)) out[(int64_t)p * g.ldo + q] = acc[a][b][r];
+                    for (int r = 0; r < 4; r++)
+                        if (pa + r < g.np && q < g.nq) out[(int64_t)q * g.ldo + pa + r] = acc[a][b][r];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int p = pa + r;
+                    if (p < g.np && q < g.nq && (!g.lower || q <= p)) out[(int64_t)p * g.ldo + q] = acc[a][b][r];
+                }
             }
+        }
 }
 
-// the token column of the int8 operands: zA = tok (<= 63), zB = 1 on live rows
+// the token column of the int8 operands: zA = tok (<= 63), zB = 1 on live rows (packed)
 __global__ void __launch_bounds__(BT) k_tokcol(pcx_mat m) {
     const int64_t grp = blockIdx.x * (int64_t)BT + threadIdx.x;
     if (grp >= m.wcd_rows / 16) return;
-    uint32_t ta[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
+    uint32_t ta[4] = {0, 0, 0, 0}, tb = 0;
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int64_t i = grp * 16 + r;
         if (i < m.n_rows) {
             ta[r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)m.tok[i] << (8 * (r & 3));
-            tb[r >> 2] |= 1u << (8 * (r & 3));
+            tb |= zpack_bit(r);
         }
     }
-    const int64_t o = (grp * m.zq + m.tokpos) * 16;
-    *(uint4*)(m.zA + o) = uint4{ta[0], ta[1], ta[2], ta[3]};
-    *(uint4*)(m.zB + o) = uint4{tb[0], tb[1], tb[2], tb[3]};
+    *(uint4*)(m.zA + (grp * m.zq + m.tokpos) * 16) = uint4{ta[0], ta[1], ta[2], ta[3]};
+    zb_packed(m)[grp * m.zq + m.tokpos] = tb;
 }
 
-// w of the general positions q < gb as 8 balanced base-128 digits of w 2^-e (|w 2^-e| <= 1/2):
-// t = 128 v, d = rint(t), v = t - d -- every step exact, |d| <= 64, residue <= 2^-57 2^e
+// tok * w of the general positions q < gb (the exact product, as a double-double) as 8 balanced
+// base-128 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 128 v, d = rint(t_hi), v = t - d
+// with the low part carried -- every step exact, |d| <= 65, residue <= 2^-56 2^e
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
@@ -1129,12 +1209,17 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
         for (int k = 0; k < 8; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            double v = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;
+            const double w = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;  // exact (power of two)
+            const double tk = m.tokp[grp * 16 + r];                       // 0 past n_rows
+            double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                const double t = v * 128.0;
-                const double di = rint(t);
-                v = t - di;
+                const double t = hi * 128.0, di = rint(t);
+                const double e = t - di;  // exact
+                const double l = lo * 128.0;
+                hi = e + l;  // two-sum: (hi, lo) = (t - di) + 128 lo exactly
+                const double bv = hi - e;
+                lo = (e - (hi - bv)) + (l - bv);
                 d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
             }
         }
@@ -1538,10 +1623,9 @@ __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
         for (int r = 0; r < 16; r++) z[r] = 0.0;
         for (int q = lane; q < ng; q += WAVE) {
             const double l = LD[m.cov_perm[gb + q]];
-            const uint4 zb = *(const uint4*)(m.zB + (g * m.zq + q) * 16);
-            const uint32_t wd[4] = {zb.x, zb.y, zb.z, zb.w};
+            const uint32_t P = zb_packed(m)[g * m.zq + q];
 #pragma unroll
-            for (int r = 0; r < 16; r++) z[r] = fma((double)((wd[r >> 2] >> (8 * (r & 3))) & 0xffu), l, z[r]);
+            for (int r = 0; r < 16; r++) z[r] = fma((double)zpack_get(P, r), l, z[r]);
         }
         double mine = 0.0;
 #pragma unroll
@@ -3995,6 +4079,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_rep_local, dim3(rg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_spart_finish, dim3(2), dim3(BT), 0, st, m, rg, 2, (int)SC_TOK, 0);
             hipLaunchKernelGGL(k_spart_finish, dim3(1), dim3(BT), 0, st, m, rg, 1, (int)SC_BIGTOK, 2);
+            hipLaunchKernelGGL(k_spart_max, dim3(1), dim3(BT), 0, st, m, rg, (int)SC_MAXTOK, 3);
             if (m.ob_order) hipLaunchKernelGGL(k_ob_sums, dim3(1), dim3(64), 0, st, m, 0);
             break;
         case M_COLSTATS:
@@ -4027,39 +4112,34 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             }
             static std::once_flag g_once;
             static hipError_t g_err = hipSuccess;
-            static int g_waves = 16;  // PCX_GEMM_I8_WAVES=8: 2 x 4 waves of 128 x 64
             std::call_once(g_once, [] {
-                const char* e = getenv("PCX_GEMM_I8_WAVES");
-                g_waves = (e && atoi(e) == 8) ? 8 : 16;
-                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)G_LDS_BYTES);
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, false>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<false>::BYTES);
                 if (g_err == hipSuccess)
-                    g_err = hipFuncSetAttribute((const void*)k_gemm_i8<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)G_LDS_BYTES);
+                    g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<true>::BYTES);
             });
             if (g_err != hipSuccess) return g_err;
-            auto gemm = [&](const GemmI8& g) {
-                const dim3 grid((unsigned)(g.tp * g.tq * g.kslices));
-                if (g_waves == 8)
-                    hipLaunchKernelGGL(k_gemm_i8<8>, grid, dim3(8 * 64), G_LDS_BYTES, st, g);
-                else
-                    hipLaunchKernelGGL(k_gemm_i8<16>, grid, dim3(16 * 64), G_LDS_BYTES, st, g);
-            };
             const int64_t rg = m.wcd_rows / 16;
+            // both products take z (zB, 2-bit packed) as the B operand
             hipLaunchKernelGGL(k_tokcol, dim3((unsigned)((rg + BT - 1) / BT)), dim3(BT), 0, st, m);
-            {  // grid x grid (lower tiles): |tok z z| <= 252 per row
-                GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg};
+            {  // grid x grid (lower tiles): P = (tok z)^T z, |tok z z| <= 252 per row
+                GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg, 0};
                 g.tp = g.tq = (np + GT - 1) / GT;
-                gemm(g);
+                hipLaunchKernelGGL((k_gemm_i8<16, true>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                                   GRing<true>::BYTES, st, g);
             }
-            if (m.cov_mixed) {  // grid x general digits: |tok z d| <= 126 * 64 per row
+            if (m.cov_mixed) {
+                // general digits x grid: digits of tok w (A, 8 per general position) times z (B);
+                // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 65 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
                 hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
-                GemmI8 g{m.zA, m.zq, m.zD, (int64_t)8 * gb, m.Pmx, (int64_t)8 * gb, m.zq * 8 * gb, np, 8 * gb,
-                         0, 0, 0, m.ks_mx, rg};
-                g.tp = (np + GT - 1) / GT;
-                g.tq = (8 * gb + GT - 1) / GT;
-                gemm(g);
+                GemmI8 g{m.zD, (int64_t)8 * gb, m.zB, m.zq, m.Pmx, (int64_t)8 * gb, m.zq * 8 * gb, 8 * gb, np,
+                         0, 0, 0, m.ks_mx, rg, 1};
+                g.tp = (8 * gb + GT - 1) / GT;
+                g.tq = (np + GT - 1) / GT;
+                hipLaunchKernelGGL((k_gemm_i8<16, true>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                                   GRing<true>::BYTES, st, g);
             }
             break;
         }

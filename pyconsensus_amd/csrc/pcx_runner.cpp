@@ -832,7 +832,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         const int64_t cpitch = CS * 2;
         // a1: reputation, tokens (:138-146)
         R.stage(m, M_REPUTATION);
-        R.gather_slots(w->scal, 1, SS * 2, 0, SC_BIGTOK_SLOT + 1, w);
+        R.gather_slots(w->scal, 1, SS * 2, 0, SC_BIGTOK_SLOT + 2, w);  // .. SC_MAXTOK
         // a2/a3: rescale + NA + present sums (:266-299)
         R.stage(m, M_COLSTATS);
         R.gather_slots(w->cstat, E, cpitch, 0, 4, w);
@@ -894,7 +894,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     return (int32_t)std::max<int64_t>(1, std::min<int64_t>(best, nst));
                 };
                 m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000);  // lower tiles only do work
-                m.ks_mx = ks_for(tp * tq, 250000);
+                m.ks_mx = ks_for(tp * tq, 8000000);  // |z d| <= 130 per row
                 if (np > 0 && !w->grow(w->pgg, (size_t)(m.ks_gg * m.zq * m.zq * 4))) {
                     err = "workspace: hipMalloc of the int8 covariance products failed";
                     throw Fail{PCX_ENOMEM};
