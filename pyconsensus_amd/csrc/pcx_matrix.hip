@@ -380,6 +380,42 @@ __device__ __forceinline__ void rows_unrolled(int64_t r0, int64_t r1, LOAD load,
     for (; i < r1; i++) proc(i, load(i));
 }
 
+// Software-pipelined row loop of the column passes: the next U rows' loads are issued before
+// the current U rows are processed, so every wave keeps loads in flight through its compute
+// (with rows_unrolled a wave alternates a load burst and a compute burst, and at the few waves
+// per CU these passes run the bursts leave HBM idle).
+#ifndef PCX_PIPE_U
+#define PCX_PIPE_U 8
+#endif
+constexpr int PIPE_U = PCX_PIPE_U;
+
+template <int U, class LOAD, class PROC>
+__device__ __forceinline__ void rows_pipelined(int64_t r0, int64_t r1, LOAD load, PROC proc) {
+#ifdef PCX_X_NOPIPE
+    rows_unrolled<2 * U>(r0, r1, load, proc);
+#else
+    int64_t i = r0;
+    if (r1 - r0 >= U) {
+        decltype(load(i)) cur[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = load(i + u);
+        for (; i + 2 * U <= r1; i += U) {
+            decltype(load(i)) nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) nxt[u] = load(i + U + u);
+#pragma unroll
+            for (int u = 0; u < U; u++) proc(i + u, cur[u]);
+#pragma unroll
+            for (int u = 0; u < U; u++) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) proc(i + u, cur[u]);
+        i += U;
+    }
+    for (; i < r1; i++) proc(i, load(i));
+#endif
+}
+
 // the same over a strided row set i = first, first + stride, ... < n
 template <int U, class LOAD, class PROC>
 __device__ __forceinline__ void rows_strided(int64_t first, int64_t stride, int64_t n, LOAD load, PROC proc) {
@@ -414,7 +450,7 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     acc2 sr, srx;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
     bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
-    rows_unrolled<16>(
+    rows_pipelined<PIPE_U>(
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
         [&](int64_t i, XW v) {
             const double x = rescale(v.x, p, m.int_dtype);
@@ -1782,7 +1818,7 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
     struct V3 {
         double x, w1, w2;
     };
-    rows_unrolled<ROW_UNROLL>(
+    rows_pipelined<PIPE_U>(
         r0, r1,
         [&](int64_t i) {
             return V3{m.reports[i * E + c], m.rowv[RV_N1 * m.n_rows + i], m.rowv[RV_N2 * m.n_rows + i]};
@@ -2004,24 +2040,13 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
     acc2 raw;
     double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     double n1 = 0, n15 = 0, n2 = 0;
-    // explicit unroll (a lambda capturing five accumulators pushed them to scratch)
-    int64_t i = r0;
-    for (; i < r1;) {
-        const int u_n = r1 - i >= ROW_UNROLL ? ROW_UNROLL : (int)(r1 - i);
-        double xv[ROW_UNROLL], wv[ROW_UNROLL];
-#pragma unroll
-        for (int u = 0; u < ROW_UNROLL; u++) {
-            const int64_t ii = u < u_n ? i + u : i;
-            xv[u] = m.reports[ii * E + c];
-            wv[u] = m.rowv[RV_SMOOTH * m.n_rows + ii];
-        }
-#pragma unroll
-        for (int u = 0; u < ROW_UNROLL; u++) {
-            if (u >= u_n) break;
-            const double x = rescale(xv[u], p, m.int_dtype);
+    rows_pipelined<PIPE_U>(
+        r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rowv[RV_SMOOTH * m.n_rows + i]}; },
+        [&](int64_t, XW v) {
+            const double x = rescale(v.x, p, m.int_dtype);
             const bool ms = missing(x);
             const double f = ms ? p.guess : x;
-            const double w = wv[u];
+            const double w = v.w;
             raw.add_prod(w, f);
             pc += w * (ms ? 1.0 : 0.0);  // np.dot(smooth_rep, na_mat): a NaN weight propagates
             b1 += f == 1.0 ? w : 0.0;
@@ -2030,9 +2055,7 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
             n1 += f == 1.0 ? 1.0 : 0.0;
             n15 += f == 1.5 ? 1.0 : 0.0;
             n2 += f == 2.0 ? 1.0 : 0.0;
-        }
-        i += u_n;
-    }
+        });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, raw.get());
     st_dd(pp + 2, {pc, 0.0});
@@ -2103,6 +2126,7 @@ enum sel_word {
     SW_CMODE,                         // 1: this rank's in-range elements are compacted in cbuf
     SW_GN, SW_GW0, SW_GW1, SW_GW2,    // phase 2, this rank: filled (missing) rows -- all at the fill
                                       // value -- count and raw weight limb sums, binned once per pass
+    SW_WB0, SW_WB1,                   // first pass: the bucket window gathered into cbuf (sampled)
     SW_NWORDS
 };
 static_assert(SW_NWORDS <= SELS, "sel_state words");
@@ -2413,6 +2437,46 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
     }
 }
 
+// The first pass's window: a strided sample of the column (every SEL_SAMPLE-th row, all ranks'
+// samples summed) histogrammed in the first pass's buckets; the bucket where the sample's
+// weight crosses half, +- SEL_WIN buckets, is the window the first pass also gathers into cbuf.
+// When the exact crossing bucket lies inside it (nearly always) the later passes read only
+// cbuf -- one read of the column per phase instead of two.  A miss (or a cbuf overflow) only
+// falls back to the plain passes: the sample never decides a result.
+constexpr int SEL_SAMPLE = 64;
+constexpr int SEL_WIN = 3;
+__device__ __forceinline__ double* sel_sample_row(const pcx_mat& m, int a) {
+    return reinterpret_cast<double*>(m.hist_w) + (int64_t)a * NB * 3;  // [NB] weight, [NB] count
+}
+
+__global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
+    const int a = blockIdx.x;
+    if (a >= (int)m.info[IN_SEL_ACTIVE]) return;
+    const int s = m.sel_act[a];
+    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    __shared__ double sw[NB], sn[NB];
+    for (int b = threadIdx.x; b < NB; b += BT) sw[b] = sn[b] = 0.0;
+    __syncthreads();
+    const uint64_t lo = st[SW_LO], hi = st[SW_HI];
+    const int sh = (int)st[SW_SHIFT];
+    const int64_t ns = m.n_rows / SEL_SAMPLE;
+    for (int64_t j = threadIdx.x; j < ns; j += BT) {
+        double x, w;
+        if (!sel_elem(m, s, j * SEL_SAMPLE, x, w)) continue;
+        const uint64_t k = dkey(x);
+        if (k < lo || k > hi) continue;
+        const int b = (int)((k - lo) >> sh);
+        atomicAdd(&sw[b], w);
+        atomicAdd(&sn[b], 1.0);
+    }
+    __syncthreads();
+    double* o = sel_sample_row(m, a);
+    for (int b = threadIdx.x; b < NB; b += BT) {
+        o[b] = sw[b];
+        o[NB + b] = sn[b];
+    }
+}
+
 // exact weight / count histogram of the keys inside [lo, hi] (NB buckets) of active event a
 // One block per active event.  Once the key range holds at most ccap elements (all ranks),
 // the pass that reads the whole column also compacts this rank's in-range (key, weight)
@@ -2442,6 +2506,34 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const bool first = m.sel_first != 0;
     const bool gfirst = first && m.sel_phase == 2;
     uint64_t wlo = ~0ull, whi = 0, ga = 0, gb = 0, gc = 0, gn = 0;
+    __shared__ int win_s[2];
+    if (first && threadIdx.x == 0) {  // the sampled window (k_sel_sample, all ranks)
+        const double* smp = sel_sample_row(m, a);
+        const bool wm = st[SW_MODE] == 0;
+        double tot = 0.0;
+        for (int b = 0; b < NB; b++) tot += wm ? smp[b] : smp[NB + b];
+        int b0 = 1, b1 = 0;  // empty
+        if (tot > 0.0 && m.cbuf) {
+            double cum = 0.0;
+            int bx = NB - 1;
+            for (int b = 0; b < NB; b++) {
+                cum += wm ? smp[b] : smp[NB + b];
+                if (2.0 * cum >= tot) {
+                    bx = b;
+                    break;
+                }
+            }
+            b0 = bx - SEL_WIN < 0 ? 0 : bx - SEL_WIN;
+            b1 = bx + SEL_WIN > NB - 1 ? NB - 1 : bx + SEL_WIN;
+        }
+        win_s[0] = b0;
+        win_s[1] = b1;
+        st[SW_WB0] = (uint64_t)b0;
+        st[SW_WB1] = (uint64_t)b1;
+    }
+    __syncthreads();
+    const int wb0 = first ? win_s[0] : 1, wb1 = first ? win_s[1] : 0;
+    const bool wgather = first && wb0 <= wb1;
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
     const int sh = (int)st[SW_SHIFT];
     const bool wmode = st[SW_MODE] == 0;
@@ -2501,7 +2593,16 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             const uint64_t k = dkey(x);
             if (k < lo || k > hi) return;
             bin(k, w);
-            if (gather) {
+            if (wgather) {
+                const int b = (int)((k - lo) >> sh);
+                if (b >= wb0 && b <= wb1) {
+                    const unsigned long long j = atomicAdd(&gcount, 1ull);
+                    if (j < (unsigned long long)m.ccap) {
+                        cb[2 * j] = k;
+                        cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
+                    }
+                }
+            } else if (gather) {
                 const unsigned long long j = atomicAdd(&gcount, 1ull);
                 cb[2 * j] = k;
                 cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
@@ -2554,6 +2655,11 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     if (gather && threadIdx.x == 0) {
         m.ccount[s] = (int64_t)gcount;
         st[SW_CMODE] = 1;
+    }
+    if (wgather && threadIdx.x == 0) {  // pending: valid once the crossing bucket is inside the window
+        const bool fits = gcount <= (unsigned long long)m.ccap;
+        m.ccount[s] = fits ? (int64_t)gcount : 0;
+        st[SW_CMODE] = fits ? 2 : 0;
     }
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
@@ -2680,6 +2786,12 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
             sel_done(st, r);
         }
     } else {
+        // the first pass's window holds this rank's elements of the crossing bucket when the
+        // bucket lies inside it: later passes read cbuf (else the column, as without a window)
+        if (st[SW_CMODE] == 2) {
+            const int b = lane * SEL_PB + first;
+            st[SW_CMODE] = (b >= (int)st[SW_WB0] && b <= (int)st[SW_WB1]) ? 1 : 0;
+        }
         st[SW_LO] = kmin;
         st[SW_HI] = kmax;
         st[SW_SHIFT] = shift_for(kmin, kmax);
@@ -4260,6 +4372,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_sel_setup, dim3(sg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_range, dim3(sg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_compact, dim3(1), dim3(1024), 0, st, m);
+            hipLaunchKernelGGL(k_sel_sample, dim3(m.n_scaled), dim3(BT), 0, st, m);
             break;
         case M_SEL_EXACT:
             if (m.n_scaled == 0) break;

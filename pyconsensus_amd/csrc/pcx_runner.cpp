@@ -437,7 +437,8 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         // known (M_COLSTATS, the fill), so one histogram pass over the whole range also collects
         // the totals the walk starts from; launched for all S events (those not needed exit),
         // its collectives sized for S.  Counting only for reputation=None interpolation medians.
-        R.stage(m, M_SEL_INIT);
+        R.stage(m, M_SEL_INIT);  // (also the sampled windows, k_sel_sample: every rank's samples summed)
+        R.allreduce(w->hist_w, (int64_t)S * SEL_NB * 3, PCX_F64, PCX_SUM);
         m.sel_first = 1;
         R.mark(M_SEL_HIST);
         R.check_err(sel_hist(m, S, R.st), "k_sel_hist");

@@ -1,14 +1,23 @@
 # One GPU call for a change set: an optional A/B of batched-kernel builds (ab/NAME/libpcx.so,
 # alternated twice), then the whole GPU suite, one C5 shard's stage times and a short bench.
-# usage: gpurun --timeout 1500 -- 'bash tools/gpu_all.sh TAG [ab/x/libpcx.so ab/y/libpcx.so ...]'
+# usage: gpurun --timeout 1500 -- 'bash tools/gpu_all.sh TAG "ab/x/libpcx.so ab/y/libpcx.so" "ab/p/libpcx.so ..."'
+#   (first list: C3 batched A/B; second list: C5 1-GPU latency A/B with stage times)
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${1:-all}; shift
+TAG=${1:-all}
+ABC3=${2:-}
+ABC5=${3:-}
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG
 mkdir -p $O
 for i in 1 2; do
-  for L in "$@"; do
+  for L in $ABC5; do
+    PCX_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-c4 --c5-steps 3 --steps 3 > $O/c5ab.json 2> $O/c5ab.err || { echo "c5 ab rc=$? ($L)"; tail -3 $O/c5ab.err; exit 16; }
+    python3 -c "import json,sys; c=json.load(open('$O/c5ab.json'))['c5']; s=c['stage_ms']; print('%-24s C5 %.1f ms ' % (sys.argv[1], c['latency_ms']) + ' '.join('%s %.2f' % (k[2:], v) for k, v in list(s.items())[:12]))" "$L"
+  done
+done
+for i in 1 2; do
+  for L in $ABC3; do
     PCX_LIB=$L timeout -k 10 120 python bench.py --no-cpu-baseline --c5-steps 0 --no-c4 --steps 30 > $O/ab.json 2> $O/ab.err || { echo "ab rc=$? ($L)"; tail -3 $O/ab.err; exit 15; }
     python3 -c "import json,sys; d=json.load(open('$O/ab.json')); print('%-30s %.4f ms  %.2fM rounds/s' % (sys.argv[1], d['roofline']['kernel_ms'], d['value']/1e6))" "$L"
   done
