@@ -1075,12 +1075,19 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int GT = 256;                              // output tile edge
 constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one int8 operand's 64-row stage: 16 KB
 constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
+#ifndef PCX_GEMM_KS
+#define PCX_GEMM_KS 1
+#endif
+constexpr int G_KS = PCX_GEMM_KS;  // MFMA k-steps (64 rows each) per ring stage and barrier
 template <bool BPACK>
 struct GRing {
-    static constexpr int NBUF = BPACK ? 6 : 4;       // LDS ring depth
-    static constexpr size_t STAGE = G_PANEL + (BPACK ? G_PANEL_PK : G_PANEL);
-    static constexpr size_t BYTES = NBUF * STAGE;    // 120 KB / 128 KB
+    static constexpr int KS = G_KS;
+    static constexpr size_t BPANEL = BPACK ? G_PANEL_PK : G_PANEL;
+    static constexpr int NBUF = KS == 1 ? (BPACK ? 6 : 4) : (BPACK ? 3 : 2);  // LDS ring depth
+    static constexpr size_t STAGE = KS * (G_PANEL + BPANEL);
+    static constexpr size_t BYTES = NBUF * STAGE;  // <= 128 KB
 };
+static_assert(GRing<true>::BYTES <= 131072 && GRing<false>::BYTES <= 131072, "int8 GEMM ring");
 
 struct GemmI8 {
     const int8_t* A;
@@ -1099,19 +1106,20 @@ struct GemmI8 {
 // LDS read traffic per MFMA).  Same items, slabs and integer results.
 template <int WAVES, bool BPACK>
 __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
-    static_assert(!BPACK || WAVES == 16, "packed B: one dword load per wave per stage");
+    static_assert(!BPACK || WAVES == 16, "packed B: one dword load per wave per k-step");
     using RG = GRing<BPACK>;
+    constexpr int KS = RG::KS;
     constexpr int WR = WAVES == 16 ? 4 : 2;  // wave rows (p); 4 wave columns (q)
     constexpr int TM = GT / WR, AF = TM / 16;
-    constexpr int LPP = 16 / WAVES;  // 1 KB loads per wave per int8 panel per stage (16 KB panels)
-    constexpr int LOADS = LPP + (BPACK ? 1 : LPP);  // vector-memory ops per wave per stage
+    constexpr int LPP = 16 / WAVES;  // 1 KB loads per wave per int8 panel per k-step (16 KB panels)
+    constexpr int LOADS = KS * (LPP + (BPACK ? 1 : LPP));  // vector-memory ops per wave per stage
     extern __shared__ __attribute__((aligned(16))) char glds[];
     const int ntiles = g.tp * g.tq;
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / ntiles, t = item % ntiles;
     const int ip = t / g.tq, iq = t % g.tq;
     if (g.lower && iq > ip) return;  // above the diagonal (square tiles)
-    const int64_t nst = g.rg / 4;
+    const int64_t nst = g.rg / (4 * KS);  // (rg is a multiple of 4 KS)
     const int64_t per = (nst + g.kslices - 1) / g.kslices;
     const int64_t s0 = ks * per < nst ? ks * per : nst;
     const int64_t s1 = s0 + per < nst ? s0 + per : nst;  // (an empty slice stores zeros)
@@ -1121,24 +1129,29 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
     auto issue = [&](int64_t st, int buf) {
         char* sbase = glds + (size_t)buf * RG::STAGE;
 #pragma unroll
-        for (int j = 0; j < LPP; j++) {  // chunk ch = (row group mg, quarter mh) of the int8 panels
-            const int ch = wv + j * WAVES, mg = ch & 3, mh = ch >> 2;
-            char* base = sbase + ((size_t)mg * GT + mh * 64) * 16;
-            const int64_t grp = st * 4 + mg;
-            const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
-            __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
-            if constexpr (!BPACK) {
-                const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
-                __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16), (lds_ptr_t)(base + G_PANEL), 16,
-                                                 0, 0);
+        for (int kk = 0; kk < KS; kk++) {
+#pragma unroll
+            for (int j = 0; j < LPP; j++) {  // chunk ch = (row group mg, quarter mh) of the int8 panels
+                const int ch = wv + j * WAVES, mg = ch & 3, mh = ch >> 2;
+                char* base = sbase + kk * G_PANEL + ((size_t)mg * GT + mh * 64) * 16;
+                const int64_t grp = (st * KS + kk) * 4 + mg;
+                const int8_t* Ab = g.A + ((int64_t)ip * GT + mh * 64 + lane) * 16;
+                __builtin_amdgcn_global_load_lds((const void*)(Ab + grp * g.lda * 16), (lds_ptr_t)base, 16, 0, 0);
+                if constexpr (!BPACK) {
+                    const int8_t* Bb = g.B + ((int64_t)iq * GT + mh * 64 + lane) * 16;
+                    __builtin_amdgcn_global_load_lds((const void*)(Bb + grp * g.ldb * 16),
+                                                     (lds_ptr_t)(base - kk * G_PANEL + KS * G_PANEL + kk * RG::BPANEL),
+                                                     16, 0, 0);
+                }
             }
-        }
-        if constexpr (BPACK) {  // packed panel [mg][256 positions] uint32: 256 B per wave
-            const int mg = wv & 3, mh = wv >> 2;
-            const uint32_t* Bb = reinterpret_cast<const uint32_t*>(g.B) + (st * 4 + mg) * g.ldb + (int64_t)iq * GT +
-                                 mh * 64 + lane;
-            __builtin_amdgcn_global_load_lds((const void*)Bb,
-                                             (lds_ptr_t)(sbase + G_PANEL + ((size_t)mg * GT + mh * 64) * 4), 4, 0, 0);
+            if constexpr (BPACK) {  // packed panel [mg][256 positions] uint32: 256 B per wave
+                const int mg = wv & 3, mh = wv >> 2;
+                const uint32_t* Bb = reinterpret_cast<const uint32_t*>(g.B) + ((st * KS + kk) * 4 + mg) * g.ldb +
+                                     (int64_t)iq * GT + mh * 64 + lane;
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)Bb, (lds_ptr_t)(sbase + KS * G_PANEL + kk * RG::BPANEL + ((size_t)mg * GT + mh * 64) * 4),
+                    4, 0, 0);
+            }
         }
     };
     v4i acc[AF][4];
@@ -1152,36 +1165,42 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
         if (k < n) issue(s0 + k, k);
     for (int64_t t = 0; t < n; t++) {
         const int buf = (int)(t % RG::NBUF);
+#ifndef PCX_X_GEMM_NOSYNC  // ablation: no waits / barriers (races: wrong results, time only)
         if (t + RG::NBUF - 2 < n)
             wait_vmcnt<LOADS * (RG::NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
         else
             wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         if (t + RG::NBUF - 1 < n) issue(s0 + t + RG::NBUF - 1, (int)((t + RG::NBUF - 1) % RG::NBUF));
         const char* sb = glds + (size_t)buf * RG::STAGE;
-        const v4i* As = (const v4i*)sb + lg * GT + wr * TM + lc;
-        v4i af[AF], bf[4];
 #pragma unroll
-        for (int a = 0; a < AF; a++) af[a] = As[a * 16];
-        if constexpr (BPACK) {
-            const uint32_t* Bs = (const uint32_t*)(sb + G_PANEL) + lg * GT + wc * 64 + lc;
-            constexpr uint32_t M2 = 0x03030303u;
+        for (int kk = 0; kk < KS; kk++) {
+            const v4i* As = (const v4i*)(sb + kk * G_PANEL) + lg * GT + wr * TM + lc;
+            v4i af[AF], bf[4];
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const uint32_t P = Bs[b * 16];
-                bf[b] = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
+            for (int a = 0; a < AF; a++) af[a] = As[a * 16];
+            if constexpr (BPACK) {
+                const uint32_t* Bs = (const uint32_t*)(sb + KS * G_PANEL + kk * RG::BPANEL) + lg * GT + wc * 64 + lc;
+                constexpr uint32_t M2 = 0x03030303u;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t P = Bs[b * 16];
+                    bf[b] = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
+                }
+            } else {
+                const v4i* Bs = (const v4i*)(sb + KS * G_PANEL + kk * RG::BPANEL) + lg * GT + wc * 64 + lc;
+#pragma unroll
+                for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
             }
-        } else {
-            const v4i* Bs = (const v4i*)(sb + G_PANEL) + lg * GT + wc * 64 + lc;
 #pragma unroll
-            for (int b = 0; b < 4; b++) bf[b] = Bs[b * 16];
+            for (int a = 0; a < AF; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
         }
-#pragma unroll
-        for (int a = 0; a < AF; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
         asm volatile("" ::: "memory");
     }
     // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r

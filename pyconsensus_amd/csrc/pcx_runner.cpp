@@ -30,7 +30,7 @@ constexpr int CM = 8;   // doubles per column in mpart / cmax
 constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
-constexpr int COV_STAGE = 64;  // wcd rows: whole 64-row stages of the int8 GEMM
+constexpr int COV_STAGE = 128;  // wcd rows: whole 128-row stages of the int8 GEMM (KS <= 2)
 constexpr int SELS = 32;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
