@@ -44,6 +44,16 @@ constexpr double DBL_EPS = 2.220446049250313080847e-16;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
+// The round's helpers that run at several call sites (the sums, the np.dot replays, the
+// medians, the power-iteration steps) are outlined: inlined, the 50 x 20 kernel is ~83 KB of
+// code, more than the instruction cache of a CU pair holds while a dozen rounds per CU sit in
+// different phases.  PCX_INLINE_ALL=1 inlines them again (A/B builds).
+#ifdef PCX_INLINE_ALL
+#define PCX_OUTLINE __forceinline__
+#else
+#define PCX_OUTLINE __noinline__
+#endif
+
 // diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
 #define STAMP(k)                                                                  \
     do {                                                                          \
@@ -162,7 +172,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 // runs as a DPP wave_shr chain (each step recomputes final lanes identically); the
 // accumulators, the fixed tree and the tail are then read back wave-uniformly.
 // Same additions in the same order as numpy (and the C oracle's pw_sum).
-__device__ __forceinline__ double wave_pw_sum(double v, bool sel) {
+__device__ PCX_OUTLINE double wave_pw_sum(double v, bool sel) {
     const int l = lane_id();
     const uint64_t m = ballot(sel);
     const int n = popc(m);
@@ -241,7 +251,7 @@ __device__ __noinline__ double ob_ddot(const double* v, const double* f, int ld,
     return d;
 }
 
-__device__ __forceinline__ double ob_vecmat(const double* v, const double* f, int ld, int N, int E, int j) {
+__device__ PCX_OUTLINE double ob_vecmat(const double* v, const double* f, int ld, int N, int E, int j) {
     if (E == 1) return ob_ddot(v, f, ld, N);
     if (j < (E & ~3)) {
         double y = 0.0;
@@ -370,7 +380,7 @@ __device__ __forceinline__ uint32_t key_hi32(double x) {
 }
 
 template <int NR>
-__device__ __forceinline__ double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
+__device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
                                                     long long* prof = nullptr) {
     const int l = lane_id();
     double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
@@ -534,7 +544,7 @@ __device__ __forceinline__ void round_to_global(double* dst, const double* F, in
 }
 
 // scipy.stats.rankdata(method='average') of v[0..E) in LDS; lane j < E returns rank j
-__device__ __forceinline__ double rank_avg(const double* v, int E) {
+__device__ PCX_OUTLINE double rank_avg(const double* v, int E) {
     const int l = lane_id();
     double r = 0.0;
     if (l < E) {
@@ -642,7 +652,7 @@ __device__ Smem carve(double* base, int N, int E, int ES, int NR, bool pk) {
 
 // y = normalize(M x) for lane j < E, x in LDS; returns y_j (0 on other lanes)
 template <bool PK>
-__device__ __forceinline__ double matvec_unit(const double* M, int ES, const double* x, int E) {
+__device__ PCX_OUTLINE double matvec_unit(const double* M, int ES, const double* x, int E) {
     const int l = lane_id();
     double y = 0.0;
     if (l < E) {
@@ -666,7 +676,7 @@ __device__ __forceinline__ d4v mfma_f64(double a, double b, d4v c) {
 // entry is bit-identical to the VALU loop.  E <= 32: a 2 x 2 grid of 16 x 16 tiles.
 // M symmetric: A[ml][mm] = B[mm][ml], one read per operand pair.
 template <bool PK>
-__device__ __forceinline__ void square_scaled(double* M, int ES, int E) {
+__device__ PCX_OUTLINE void square_scaled(double* M, int ES, int E) {
     const int l = lane_id(), ml = l & 15, kq = l >> 4;
     const bool two = E > 16;
     d4v t00 = {0, 0, 0, 0}, t01 = {0, 0, 0, 0}, t10 = {0, 0, 0, 0}, t11 = {0, 0, 0, 0};

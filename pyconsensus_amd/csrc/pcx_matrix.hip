@@ -1076,7 +1076,7 @@ constexpr int GT = 256;                              // output tile edge
 constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one int8 operand's 64-row stage: 16 KB
 constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
 #ifndef PCX_GEMM_KS
-#define PCX_GEMM_KS 1
+#define PCX_GEMM_KS 2
 #endif
 constexpr int G_KS = PCX_GEMM_KS;  // MFMA k-steps (64 rows each) per ring stage and barrier
 template <bool BPACK>
@@ -2542,8 +2542,26 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
                     break;
                 }
             }
-            b0 = bx - SEL_WIN < 0 ? 0 : bx - SEL_WIN;
-            b1 = bx + SEL_WIN > NB - 1 ? NB - 1 : bx + SEL_WIN;
+            // widen by up to SEL_WIN buckets a side while this rank's estimated share of the
+            // window (sampled count x SEL_SAMPLE / world) stays within half of cbuf; a crossing
+            // bucket denser than that gets no window (the plain passes narrow it first)
+#ifdef PCX_X_NOWIN  // A/B: no window
+            const double cap = -1.0;
+#else
+            const double cap = 0.5 * (double)m.ccap * (double)m.world / (double)SEL_SAMPLE;
+#endif
+            double est = smp[NB + bx];
+            if (est <= cap) {
+                b0 = b1 = bx;
+                for (int r = 1; r <= SEL_WIN; r++) {
+                    const double l = bx - r >= 0 ? smp[NB + bx - r] : 0.0;
+                    const double h = bx + r < NB ? smp[NB + bx + r] : 0.0;
+                    if (est + l + h > cap) break;
+                    est += l + h;
+                    b0 = bx - r >= 0 ? bx - r : 0;
+                    b1 = bx + r < NB ? bx + r : NB - 1;
+                }
+            }
         }
         win_s[0] = b0;
         win_s[1] = b1;
@@ -2612,19 +2630,23 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             const uint64_t k = dkey(x);
             if (k < lo || k > hi) return;
             bin(k, w);
-            if (wgather) {
+            if (wgather || gather) {
                 const int b = (int)((k - lo) >> sh);
-                if (b >= wb0 && b <= wb1) {
-                    const unsigned long long j = atomicAdd(&gcount, 1ull);
-                    if (j < (unsigned long long)m.ccap) {
+                const bool put = gather || (b >= wb0 && b <= wb1);
+                // one LDS atomic per wave: the lanes that append take consecutive slots
+                const uint64_t pm = __ballot(put);
+                if (pm) {
+                    const int lead = __ffsll((long long)pm) - 1;
+                    const int lane = threadIdx.x % WAVE;
+                    unsigned long long base = 0;
+                    if (lane == lead) base = atomicAdd(&gcount, (unsigned long long)__popcll(pm));
+                    base = (unsigned long long)__shfl((long long)base, lead, WAVE);
+                    const unsigned long long j = base + __popcll(pm & ((1ull << lane) - 1ull));
+                    if (put && j < (unsigned long long)m.ccap) {
                         cb[2 * j] = k;
                         cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
                     }
                 }
-            } else if (gather) {
-                const unsigned long long j = atomicAdd(&gcount, 1ull);
-                cb[2 * j] = k;
-                cb[2 * j + 1] = (uint64_t)__double_as_longlong(w);
             }
         });
     }
