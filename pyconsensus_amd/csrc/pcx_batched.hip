@@ -44,14 +44,14 @@ constexpr double DBL_EPS = 2.220446049250313080847e-16;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
-// The round's helpers that run at several call sites (the sums, the np.dot replays, the
-// medians, the power-iteration steps) are outlined: inlined, the 50 x 20 kernel is ~83 KB of
-// code, more than the instruction cache of a CU pair holds while a dozen rounds per CU sit in
-// different phases.  PCX_INLINE_ALL=1 inlines them again (A/B builds).
-#ifdef PCX_INLINE_ALL
-#define PCX_OUTLINE __forceinline__
-#else
+// The round's helpers run inlined: the 50 x 20 kernel is ~83 KB of code, yet the instruction
+// cache misses 0.14 % of its fetches (SQC_ICACHE_MISSES / HITS, profiles/r3); outlined (calls,
+// PCX_OUTLINE_HELPERS=1, 49 KB + shared helpers) the call ABI spills and the kernel ran 29 %
+// slower (24.4 M vs 34.4 M rounds/s).
+#ifdef PCX_OUTLINE_HELPERS
 #define PCX_OUTLINE __noinline__
+#else
+#define PCX_OUTLINE __forceinline__
 #endif
 
 // diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries

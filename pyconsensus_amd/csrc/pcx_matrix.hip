@@ -2548,7 +2548,10 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
 #ifdef PCX_X_NOWIN  // A/B: no window
             const double cap = -1.0;
 #else
-            const double cap = 0.5 * (double)m.ccap * (double)m.world / (double)SEL_SAMPLE;
+            // (and within 1/16 of the column: a wider window re-reads about as much from cbuf
+            // as the plain pass reads from the column, after paying for the gather)
+            const double share = fmin(0.5 * (double)m.ccap, (double)m.n_rows / 16.0);
+            const double cap = share * (double)m.world / (double)SEL_SAMPLE;
 #endif
             double est = smp[NB + bx];
             if (est <= cap) {
