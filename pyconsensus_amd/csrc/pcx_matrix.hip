@@ -450,13 +450,21 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     acc2 sr, srx;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
     bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
-    rows_pipelined<PIPE_U>(
+#ifdef PCX_X_CS_NOMATH  // ablation (wrong results): the loads and a plain sum only
+    double acc = 0.0;
+    rows_pipelined<16>(r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
+                       [&](int64_t, XW v) { acc += v.x * v.w; });
+    cnt = acc;
+#else
+    rows_pipelined<16>(  // 16: whole 128-byte lines of T per lane
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
         [&](int64_t i, XW v) {
             const double x = rescale(v.x, p, m.int_dtype);
             const bool isn = __builtin_isnan(x);
             const bool z = x == 0.0;
+#ifndef PCX_X_CS_NOT  // ablation (wrong results): no T writes
             if (Tc) Tc[i] = (isn || z) ? __builtin_nan("") : x;
+#endif
             nz += z ? 1.0 : 0.0;
             if (isn || z) return;
             const double r = v.w;
@@ -471,6 +479,7 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             mx_x = fmax(mx_x, x);
             offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);
         });
+#endif
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, {cnt, 0.0});
     st_dd(pp + 2, sr.get());
