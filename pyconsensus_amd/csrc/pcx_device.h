@@ -77,6 +77,12 @@ __device__ __forceinline__ dd dd_mul_d(dd a, double b) {
 
 __device__ __forceinline__ dd dd_sub(dd a, dd b) { return dd_add(a, dd{-b.hi, -b.lo}); }
 
+// the exact product a b as a double-double
+__device__ __forceinline__ dd two_prod_dd(double a, double b) {
+    const double p = a * b;
+    return fast_two_sum(p, fma(a, b, -p));
+}
+
 // ---------------------------------------------------------------- keys
 // order-preserving map double -> uint64 (-0.0 is folded onto +0.0)
 __device__ __forceinline__ uint64_t dkey(double x) {

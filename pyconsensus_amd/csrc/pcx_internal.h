@@ -106,6 +106,9 @@ typedef struct {
     int32_t  cov_jb;              /* first pure-grid 128-column tile (= wcd_ld / 128: none)          */
     int32_t  cov_fp_tiles;        /* fp64 tiles: the Jb x Jb triangle (mixed pairs on int8) or the trapezoid J < cov_jb */
     int32_t  cov_mixed;           /* general x grid pairs on int8 slices of w (M_COV_I8)             */
+    double*  Fg;                  /* [wcd_rows][128 cov_jb] the filled F of the general positions (or NULL) */
+    uint16_t* nam;                /* [wcd_rows/16][wcd_ld] missing-report bits of 16 rows per position */
+    int32_t  compact;             /* M_GEMV2 / M_OUTCOMES read Fg, zB and nam, not the reports      */
     int32_t  tokpos;              /* local int8 position of the token column: E - 128 cov_jb          */
     /* mixed pairs: w of the general positions (< 128 cov_jb) in 8 balanced int8 digits of 7 bits,
        fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */

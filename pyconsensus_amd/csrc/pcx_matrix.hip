@@ -436,6 +436,7 @@ struct XW {
 
 // PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
 // min/max present value; writes the scaled columns (column-major) into T.
+template <bool EQW>  // EQW: reputation=None (every weight 1/N)
 __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     const int c = blockIdx.x * BT + threadIdx.x;
     if (c >= m.n_events) return;
@@ -447,7 +448,8 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     // 16 rows per step: each lane writes whole 128-byte lines of its T column (with 8,
     // half-line partial writes doubled the write traffic: 14 GB for 8 GB of T at C5)
     row_range(m, r0, r1, 16);
-    acc2 sr, srx;
+    acc2 sr, srx, sx;
+    constexpr bool eqw = EQW;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
     bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
 #ifdef PCX_X_CS_NOMATH  // ablation (wrong results): the loads and a plain sum only
@@ -469,8 +471,12 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             if (isn || z) return;
             const double r = v.w;
             cnt += 1.0;
-            sr.add(r);
-            srx.add_prod(r, x);
+            if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
+                sx.add(x);
+            } else {
+                sr.add(r);
+                srx.add_prod(r, x);
+            }
             if (r > mx) {
                 mx = r;
                 arg = (double)(m.row_offset + i);
@@ -482,8 +488,14 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
 #endif
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, {cnt, 0.0});
-    st_dd(pp + 2, sr.get());
-    st_dd(pp + 4, srx.get());
+    if constexpr (eqw) {  // sum r = cnt r exactly, sum r x = (sum x) r to dd accuracy
+        const double r = 1.0 / (double)m.n_total;  // = m.rep[i] (k_rep_local)
+        st_dd(pp + 2, two_prod_dd(cnt, r));
+        st_dd(pp + 4, dd_mul_d(sx.get(), r));
+    } else {
+        st_dd(pp + 2, sr.get());
+        st_dd(pp + 4, srx.get());
+    }
     st_dd(pp + 6, {nz, 0.0});
     double* mp = m.mpart + ((int64_t)blockIdx.y * E + c) * CM;
     mp[0] = mx;
@@ -835,7 +847,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int64_t g0 = r0; g0 < r1; g0 += 64) {
         const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;  // a multiple of 16 (wcd_rows % 16 == 0)
         for (int q0 = 0; q0 < gn; q0 += 16) {
-            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0};
+            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0}, nb[2] = {0, 0};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
                 double rv[4][2];
@@ -864,6 +876,10 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                             w[k] = f - p[k].mu;
                             xo[k] = x;
                             fo[k] = f;
+                            if (m.compact) {  // the compact sources of M_GEMV2 / M_OUTCOMES
+                                nb[k] |= missing(x) ? 1u << (4 * h + u) : 0u;
+                                if (pos[k] < gb) m.Fg[i * gb + pos[k]] = f;
+                            }
                             if (zc[k]) {
                                 const int z = (int)((f - 1.0) * 2.0);
                                 za[k][h] |= (uint32_t)(uint8_t)(int8_t)(tk * z) << (8 * u);
@@ -899,6 +915,11 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                 }
             }
             const int64_t grp = (g0 + q0) >> 4;
+            if (m.compact) {
+#pragma unroll
+                for (int k = 0; k < 2; k++)
+                    if (ok[k]) m.nam[grp * ld + pos[k]] = (uint16_t)nb[k];
+            }
 #pragma unroll
             for (int k = 0; k < 2; k++)
                 if (zc[k]) {
@@ -1861,6 +1882,48 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
     st_dd(pp + 2, a2.get());
 }
 
+// M_GEMV2 from the compact sources (m.compact): thread = one wcd position (general positions
+// read the filled values Fg, grid positions F = 1 + z / 2 from the 2-bit codes), 16-row groups;
+// the same per-row products and compensated sums as k_gemv2, into the same partial slots
+__global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
+    const int q = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (q >= E) return;
+    const int c = m.cov_perm[q];
+    if (c < 0) return;  // (padding)
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    const double* n1 = m.rowv + RV_N1 * m.n_rows;
+    const double* n2 = m.rowv + RV_N2 * m.n_rows;
+    acc2 a1, a2;
+    if (q < gb) {
+        rows_pipelined<PIPE_U>(
+            r0, r1, [&](int64_t i) { return XW{m.Fg[i * gb + q], n1[i]}; },
+            [&](int64_t i, XW v) {
+                a1.add_prod(v.w, v.x);
+                a2.add_prod(n2[i], v.x);
+            });
+    } else {
+        const uint32_t* zb = zb_packed(m) + (q - gb);
+        for (int64_t g = r0 / 16; g * 16 < r1; g++) {
+            const uint32_t P = zb[g * m.zq];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t i = g * 16 + r;
+                if (i < r1) {
+                    const double f = 1.0 + 0.5 * (double)zpack_get(P, r);
+                    a1.add_prod(n1[i], f);
+                    a2.add_prod(n2[i], f);
+                }
+            }
+        }
+    }
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, a1.get());
+    st_dd(pp + 2, a2.get());
+}
+
 // ob_order: the scalar sums of the reference in numpy's pairwise order, written over the dd
 // totals of scal[rank] (one thread; N < 9216).  which 0: sum(rep) (np.mean(rep), :461, and
 // np.ma.average's denominator, :317); 1: normalize(set1 / set2) totals (:244-249, :491-492);
@@ -2084,6 +2147,57 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
             n15 += f == 1.5 ? 1.0 : 0.0;
             n2 += f == 2.0 ? 1.0 : 0.0;
         });
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, raw.get());
+    st_dd(pp + 2, {pc, 0.0});
+    st_dd(pp + 4, {b1, 0.0});
+    st_dd(pp + 6, {b15, 0.0});
+    st_dd(pp + 8, {b2, 0.0});
+    st_dd(pp + 10, {n1, 0.0});
+    st_dd(pp + 12, {n15, 0.0});
+    st_dd(pp + 14, {n2, 0.0});
+}
+
+// M_OUTCOMES from the compact sources (m.compact): as k_gemv2_c, with the missing bits nam
+__global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
+    const int q = blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
+    if (q >= E) return;
+    const int c = m.cov_perm[q];
+    if (c < 0) return;
+    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
+    acc2 raw;
+    double pc = 0, b1 = 0, b15 = 0, b2 = 0;
+    double n1 = 0, n15 = 0, n2 = 0;
+    auto cell = [&](double f, double w, bool ms) {
+        raw.add_prod(w, f);
+        pc += w * (ms ? 1.0 : 0.0);  // np.dot(smooth_rep, na_mat): a NaN weight propagates
+        b1 += f == 1.0 ? w : 0.0;
+        b15 += f == 1.5 ? w : 0.0;
+        b2 += f == 2.0 ? w : 0.0;
+        n1 += f == 1.0 ? 1.0 : 0.0;
+        n15 += f == 1.5 ? 1.0 : 0.0;
+        n2 += f == 2.0 ? 1.0 : 0.0;
+    };
+    const bool general = q < gb;
+    const uint32_t* zb = zb_packed(m) + (general ? 0 : q - gb);
+    for (int64_t g = r0 / 16; g * 16 < r1; g++) {
+        const uint32_t M = m.nam[g * ld + q];
+        const uint32_t P = general ? 0u : zb[g * m.zq];
+        double fv[16];
+        if (general) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) fv[r] = g * 16 + r < r1 ? m.Fg[(g * 16 + r) * gb + q] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int64_t i = g * 16 + r;
+            if (i < r1) cell(general ? fv[r] : 1.0 + 0.5 * (double)zpack_get(P, r), sm[i], (M >> r) & 1u);
+        }
+    }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, raw.get());
     st_dd(pp + 2, {pc, 0.0});
@@ -2557,9 +2671,9 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
 #ifdef PCX_X_NOWIN  // A/B: no window
             const double cap = -1.0;
 #else
-            // (and within 1/16 of the column: a wider window re-reads about as much from cbuf
+            // (and within 1/8 of the column: a wider window re-reads about as much from cbuf
             // as the plain pass reads from the column, after paying for the gather)
-            const double share = fmin(0.5 * (double)m.ccap, (double)m.n_rows / 16.0);
+            const double share = fmin(0.5 * (double)m.ccap, (double)m.n_rows / 8.0);
             const double cap = share * (double)m.world / (double)SEL_SAMPLE;
 #endif
             double est = smp[NB + bx];
@@ -4248,7 +4362,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (m.ob_order) hipLaunchKernelGGL(k_ob_sums, dim3(1), dim3(64), 0, st, m, 0);
             break;
         case M_COLSTATS:
-            hipLaunchKernelGGL(k_colstats, colgrid, dim3(BT), 0, st, m);
+            if (m.rep_raw)
+                hipLaunchKernelGGL(k_colstats<false>, colgrid, dim3(BT), 0, st, m);
+            else
+                hipLaunchKernelGGL(k_colstats<true>, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
             break;
         case M_GUESS:
@@ -4373,7 +4490,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
-            hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
+            if (m.compact && m.Fg && m.nam && m.zB)
+                hipLaunchKernelGGL(k_gemv2_c, colgrid, dim3(BT), 0, st, m);
+            else
+                hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
             break;
         case M_DECIDE:
@@ -4395,7 +4515,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);
             break;
         case M_OUTCOMES:
-            hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
+            if (m.compact && m.Fg && m.nam && m.zB)
+                hipLaunchKernelGGL(k_outcomes_c, colgrid, dim3(BT), 0, st, m);
+            else
+                hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
             break;
         case M_EVENTS:

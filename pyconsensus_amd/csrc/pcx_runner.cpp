@@ -70,7 +70,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx, clw;
+    } pgg, zd, pmx, clw, fg, nam;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -84,7 +84,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx, &clw})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -908,6 +908,15 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                                   : 0;
                 r->mixed_int8 = m.cov_mixed;
                 m.zD = (int8_t*)w->zd.p;
+                // mixed: the later full passes (M_GEMV2, M_OUTCOMES) read F compactly -- the general
+                // positions' filled values (Fg, written by k_wcd), the grid ones from the 2-bit codes
+                // and the missing bits (nam) -- instead of the reports (a quarter of the bytes at C5)
+                m.compact = m.cov_mixed && w->grow(w->fg, (size_t)(w->wcd_rows * gb * 8)) &&
+                                    w->grow(w->nam, (size_t)(w->wcd_rows / 16 * w->wcd_ld * 2))
+                                ? 1
+                                : 0;
+                m.Fg = m.compact ? (double*)w->fg.p : nullptr;
+                m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
                 m.Pmx = (int32_t*)w->pmx.p;
                 m.cov_fp_tiles = (int32_t)(m.cov_mixed ? jb * (jb + 1) / 2 : jb * nb - jb * (jb - 1) / 2);
                 // fp64 slabs: [E][E] for the trapezoid; the mixed triangle's [gb][gb] slabs are
