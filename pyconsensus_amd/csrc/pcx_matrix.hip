@@ -354,6 +354,8 @@ __global__ void __launch_bounds__(BT) k_spart_finish(pcx_mat m, int nblk, int k,
 // grid (ceil(E/BT), G): thread = one event column, loop over a chunk of rows.
 // align > 1 rounds the chunk up to a multiple of align rows (whole 128-byte lines for
 // the column-major T writes of k_colstats); trailing blocks may get an empty range.
+// [r0, r1) of this block's row chunk; align: chunk starts a multiple of it -- except an empty
+// trailing chunk, which is [n_rows, n_rows) (callers stepping in aligned groups test r0 < r1)
 __device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t& r1, int64_t align = 1) {
     int64_t per = (m.n_rows + gridDim.y - 1) / gridDim.y;
     per = (per + align - 1) / align * align;
@@ -1906,7 +1908,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
             });
     } else {
         const uint32_t* zb = zb_packed(m) + (q - gb);
-        for (int64_t g = r0 / 16; g * 16 < r1; g++) {
+        for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {
             const uint32_t P = zb[g * m.zq];
 #pragma unroll
             for (int r = 0; r < 16; r++) {
@@ -2184,7 +2186,7 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     };
     const bool general = q < gb;
     const uint32_t* zb = zb_packed(m) + (general ? 0 : q - gb);
-    for (int64_t g = r0 / 16; g * 16 < r1; g++) {
+    for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {  // (an empty range capped at a ragged n_rows)
         const uint32_t M = m.nam[g * ld + q];
         const uint32_t P = general ? 0u : zb[g * m.zq];
         double fv[16];
