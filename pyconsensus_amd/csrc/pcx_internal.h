@@ -114,6 +114,7 @@ typedef struct {
        fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */
     int8_t*  zD;                  /* [wcd_rows/16][8 * 128 cov_jb][16] digit s of position q at s * 128 cov_jb + q */
     double*  dscale;              /* [wcd_ld] 2^-e per general position                               */
+    double*  mupos;               /* [wcd_ld] mu of the event at each wcd position (0 past E; M_COV_PLAN) */
     int32_t* Pgg;                 /* [ks_gg][zq][zq] int32 zA^T zB per k-slice (lower part)           */
     int32_t* Pmx;                 /* [ks_mx][zq][8 * 128 cov_jb] int32 zA^T zD per k-slice            */
     int32_t  ks_gg, ks_mx;        /* k-slices of the two int8 products (int32-exact row ranges)       */
@@ -125,6 +126,17 @@ typedef struct {
     double  variance_threshold;   /* "fixed-variance" stop                                          */
     const double* aux_scores;     /* [n_rows] cokurtosis scores / given scores                      */
 } pcx_mat;
+
+// int8 covariance GEMM (k_gemm_i8): 64-row MFMA k-steps per LDS ring stage; the workspace pads
+// wcd_rows to whole stages (pcx_runner.cpp COV_STAGE)
+#ifndef PCX_GEMM_KS
+#define PCX_GEMM_KS 2
+#endif
+// mixed block (general x grid pairs): base-128 int8 digits per general position.  7 digits leave
+// a residue <= 2^-50 of the column's largest |tok w| (8: 2^-57); pcx_matrix.hip k_digits
+#ifndef PCX_NDIG
+#define PCX_NDIG 7
+#endif
 
 namespace pcx {
 

@@ -57,6 +57,13 @@ enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARG
                  IN_COV_GENERAL, IN_COV_MIXED };
 
 // ------------------------------------------------------------------ element transform
+// PCX_FG_ONLY (A/B switch, default off): with the compact sources, drop the wcd copy of the general
+// positions and centre Fg on the fly in k_syrk / k_scores_grid / k_digits
+#ifndef PCX_FG_ONLY
+#define PCX_FG_ONLY 0
+#endif
+__host__ __device__ __forceinline__ bool fg_only(const pcx_mat& m) { return PCX_FG_ONLY && m.compact; }
+
 struct ColParam {
     bool scaled;
     double lo, range, guess, mu;
@@ -463,7 +470,11 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     rows_pipelined<16>(  // 16: whole 128-byte lines of T per lane
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
         [&](int64_t i, XW v) {
+#ifdef PCX_X_CS_NODIV  // ablation (wrong results): no rescale division
+            const double x = p.scaled ? v.x - p.lo : v.x;
+#else
             const double x = rescale(v.x, p, m.int_dtype);
+#endif
             const bool isn = __builtin_isnan(x);
             const bool z = x == 0.0;
 #ifndef PCX_X_CS_NOT  // ablation (wrong results): no T writes
@@ -474,7 +485,11 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             const double r = v.w;
             cnt += 1.0;
             if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
+#ifdef PCX_X_CS_NOTWOSUM  // ablation (wrong results): plain sum
+                sx.s += x;
+#else
                 sx.add(x);
+#endif
             } else {
                 sr.add(r);
                 srx.add_prod(r, x);
@@ -483,9 +498,11 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
                 mx = r;
                 arg = (double)(m.row_offset + i);
             }
+#ifndef PCX_X_CS_NOMINMAX  // ablation (wrong results): no extremes / grid flag
             mn_x = fmin(mn_x, x);
             mx_x = fmax(mx_x, x);
             offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);
+#endif
         });
 #endif
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
@@ -777,6 +794,8 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
     __syncthreads();
     const int G = base[0];
     const int gb = (G + CT - 1) / CT * CT;
+    if (m.mupos)  // wcd = F - mupos: k_syrk / k_scores_grid / k_digits centre the compact Fg on the fly
+        for (int64_t p = tid; p < m.wcd_ld; p += 1024) m.mupos[p] = m.cov_perm[p] >= 0 ? m.ev[EV_MU * E + m.cov_perm[p]] : 0.0;
     int bad = 0;
     double maxtok = 0.0;  // the largest token over all ranks (scal slot SC_MAXTOK, an integer)
     for (int w = 0; w < m.world; w++) maxtok = fmax(maxtok, m.scal[((int64_t)w * SS + SC_MAXTOK) * 2]);
@@ -878,10 +897,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                             w[k] = f - p[k].mu;
                             xo[k] = x;
                             fo[k] = f;
-                            if (m.compact) {  // the compact sources of M_GEMV2 / M_OUTCOMES
-                                nb[k] |= missing(x) ? 1u << (4 * h + u) : 0u;
-                                if (pos[k] < gb) m.Fg[i * gb + pos[k]] = f;
-                            }
+                            if (m.compact) nb[k] |= missing(x) ? 1u << (4 * h + u) : 0u;
                             if (zc[k]) {
                                 const int z = (int)((f - 1.0) * 2.0);
                                 za[k][h] |= (uint32_t)(uint8_t)(int8_t)(tk * z) << (8 * u);
@@ -891,8 +907,16 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                         }
                     }
 #pragma unroll
-                    for (int k = 0; k < 2; k++)  // mixed_int8: the grid positions live in zA / zB only
-                        if (pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb)) m.wcd[i * ld + pos[k]] = w[k];
+                    for (int k = 0; k < 2; k++) {
+                        // compact: the general positions' filled values Fg (padding rows: mu, F - mu = 0)
+                        // for M_GEMV2 / M_OUTCOMES; the grid positions live in zA / zB only
+                        if (m.compact && pos[k] >= 0 && pos[k] < gb)
+                            m.Fg[i * gb + pos[k]] = (live && ok[k]) ? fo[k] : p[k].mu;
+                        // wcd = F - mu of the general positions (all of them without the int8 mixed
+                        // block) for k_syrk / k_scores_grid / k_digits -- unless they centre Fg on the
+                        // fly (fg_only: 8 GB less written at C5, but k_syrk runs 26 ms instead of 18)
+                        if (!fg_only(m) && pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb)) m.wcd[i * ld + pos[k]] = w[k];
+                    }
                     // result["original"] / result["filled"] (:266-313), event order
                     if (live && (m.original || m.filled)) {
                         const int64_t o = i * E + c0;
@@ -965,7 +989,7 @@ struct SyRing {
     static constexpr int STRIDE = T_OFF + 4 * 32;             // doubles per buffer
     static constexpr int LPW = (DIAG ? SY_BK / 4 : SY_BK / 2) + 1;  // DMAs per wave per stage
 };
-constexpr size_t SY_LDS_BYTES = (size_t)SY_NBUF * SyRing<false>::STRIDE * sizeof(double);
+constexpr size_t SY_LDS_BYTES = (size_t)SY_NBUF * SyRing<false>::STRIDE * sizeof(double) + 2 * CT * sizeof(double);  // + mu
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -975,9 +999,13 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <bool DIAG>
+// MU: W is the compact filled matrix Fg; each fragment is centred (F - mu, k_wcd's rounding)
+// as it leaves LDS -- two f64 subtractions per operand pair beside a 64-cycle f64 MFMA
+// (the tile's 2 x 128 means sit in LDS after the ring, mus: read beside each fragment -- the 16
+// accumulators and 8 fragments already fill the 168-VGPR budget of 3 workgroups per CU)
+template <bool DIAG, bool MU>
 __device__ __forceinline__ void syrk_tile(const double* W, const double* tok, int64_t ld, int I, int J, int64_t s0,
-                                          int64_t ns, double* lds, d4 (&acc)[4][4]) {
+                                          int64_t ns, double* lds, d4 (&acc)[4][4], const double* mus) {
     using R = SyRing<DIAG>;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wr = wv >> 1, wc = wv & 1;
@@ -1028,14 +1056,21 @@ __device__ __forceinline__ void syrk_tile(const double* W, const double* tok, in
             const double tk = Ts[kr];
             double af[4], bf[4];
 #pragma unroll
-            for (int a = 0; a < 4; a++) af[a] = As[kr * SY_LDP + wr * 64 + a * 16 + (lane & 15)] * tk;
+            for (int a = 0; a < 4; a++) {
+                const double v = As[kr * SY_LDP + wr * 64 + a * 16 + (lane & 15)];
+                af[a] = (MU ? v - mus[wr * 64 + a * 16 + (lane & 15)] : v) * tk;
+            }
 #pragma unroll
-            for (int b = 0; b < 4; b++) bf[b] = Bs[kr * SY_LDP + wc * 64 + b * 16 + (lane & 15)];
+            for (int b = 0; b < 4; b++) {
+                const double v = Bs[kr * SY_LDP + wc * 64 + b * 16 + (lane & 15)];
+                bf[b] = MU ? v - mus[CT + wc * 64 + b * 16 + (lane & 15)] : v;
+            }
 #pragma unroll
             for (int a = 0; a < 4; a++)
 #pragma unroll
                 for (int b = 0; b < 4; b++)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+            if constexpr (MU) asm volatile("" ::: "memory");  // (keeps the next k-step's reads below: no spills)
         }
         asm volatile("" ::: "memory");
     }
@@ -1050,6 +1085,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 // one work item = (tile (I,J) of the trapezoid J < cov_jb of the lower triangle, row
 // slice ks) -> cslab[ks] (lower part, wcd positions); the pure-grid tiles are k_syrk_i8's
+template <bool CMP>  // CMP: the general block from the compact Fg (m.compact), centred on the fly
 __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
     extern __shared__ __attribute__((aligned(16))) double sy_lds[];
     const int E = (int)m.n_events;
@@ -1072,10 +1108,19 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
     const int64_t s0 = ks * per < nst ? ks * per : nst;
     const int64_t s1 = s0 + per < nst ? s0 + per : nst;
     d4 acc[4][4];
+    const int64_t gbl = (int64_t)m.cov_jb * CT;
+    const double* W = CMP ? m.Fg : m.wcd;
+    const int64_t wld = CMP ? gbl : m.wcd_ld;
+    double* mus = sy_lds + SY_NBUF * SyRing<false>::STRIDE;  // [2][CT]: the row tile's and column tile's means
+    if constexpr (CMP) {
+        const int t = threadIdx.x;  // 256 threads
+        mus[t] = m.mupos[(t < CT ? I : J) * CT + (t & (CT - 1))];
+        __syncthreads();
+    }
     if (I == J)
-        syrk_tile<true>(m.wcd, m.tokp, m.wcd_ld, I, J, s0, s1 - s0, sy_lds, acc);
+        syrk_tile<true, CMP>(W, m.tokp, wld, I, J, s0, s1 - s0, sy_lds, acc, mus);
     else
-        syrk_tile<false>(m.wcd, m.tokp, m.wcd_ld, I, J, s0, s1 - s0, sy_lds, acc);
+        syrk_tile<false, CMP>(W, m.tokp, wld, I, J, s0, s1 - s0, sy_lds, acc, mus);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wr = wv >> 1, wc = wv & 1;
     const int64_t ld = m.fp_ld, pmax = ld < E ? ld : E;
@@ -1106,20 +1151,29 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int GT = 256;                              // output tile edge
 constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one int8 operand's 64-row stage: 16 KB
-constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
-#ifndef PCX_GEMM_KS
-#define PCX_GEMM_KS 2
+#ifndef PCX_GEMM_BSWZ
+#define PCX_GEMM_BSWZ 1
 #endif
+// packed B rows in LDS are XOR-swizzled: position p of row group g sits at dword p ^ (16 g), so
+// the row groups one ds_read_b32 reads together (lanes 16 g + c) fall in different banks (a
+// plain layout, rows a multiple of 32 dwords apart, 2-way conflicts; padding would cost the
+// ring's fourth stage).  The DMA lanes fetch the swizzled positions.
+constexpr int G_BSWZ = PCX_GEMM_BSWZ ? 16 : 0;
+constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
 constexpr int G_KS = PCX_GEMM_KS;  // MFMA k-steps (64 rows each) per ring stage and barrier
 template <bool BPACK>
 struct GRing {
     static constexpr int KS = G_KS;
     static constexpr size_t BPANEL = BPACK ? G_PANEL_PK : G_PANEL;
+#ifdef PCX_GEMM_NBUF
+    static constexpr int NBUF = BPACK ? PCX_GEMM_NBUF : (KS == 1 ? 4 : 2);
+#else
     static constexpr int NBUF = KS == 1 ? (BPACK ? 6 : 4) : (BPACK ? 3 : 2);  // LDS ring depth
+#endif
     static constexpr size_t STAGE = KS * (G_PANEL + BPANEL);
     static constexpr size_t BYTES = NBUF * STAGE;  // <= 128 KB
 };
-static_assert(GRing<true>::BYTES <= 131072 && GRing<false>::BYTES <= 131072, "int8 GEMM ring");
+static_assert(GRing<true>::BYTES <= 163840, "int8 GEMM ring (160 KB of LDS)");  // (only the packed-B form is launched)
 
 struct GemmI8 {
     const int8_t* A;
@@ -1179,7 +1233,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
             if constexpr (BPACK) {  // packed panel [mg][256 positions] uint32: 256 B per wave
                 const int mg = wv & 3, mh = wv >> 2;
                 const uint32_t* Bb = reinterpret_cast<const uint32_t*>(g.B) + ((st * KS + kk) * 4 + mg) * g.ldb +
-                                     (int64_t)iq * GT + mh * 64 + lane;
+                                     (int64_t)iq * GT + ((mh * 64 + lane) ^ (G_BSWZ * mg));
                 __builtin_amdgcn_global_load_lds(
                     (const void*)Bb, (lds_ptr_t)(sbase + KS * G_PANEL + kk * RG::BPANEL + ((size_t)mg * GT + mh * 64) * 4),
                     4, 0, 0);
@@ -1219,7 +1273,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
                 constexpr uint32_t M2 = 0x03030303u;
 #pragma unroll
                 for (int b = 0; b < 4; b++) {
-                    const uint32_t P = Bs[b * 16];
+                    const uint32_t P = Bs[(b * 16) ^ (G_BSWZ * lg)];
                     bf[b] = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
                 }
             } else {
@@ -1280,27 +1334,30 @@ __global__ void __launch_bounds__(BT) k_tokcol(pcx_mat m) {
 
 // tok * w of the general positions q < gb (the exact product, as a double-double) as 8 balanced
 // base-128 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 128 v, d = rint(t_hi), v = t - d
-// with the low part carried -- every step exact, |d| <= 65, residue <= 2^-56 2^e
+// with the low part carried -- every step exact, |d| <= 65; PCX_NDIG digits leave a residue
+// <= 2^-(7 NDIG + 1) 2^e (7: 2^-50 of the column's bound on |tok w|, 1.8e-15 relative)
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
     if (q >= gb) return;
     const double sc = m.dscale[q];
+    const double mu = fg_only(m) ? m.mupos[q] : 0.0;
     const int64_t ng = m.wcd_rows / 16;
     const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
     const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
-    const int64_t ldd = (int64_t)8 * gb;
+    const int64_t ldd = (int64_t)PCX_NDIG * gb;
     for (int64_t grp = g0; grp < g1; grp++) {
-        uint32_t d[8][4];
+        uint32_t d[PCX_NDIG][4];
 #pragma unroll
-        for (int k = 0; k < 8; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
+        for (int k = 0; k < PCX_NDIG; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            const double w = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;  // exact (power of two)
+            const double w = (fg_only(m) ? m.Fg[(grp * 16 + r) * gb + q] - mu : m.wcd[(grp * 16 + r) * m.wcd_ld + q]) *
+                             sc;  // exact (power of two)
             const double tk = m.tokp[grp * 16 + r];                       // 0 past n_rows
             double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < PCX_NDIG; k++) {
                 const double t = hi * 128.0, di = rint(t);
                 const double e = t - di;  // exact
                 const double l = lo * 128.0;
@@ -1311,7 +1368,7 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             }
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++)
+        for (int k = 0; k < PCX_NDIG; k++)
             *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
     }
 }
@@ -1384,14 +1441,14 @@ __device__ __forceinline__ int64_t slab_sum(const int32_t* P, int64_t slab, int 
     return (a0 + a1) + (a2 + a3);
 }
 
-// sum tok z_row w_q of the mixed block from its eight digit products, Horner in dd (2^-7)
+// sum tok z_row w_q of the mixed block from its PCX_NDIG digit products, Horner in dd (2^-7)
 __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t q) {
-    const int64_t gb = (int64_t)m.cov_jb * CT, ldm = 8 * gb;
+    const int64_t gb = (int64_t)m.cov_jb * CT, ldm = PCX_NDIG * gb;
     const double sc = ldexp(0x1p-7, -ilogb(m.dscale[q]));  // 2^(e - 7)
     const int32_t* P = m.Pmx + row * ldm + q;
     const int64_t slab = m.zq * ldm;
-    dd a{(double)slab_sum(P + 7 * gb, slab, m.ks_mx), 0.0};
-    for (int d = 6; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
+    dd a{(double)slab_sum(P + (PCX_NDIG - 1) * gb, slab, m.ks_mx), 0.0};
+    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
     return dd_mul_d(a, sc);
 }
 
@@ -1679,6 +1736,7 @@ __global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
 // PCX_M_SCORES with mixed_int8 (wcd holds only the general positions): one wave per 16-row
 // group; general positions from wcd, grid positions from the int8 codes, F - mu = c + z / 2:
 //   s_i = sum_{q < gb} wcd_iq ld_q + K + (1/2) sum_{q >= gb} z_iq ld_q,  K = sum_{q >= gb} c_q ld_q
+template <bool CMP>  // CMP: the general positions from the compact Fg (m.compact), else wcd
 __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
     const int lane = threadIdx.x % WAVE, wv = threadIdx.x / WAVE;
     const int64_t ld = m.wcd_ld;
@@ -1699,11 +1757,24 @@ __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
         double a[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) a[r] = 0.0;
-        for (int q = lane; q < gb; q += WAVE) {
-            const double l = LD[m.cov_perm[q]];
-            const double* w = m.wcd + g * 16 * ld + q;
+        if constexpr (CMP) {  // wcd = Fg - mu (the same rounding as k_wcd's)
+            const int64_t gbl = gb;
+            for (int q = lane; q < gb; q += WAVE) {
+                const double* f = m.Fg + g * 16 * gbl + q;
+                double v[16];  // the 16 rows' loads in flight together
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
+                for (int r = 0; r < 16; r++) v[r] = f[r * gbl];
+                const double l = LD[m.cov_perm[q]], mu = m.mupos[q];
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = fma(v[r] - mu, l, a[r]);
+            }
+        } else {
+            for (int q = lane; q < gb; q += WAVE) {
+                const double l = LD[m.cov_perm[q]];
+                const double* w = m.wcd + g * 16 * ld + q;
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
+            }
         }
         double z[16];
 #pragma unroll
@@ -2271,6 +2342,8 @@ enum sel_word {
     SW_GN, SW_GW0, SW_GW1, SW_GW2,    // phase 2, this rank: filled (missing) rows -- all at the fill
                                       // value -- count and raw weight limb sums, binned once per pass
     SW_WB0, SW_WB1,                   // first pass: the bucket window gathered into cbuf (sampled)
+    SW_CERTN, SW_CW0, SW_CW1, SW_CW2, // phase 2, weight walk ended on one key: the elements (all ranks)
+                                      // holding it and their exact weight -- the certainty (:540-546)
     SW_NWORDS
 };
 static_assert(SW_NWORDS <= SELS, "sel_state words");
@@ -2316,6 +2389,8 @@ __device__ __forceinline__ bool near_half(L3 P, L3 T, uint64_t n) {
 }
 
 __device__ __forceinline__ XW sel_load(const pcx_mat& m, int s, int64_t i) {
+    // phase 1 with reputation=None: every weight is rep = 1 / N (k_rep_local) -- not loaded
+    if (m.sel_phase == 1 && !m.rep_raw) return XW{m.T[(int64_t)s * m.n_rows + i], 1.0 / (double)m.n_total};
     return XW{m.T[(int64_t)s * m.n_rows + i], m.sel_phase == 1 ? m.rep[i] : m.rowv[RV_SMOOTH * m.n_rows + i]};
 }
 
@@ -2606,12 +2681,15 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
     const int64_t ns = m.n_rows / SEL_SAMPLE;
     for (int64_t j = threadIdx.x; j < ns; j += BT) {
         double x, w;
-        if (!sel_elem(m, s, j * SEL_SAMPLE, x, w)) continue;
+        const XW v = sel_load(m, s, j * SEL_SAMPLE);
+        if (!sel_decode(m, s, v, x, w)) continue;
         const uint64_t k = dkey(x);
         if (k < lo || k > hi) continue;
         const int b = (int)((k - lo) >> sh);
         atomicAdd(&sw[b], w);
-        atomicAdd(&sn[b], 1.0);
+        // phase 2: a filled row (all at the fill value) is binned once by k_sel_hist, never
+        // gathered into cbuf -- it weighs in the crossing, not in the window's size estimate
+        if (!(m.sel_phase == 2 && __builtin_isnan(v.x))) atomicAdd(&sn[b], 1.0);
     }
     __syncthreads();
     double* o = sel_sample_row(m, a);
@@ -2942,6 +3020,10 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
             if (near_half(below, tot, n_all) || near_half(upto, tot, n_all)) {
                 mark_hard(m, s, st);
                 return;
+            }
+            if (m.sel_phase == 2) {  // every element equal to the outcome is in this bucket
+                st[SW_CERTN] = n;
+                st_l3(st + SW_CW0, hw[first]);
             }
             sel_done(st, xs);
         } else {
@@ -3399,6 +3481,19 @@ __global__ void __launch_bounds__(BT) k_scaled_cert(pcx_mat m) {
     const int E = (int)m.n_events;
     const int c = m.scaled_cols[s];
     const double adj = m.ev[EV_ADJ * E + c];
+    const uint64_t* st = m.sel_state + (int64_t)s * SELS;
+    if (st[SW_CERTN] != 0 && adj != 0.0 && !m.int_dtype) {
+        // the selection's last histogram bucket held exactly the elements equal to the outcome
+        // (all ranks, exact weight limbs): no pass over the column.  (+-0.0 and the int dtype's
+        // truncated fills -- which may fold -0.0 -- take the pass.)
+        if (threadIdx.x == 0) {
+            const bool r0 = m.rank == 0;  // the totals are global: rank 0 carries them
+            const double w = r0 ? l3_to_double(ld_l3(st + SW_CW0)) : 0.0;
+            st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + 14) * 2, {w, 0.0});
+            st_dd(m.cstat + (((int64_t)m.rank * E + c) * CS + 15) * 2, {r0 ? (double)st[SW_CERTN] : 0.0, 0.0});
+        }
+        return;
+    }
     acc2 a;
     double n = 0.0;
     const double guess = m.ev[EV_GUESS * E + c];
@@ -4390,18 +4485,15 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int np = (int)(m.n_events - gb) + 1;  // grid positions + the token column
             if (!m.zA || !m.zB || !m.zsum || !m.Pgg || m.cov_jb < 0 || m.cov_jb > nb || m.zq < np || m.ks_gg < 1 ||
                 (m.cov_mixed && m.ks_mx < 1) ||
-                m.zq % GT || m.tokpos != np - 1 || m.wcd_rows % 64 || (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale))) {
+                m.zq % GT || m.tokpos != np - 1 || m.wcd_rows % (64 * G_KS) || (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale))) {
                 err = "M_COV_I8: int8 operands missing or plan inconsistent";
                 return hipErrorInvalidValue;
             }
             static std::once_flag g_once;
             static hipError_t g_err = hipSuccess;
             std::call_once(g_once, [] {
-                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, false>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<false>::BYTES);
-                if (g_err == hipSuccess)
-                    g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, true>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<true>::BYTES);
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, true>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<true>::BYTES);
             });
             if (g_err != hipSuccess) return g_err;
             const int64_t rg = m.wcd_rows / 16;
@@ -4414,13 +4506,13 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                                    GRing<true>::BYTES, st, g);
             }
             if (m.cov_mixed) {
-                // general digits x grid: digits of tok w (A, 8 per general position) times z (B);
+                // general digits x grid: digits of tok w (A, PCX_NDIG per general position) times z (B);
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 65 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
                 hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
-                GemmI8 g{m.zD, (int64_t)8 * gb, m.zB, m.zq, m.Pmx, (int64_t)8 * gb, m.zq * 8 * gb, 8 * gb, np,
+                GemmI8 g{m.zD, (int64_t)PCX_NDIG * gb, m.zB, m.zq, m.Pmx, (int64_t)PCX_NDIG * gb, m.zq * PCX_NDIG * gb, PCX_NDIG * gb, np,
                          0, 0, 0, m.ks_mx, rg, 1};
-                g.tp = (8 * gb + GT - 1) / GT;
+                g.tp = (PCX_NDIG * gb + GT - 1) / GT;
                 g.tq = (np + GT - 1) / GT;
                 hipLaunchKernelGGL((k_gemm_i8<16, true>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
                                    GRing<true>::BYTES, st, g);
@@ -4448,12 +4540,16 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             static std::once_flag lds_once;
             static hipError_t lds_err = hipSuccess;
             std::call_once(lds_once, [] {
-                lds_err = hipFuncSetAttribute((const void*)k_syrk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                lds_err = hipFuncSetAttribute((const void*)k_syrk<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)SY_LDS_BYTES);
+                if (lds_err == hipSuccess)
+                    lds_err = hipFuncSetAttribute((const void*)k_syrk<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)SY_LDS_BYTES);
             });
             if (lds_err != hipSuccess) return lds_err;
             if (m.cov_fp_tiles > 0)
-                hipLaunchKernelGGL(k_syrk, dim3(m.cov_fp_tiles * m.fp_ks), dim3(256), SY_LDS_BYTES, st, m);
+                hipLaunchKernelGGL(fg_only(m) ? k_syrk<true> : k_syrk<false>, dim3(m.cov_fp_tiles * m.fp_ks), dim3(256),
+                                   SY_LDS_BYTES, st, m);
             break;
         }
         case M_COV_REDUCE: {  // position-space lower triangle -> mirrored -> event order (Mw as scratch)
@@ -4478,7 +4574,14 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_skey_init, dim3(1), dim3(1), 0, st, m);
             if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart &&
                 m.cov_perm && m.cov_mixed)
-                hipLaunchKernelGGL(k_scores_grid, dim3(grid_rows((m.n_rows + 15) / 16, BT / WAVE)), dim3(BT), 0, st, m);
+            {
+                if (fg_only(m))
+                    hipLaunchKernelGGL(k_scores_grid<true>, dim3(grid_rows((m.n_rows + 15) / 16, BT / WAVE)), dim3(BT), 0,
+                                       st, m);
+                else
+                    hipLaunchKernelGGL(k_scores_grid<false>, dim3(grid_rows((m.n_rows + 15) / 16, BT / WAVE)), dim3(BT),
+                                       0, st, m);
+            }
             else if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd &&
                      m.rowpart && m.cov_perm)
                 hipLaunchKernelGGL(k_scores_wcd, dim3(grid_rows(m.n_rows, BT / WAVE)), dim3(BT), 0, st, m);

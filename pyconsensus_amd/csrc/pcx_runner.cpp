@@ -30,7 +30,7 @@ constexpr int CM = 8;   // doubles per column in mpart / cmax
 constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
-constexpr int COV_STAGE = 128;  // wcd rows: whole 128-row stages of the int8 GEMM (KS <= 2)
+constexpr int COV_STAGE = 64 * PCX_GEMM_KS > 128 ? 64 * PCX_GEMM_KS : 128;  // wcd rows: whole stages of the int8 GEMM
 constexpr int SELS = 32;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
@@ -63,6 +63,7 @@ struct pcx_workspace {
     int8_t *zA, *zB;
     int64_t* zsum;
     double* dscale;
+    double* mupos;
     uint64_t* cbuf;
     int64_t* ccount;
     int64_t ccap = 0;
@@ -278,6 +279,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->dscale, (size_t)w->wcd_ld * 8, false},
+        {(void**)&w->mupos, (size_t)w->wcd_ld * 8, false},
     };
     auto align = [](size_t b) { return (b + 255) / 256 * 256; };
     size_t zb = 0;
@@ -858,6 +860,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.zB = w->zB;
                 m.zsum = w->zsum;
                 m.dscale = w->dscale;
+                m.mupos = w->mupos;
                 R.stage(m, M_COV_PLAN);
                 int64_t plan[2];  // general events, mixed pairs on int8
                 R.hip(hipMemcpyAsync(plan, m.info + INFO_COV_GENERAL, sizeof(plan), hipMemcpyDeviceToHost, R.st),
@@ -873,7 +876,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 r->grid_events = (int32_t)(np > 0 ? E - gb : 0);  // grid events past the general tiles
                 // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
                 // |tok z d| <= 126 * 64 per row) and at least two WGs per CU
-                const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (8 * gb + 255) / 256;
+                const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (PCX_NDIG * gb + 255) / 256;
                 // one 128 KB workgroup per CU runs every (tile, k-slice) item for the same time, so
                 // the launch takes ceil(items / CUs) rounds: pick the k in [int32-exact minimum,
                 // 32] with the least rounds per unit of work (no half-empty last round)
@@ -902,8 +905,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 }
                 m.Pgg = (int32_t*)w->pgg.p;
                 // mixed pairs on int8 digits when the bounds are finite and the memory is there
-                m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * 8 * gb)) &&
-                                      w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * 8 * gb * 4))
+                m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * PCX_NDIG * gb)) &&
+                                      w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4))
                                   ? 1
                                   : 0;
                 r->mixed_int8 = m.cov_mixed;
