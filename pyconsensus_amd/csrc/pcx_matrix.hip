@@ -2674,7 +2674,7 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
     }
 }
 
-// The first pass's window: a strided sample of the column (every SEL_SAMPLE-th row, all ranks'
+// The first pass's window: a sample of the column (1 / SEL_SAMPLE of its rows, all ranks'
 // samples summed) histogrammed in the first pass's buckets; the bucket where the sample's
 // weight crosses half, +- SEL_WIN buckets, is the window the first pass also gathers into cbuf.
 // When the exact crossing bucket lies inside it (nearly always) the later passes read only
@@ -2696,10 +2696,15 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
     __syncthreads();
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
     const int sh = (int)st[SW_SHIFT];
-    const int64_t ns = m.n_rows / SEL_SAMPLE;
+    // runs of SEL_RUN consecutive rows every SEL_RUN * SEL_SAMPLE rows (the same 1/64 of the column
+    // as every 64th row, in whole cache lines: a strided sample read a line per element)
+    constexpr int SEL_RUN = 16;
+    const int64_t span = (int64_t)SEL_RUN * SEL_SAMPLE, full = m.n_rows / span;
+    const int64_t rem = m.n_rows - full * span;
+    const int64_t ns = full * SEL_RUN + (rem < SEL_RUN ? rem : SEL_RUN);
     for (int64_t j = threadIdx.x; j < ns; j += BT) {
         double x, w;
-        const XW v = sel_load(m, s, j * SEL_SAMPLE);
+        const XW v = sel_load(m, s, (j / SEL_RUN) * span + (j % SEL_RUN));
         if (!sel_decode(m, s, v, x, w)) continue;
         const uint64_t k = dkey(x);
         if (k < lo || k > hi) continue;
@@ -2727,7 +2732,9 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hn[NB], hmin[NB], hmax[NB];
+    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hmin[NB], hmax[NB];
+    __shared__ unsigned long long hn[NB];
+    typedef unsigned long long hn_t;
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
@@ -2819,7 +2826,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             atomicAdd(&hb[b], (unsigned long long)L.l1);
             atomicAdd(&hc[b], (unsigned long long)L.l2);
         }
-        atomicAdd(&hn[b], 1ull);
+        atomicAdd(&hn[b], (hn_t)1);
         atomicMin(&hmin[b], (unsigned long long)k);
         atomicMax(&hmax[b], (unsigned long long)k);
     };
@@ -2899,7 +2906,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
                     atomicAdd(&hb[b], f_gb);
                     atomicAdd(&hc[b], f_gc);
                 }
-                atomicAdd(&hn[b], f_gn);
+                atomicAdd(&hn[b], (hn_t)f_gn);
                 atomicMin(&hmin[b], (unsigned long long)fk);
                 atomicMax(&hmax[b], (unsigned long long)fk);
             }
@@ -2912,7 +2919,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             atomicAdd(&hb[b], (unsigned long long)st[SW_GW1]);
             atomicAdd(&hc[b], (unsigned long long)st[SW_GW2]);
         }
-        atomicAdd(&hn[b], (unsigned long long)st[SW_GN]);
+        atomicAdd(&hn[b], (hn_t)st[SW_GN]);
         atomicMin(&hmin[b], (unsigned long long)gk);
         atomicMax(&hmax[b], (unsigned long long)gk);
     }
