@@ -136,13 +136,17 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     i8_ms = prof.get("M_COV_I8", float("nan"))
     # unique (j, k<=j) covariance pairs: those with a general event on fp64 MFMA (k_syrk),
     # the grid-grid pairs on int8 MFMA (k_syrk_i8); one multiply-add per pair per row
-    # with mixed_int8 the general x grid pairs run on int8 too, as 8 digit slices of w (and
-    # the token column): int8 work = grid pairs + 8 x general x (grid + 1) per row
+    # with mixed_int8 the general x grid pairs run on int8 too, as D digit slices of w (and
+    # the token column; D = pcx_mixed_digits(), a build parameter): int8 work = grid pairs +
+    # D x general x (grid + 1) per row
+    from pyconsensus_amd import _lib
+
     ng = meta["grid_events"]
     G = E - ng
     mixed = meta.get("mixed_int8", 0)
+    digits = int(_lib.lib().pcx_mixed_digits())
     fp_pairs = G * (G + 1) // 2 + (0 if mixed else G * ng)
-    i8_pairs = ng * (ng + 1) // 2 + (8 * G * (ng + 1) if mixed else 0)
+    i8_pairs = ng * (ng + 1) // 2 + (digits * G * (ng + 1) if mixed else 0)
     cov_flops_rank = 2.0 * cnt * fp_pairs
     i8_ops_rank = 2.0 * cnt * i8_pairs
     tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms and fp_pairs else None
@@ -159,7 +163,8 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
                                        "on int8 slices: %s)" % (G, ng, bool(mixed)))},
             "roofline_cov_i8": {"bound": "mfma", "kernel": "k_syrk_i8", "achieved": tops, "peak": I8_MFMA_PEAK_TOPS,
                                 "unit": "TOP/s", "frac": (tops / I8_MFMA_PEAK_TOPS) if tops else None,
-                                "ops_per_launch": i8_ops_rank, "traffic": load_traffic("k_syrk_i8")},
+                                "ops_per_launch": i8_ops_rank, "mixed_digits": digits,
+                                "traffic": load_traffic("k_syrk_i8")},
             "grid_events": ng, "mixed_int8": mixed,
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}

@@ -60,6 +60,7 @@ def _declare(lib):
         ("pcx_ctx_progress", i32, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         ("pcx_seqsum_const", C.c_double, [C.c_double, i64]),
         ("pcx_seqsum_first_above", i64, [C.c_double, C.c_double, i64]),
+        ("pcx_mixed_digits", i32, []),
     ]:
         f = getattr(lib, name)
         f.restype = res

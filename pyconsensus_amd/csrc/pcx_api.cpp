@@ -549,5 +549,6 @@ int pcx_ctx_progress(const pcx_ctx* ctx, int* stage, int* host_waiting) {
 double pcx_seqsum_const(double c, int64_t k) { return pcx::seqsum_const(c, k); }
 
 int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax) { return pcx::seqsum_first_above(c, t, kmax); }
+int pcx_mixed_digits(void) { return PCX_NDIG; }
 
 }  // extern "C"
