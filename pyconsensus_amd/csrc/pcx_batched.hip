@@ -379,9 +379,12 @@ __device__ __forceinline__ uint32_t key_hi32(double x) {
     return (uint32_t)(u >> 32);
 }
 
+// use_rank (wave-uniform): `rank` is already each selected lane's count of selected keys below
+// its own (the rank loop is skipped); rank_out: when the rank loop runs, each lane's count
 template <int NR>
 __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
-                                                    long long* prof = nullptr) {
+                                                    long long* prof = nullptr, bool use_rank = false, int rank = 0,
+                                                    int* rank_out = nullptr) {
     const int l = lane_id();
     double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
     int* cnt = reinterpret_cast<int*>(scr + 3 * NR + med_ow(NR));
@@ -416,10 +419,15 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
 #ifdef PCX_X_NORANK  // ablation: no rank loop
     r = l;
 #else
+    if (use_rank) {
+        r = rank;
+    } else {
 #pragma unroll
-    for (int m = 0; m < NR; m++) {
-        if (NR == 64 && m >= N) break;
-        r += kx[m] < key ? 1 : 0;
+        for (int m = 0; m < NR; m++) {
+            if (NR == 64 && m >= N) break;
+            r += kx[m] < key ? 1 : 0;
+        }
+        if (rank_out) *rank_out = r;
     }
 #endif
     if (sel) atomicAdd(&cnt[r], 1);
@@ -1296,6 +1304,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
     uint64_t miss_j = 0;
     if (col) miss_j = S.nanm[l] | S.zerm[l];
+    constexpr int RKW = (ET > 0 ? ET + 3 : EMAX) / 4;  // interpolation-median ranks, a byte per column
+    uint32_t rkq[RKW];
+#pragma unroll
+    for (int k = 0; k < RKW; k++) rkq[k] = 0;
+    uint32_t rk_valid = 0;
     {
         // tot: the SPEC's sequential sum of the present reputations (a missing row adds
         // +0.0, which leaves a sum that starts at +0.0 unchanged).  A binary column's
@@ -1371,14 +1384,23 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             if (a.int_dtype) g = trunc(g);
             if (l == 0) S.guess[j] = g;
         };
-        // one median at a time: the scratch lives in M, dead until the covariance
+        // one median at a time: the scratch lives in M, dead until the covariance.  Each lane's
+        // rank among the present keys is kept (one byte per column) for the outcome median of the
+        // same column, whose keys are these plus the fill's (a8 below: no second rank loop)
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             double x0, w0, W0;
             bool p0;
             pair_of(j, x0, w0, p0, W0);
-            finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.M, a.stamps ? mprof : nullptr));
+            int rk = -1;
+            finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.M, a.stamps ? mprof : nullptr,
+                                                            false, 0, &rk));
+            if (ballot(rk >= 0)) {  // the rank loop ran (no dominant weight, no NaN)
+                rk_valid |= 1u << j;
+                const int sh = 8 * (j & 3);
+                rkq[j >> 2] = (rkq[j >> 2] & ~(0xffu << sh)) | ((uint32_t)(rk & 0xff) << sh);
+            }
             wsync();
         }
     }
@@ -1704,7 +1726,23 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const double x0 = row ? S.F[l * ES + j] : 0.0;
-            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, smooth_i, row, Wsm, N, S.M, a.stamps ? mprof : nullptr);
+            // the filled column's keys are the interpolation median's (present rows) plus the
+            // fill's (missing rows, all equal): a present row's count of smaller keys is its
+            // recorded one plus the missing rows when the fill's key is below its own, a missing
+            // row's is the present keys below the fill's -- the same counts the loop would make
+            const bool reuse = (rk_valid >> j) & 1;
+            int rk = 0;
+            if (reuse) {
+                const uint64_t mj = S.nanm[j] | S.zerm[j];
+                const bool ms = (mj >> l) & 1;
+                const uint32_t key = key_hi32(x0);
+                const uint32_t kg = (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(mj));
+                const int below = popc(ballot(row && !ms && key < kg));
+                const int own = (int)((rkq[j >> 2] >> (8 * (j & 3))) & 0xffu);
+                rk = ms ? below : own + (kg < key ? popc(mj) : 0);
+            }
+            const double m = wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, smooth_i, row, Wsm, N, S.M,
+                                                                   a.stamps ? mprof : nullptr, reuse, rk);
             if (l == j) rawj = m;
             wsync();
         }
@@ -1781,12 +1819,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(10);
     // ---- a15: participation and bonuses (:549-581) -------------------------
     double pcj = 0.0, nzj = 0.0;
+    // every smooth_rep finite: a row with na = 0 adds p = x * 0 = +-0 and pe = +-0, which leave
+    // (s, c) bit for bit as they were (neither is ever -0.0), so only the missing rows are visited
+    const bool smooth_finite = !ballot(row && !__builtin_isfinite(smooth_i));
     if (col) {
         const uint64_t nam = S.nanm[l] | S.zerm[l];
         // dot2(smooth, na) with na in {0,1}
         double s = 0.0, c = 0.0;
-        for (int i = 0; i < N; i++) {
-            const double x = S.smooth[i], y = ((nam >> i) & 1) ? 1.0 : 0.0;
+        auto step = [&](double x, double y) {
             const double p = x * y;
             const double pe = fma(x, y, -p);
             const double t = s + p;
@@ -1794,6 +1834,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             const double se = (s - (t - z)) + (p - z);
             s = t;
             c = c + (pe + se);
+        };
+        if (smooth_finite) {
+            for (uint64_t mm = nam; mm; mm &= mm - 1) step(S.smooth[__builtin_ctzll(mm)], 1.0);
+        } else {
+            for (int i = 0; i < N; i++) step(S.smooth[i], ((nam >> i) & 1) ? 1.0 : 0.0);
         }
         pcj = 1.0 - (s + c);
         nzj = (double)popc(S.zerm[l]);

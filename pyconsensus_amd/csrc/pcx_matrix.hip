@@ -45,7 +45,7 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
-constexpr int SELS = 32;         // sel_state words per scaled event
+constexpr int SELS = 40;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
 
@@ -371,6 +371,14 @@ __device__ __forceinline__ void row_range(const pcx_mat& m, int64_t& r0, int64_t
     r1 = r0 + per < m.n_rows ? r0 + per : m.n_rows;
 }
 
+// compensated sum of v[r0 .. r1), identical in every lane of the wave (lanes stride the
+// rows, then a fixed butterfly); every lane of the wave must call it
+__device__ __forceinline__ dd chunk_sum_dd(const double* v, int64_t r0, int64_t r1) {
+    acc2 a;
+    for (int64_t i = r0 + (threadIdx.x & (WAVE - 1)); i < r1; i += WAVE) a.add(v[i]);
+    return wave_sum_dd(a.get());
+}
+
 // Row loop of the column passes: U rows' loads are issued before any of them is
 // consumed (the per-row work carries a dependency through the running sums, so
 // without this each thread keeps one 8-byte load in flight -- ~2 TB/s at C5).
@@ -472,8 +480,11 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
                        [&](int64_t, XW v) { acc += v.x * v.w; });
     cnt = acc;
 #else
+    // EQW: every weight is 1 / N (k_rep_local), so the largest one is the first present row's:
+    // no weight loads, and the argmax is that row's index, converted once at the end
+    int64_t first_row = -1;
     rows_pipelined<16>(  // 16: whole 128-byte lines of T per lane
-        r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], m.rep[i]}; },
+        r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], eqw ? 0.0 : m.rep[i]}; },
         [&](int64_t i, XW v) {
 #ifdef PCX_X_CS_NODIV  // ablation (wrong results): no rescale division
             const double x = p.scaled ? v.x - p.lo : v.x;
@@ -497,7 +508,6 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
 #endif
             nz += z ? 1.0 : 0.0;
             if (isn || z) return;
-            const double r = v.w;
             cnt += 1.0;
             if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
 #ifdef PCX_X_CS_NOTWOSUM  // ablation (wrong results): plain sum
@@ -505,13 +515,15 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
 #else
                 sx.add(x);
 #endif
+                first_row = first_row < 0 ? i : first_row;
             } else {
+                const double r = v.w;
                 sr.add(r);
                 srx.add_prod(r, x);
-            }
-            if (r > mx) {
-                mx = r;
-                arg = (double)(m.row_offset + i);
+                if (r > mx) {
+                    mx = r;
+                    arg = (double)(m.row_offset + i);
+                }
             }
 #ifndef PCX_X_CS_NOMINMAX  // ablation (wrong results): no extremes / grid flag
             mn_x = fmin(mn_x, x);
@@ -523,6 +535,10 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
 #ifndef PCX_X_CS_NOT
     if (t2 && r1 > r0 && (r1 & 1)) Tc[r1 - 1] = tprev;  // an odd end: the last (even) row alone
 #endif
+    if (eqw && first_row >= 0) {
+        mx = 1.0 / (double)m.n_total;  // = m.rep[i] (k_rep_local)
+        arg = (double)(m.row_offset + first_row);
+    }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, {cnt, 0.0});
     if constexpr (eqw) {  // sum r = cnt r exactly, sum r x = (sum x) r to dd accuracy
@@ -1976,40 +1992,73 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
 // M_GEMV2 from the compact sources (m.compact): thread = one wcd position (general positions
 // read the filled values Fg, grid positions F = 1 + z / 2 from the 2-bit codes), 16-row groups;
 // the same per-row products and compensated sums as k_gemv2, into the same partial slots
+// GRID: one launch for the general tile positions [0, gb), one for the grid ones [gb, E) -- the two
+// loops differ in registers, and the general one (a latency-bound stream of Fg) keeps its occupancy
+template <bool GRID>
 __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
-    const int q = blockIdx.x * BT + threadIdx.x;
-    const int E = (int)m.n_events;
-    if (q >= E) return;
-    const int c = m.cov_perm[q];
-    if (c < 0) return;  // (padding)
     const int64_t gb = (int64_t)m.cov_jb * CT;
+    const int q = (GRID ? (int)gb : 0) + blockIdx.x * BT + threadIdx.x;
+    const int E = (int)m.n_events;
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     const double* n1 = m.rowv + RV_N1 * m.n_rows;
     const double* n2 = m.rowv + RV_N2 * m.n_rows;
+    // grid positions: sum v F = S_v + (sum v z) / 2 (F = 1 + z / 2, v z exact), S_v the chunk's
+    // weight totals (wave reductions, before any lane leaves) -- one compensated add per
+    // element and weight vector instead of a compensated product
+    dd S1{0.0, 0.0}, S2{0.0, 0.0};
+    if (GRID) {
+        S1 = chunk_sum_dd(n1, r0, r1);
+        S2 = chunk_sum_dd(n2, r0, r1);
+    }
+    if (q >= E || (!GRID && q >= gb)) return;
+    const int c = m.cov_perm[q];
+    if (c < 0) return;  // (padding)
     acc2 a1, a2;
-    if (q < gb) {
-        rows_pipelined<PIPE_U>(
-            r0, r1, [&](int64_t i) { return XW{m.Fg[i * gb + q], n1[i]}; },
-            [&](int64_t i, XW v) {
-                a1.add_prod(v.w, v.x);
-                a2.add_prod(n2[i], v.x);
-            });
-    } else {
+    if constexpr (GRID) {
         const uint32_t* zb = zb_packed(m) + (q - gb);
-        for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {
-            const uint32_t P = zb[g * m.zq];
+        // whole 16-row groups: the group's (uniform) weights as one batch of scalar loads, the
+        // next group's code word in flight during this group's adds; then the ragged tail
+        const int64_t g0 = r0 / 16, gf = r1 / 16;
+        uint32_t Pn = g0 < gf ? zb[g0 * m.zq] : 0u;
+        for (int64_t g = g0; g < gf; g++) {
+            const uint32_t P = Pn;
+            if (g + 1 < gf) Pn = zb[(g + 1) * m.zq];
+            double w1[16], w2[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const int64_t i = g * 16 + r;
-                if (i < r1) {
-                    const double f = 1.0 + 0.5 * (double)zpack_get(P, r);
-                    a1.add_prod(n1[i], f);
-                    a2.add_prod(n2[i], f);
-                }
+                w1[r] = n1[g * 16 + r];
+                w2[r] = n2[g * 16 + r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const double z = (double)zpack_get(P, r);
+                a1.add(w1[r] * z);
+                a2.add(w2[r] * z);
             }
         }
+        if (r0 < r1 && gf * 16 < r1) {  // (r0 < r1: r0 is 16-aligned; an empty chunk capped at a ragged n_rows has none)
+            const uint32_t P = zb[gf * m.zq];
+            for (int64_t i = gf * 16; i < r1; i++) {
+                const double z = (double)zpack_get(P, (int)(i - gf * 16));
+                a1.add(n1[i] * z);
+                a2.add(n2[i] * z);
+            }
+        }
+        const dd Z1 = a1.get(), Z2 = a2.get();
+        double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+        st_dd(pp + 0, dd_add(S1, dd{0.5 * Z1.hi, 0.5 * Z1.lo}));
+        st_dd(pp + 2, dd_add(S2, dd{0.5 * Z2.hi, 0.5 * Z2.lo}));
+        return;
     }
+    (void)S1;
+    (void)S2;
+    rows_pipelined<PIPE_U>(
+        r0, r1, [&](int64_t i) { return XW{m.Fg[i * gb + q], n1[i]}; },
+        [&](int64_t i, XW v) {
+            a1.add_prod(v.w, v.x);
+            a2.add_prod(n2[i], v.x);
+        });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, a1.get());
     st_dd(pp + 2, a2.get());
@@ -2250,16 +2299,14 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
 }
 
 // M_OUTCOMES from the compact sources (m.compact): as k_gemv2_c, with the missing bits nam
-__global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
-    const int q = blockIdx.x * BT + threadIdx.x;
+// the general positions' (GRID false) and the grid positions' bodies; S: the chunk's weight total
+template <bool GRID>
+__device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S) {
+    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
     const int E = (int)m.n_events;
-    if (q >= E) return;
+    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
     const int c = m.cov_perm[q];
     if (c < 0) return;
-    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
-    int64_t r0, r1;
-    row_range(m, r0, r1, 16);
-    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
     acc2 raw;
     double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     double n1 = 0, n15 = 0, n2 = 0;
@@ -2273,20 +2320,98 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
         n15 += f == 1.5 ? 1.0 : 0.0;
         n2 += f == 2.0 ? 1.0 : 0.0;
     };
-    const bool general = q < gb;
-    const uint32_t* zb = zb_packed(m) + (general ? 0 : q - gb);
+    const bool general = !GRID;
+    if (general && m.scaled && m.scaled[c]) {
+        // a scaled event's raw is its weighted median (:520-523) and its certainty comes from
+        // the selection (:540-546): only np.dot(smooth_rep, na_mat) (:559) is read here, from
+        // the missing bits alone (no filled values), in the same row order and arithmetic
+        for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {
+            const uint32_t M = m.nam[g * ld + q];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int64_t i = g * 16 + r;
+                if (i < r1) pc += sm[i] * (((M >> r) & 1u) ? 1.0 : 0.0);
+            }
+        }
+        double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+        st_dd(pp + 2, {pc, 0.0});
+        return;
+    }
+    if constexpr (GRID) {
+        // grid event: F = 1 + z / 2, z in {0, 1, 2} from the 2-bit codes.  raw = sum w F =
+        // S + (sum w z) / 2 with S = sum w over the chunk (the same for every column: one dd
+        // sum per wave) and w z exact, so one compensated add per element replaces the
+        // product's; b1 / b15 / b2 are the same plain row-order sums as the general path's
+        // and the counts are popcounts of the code bits (code 1 = value 1.5, 2 = value 2)
+        const uint32_t* zb = zb_packed(m) + (q - gb);
+        acc2 zs;
+        uint32_t c15 = 0, c2 = 0;
+        auto row = [&](uint32_t z, double w, uint32_t ms) {
+            zs.add(w * (double)z);
+            pc += w * (ms ? 1.0 : 0.0);
+            b1 += z == 0u ? w : 0.0;
+            b15 += z == 1u ? w : 0.0;
+            b2 += z == 2u ? w : 0.0;
+        };
+        // whole 16-row groups (weights as one batch of scalar loads, the next group's code and
+        // missing words in flight during this group's adds), then the ragged tail
+        const int64_t g0 = r0 / 16, gf = r1 / 16;
+        uint32_t Pn = 0, Mn = 0;
+        if (g0 < gf) {
+            Pn = zb[g0 * m.zq];
+            Mn = m.nam[g0 * ld + q];
+        }
+        for (int64_t g = g0; g < gf; g++) {
+            const uint32_t P = Pn, M = Mn;
+            if (g + 1 < gf) {
+                Pn = zb[(g + 1) * m.zq];
+                Mn = m.nam[(g + 1) * ld + q];
+            }
+            c15 += __popc(P & 0x55555555u);
+            c2 += __popc(P & 0xAAAAAAAAu);
+            double w[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) w[r] = sm[g * 16 + r];
+#pragma unroll
+            for (int r = 0; r < 16; r++) row(zpack_get(P, r), w[r], (M >> r) & 1u);
+        }
+        if (r0 < r1 && gf * 16 < r1) {  // (r0 < r1: r0 is 16-aligned; an empty chunk capped at a ragged n_rows has none)
+            const uint32_t P = zb[gf * m.zq], M = m.nam[gf * ld + q];
+            for (int64_t i = gf * 16; i < r1; i++) {
+                const int r = (int)(i - gf * 16);
+                const uint32_t z = zpack_get(P, r);
+                c15 += z == 1u;
+                c2 += z == 2u;
+                row(z, sm[i], (M >> r) & 1u);
+            }
+        }
+        const dd Z = zs.get();
+        const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
+        n15 = (double)c15;
+        n2 = (double)c2;
+        n1 = rows - n15 - n2;
+        double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+        st_dd(pp + 0, dd_add(S, dd{0.5 * Z.hi, 0.5 * Z.lo}));
+        st_dd(pp + 2, {pc, 0.0});
+        st_dd(pp + 4, {b1, 0.0});
+        st_dd(pp + 6, {b15, 0.0});
+        st_dd(pp + 8, {b2, 0.0});
+        st_dd(pp + 10, {n1, 0.0});
+        st_dd(pp + 12, {n15, 0.0});
+        st_dd(pp + 14, {n2, 0.0});
+        return;
+    }
+    (void)S;
+    // a general binary event (off the grid): the filled values Fg
     for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {  // (an empty range capped at a ragged n_rows)
         const uint32_t M = m.nam[g * ld + q];
-        const uint32_t P = general ? 0u : zb[g * m.zq];
         double fv[16];
-        if (general) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) fv[r] = g * 16 + r < r1 ? m.Fg[(g * 16 + r) * gb + q] : 0.0;
-        }
+        for (int r = 0; r < 16; r++) fv[r] = g * 16 + r < r1 ? m.Fg[(g * 16 + r) * gb + q] : 0.0;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const int64_t i = g * 16 + r;
-            if (i < r1) cell(general ? fv[r] : 1.0 + 0.5 * (double)zpack_get(P, r), sm[i], (M >> r) & 1u);
+            if (i < r1) cell(fv[r], sm[i], (M >> r) & 1u);
         }
     }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
@@ -2298,6 +2423,24 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     st_dd(pp + 10, {n1, 0.0});
     st_dd(pp + 12, {n15, 0.0});
     st_dd(pp + 14, {n2, 0.0});
+}
+
+// one launch over every position (unlike k_gemv2_c: here the general positions of a scaled event
+// read only their missing bits, and the two ranges' blocks fill the chip together)
+__global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    const int q = blockIdx.x * BT + threadIdx.x;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    // the chunk's weight total for the grid positions, by every lane of a wave holding one
+    // (before any lane leaves: the sum is a wave reduction)
+    dd S{0.0, 0.0};
+    if ((q | (WAVE - 1)) >= gb) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
+    if (q >= m.n_events) return;
+    if (q >= gb)
+        outcomes_c_body<true>(m, q, r0, r1, S);
+    else
+        outcomes_c_body<false>(m, q, r0, r1, S);
 }
 
 // certainty of an event no reporter matched (:542): NaN on the PCA path (smooth_rep is a
@@ -2362,6 +2505,8 @@ enum sel_word {
     SW_WB0, SW_WB1,                   // first pass: the bucket window gathered into cbuf (sampled)
     SW_CERTN, SW_CW0, SW_CW1, SW_CW2, // phase 2, weight walk ended on one key: the elements (all ranks)
                                       // holding it and their exact weight -- the certainty (:540-546)
+    SW_XWIN,                          // 1: the last histogram's exact key extremes cover only the
+                                      // window [SW_WB0, SW_WB1] (and the largest key below it)
     SW_NWORDS
 };
 static_assert(SW_NWORDS <= SELS, "sel_state words");
@@ -2499,16 +2644,19 @@ __device__ __forceinline__ void mark_hard(const pcx_mat& m, int s, uint64_t* st)
 // The totals come from the first pass's histogram (all ranks, reduced): exact integer sums of
 // its bucket counts and weight limbs, the extreme keys of its buckets; one thread per event of
 // that pass (active index a), whose histogram row k_sel_step then narrows in the same pass.
+// One wave per event: the lanes read the histogram row's buckets (coalesced) and reduce the
+// exact integer totals and key extremes; lane 0 then decides.
 __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
-    const int a = blockIdx.x * BT + threadIdx.x;
-    if (a >= (int)m.info[IN_SEL_ACTIVE]) return;
+    const int a = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // wave-uniform
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     if (st[SW_STATUS] != 1) return;
     const bool wsum = st[SW_MODE] == 0;  // the first pass summed weight limbs
     const int64_t o = (int64_t)a * NB;
     uint64_t ta = 0, tb = 0, tc = 0, n = 0, kmin = ~0ull, kmax = 0;
-    for (int b = 0; b < NB; b++) {
+    for (int b = lane; b < NB; b += WAVE) {
         const uint64_t c = m.hist_n[o + b];
         if (!c) continue;
         n += c;
@@ -2520,6 +2668,17 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
         kmin = m.hist_min[o + b] < kmin ? m.hist_min[o + b] : kmin;
         kmax = m.hist_max[o + b] > kmax ? m.hist_max[o + b] : kmax;
     }
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) {  // exact integer sums: any order
+        ta += __shfl_xor(ta, d, WAVE);
+        tb += __shfl_xor(tb, d, WAVE);
+        tc += __shfl_xor(tc, d, WAVE);
+        n += __shfl_xor(n, d, WAVE);
+        const uint64_t omn = __shfl_xor(kmin, d, WAVE), omx = __shfl_xor(kmax, d, WAVE);
+        kmin = omn < kmin ? omn : kmin;
+        kmax = omx > kmax ? omx : kmax;
+    }
+    if (lane != 0) return;
     const uint64_t wminb = m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
     // count mode known up front (equal weights): the total only needs to be nonzero
     const L3 tot = wsum ? l3_norm({ta, tb, tc}) : L3{n && wmaxb ? 1ull : 0ull, 0, 0};
@@ -2735,7 +2894,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hmin[NB], hmax[NB];
     __shared__ unsigned long long hn[NB];
     typedef unsigned long long hn_t;
-    __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
+    __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn, f_bmax;
     for (int b = threadIdx.x; b < NB; b += BT) {
         ha[b] = hb[b] = hc[b] = hn[b] = 0;
         hmin[b] = ~0ull;
@@ -2746,6 +2905,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         f_wlo = ~0ull;
         f_whi = 0;
         f_ga = f_gb = f_gc = f_gn = 0;
+        f_bmax = 0;
     }
     __syncthreads();
     // first pass (sel_first): the weight extremes of every element, and in phase 2 the filled
@@ -2818,6 +2978,14 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const bool gather = !from_buf && m.cbuf && st[SW_INRANGE] > 0 && need <= (uint64_t)m.ccap &&
                         8 * need <= st[SW_COUNT];
     uint64_t* cb = m.cbuf ? m.cbuf + (int64_t)s * m.ccap * 2 : nullptr;
+    // a first pass with a window keeps exact key extremes only where k_sel_step can use them when
+    // the crossing bucket lies in the window (nearly always): the window's buckets, and the largest
+    // key below it (the predecessor of a crossing at the window's first non-empty bucket) in a
+    // register; the other buckets get their nominal key bounds.  A crossing outside the window
+    // makes k_sel_step skip that narrowing (the next, plain pass tracks every bucket): the LDS
+    // atomics bound these passes, and this leaves one (count mode) or four (weights) per element
+    const bool xwin = wgather;
+    uint64_t bmax = 0;
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh);
         if (wmode) {
@@ -2827,6 +2995,14 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             atomicAdd(&hc[b], (unsigned long long)L.l2);
         }
         atomicAdd(&hn[b], (hn_t)1);
+        if (xwin && (b < wb0 || b > wb1)) {
+            if (b < wb0) bmax = k > bmax ? k : bmax;
+            return;
+        }
+        // (measured: reading the extremes first and skipping the atomics that cannot change them
+        // is slower, 9.4 -> 12.0 ms at C5 -- the read's latency sits in every element's path,
+        // where the no-return atomics are fire-and-forget; min / max interleaved in one array,
+        // 9.4 -> 9.7 ms -- twice the bank conflicts of two arrays)
         atomicMin(&hmin[b], (unsigned long long)k);
         atomicMax(&hmax[b], (unsigned long long)k);
     };
@@ -2881,6 +3057,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             }
         });
     }
+    if (xwin && bmax) atomicMax(&f_bmax, (unsigned long long)bmax);
     if (first) {
         atomicMin(&f_wlo, (unsigned long long)wlo);
         atomicMax(&f_whi, (unsigned long long)whi);
@@ -2909,6 +3086,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
                 atomicAdd(&hn[b], (hn_t)f_gn);
                 atomicMin(&hmin[b], (unsigned long long)fk);
                 atomicMax(&hmax[b], (unsigned long long)fk);
+                if (xwin && b < wb0 && fk > f_bmax) f_bmax = fk;
             }
         }
     }
@@ -2933,8 +3111,14 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         m.ccount[s] = fits ? (int64_t)gcount : 0;
         st[SW_CMODE] = fits ? 2 : 0;
     }
+    if (xwin && threadIdx.x == 0) st[SW_XWIN] = 1;
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
+        if (xwin && hn[b] && (b < wb0 || b > wb1)) {  // (written by this thread only)
+            const uint64_t blo = lo + ((uint64_t)b << sh), bhi = blo + ((1ull << sh) - 1);
+            hmin[b] = blo;
+            hmax[b] = b < wb0 ? (unsigned long long)f_bmax : (bhi < hi ? bhi : hi);
+        }
         if (wmode) {
             m.hist_w[(o + b) * 3 + 0] = ha[b];
             m.hist_w[(o + b) * 3 + 1] = hb[b];
@@ -3038,6 +3222,14 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
         return;
     }
     if (lane != __ffsll((long long)mask) - 1) return;
+    if (st[SW_XWIN]) {  // a windowed first pass: its extremes are exact inside the window only
+        st[SW_XWIN] = 0;
+        const int b = lane * SEL_PB + first;
+        if (b < (int)st[SW_WB0] || b > (int)st[SW_WB1]) {  // missed: the next (plain) pass redoes it
+            if (st[SW_CMODE] == 2) st[SW_CMODE] = 0;
+            return;
+        }
+    }
     const uint64_t n = nb[first], kmin = kmn[first], kmax = kmx[first];
     if (kmin == kmax) {
         const double xs = dkey_inv(kmin);
@@ -4468,6 +4660,15 @@ hipError_t hard_stage(pcx_mat& m, const HardArgs& h, int stage, hipStream_t st, 
     return hipGetLastError();
 }
 
+// the compact column passes: general tile positions [0, gb) and grid positions [gb, E) as two
+// launches of the same row chunks (blockIdx.y)
+template <class KG, class KR>
+static void launch_compact(KG kgen, KR kgrid, const pcx_mat& m, hipStream_t st) {
+    const int64_t E = m.n_events, gb = std::min<int64_t>((int64_t)m.cov_jb * CT, E);
+    if (gb > 0) hipLaunchKernelGGL(kgen, dim3((unsigned)((gb + BT - 1) / BT), m.col_blocks), dim3(BT), 0, st, m);
+    if (E > gb) hipLaunchKernelGGL(kgrid, dim3((unsigned)((E - gb + BT - 1) / BT), m.col_blocks), dim3(BT), 0, st, m);
+}
+
 hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
     const int E = (int)m.n_events;
     const int ceb = (E + BT - 1) / BT;
@@ -4621,7 +4822,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
             if (m.compact && m.Fg && m.nam && m.zB)
-                hipLaunchKernelGGL(k_gemv2_c, colgrid, dim3(BT), 0, st, m);
+                launch_compact(k_gemv2_c<false>, k_gemv2_c<true>, m, st);
             else
                 hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
@@ -4692,7 +4893,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_SEL_START:
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_info_clear, dim3(1), dim3(1), 0, st, m, (int)IN_SEL_ARGMAX);
-            hipLaunchKernelGGL(k_sel_start, dim3(sg), dim3(BT), 0, st, m);
+            hipLaunchKernelGGL(k_sel_start, dim3((unsigned)((m.n_scaled + BT / WAVE - 1) / (BT / WAVE))), dim3(BT), 0,
+                               st, m);
             break;
         case M_SEL_ARGMAX:
             if (m.n_scaled == 0) break;

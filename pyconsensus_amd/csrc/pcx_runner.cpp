@@ -31,7 +31,7 @@ constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
 constexpr int COV_STAGE = 64 * PCX_GEMM_KS > 128 ? 64 * PCX_GEMM_KS : 128;  // wcd rows: whole stages of the int8 GEMM
-constexpr int SELS = 32;
+constexpr int SELS = 40;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
 template <class T>
