@@ -46,6 +46,12 @@ constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
 constexpr int SELS = 40;         // sel_state words per scaled event
+#ifndef PCX_OUT_SPLIT
+#define PCX_OUT_SPLIT 0
+#endif
+#ifndef PCX_SEL_XWIN
+#define PCX_SEL_XWIN 1
+#endif
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
 
@@ -2053,11 +2059,14 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
     }
     (void)S1;
     (void)S2;
-    rows_pipelined<PIPE_U>(
-        r0, r1, [&](int64_t i) { return XW{m.Fg[i * gb + q], n1[i]}; },
-        [&](int64_t i, XW v) {
-            a1.add_prod(v.w, v.x);
-            a2.add_prod(n2[i], v.x);
+    struct V3 {
+        double x, w1, w2;
+    };
+    rows_pipelined<PIPE_U>(  // (both weights loaded with the value: every load ahead of its use)
+        r0, r1, [&](int64_t i) { return V3{m.Fg[i * gb + q], n1[i], n2[i]}; },
+        [&](int64_t, V3 v) {
+            a1.add_prod(v.w1, v.x);
+            a2.add_prod(v.w2, v.x);
         });
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
     st_dd(pp + 0, a1.get());
@@ -2325,13 +2334,22 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
         // a scaled event's raw is its weighted median (:520-523) and its certainty comes from
         // the selection (:540-546): only np.dot(smooth_rep, na_mat) (:559) is read here, from
         // the missing bits alone (no filled values), in the same row order and arithmetic
-        for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {
-            const uint32_t M = m.nam[g * ld + q];
+        // whole 16-row groups: the weights as one batch of loads ahead of the adds (a load per
+        // row waited on in turn left this pass latency-bound), the next missing word in flight
+        const int64_t g0 = r0 / 16, gf = r1 / 16;
+        uint32_t Mn = g0 < gf ? m.nam[g0 * ld + q] : 0u;
+        for (int64_t g = g0; g < gf; g++) {
+            const uint32_t M = Mn;
+            if (g + 1 < gf) Mn = m.nam[(g + 1) * ld + q];
+            double w[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int64_t i = g * 16 + r;
-                if (i < r1) pc += sm[i] * (((M >> r) & 1u) ? 1.0 : 0.0);
-            }
+            for (int r = 0; r < 16; r++) w[r] = sm[g * 16 + r];
+#pragma unroll
+            for (int r = 0; r < 16; r++) pc += w[r] * (((M >> r) & 1u) ? 1.0 : 0.0);
+        }
+        if (r0 < r1 && gf * 16 < r1) {  // the ragged tail (r0 < r1: r0 is 16-aligned)
+            const uint32_t M = m.nam[gf * ld + q];
+            for (int64_t i = gf * 16; i < r1; i++) pc += sm[i] * (((M >> (i - gf * 16)) & 1u) ? 1.0 : 0.0);
         }
         double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
         st_dd(pp + 2, {pc, 0.0});
@@ -2405,13 +2423,17 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     // a general binary event (off the grid): the filled values Fg
     for (int64_t g = r0 / 16; r0 < r1 && g * 16 < r1; g++) {  // (an empty range capped at a ragged n_rows)
         const uint32_t M = m.nam[g * ld + q];
-        double fv[16];
+        double fv[16], w[16];
 #pragma unroll
-        for (int r = 0; r < 16; r++) fv[r] = g * 16 + r < r1 ? m.Fg[(g * 16 + r) * gb + q] : 0.0;
+        for (int r = 0; r < 16; r++) {
+            const bool in = g * 16 + r < r1;
+            fv[r] = in ? m.Fg[(g * 16 + r) * gb + q] : 0.0;
+            w[r] = in ? sm[g * 16 + r] : 0.0;
+        }
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const int64_t i = g * 16 + r;
-            if (i < r1) cell(fv[r], sm[i], (M >> r) & 1u);
+            if (i < r1) cell(fv[r], w[r], (M >> r) & 1u);
         }
     }
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
@@ -2441,6 +2463,19 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
         outcomes_c_body<true>(m, q, r0, r1, S);
     else
         outcomes_c_body<false>(m, q, r0, r1, S);
+}
+
+// the same as two launches (general tile positions, grid positions), PCX_OUT_SPLIT
+template <bool GRID>
+__global__ void __launch_bounds__(BT) k_outcomes_cs(pcx_mat m) {
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    const int q = (GRID ? (int)gb : 0) + blockIdx.x * BT + threadIdx.x;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    dd S{0.0, 0.0};
+    if (GRID) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
+    if (q >= m.n_events || (!GRID && q >= gb)) return;
+    outcomes_c_body<GRID>(m, q, r0, r1, S);
 }
 
 // certainty of an event no reporter matched (:542): NaN on the PCA path (smooth_rep is a
@@ -2984,7 +3019,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     // register; the other buckets get their nominal key bounds.  A crossing outside the window
     // makes k_sel_step skip that narrowing (the next, plain pass tracks every bucket): the LDS
     // atomics bound these passes, and this leaves one (count mode) or four (weights) per element
-    const bool xwin = wgather;
+    const bool xwin = PCX_SEL_XWIN && wgather;
     uint64_t bmax = 0;
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh);
@@ -4847,7 +4882,11 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_OUTCOMES:
             if (m.compact && m.Fg && m.nam && m.zB)
+#if PCX_OUT_SPLIT
+                launch_compact(k_outcomes_cs<false>, k_outcomes_cs<true>, m, st);
+#else
                 hipLaunchKernelGGL(k_outcomes_c, colgrid, dim3(BT), 0, st, m);
+#endif
             else
                 hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
