@@ -49,6 +49,9 @@ constexpr int SELS = 40;         // sel_state words per scaled event
 #ifndef PCX_OUT_SPLIT
 #define PCX_OUT_SPLIT 0
 #endif
+#ifndef PCX_SEL_HN32
+#define PCX_SEL_HN32 0
+#endif
 #ifndef PCX_SEL_XWIN
 #define PCX_SEL_XWIN 0  // measured 9.4 -> 9.7 ms at C5 with the window-only extremes: off
 #endif
@@ -2927,11 +2930,16 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hmin[NB], hmax[NB];
-    __shared__ unsigned long long hn[NB];
+#if PCX_SEL_HN32  // bucket counts as 32-bit LDS atomics (a rank's rows < 2^32)
+    typedef unsigned int hn_t;
+#else
     typedef unsigned long long hn_t;
+#endif
+    __shared__ hn_t hn[NB];
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn, f_bmax;
     for (int b = threadIdx.x; b < NB; b += BT) {
-        ha[b] = hb[b] = hc[b] = hn[b] = 0;
+        ha[b] = hb[b] = hc[b] = 0;
+        hn[b] = 0;
         hmin[b] = ~0ull;
         hmax[b] = 0;
     }
@@ -3159,7 +3167,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             m.hist_w[(o + b) * 3 + 1] = hb[b];
             m.hist_w[(o + b) * 3 + 2] = hc[b];
         }
-        m.hist_n[o + b] = hn[b];
+        m.hist_n[o + b] = (uint64_t)hn[b];
         m.hist_min[o + b] = hmin[b];
         m.hist_max[o + b] = hmax[b];
     }
