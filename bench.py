@@ -19,6 +19,7 @@ import json
 import os
 import sys
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -115,7 +116,7 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     for _ in range(warmup):
         run()
     _C5_STATE["phase"] = "timed steps"
-    times, prof = [], {}
+    times, prof, step_prof = [], {}, []
     ev = ag = None
     for _ in range(steps):
         ev = ag = None  # drop the last step's 65 GB of outputs first (else a fresh hipMalloc is timed)
@@ -123,7 +124,8 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        ev, ag, meta = run(prof)
+        p1 = {}
+        ev, ag, meta = run(p1)
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         if world > 1:
@@ -131,7 +133,11 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
             torch.distributed.all_reduce(m, op=torch.distributed.ReduceOp.MAX)
             el = float(m.item())
         times.append(el)
+        step_prof.append(p1)
+        for k, v in p1.items():
+            prof[k] = prof.get(k, 0.0) + v
     prof = {k: v / steps for k, v in prof.items()}
+    top = [k for k, _ in sorted(prof.items(), key=lambda kv: -kv[1])[:6]]
     cov_ms = prof.get("M_COV", float("nan"))
     i8_ms = prof.get("M_COV_I8", float("nan"))
     # unique (j, k<=j) covariance pairs: those with a general event on fp64 MFMA (k_syrk),
@@ -154,6 +160,8 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     del R
     return {"metric": "1M x 4k consensus latency (every output, original and filled included)", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
             "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
+            "latency_ms_mean": 1e3 * sum(times) / len(times), "warmup_steps": warmup,
+            "stage_ms_per_step": [{k: round(p.get(k, 0.0), 3) for k in top} for p in step_prof],
             "branch": meta["branch"], "pi_iters": meta["pi_iters"], "flags": meta["flags"],
             "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
             "roofline_cov": {"bound": "mfma", "kernel": "k_syrk", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
@@ -255,6 +263,8 @@ def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
 
 C5_TIMEOUT_S = 300          # multi-rank C5 watchdog (bench main)
 C5_WATCHDOG_EXIT = 3        # exit status of a rank whose C5 stalled
+BENCH_FAILED_EXIT = 4       # exit status after the line when a C5 / C4 / medium entry raised
+C5_WARMUP = 2               # untimed C5 consensus runs (the first run allocates the workspace and outputs)
 _C5_STATE = {"comm": None, "dev": None, "phase": "setup"}
 
 
@@ -403,6 +413,7 @@ def main():
     del Rd, out
     torch.cuda.empty_cache()
     c5 = c4 = None
+    failed = []  # secondary entries that raised: recorded in the line, and the run exits non-zero
     if args.c5_steps > 0:
         # a failure here is recorded in the line; the C3 headline above stands.  With several
         # ranks a watchdog also guards against a stuck collective: after C5_TIMEOUT_S every rank
@@ -425,8 +436,10 @@ def main():
             watchdog.daemon = True
             watchdog.start()
         try:
-            c5 = bench_c5(world, rank, dev, args.c5_steps, 1)
+            c5 = bench_c5(world, rank, dev, args.c5_steps, C5_WARMUP)
         except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            failed.append("c5")
             c5 = {"metric": "1M x 4k consensus latency", "n_gpus": world, "error": repr(e)[:400]}
         if watchdog is not None:
             watchdog.cancel()
@@ -434,12 +447,16 @@ def main():
         try:
             c4 = bench_c4(dev, oracle=not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            failed.append("c4")
             c4 = {"metric": "100k x 1k consensus latency", "error": repr(e)[:400]}
     medium = None
     if args.c4 and world == 1:
         try:
             medium = bench_medium(dev)
         except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            failed.append("medium")
             medium = {"metric": "oracle rounds/sec (batched 100x50)", "error": repr(e)[:400]}
     if rank == 0:
         if medium is not None:
@@ -456,6 +473,9 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    if failed:
+        print("bench.py: %s raised (see the line's \"error\" entries)" % ", ".join(failed), file=sys.stderr, flush=True)
+        sys.exit(BENCH_FAILED_EXIT)
 
 
 if __name__ == "__main__":

@@ -319,6 +319,19 @@ int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax);
  * (grid + 1)).  For roofline accounting. */
 int pcx_mixed_digits(void);
 
+/* The RCCL that serves libpcx's collectives: *runtime = ncclGetVersion() of the librccl the
+ * process resolved (with torch loaded first: torch's bundled copy), *compiled = the
+ * NCCL_VERSION_CODE of the headers libpcx was built against.  Returns *runtime.  RCCL
+ * contexts are refused (PCX_ECOMM, both versions named) unless the major versions agree and
+ * the runtime is >= 2.18 (version code 21800). */
+int pcx_rccl_version(int* runtime, int* compiled);
+
+/* CPU self-test of the communicator abort path (no RCCL, no GPU): `users` threads run
+ * exchanges on a fake handle while `aborters` threads abort it.  Returns the number of
+ * violations (the handle freed other than exactly once, used after it was freed, or used
+ * successfully after an abort returned); 0 = pass, -1 = bad arguments.  For the tests. */
+int pcx_selftest_abort_once(int users, int aborters, int iters);
+
 #ifdef __cplusplus
 }
 #endif

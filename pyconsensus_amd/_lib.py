@@ -61,6 +61,8 @@ def _declare(lib):
         ("pcx_seqsum_const", C.c_double, [C.c_double, i64]),
         ("pcx_seqsum_first_above", i64, [C.c_double, C.c_double, i64]),
         ("pcx_mixed_digits", i32, []),
+        ("pcx_rccl_version", i32, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        ("pcx_selftest_abort_once", i32, [i32, i32, i32]),
     ]:
         f = getattr(lib, name)
         f.restype = res

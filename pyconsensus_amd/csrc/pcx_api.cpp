@@ -550,5 +550,9 @@ double pcx_seqsum_const(double c, int64_t k) { return pcx::seqsum_const(c, k); }
 
 int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax) { return pcx::seqsum_first_above(c, t, kmax); }
 int pcx_mixed_digits(void) { return PCX_NDIG; }
+int pcx_rccl_version(int* runtime, int* compiled) { return pcx::rccl_version(runtime, compiled); }
+int pcx_selftest_abort_once(int users, int aborters, int iters) {
+    return pcx::selftest_abort_once(users, aborters, iters);
+}
 
 }  // extern "C"

@@ -46,13 +46,9 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
 // The round's helpers run inlined: the 50 x 20 kernel is ~83 KB of code, yet the instruction
 // cache misses 0.14 % of its fetches (SQC_ICACHE_MISSES / HITS, profiles/r3); outlined (calls,
-// PCX_OUTLINE_HELPERS=1, 49 KB + shared helpers) the call ABI spills and the kernel ran 29 %
+// __noinline__, 49 KB + shared helpers) the call ABI spills and the kernel ran 29 %
 // slower (24.4 M vs 34.4 M rounds/s).
-#ifdef PCX_OUTLINE_HELPERS
-#define PCX_OUTLINE __noinline__
-#else
 #define PCX_OUTLINE __forceinline__
-#endif
 
 // diagnostic phase stamps (PCX_STAMPS=1): shader-clock reads at phase boundaries
 #define STAMP(k)                                                                  \
@@ -389,9 +385,6 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
     int* cnt = reinterpret_cast<int*>(scr + 3 * NR + med_ow(NR));
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-#ifdef PCX_X_NOMED  // ablation (tools/ab_variant.sh): wrong results, time without the medians
-    return bcast(x, 0) + 0.0 * Wtot;
-#endif
     const double mid = 0.5 * Wtot;
     if (ballot(sel && w > mid)) {  // weightedstats: a weight above half the total wins outright
         const double mx = wave_max(sel ? w : -__builtin_inf());
@@ -416,9 +409,6 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     for (int q = l; q < med_ow(NR); q += 64) ow[q] = 0.0;  // slots past n add +0.0 in the walk
     wsync();
     int r = 0;
-#ifdef PCX_X_NORANK  // ablation: no rank loop
-    r = l;
-#else
     if (use_rank) {
         r = rank;
     } else {
@@ -429,7 +419,6 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
         }
         if (rank_out) *rank_out = r;
     }
-#endif
     if (sel) atomicAdd(&cnt[r], 1);
     wsync();
     // rows sharing a key (equal x: e.g. the filled guesses of the outcome median, or a
@@ -466,9 +455,6 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     // the current group's dependent adds
     double cum = 0.0, before = 0.0;
     int k = 0;
-#ifdef PCX_X_NOWALK  // ablation: no walk
-    return ox[n >> 1] + 0.0 * mid;
-#endif
     double v[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) v[q] = ow[q];
@@ -1282,9 +1268,6 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                 if (a.int_dtype) x = trunc(x);
                 S.F[l * ES + j] = x;
             }
-#ifdef PCX_X_COLWRITES
-            if (a.original) a.original[(b * N + l) * E + j] = x;
-#endif
         }
         const uint64_t nm = ballot(row && __builtin_isnan(x));
         const uint64_t zm = ballot(row && x == 0.0);
@@ -1294,11 +1277,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         }
     }
     wsync();
-#ifndef PCX_X_COLWRITES
     // result["original"] (the rescaled reports), from LDS in row-major order: every store
     // instruction writes 64 consecutive doubles (whole lines), not one column's 50 strided ones
     if (a.original) round_to_global(a.original + b * (int64_t)N * E, S.F, N, E, ES, NT, ET);
-#endif
 
     STAMP(2);
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
@@ -1373,12 +1354,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             ws[l] = w;
             wsync();
             Wsum = 0.0;
-#ifdef PCX_X_TREEW  // ablation: tree sum instead of the sequential one
-            Wsum = wave_pw_sum(w, row);
-#else
 #pragma unroll 8
             for (int i = 0; i < N; i++) Wsum = Wsum + ws[i];
-#endif
         };
         auto finish = [&](int j, double g) {
             if (a.int_dtype) g = trunc(g);
@@ -1414,12 +1391,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         }
     }
     wsync();
-#ifdef PCX_X_COLWRITES
-    if (a.filled && row)
-        for (int j = 0; j < E; j++) a.filled[(b * N + l) * E + j] = S.F[l * ES + j];
-#else
     if (a.filled) round_to_global(a.filled + b * (int64_t)N * E, S.F, N, E, ES, NT, ET);
-#endif
 
     STAMP(3);
     // ---- old = rep . F (np.dot) -------------------------------------------
@@ -1507,10 +1479,6 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         } else if (!any_nz) {
             xv = l == 0 ? 1.0 : 0.0;
             flags |= 1;
-#ifdef PCX_X_NOPI  // ablation: wrong results, time without the power iteration
-        } else if (true) {
-            xv = col ? S.C[sym_at<PK>(l, 0, ES)] : 0.0;
-#endif
         } else {
             // start: the column with the largest diagonal entry (first max; C is finite here)
             const double dg = col ? S.C[sym_at<PK>(l, l, ES)] : -__builtin_inf();

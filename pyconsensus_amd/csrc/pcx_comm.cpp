@@ -13,10 +13,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "pcx_internal.h"
@@ -83,45 +85,74 @@ int hip_err(hipError_t e, const char* what, std::string& err) {
 }
 
 // ------------------------------------------------------------------ RCCL
+constexpr int ABORT_SELFTEST_WAIT_MS = 100;
+// A communicator handle that many threads use and any of them may abort: `use` loads the
+// handle and runs the enqueue under `mu`; `abort` marks the handle dead (later uses fail),
+// waits for a use in progress a bounded time, then swaps the handle out and frees it exactly
+// once, whatever the number of callers.  No handle is freed between another thread's load and
+// its enqueue.  An enqueue blocked inside RCCL (lazy connection set-up with a peer that failed)
+// is what ncclCommAbort exists to interrupt, hence the bounded wait rather than a plain lock.
+template <class H>
+struct AbortOnce {
+    std::atomic<H> h{H{}};
+    std::timed_mutex mu;
+    std::atomic<bool> dead{false};
+    template <class F>
+    int use(F&& f, int gone_rc) {
+        std::lock_guard<std::timed_mutex> lk(mu);
+        const H c = h.load();
+        if (c == H{} || dead) return gone_rc;
+        return f(c);
+    }
+    template <class F>
+    void abort(F&& free_fn, int wait_ms) {
+        dead = true;  // uses that have not taken `mu` yet fail from here on
+        const bool locked = mu.try_lock_for(std::chrono::milliseconds(wait_ms));
+        if (H c = h.exchange(H{})) free_fn(c);
+        if (locked) mu.unlock();
+    }
+};
+
 struct RcclComm : Comm {
-    // the handle is swapped out atomically by abort(): ncclCommAbort runs exactly once even
-    // when several failing worker threads abort the same communicator, and an exchange that
-    // starts after the abort sees nullptr and fails instead of using a freed communicator
-    std::atomic<ncclComm_t> comm{nullptr};
+    AbortOnce<ncclComm_t> handle;
+    static constexpr int ABORT_WAIT_MS = 2000;
     ~RcclComm() override {
-        if (ncclComm_t c = comm.exchange(nullptr)) ncclCommDestroy(c);
+        if (ncclComm_t c = handle.h.exchange(nullptr)) ncclCommDestroy(c);
     }
     void abort() override {
         aborted = true;
-        if (ncclComm_t c = comm.exchange(nullptr)) ncclCommAbort(c);
+        handle.abort([](ncclComm_t c) { ncclCommAbort(c); }, ABORT_WAIT_MS);
     }
     static ncclDataType_t dt(int d) { return d == PCX_F64 ? ncclFloat64 : ncclUint64; }
     static ncclRedOp_t op_of(int o) { return o == PCX_SUM ? ncclSum : (o == PCX_MIN ? ncclMin : ncclMax); }
+    static constexpr int GONE = 1;  // (positive: never a PCX_ status)
     static int gone(std::string& err) {
         err = "RCCL communicator aborted after a failed call: recreate the context";
         return PCX_ECOMM;
     }
     int allreduce(void* buf, int64_t count, int dtype, int op, hipStream_t st, std::string& err) override {
         if (count <= 0) return 0;
-        ncclComm_t c = comm.load();
-        if (!c || aborted) return gone(err);
-        ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt(dtype), op_of(op), c, st);
-        if (r != ncclSuccess) {
-            err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
-            return PCX_ECOMM;
-        }
-        return 0;
+        const int rc = handle.use(
+            [&](ncclComm_t c) {
+                ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dt(dtype), op_of(op), c, st);
+                if (r == ncclSuccess) return 0;
+                err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+                return (int)PCX_ECOMM;
+            },
+            GONE);
+        return rc == GONE ? gone(err) : rc;
     }
     int allgather(const void* send, void* recv, int64_t bytes, hipStream_t st, std::string& err) override {
         if (bytes <= 0) return 0;
-        ncclComm_t c = comm.load();
-        if (!c || aborted) return gone(err);
-        ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c, st);
-        if (r != ncclSuccess) {
-            err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
-            return PCX_ECOMM;
-        }
-        return 0;
+        const int rc = handle.use(
+            [&](ncclComm_t c) {
+                ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c, st);
+                if (r == ncclSuccess) return 0;
+                err = std::string("ncclAllGather: ") + ncclGetErrorString(r);
+                return (int)PCX_ECOMM;
+            },
+            GONE);
+        return rc == GONE ? gone(err) : rc;
     }
     const char* kind() const override { return "rccl"; }
 };
@@ -208,8 +239,36 @@ struct CustomComm : StagedComm {
 
 }  // namespace
 
+// The RCCL that serves libpcx's calls is whichever librccl the process loaded first: with
+// torch imported, torch's bundled copy (2.26.x next to /opt/rocm's 2.27.x headers).
+// libpcx calls only the version-2 core API (unique id, CommInitRank / InitAll, AllReduce,
+// AllGather, CommAbort / Destroy, GetErrorString), whose signatures and 128-byte ncclUniqueId
+// are fixed across 2.x; a runtime of another major version, or older than the 2.18 this was
+// validated against, is refused with both versions named.
+int rccl_version(int* runtime, int* compiled) {
+    int v = 0;
+    if (ncclGetVersion(&v) != ncclSuccess) v = 0;
+    if (runtime) *runtime = v;
+    if (compiled) *compiled = NCCL_VERSION_CODE;
+    return v;
+}
+
+int rccl_check_version(std::string& err) {
+    int rt = 0, ct = 0;
+    rccl_version(&rt, &ct);
+    const int rt_major = rt >= 10000 ? rt / 10000 : rt / 1000;
+    const int ct_major = ct >= 10000 ? ct / 10000 : ct / 1000;
+    if (rt_major != ct_major || rt < 21800) {
+        err = "RCCL runtime " + std::to_string(rt) + " is incompatible with the headers libpcx was built against (" +
+              std::to_string(ct) + "): need the same major version and >= 2.18 (version code 21800)";
+        return PCX_ECOMM;
+    }
+    return 0;
+}
+
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err) {
     static_assert(sizeof(pcx_comm_id) == sizeof(ncclUniqueId), "pcx_comm_id mirrors ncclUniqueId");
+    if (const int rc = rccl_check_version(err)) return rc;
     ncclUniqueId id;
     ncclResult_t r = ncclGetUniqueId(&id);
     if (r != ncclSuccess) {
@@ -221,6 +280,7 @@ int comm_rccl_unique_id(pcx_comm_id* out, std::string& err) {
 }
 
 Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err) {
+    if (rccl_check_version(err)) return nullptr;
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) {
         err = std::string("hipSetDevice: ") + hipGetErrorString(e);
@@ -237,13 +297,14 @@ Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::str
         delete c;
         return nullptr;
     }
-    c->comm = h;
+    c->handle.h = h;
     c->world = world;
     c->rank = rank;
     return c;
 }
 
 int comm_rccl_all(int n, const int* devices, std::vector<Comm*>& out, std::string& err) {
+    if (const int rc = rccl_check_version(err)) return rc;
     std::vector<ncclComm_t> comms(n, nullptr);
     ncclResult_t r = ncclCommInitAll(comms.data(), n, devices);
     if (r != ncclSuccess) {
@@ -257,12 +318,58 @@ int comm_rccl_all(int n, const int* devices, std::vector<Comm*>& out, std::strin
             err = "out of host memory";
             return PCX_ENOMEM;
         }
-        c->comm = comms[k];
+        c->handle.h = comms[k];
         c->world = n;
         c->rank = k;
         out.push_back(c);
     }
     return 0;
+}
+
+// CPU self-test of AbortOnce (the RCCL abort path without RCCL): `users` threads exchange in a
+// loop on a fake handle while `aborters` threads abort it.  Returns the number of violations
+// (a free that ran more or less than once, a use that saw a freed handle, a use that succeeded
+// after abort() returned), or -1 on a setup error.
+int selftest_abort_once(int users, int aborters, int iters) {
+    if (users < 1 || aborters < 1 || iters < 1 || users + aborters > 256) return -1;
+    struct Fake {
+        std::atomic<int> freed{0}, frees{0}, bad{0};
+    };
+    AbortOnce<Fake*> a;
+    Fake f;
+    a.h = &f;
+    std::atomic<bool> go{false}, aborted_done{false};
+    std::atomic<int> ok_after{0};
+    std::vector<std::thread> th;
+    for (int u = 0; u < users; u++)
+        th.emplace_back([&] {
+            while (!go) std::this_thread::yield();
+            for (int i = 0; i < iters; i++) {
+                const bool after = aborted_done;
+                const int rc = a.use(
+                    [&](Fake* p) {
+                        if (p->freed) p->bad++;  // the handle was freed while in use
+                        return 0;
+                    },
+                    1);
+                if (rc == 0 && after) ok_after++;  // a use that started after abort() returned succeeded
+            }
+        });
+    for (int k = 0; k < aborters; k++)
+        th.emplace_back([&, k] {
+            while (!go) std::this_thread::yield();
+            for (int i = 0; i < iters / 4 + k; i++) std::this_thread::yield();
+            a.abort(
+                [](Fake* p) {
+                    p->frees++;
+                    p->freed = 1;
+                },
+                ABORT_SELFTEST_WAIT_MS);
+            aborted_done = true;
+        });
+    go = true;
+    for (auto& t : th) t.join();
+    return (f.frees != 1) + f.bad + ok_after;
 }
 
 pcx_group* group_create(int world) {

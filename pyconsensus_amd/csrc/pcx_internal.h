@@ -114,7 +114,6 @@ typedef struct {
        fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */
     int8_t*  zD;                  /* [wcd_rows/16][8 * 128 cov_jb][16] digit s of position q at s * 128 cov_jb + q */
     double*  dscale;              /* [wcd_ld] 2^-e per general position                               */
-    double*  mupos;               /* [wcd_ld] mu of the event at each wcd position (0 past E; M_COV_PLAN) */
     int32_t* Pgg;                 /* [ks_gg][zq][zq] int32 zA^T zB per k-slice (lower part)           */
     int32_t* Pmx;                 /* [ks_mx][zq][8 * 128 cov_jb] int32 zA^T zD per k-slice            */
     int32_t  ks_gg, ks_mx;        /* k-slices of the two int8 products (int32-exact row ranges)       */
@@ -127,16 +126,18 @@ typedef struct {
     const double* aux_scores;     /* [n_rows] cokurtosis scores / given scores                      */
 } pcx_mat;
 
-// int8 covariance GEMM (k_gemm_i8): 64-row MFMA k-steps per LDS ring stage; the workspace pads
-// wcd_rows to whole stages (pcx_runner.cpp COV_STAGE)
-#ifndef PCX_GEMM_KS
-#define PCX_GEMM_KS 2
-#endif
+// int8 covariance GEMM (k_gemm_i8, pcx_gemm_i8.h: PCX_GEMM_KS 64-row MFMA k-steps per LDS ring
+// stage); the workspace pads wcd_rows to whole stages (pcx_runner.cpp COV_STAGE)
+#include "pcx_gemm_i8.h"
 // mixed block (general x grid pairs): base-128 int8 digits per general position.  7 digits leave
 // a residue <= 2^-50 of the column's largest |tok w| (8: 2^-57); pcx_matrix.hip k_digits
 #ifndef PCX_NDIG
 #define PCX_NDIG 7
 #endif
+// positions per 16-row group of the digit operand zD: PCX_NDIG * gb rounded up to the GEMM's
+// 256-position tile, so the last p-tile's loads stay inside the row group (7 * 128 * odd
+// general tiles is not a multiple of 256); the pad positions only feed discarded rows
+__host__ __device__ inline int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }
 
 namespace pcx {
 
@@ -277,6 +278,8 @@ struct Comm {
 };
 Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err);
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);
+int rccl_version(int* runtime, int* compiled);
+int selftest_abort_once(int users, int aborters, int iters);
 Comm* comm_group(pcx_group* g, int rank, std::string& err);
 Comm* comm_custom(int world, int rank, const pcx_comm_ops* ops, std::string& err);
 // one communicator per listed device, all in this process (ncclCommInitAll); 0 = ok

@@ -32,6 +32,10 @@ constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63
 constexpr int COV_TILE = 128;
 constexpr int COV_STAGE = 64 * PCX_GEMM_KS > 128 ? 64 * PCX_GEMM_KS : 128;  // wcd rows: whole stages of the int8 GEMM
 constexpr int SELS = 40;
+// k-slice cost model of the covariance products (calibrated on C5, profiles/r3): one 64-row
+// stage of one 256 x 256 int8 tile, one 8-row stage of one 128 x 128 fp64 tile (3 per CU), and
+// the effective rate at which a slab is written and read back by k_cov_reduce
+constexpr double GEMM_I8_STAGE_S = 0.55e-6, SYRK_STAGE_S = 2.8e-6, SLAB_BW = 4.0e12;
 constexpr int MAX_SEL_PASSES = 12;  // 64-bit keys, >= 8 bits resolved per pass
 
 template <class T>
@@ -63,7 +67,6 @@ struct pcx_workspace {
     int8_t *zA, *zB;
     int64_t* zsum;
     double* dscale;
-    double* mupos;
     uint64_t* cbuf;
     int64_t* ccount;
     int64_t ccap = 0;
@@ -279,7 +282,6 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->dscale, (size_t)w->wcd_ld * 8, false},
-        {(void**)&w->mupos, (size_t)w->wcd_ld * 8, false},
     };
     auto align = [](size_t b) { return (b + 255) / 256 * 256; };
     size_t zb = 0;
@@ -860,7 +862,6 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.zB = w->zB;
                 m.zsum = w->zsum;
                 m.dscale = w->dscale;
-                m.mupos = w->mupos;
                 R.stage(m, M_COV_PLAN);
                 int64_t plan[2];  // general events, mixed pairs on int8
                 R.hip(hipMemcpyAsync(plan, m.info + INFO_COV_GENERAL, sizeof(plan), hipMemcpyDeviceToHost, R.st),
@@ -877,19 +878,23 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
                 // |tok z d| <= 126 * 64 per row) and at least two WGs per CU
                 const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (PCX_NDIG * gb + 255) / 256;
-                // one 128 KB workgroup per CU runs every (tile, k-slice) item for the same time, so
-                // the launch takes ceil(items / CUs) rounds: pick the k in [int32-exact minimum,
-                // 32] with the least rounds per unit of work (no half-empty last round)
+                // one workgroup per CU runs every (tile, k-slice) item for the same time, so the
+                // launch takes ceil(items / CUs) rounds of items of 1/k of the rows; each k-slice
+                // also writes an int32 slab that k_cov_reduce reads back.  Pick the k in
+                // [int32-exact minimum, 32] with the least modelled time: rounds x item time +
+                // slab traffic (a C5 shard: k = 2 instead of 26 for the mixed block, 4.6 GB less)
                 int ncu = 256;
                 (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-                auto ks_for = [&](int64_t tiles, int64_t max_rows) {
+                auto ks_for = [&](int64_t tiles, int64_t max_rows, double slab_bytes) {
                     tiles = std::max<int64_t>(1, tiles);
                     const int64_t kmin = std::max<int64_t>(1, (w->wcd_rows + max_rows - 1) / max_rows);
                     const int64_t kmax = std::max<int64_t>(kmin, std::min<int64_t>(32, nst));
                     int64_t best = kmin;
                     double best_cost = 1e300;
                     for (int64_t k = kmin; k <= kmax; k++) {
-                        const double cost = (double)((tiles * k + ncu - 1) / ncu) / (double)k;
+                        const double rounds = (double)((tiles * k + ncu - 1) / ncu);
+                        const double cost = rounds / (double)k * (double)nst * GEMM_I8_STAGE_S +
+                                            2.0 * (double)k * slab_bytes / SLAB_BW;
                         if (cost < best_cost * (1.0 - 1e-9)) {
                             best_cost = cost;
                             best = k;
@@ -897,15 +902,16 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     }
                     return (int32_t)std::max<int64_t>(1, std::min<int64_t>(best, nst));
                 };
-                m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000);  // lower tiles only do work
-                m.ks_mx = ks_for(tp * tq, 8000000);  // |z d| <= 130 per row
+                // lower tiles only do work; their slabs hold the lower triangle
+                m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000, 2.0 * (double)np * (double)np);
+                m.ks_mx = ks_for(tp * tq, 8000000, 4.0 * (double)np * (double)(PCX_NDIG * gb));  // |z d| <= 130 per row
                 if (np > 0 && !w->grow(w->pgg, (size_t)(m.ks_gg * m.zq * m.zq * 4))) {
                     err = "workspace: hipMalloc of the int8 covariance products failed";
                     throw Fail{PCX_ENOMEM};
                 }
                 m.Pgg = (int32_t*)w->pgg.p;
                 // mixed pairs on int8 digits when the bounds are finite and the memory is there
-                m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * PCX_NDIG * gb)) &&
+                m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * zd_ld(gb))) &&
                                       w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4))
                                   ? 1
                                   : 0;
@@ -927,15 +933,17 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.fp_ld = m.cov_mixed ? gb : E;
                 m.fp_ks = (int32_t)w->cov_kslices;
                 if (m.cov_mixed && m.cov_fp_tiles > 0) {
-                    const int64_t want = (16 * 256 + m.cov_fp_tiles - 1) / m.cov_fp_tiles;
+                    // k_syrk holds 3 WGs per CU: the k up to `cap` with the least modelled time
+                    // (rounds of items of 1/k of the rows + the [gb][gb] slabs' lower halves)
                     const int64_t cap = std::min<int64_t>(w->cov_kslices * E * E / (gb * gb),
                                                           std::max<int64_t>(1, w->wcd_rows / (8 * 8)));
-                    // k_syrk holds 3 WGs per CU: the k in [want / 2, 2 want] with whole rounds
                     const int64_t slots = 3 * (int64_t)ncu, T = m.cov_fp_tiles;
-                    int64_t best = std::max<int64_t>(1, std::min(want, cap));
-                    double best_cost = (double)((T * best + slots - 1) / slots) / (double)best;
-                    for (int64_t k = std::max<int64_t>(1, want / 2); k <= std::min(cap, 2 * want); k++) {
-                        const double cost = (double)((T * k + slots - 1) / slots) / (double)k;
+                    const double nst8 = (double)(w->wcd_rows / 8), slab = 4.0 * (double)gb * (double)gb;
+                    int64_t best = 1;
+                    double best_cost = 1e300;
+                    for (int64_t k = 1; k <= cap; k++) {
+                        const double cost = (double)((T * k + slots - 1) / slots) / (double)k * nst8 * SYRK_STAGE_S +
+                                            2.0 * (double)k * slab / SLAB_BW;
                         if (cost < best_cost * (1.0 - 1e-9)) {
                             best_cost = cost;
                             best = k;

@@ -252,7 +252,8 @@ class Oracle(object):
             comps = int(meta["components"])
             self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
                               "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"], "path": "matrix",
-                              "devices": self.devices or [self._device_index()], "comm_bytes": meta["comm_bytes"]}
+                              "devices": self.devices or [self._device_index()], "comm_bytes": meta["comm_bytes"],
+                              "grid_events": meta["grid_events"], "mixed_int8": meta["mixed_int8"]}
         if self.algorithm in ("big-five", "fixed-variance") and self.last_info["flags"] & _abi.FLAG_SVD_FAIL:
             # the reference's second svd (:375, :431) is outside the try of :329-333
             raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")

@@ -349,7 +349,9 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
         setattr(res, k, outs[k].ctypes.data)
     h = _lib.context(device_index) if devices is None else _lib.devices_context(devices)
     rc = getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res))
-    if rc == _lib.PCX_ECOMM and devices is not None:  # the failed call aborted the context's communicators
+    if rc != 0 and devices is not None:
+        # a failing rank aborts every other rank's communicator, whatever its own status
+        # (ENOMEM, EHIP, a per-rank EINVAL): the context is unusable, so the next call makes a fresh one
         err = _lib.PcxError("libpcx error %d: %s" % (rc, _lib.lib().pcx_last_error().decode(errors="replace")))
         _lib.drop_devices_context(devices)
         raise err

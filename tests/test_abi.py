@@ -120,3 +120,29 @@ def test_stage_names():
 
     names = [_lib.lib().pcx_stage_name(k).decode() for k in range(_abi.NSTAGES)]
     assert names[1] == "REPUTATION" and "SEL_HIST" in names and "HARD_WALK" in names
+
+
+def test_comm_abort_once_selftest():
+    """The RCCL abort path's exactly-once semantics (pcx_comm.cpp AbortOnce) without RCCL:
+    threads exchanging on a fake handle while others abort it -- one free, no use of a freed
+    handle, no successful exchange after an abort returned."""
+    from pyconsensus_amd import _lib
+
+    h = _lib.lib()
+    for users, aborters in ((1, 1), (4, 1), (8, 8), (2, 16)):
+        assert h.pcx_selftest_abort_once(users, aborters, 20000) == 0, (users, aborters)
+    assert h.pcx_selftest_abort_once(0, 1, 10) == -1
+
+
+def test_rccl_version_compatible():
+    """The librccl this process resolves has the major version of the headers libpcx was built
+    against and is >= 2.18, so RCCL contexts are not refused (pcx_rccl_version)."""
+    import ctypes as C
+
+    from pyconsensus_amd import _lib
+
+    rt, ct = C.c_int(0), C.c_int(0)
+    v = _lib.lib().pcx_rccl_version(C.byref(rt), C.byref(ct))
+    assert v == rt.value and ct.value >= 21800
+    major = lambda x: x // 10000 if x >= 10000 else x // 1000
+    assert major(rt.value) == major(ct.value) and rt.value >= 21800, (rt.value, ct.value)

@@ -80,7 +80,10 @@ def _big_case(name):
     reputation=None: every interpolation weight of a column is the same double) at 250k x 1024.
     C5r_1M: the same recipe at C5's own row count, 1M x 1024 -- there every token is
     int(1e-6 * 1e6) = 1 (__init__.py:146) and every median is a 1M-row equal-weight walk
-    (:303, :520-523); the restatement needs ~60 GB of host memory and a few minutes."""
+    (:303, :520-523); the restatement needs ~60 GB of host memory and a few minutes.
+    C5w: the recipe at C5's own event width, 250k x 4096 -- the 7-digit int8 mixed block over
+    ~3,072 grid events x ~1,024 general ones (:326), the E = 4096 power iteration (:330-337) and
+    the rank rule's `old` ties among 3,072 binary events under equal weights (:489-498)."""
     if name in _REF:
         return _REF[name]
     from oracle.pcx_oracle import OracleCPU
@@ -88,11 +91,12 @@ def _big_case(name):
 
     if name == "C4":
         R, sc, lo, hi, rep = synthetic.matrix(100_000, 1000, seed=2)
-    elif name in ("C5r", "C5r_1M"):
+    elif name in ("C5r", "C5r_1M", "C5w"):
         import torch
 
-        N = 250_000 if name == "C5r" else 1_000_000
-        Rd, scd, lod, hid, _ = synthetic.matrix_device(N, 1024, seed=3, n_shards=8, device="cuda:0")
+        N = 1_000_000 if name == "C5r_1M" else 250_000
+        E = 4096 if name == "C5w" else 1024
+        Rd, scd, lod, hid, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, device="cuda:0")
         R, sc, lo, hi, rep = Rd.cpu().numpy(), scd.cpu().numpy().astype(bool), lod.cpu().numpy(), hid.cpu().numpy(), None
         del Rd
         torch.cuda.empty_cache()
@@ -118,7 +122,9 @@ def _record(name, world, info):
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "large_cases.jsonl"), "a") as f:
             f.write(json.dumps({"case": name, "world": world, "n_hard": info.get("n_hard"),
-                                "sel_passes": info.get("sel_passes"), "branch": info.get("branch")}) + "\n")
+                                "sel_passes": info.get("sel_passes"), "branch": info.get("branch"),
+                                "pi_iters": info.get("pi_iters"), "grid_events": info.get("grid_events"),
+                                "mixed_int8": info.get("mixed_int8")}) + "\n")
     except OSError:
         pass
 
@@ -174,11 +180,12 @@ def _abi_events():
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), "C4", "C5r", "C5r_1M"],
+@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), "C4", "C5r", "C5r_1M",
+                                  "C5w"],
                          ids=["3000x150", "20000x400", "20008x400_ragged16",
                               "16648x2048_repNone_ragged16_empty_chunks", "C4_100k_x_1k_intrep",
                               "C5recipe_250k_x_1024_repNone",
-                              "C5r_1M_x_1024_repNone"])
+                              "C5r_1M_x_1024_repNone", "C5width_250k_x_4096_repNone"])
 @pytest.mark.parametrize("world", [1, 2])
 def test_matrix_vs_numpy_oracle(gpu_lib, case, world):
     """Against the numpy restatement run on the box, no exemption: binary outcomes and the
@@ -196,11 +203,15 @@ def test_matrix_vs_numpy_oracle(gpu_lib, case, world):
         ours, info = _sharded(R, rep, sc, lo, hi, world)
     print(case, world, {k: info[k] for k in ("n_hard", "sel_passes") if k in info})
     bad, sign = P.compare(ref, ours)
+    if case in ("C4", "C5r", "C5r_1M", "C5w"):
+        _record(case, world, info)
     assert not bad, bad
-    if case == "C5r_1M":
-        if world == 1:  # the drop-in's tokens: int(1e-6 * 1e6) = 1 for every reporter (:146)
-            assert set(o.reptokens) == {1}
-        _record("C5r_1M", world, info)
+    if case == "C5r_1M" and world == 1:  # the drop-in's tokens: int(1e-6 * 1e6) = 1 for every reporter (:146)
+        assert set(o.reptokens) == {1}
+    if case in ("C4", "C5w"):
+        # C4: integer reputations, tokens int(r / sum(r) 1e6) in [0, 19] -- non-uniform tokens through
+        # the int8 blocks (the mixed block's digits of tok * w); C5w: the 3,072-event grid
+        assert info.get("mixed_int8") == 1 and info.get("grid_events", 0) > 0, info
 
 
 def test_virtual_shards_match_single(gpu_lib):

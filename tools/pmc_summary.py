@@ -8,7 +8,14 @@ HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a coalesced streaming read, so
 bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  Each counter comes from its own
 --pmc pass (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2).
+
+    python tools/pmc_summary.py --per-kernel DIR
+
+prints every counter of every pass under DIR/p*/ per kernel (median over launches), the int8
+GEMM's launches split into the grid x grid and the mixed block (they alternate).
 """
+import glob
+import re
 import argparse
 import csv
 import json
@@ -36,15 +43,43 @@ def per_kernel(path, counter):
     return {k: statistics.median(v) for k, v in out.items()}
 
 
+def per_kernel_passes(d):
+    vals, seen = {}, {}
+    for f in sorted(glob.glob(d + "/p*/**/pmc_counter_collection.csv", recursive=True)):
+        for r in csv.DictReader(open(f)):
+            n = r["Kernel_Name"]
+            if not ours(n):
+                continue
+            m = re.search(r"(k_[a-z0-9_]+)", n)
+            k = m.group(1) if m else kname(n)
+            if k == "k_gemm_i8":  # launches alternate: grid x grid, then the mixed block
+                key = (f, r["Counter_Name"])
+                seen[key] = seen.get(key, -1) + 1
+                k += "_grid" if seen[key] % 2 == 0 else "_mixed"
+            vals.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    for k in sorted(vals):
+        med = {c: statistics.median(v) for c, v in vals[k].items()}
+        if med.get("SQ_WAVE_CYCLES", 0) == 0 and med.get("FETCH_SIZE", 0) < 1e5:
+            continue
+        gb = (2 * med.get("FETCH_SIZE", 0) * 1024 + med.get("WRITE_SIZE", 0) * 1024) / 1e9
+        print("%-22s hbm_GB=%.2f " % (k, gb) + " ".join("%s=%.4g" % (c, v) for c, v in sorted(med.items())))
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--per-kernel", help="directory of --pmc passes p1, p2, ...: print per-kernel medians")
     ap.add_argument("--stats")
-    ap.add_argument("--fetch", required=True)
-    ap.add_argument("--write", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
     ap.add_argument("--valu", help="pmc_counter_collection.csv of an SQ_INSTS_VALU pass")
-    ap.add_argument("--out", required=True)
+    ap.add_argument("--out")
     ap.add_argument("--note", default="")
     a = ap.parse_args()
+    if a.per_kernel:
+        per_kernel_passes(a.per_kernel)
+        return
+    if not (a.fetch and a.write and a.out):
+        ap.error("--fetch, --write and --out are required without --per-kernel")
     f = per_kernel(a.fetch, "FETCH_SIZE")
     w = per_kernel(a.write, "WRITE_SIZE")
     res = {}
