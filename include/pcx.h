@@ -314,7 +314,7 @@ int pcx_ctx_progress(const pcx_ctx* ctx, int* stage, int* host_waiting);
 double  pcx_seqsum_const(double c, int64_t k);
 int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax);
 
-/* Build parameter: base-128 int8 digits per general event in the covariance's mixed block
+/* Build parameter: balanced base-254 int8 digits per general event in the covariance's mixed block
  * (pcx_result.mixed_int8; the int8 work per row is then grid pairs + digits x general x
  * (grid + 1)).  For roofline accounting. */
 int pcx_mixed_digits(void);

@@ -115,7 +115,7 @@ typedef struct {
     int8_t*  zD;                  /* [wcd_rows/16][8 * 128 cov_jb][16] digit s of position q at s * 128 cov_jb + q */
     double*  dscale;              /* [wcd_ld] 2^-e per general position                               */
     int32_t* Pgg;                 /* [ks_gg][zq][zq] int32 zA^T zB per k-slice (lower part)           */
-    int32_t* Pmx;                 /* [ks_mx][zq][8 * 128 cov_jb] int32 zA^T zD per k-slice            */
+    int32_t* Pmx;                 /* [ks_mx][zq][PCX_NDIG * 128 cov_jb] int32 zA^T zD per k-slice            */
     int32_t  ks_gg, ks_mx;        /* k-slices of the two int8 products (int32-exact row ranges)       */
     int32_t  fp_ks;               /* k-slices of the fp64 tiles (k_syrk)                              */
     int64_t  fp_ld;               /* row length of one fp64 slab: E, or 128 cov_jb when mixed          */
@@ -129,14 +129,15 @@ typedef struct {
 // int8 covariance GEMM (k_gemm_i8, pcx_gemm_i8.h: PCX_GEMM_KS 64-row MFMA k-steps per LDS ring
 // stage); the workspace pads wcd_rows to whole stages (pcx_runner.cpp COV_STAGE)
 #include "pcx_gemm_i8.h"
-// mixed block (general x grid pairs): base-128 int8 digits per general position.  7 digits leave
-// a residue <= 2^-50 of the column's largest |tok w| (8: 2^-57); pcx_matrix.hip k_digits
+// mixed block (general x grid pairs): balanced base-254 int8 digits per general position.  6
+// digits leave a residue <= 2^-48.9 of the column's largest |tok w|; pcx_matrix.hip k_digits
 #ifndef PCX_NDIG
-#define PCX_NDIG 7
+#define PCX_NDIG 6
 #endif
+#define PCX_DBASE 254.0
 // positions per 16-row group of the digit operand zD: PCX_NDIG * gb rounded up to the GEMM's
-// 256-position tile, so the last p-tile's loads stay inside the row group (7 * 128 * odd
-// general tiles is not a multiple of 256); the pad positions only feed discarded rows
+// 256-position tile, so the last p-tile's loads stay inside the row group (NDIG * 128 * odd
+// general tiles need not be a multiple of 256); the pad positions only feed discarded rows
 __host__ __device__ inline int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }
 
 namespace pcx {

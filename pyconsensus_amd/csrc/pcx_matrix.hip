@@ -716,7 +716,7 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
 }
 
 // ---------------------------------------------------------------- covariance operands
-// z in {0, 1, 2} of 16 rows packed into one uint32 (k_gemm_i8 BPACK): row r at bit
+// z in {0, 1, 2} of 16 rows packed into one uint32 (the B operand of k_gemm_i8): row r at bit
 // 8 (r % 4) + 2 (r / 4); zpack_bit(r) is the bit of value 1
 __device__ __forceinline__ uint32_t zpack_bit(int r) { return 1u << (8 * (r & 3) + 2 * (r >> 2)); }
 __device__ __forceinline__ uint32_t zpack_get(uint32_t P, int r) { return (P >> (8 * (r & 3) + 2 * (r >> 2))) & 3u; }
@@ -1115,10 +1115,11 @@ __global__ void __launch_bounds__(BT) k_tokcol(pcx_mat m) {
     zb_packed(m)[grp * m.zq + m.tokpos] = tb;
 }
 
-// tok * w of the general positions q < gb (the exact product, as a double-double) as 8 balanced
-// base-128 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 128 v, d = rint(t_hi), v = t - d
-// with the low part carried -- every step exact, |d| <= 65; PCX_NDIG digits leave a residue
-// <= 2^-(7 NDIG + 1) 2^e (7: 2^-50 of the column's bound on |tok w|, 1.8e-15 relative)
+// tok * w of the general positions q < gb (the exact product, as a double-double) as PCX_NDIG
+// balanced base-254 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 254 v (the double-double
+// product, its rounding below 2^-95), d = rint(t_hi), v = t - d -- |d| <= 127, the widest balanced
+// digit int8 holds.  PCX_NDIG digits leave a residue <= 254^-NDIG / 2 of 2^e (6: 2^-48.9 of the
+// column's bound on |tok w|, 3.7e-15 relative)
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
@@ -1139,10 +1140,11 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
 #pragma unroll
             for (int k = 0; k < PCX_NDIG; k++) {
-                const double t = hi * 128.0, di = rint(t);
-                const double e = t - di;  // exact
-                const double l = lo * 128.0;
-                hi = e + l;  // two-sum: (hi, lo) = (t - di) + 128 lo exactly
+                const double t = hi * PCX_DBASE, te = fma(hi, PCX_DBASE, -t);  // hi 254 = t + te exactly
+                const double di = rint(t);
+                const double e = t - di;               // exact
+                const double l = fma(lo, PCX_DBASE, te);  // lo 254 + te (|l| < 2^-44)
+                hi = e + l;                            // two-sum: (hi, lo) = e + l exactly
                 const double bv = hi - e;
                 lo = (e - (hi - bv)) + (l - bv);
                 d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
@@ -1222,15 +1224,22 @@ __device__ __forceinline__ int64_t slab_sum(const int32_t* P, int64_t slab, int 
     return (a0 + a1) + (a2 + a3);
 }
 
-// sum tok z_row w_q of the mixed block from its PCX_NDIG digit products, Horner in dd (2^-7)
+// a / 254 in double-double: q1 = hi / 254, the remainder hi - 254 q1 is exact (fma)
+__device__ __forceinline__ dd dd_div_base(dd a) {
+    const double q1 = a.hi / PCX_DBASE;
+    const double r = fma(-q1, PCX_DBASE, a.hi) + a.lo;
+    return fast_two_sum(q1, r / PCX_DBASE);
+}
+
+// sum tok z_row w_q of the mixed block from its PCX_NDIG digit products: Horner in double-double
+// over 1/254 (sum_k P_k 254^-(k+1)), times 2^e
 __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t q) {
     const int64_t gb = (int64_t)m.cov_jb * CT, ldm = PCX_NDIG * gb;
-    const double sc = ldexp(0x1p-7, -ilogb(m.dscale[q]));  // 2^(e - 7)
     const int32_t* P = m.Pmx + row * ldm + q;
     const int64_t slab = m.zq * ldm;
     dd a{(double)slab_sum(P + (PCX_NDIG - 1) * gb, slab, m.ks_mx), 0.0};
-    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_mul_d(a, 0x1p-7), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
-    return dd_mul_d(a, sc);
+    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
+    return dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q])));  // 2^e
 }
 
 // the token column's S_q = sum tok w_q of every general position (shared by all grid rows)
@@ -4460,8 +4469,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             static std::once_flag g_once;
             static hipError_t g_err = hipSuccess;
             std::call_once(g_once, [] {
-                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, true>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRing<true>::BYTES);
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, GEMM_I8_NBUF>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8_LDS);
             });
             if (g_err != hipSuccess) return g_err;
             const int64_t rg = m.wcd_rows / 16;
@@ -4470,12 +4479,12 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             {  // grid x grid (lower tiles): P = (tok z)^T z, |tok z z| <= 252 per row
                 GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg, 0};
                 g.tp = g.tq = (np + GT - 1) / GT;
-                hipLaunchKernelGGL((k_gemm_i8<16, true>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
-                                   GRing<true>::BYTES, st, g);
+                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                                   GEMM_I8_LDS, st, g);
             }
             if (m.cov_mixed) {
                 // general digits x grid: digits of tok w (A, PCX_NDIG per general position) times z (B);
-                // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 65 per row
+                // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
                 hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
                 GemmI8 g{m.zD, zd_ld(gb), m.zB, m.zq, m.Pmx, (int64_t)PCX_NDIG * gb, m.zq * PCX_NDIG * gb, PCX_NDIG * gb, np,
@@ -4486,8 +4495,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                     err = "M_COV_I8: operand row groups narrower than the tiles";
                     return hipErrorInvalidValue;
                 }
-                hipLaunchKernelGGL((k_gemm_i8<16, true>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
-                                   GRing<true>::BYTES, st, g);
+                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                                   GEMM_I8_LDS, st, g);
             }
             break;
         }

@@ -876,7 +876,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.tokpos = (int32_t)(np - 1);
                 r->grid_events = (int32_t)(np > 0 ? E - gb : 0);  // grid events past the general tiles
                 // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
-                // |tok z d| <= 126 * 64 per row) and at least two WGs per CU
+                // |z d| <= 254 per row) and at least two WGs per CU
                 const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (PCX_NDIG * gb + 255) / 256;
                 // one workgroup per CU runs every (tile, k-slice) item for the same time, so the
                 // launch takes ceil(items / CUs) rounds of items of 1/k of the rows; each k-slice
@@ -904,7 +904,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 };
                 // lower tiles only do work; their slabs hold the lower triangle
                 m.ks_gg = ks_for(tp * (tp + 1) / 2, 8000000, 2.0 * (double)np * (double)np);
-                m.ks_mx = ks_for(tp * tq, 8000000, 4.0 * (double)np * (double)(PCX_NDIG * gb));  // |z d| <= 130 per row
+                m.ks_mx = ks_for(tp * tq, 8000000, 4.0 * (double)np * (double)(PCX_NDIG * gb));  // |z d| <= 254 per row
                 if (np > 0 && !w->grow(w->pgg, (size_t)(m.ks_gg * m.zq * m.zq * 4))) {
                     err = "workspace: hipMalloc of the int8 covariance products failed";
                     throw Fail{PCX_ENOMEM};

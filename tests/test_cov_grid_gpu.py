@@ -3,7 +3,7 @@
 Binary events whose filled values all lie on {1, 1.5, 2} ("grid" events) take the wcd
 positions after the general events; the covariance tiles made only of grid positions are
 P = sum tok z z^T on int8 MFMA with z = 2 (F - 1), combined with the exact T and Z sums;
-the general x grid pairs multiply eight int8 digit slices of w = F - mu with tok z.
+the general x grid pairs multiply PCX_NDIG (6) base-254 int8 digit slices of tok w (w = F - mu) with z.
 The wpca entry's covariance is checked against the reference formula
 (pyconsensus/__init__.py:317-326) evaluated in numpy: all-general, mixed, all-grid,
 varying tokens (tok * z operand), off-grid values and tokens above 63 (no int8 path).

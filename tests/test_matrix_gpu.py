@@ -81,7 +81,7 @@ def _big_case(name):
     C5r_1M: the same recipe at C5's own row count, 1M x 1024 -- there every token is
     int(1e-6 * 1e6) = 1 (__init__.py:146) and every median is a 1M-row equal-weight walk
     (:303, :520-523); the restatement needs ~60 GB of host memory and a few minutes.
-    C5w: the recipe at C5's own event width, 250k x 4096 -- the 7-digit int8 mixed block over
+    C5w: the recipe at C5's own event width, 250k x 4096 -- the 6-digit int8 mixed block over
     ~3,072 grid events x ~1,024 general ones (:326), the E = 4096 power iteration (:330-337) and
     the rank rule's `old` ties among 3,072 binary events under equal weights (:489-498)."""
     if name in _REF:

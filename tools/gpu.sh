@@ -16,6 +16,7 @@
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
 #   i8bench      the int8 covariance GEMM variants at the C5 shapes (tools/i8bench, built on the CPU)
+#   i8pmc=V      SQ / LDS / cache PMC passes over the mixed-block GEMM, reference kernel and variant V
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -94,6 +95,17 @@ for STEP in "$@"; do
     i8bench)
       timeout -k 10 300 tools/i8bench/i8bench 5 > $O/i8bench.txt 2>&1 || { echo "i8bench rc=$?"; tail -20 $O/i8bench.txt; exit 24; }
       cat $O/i8bench.txt ;;
+    i8pmc=*)
+      V=${STEP#i8pmc=}
+      i=0
+      for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU" \
+               "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE" \
+               "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/i8p$i -o pmc -- tools/i8bench/i8bench 2 1000064 "$V" mixed > $O/i8p$i.log 2>&1 || { echo "i8pmc pass $i rc=$?"; tail -5 $O/i8p$i.log; exit 25; }
+      done
+      python3 tools/pmc_summary.py --per-kernel "$O" --glob "i8p*" > $O/i8pmc.txt 2>&1 || { echo "i8pmc summary failed"; tail -5 $O/i8pmc.txt; exit 26; }
+      cat $O/i8pmc.txt ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

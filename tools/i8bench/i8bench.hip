@@ -1,14 +1,15 @@
 // i8bench.hip -- standalone benchmark of the M_COV_I8 int8 products (pyconsensus_amd/csrc/pcx_gemm_i8.h)
-// at the C5 shapes (1M rows: 62,504 groups of 16), every variant checked against k_gemm_i8 (the
-// validated product kernel) as the int64 sum of its k-slice slabs, and k_gemm_i8 against a CPU
-// reference on a small case.
-//   mixed: A = 7 int8 digits x 1,024 general positions (lda 7,168), B = z of 3,072 grid events +
+// at the C5 shapes (1M rows: 62,504 groups of 16), every configuration checked against the
+// product's (k_gemm_i8<16, GEMM_I8_NBUF>) as the int64 sum of its k-slice slabs, and all of them
+// against a CPU reference on a small case.
+//   mixed: A = PCX_NDIG int8 digits x 1,024 general positions, B = z of 3,072 grid events +
 //          the token column (packed 2 bits, ldb 3,328), stored transposed;
 //   grid:  A = tok z (int8, lda 3,328), B = z packed, lower tiles.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/i8bench/i8bench.hip -o tools/i8bench/i8bench
-// usage: i8bench [reps=5] [rows=1000064]
+// usage: i8bench [reps=5] [rows=1000064] [variant substring] [shape substring]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,10 @@
 #include <vector>
 
 #include "../../pyconsensus_amd/csrc/pcx_gemm_i8.h"
+
+#ifndef PCX_NDIG
+#define PCX_NDIG 6  // (pcx_internal.h)
+#endif
 
 using namespace pcx;
 
@@ -96,15 +101,15 @@ struct Variant {
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
     const int64_t rows = argc > 2 ? atoll(argv[2]) : 1000064;
+    const char* vsel = argc > 3 ? argv[3] : "";
+    const char* ssel = argc > 4 ? argv[4] : "";
     const int64_t rg = rows / 16;
     int ncu = 256;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<Variant> vs = {
-        {"k_gemm_i8<16,packed>", k_gemm_i8<16, true>, 1024, GRing<true>::BYTES},
-        {"k_gemm_i8u<16,NA4>", k_gemm_i8u<16, 4>, 1024, GRingU<4>::BYTES},
-        {"k_gemm_i8u<16,NA6>", k_gemm_i8u<16, 6>, 1024, GRingU<6>::BYTES},
-        {"k_gemm_i8u<8,NA4>", k_gemm_i8u<8, 4>, 512, GRingU<4>::BYTES},
-        {"k_gemm_i8u<8,NA6>", k_gemm_i8u<8, 6>, 512, GRingU<6>::BYTES},
+        {"k_gemm_i8<16,3> (product)", k_gemm_i8<16, 3>, 1024, 3 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
+        {"k_gemm_i8<16,4>", k_gemm_i8<16, 4>, 1024, 4 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
+        {"k_gemm_i8<8,3>", k_gemm_i8<8, 3>, 512, 3 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
     };
     for (auto& v : vs) CK(hipFuncSetAttribute((const void*)v.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
 
@@ -114,7 +119,7 @@ int main(int argc, char** argv) {
         const int np = 300, nq = 260;
         std::vector<int8_t> hA(srg * lda * 16);
         std::vector<uint32_t> hB(srg * ldb);
-        for (size_t i = 0; i < hA.size(); i++) hA[i] = (int8_t)((int)((i * 2654435761u) % 131) - 65);
+        for (size_t i = 0; i < hA.size(); i++) hA[i] = (int8_t)((int)((i * 2654435761u) % 255) - 127);
         for (size_t i = 0; i < hB.size(); i++) {
             uint32_t P = 0, r = (uint32_t)(i * 40503u + 17u);
             for (int f = 0; f < 16; f++) {
@@ -163,15 +168,16 @@ int main(int argc, char** argv) {
     }
 
     const Shape shapes[] = {
-        {"mixed", 7168, 3328, 7168, 3073, 0, 1},
+        {"mixed", PCX_NDIG * 1024, 3328, PCX_NDIG * 1024, 3073, 0, 1},
         {"grid", 3328, 3328, 3073, 3073, 1, 0},
     };
     for (const Shape& sh : shapes) {
+        if (!strstr(sh.name, ssel)) continue;
         int8_t* dA;
         uint32_t* dB;
         CK(hipMalloc(&dA, (size_t)rg * sh.lda * 16));
         CK(hipMalloc(&dB, (size_t)rg * sh.ldb * 4));
-        hipLaunchKernelGGL(k_fill_a, dim3(4096), dim3(256), 0, 0, dA, rg * sh.lda * 16, sh.trans ? 65 : 63, 11ull);
+        hipLaunchKernelGGL(k_fill_a, dim3(4096), dim3(256), 0, 0, dA, rg * sh.lda * 16, sh.trans ? 127 : 63, 11ull);
         hipLaunchKernelGGL(k_fill_b, dim3(4096), dim3(256), 0, 0, dB, rg * sh.ldb, 977ull);
         const int tp = (sh.np + GT - 1) / GT, tq = (sh.nq + GT - 1) / GT;
         const int64_t tiles = sh.lower ? (int64_t)tp * (tp + 1) / 2 : (int64_t)tp * tq;
@@ -184,8 +190,8 @@ int main(int argc, char** argv) {
         const double ops = 2.0 * (double)rg * 16 * sh.np * (double)sh.nq * (sh.lower ? 0.5 : 1.0);
         for (size_t vi = 0; vi < vs.size(); vi++) {
             const Variant& v = vs[vi];
-            const int64_t stage_groups = vi == 0 ? 4 * PCX_GEMM_KS : 4;
-            const int ks = ks_for(tiles, rg / stage_groups, ncu);
+            if (vi > 0 && !strstr(v.name, vsel)) continue;
+            const int ks = ks_for(tiles, rg / (4 * PCX_GEMM_KS), ncu);
             int32_t* dP;
             CK(hipMalloc(&dP, (size_t)ks * outn * 4));
             CK(hipMemset(dP, 0, (size_t)ks * outn * 4));

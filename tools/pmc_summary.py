@@ -43,16 +43,16 @@ def per_kernel(path, counter):
     return {k: statistics.median(v) for k, v in out.items()}
 
 
-def per_kernel_passes(d):
+def per_kernel_passes(d, pattern="p*"):
     vals, seen = {}, {}
-    for f in sorted(glob.glob(d + "/p*/**/pmc_counter_collection.csv", recursive=True)):
+    for f in sorted(glob.glob(d + "/" + pattern + "/**/pmc_counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
             n = r["Kernel_Name"]
             if not ours(n):
                 continue
-            m = re.search(r"(k_[a-z0-9_]+)", n)
+            m = re.search(r"(k_[a-z0-9_]+(<[^>]*>)?)", n)
             k = m.group(1) if m else kname(n)
-            if k == "k_gemm_i8":  # launches alternate: grid x grid, then the mixed block
+            if k == "k_gemm_i8<16, true>" and pattern == "p*":  # launches alternate: grid x grid, then the mixed block
                 key = (f, r["Counter_Name"])
                 seen[key] = seen.get(key, -1) + 1
                 k += "_grid" if seen[key] % 2 == 0 else "_mixed"
@@ -68,6 +68,7 @@ def per_kernel_passes(d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--per-kernel", help="directory of --pmc passes p1, p2, ...: print per-kernel medians")
+    ap.add_argument("--glob", default="p*", help="--per-kernel: the pass directories' pattern")
     ap.add_argument("--stats")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
@@ -76,7 +77,7 @@ def main():
     ap.add_argument("--note", default="")
     a = ap.parse_args()
     if a.per_kernel:
-        per_kernel_passes(a.per_kernel)
+        per_kernel_passes(a.per_kernel, a.glob)
         return
     if not (a.fetch and a.write and a.out):
         ap.error("--fetch, --write and --out are required without --per-kernel")
