@@ -442,21 +442,57 @@ struct XW {
 };
 
 // PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
-// min/max present value; writes the scaled columns (column-major) into T.
+// min/max present value; writes the scaled columns (column-major) into T.  A lane owns a column
+// and walks the rows, so its T column is one contiguous run; the lanes' values go through a
+// per-wave LDS tile of 16 rows, and the wave writes them out as 8 whole 128-byte segments per
+// store instruction (lanes 8 k .. 8 k + 7 one column's 16 rows), where a lane-per-column store
+// touched 64 lines with 16 bytes each (C5: 9.1 -> 8.3 ms; 6.9 with no T at all).  Rejected: T in
+// 16-row blocks [row / 16][scaled column][16], so a wave's stores form one contiguous run
+// (8.3 ms either way).
+constexpr int CS_TLD = 18;  // doubles per column in the transpose tile (16 rows + pad: 16-byte aligned pairs)
 template <bool EQW>  // EQW: reputation=None (every weight 1/N)
 __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
-    const int c = blockIdx.x * BT + threadIdx.x;
-    if (c >= m.n_events) return;
+    __shared__ __attribute__((aligned(16))) double tile[BT / WAVE][WAVE * CS_TLD];
     const int E = (int)m.n_events;
+    const int c0 = blockIdx.x * BT + (threadIdx.x & ~(WAVE - 1));  // the wave's first column
+    if (c0 >= E) return;  // wave-uniform
+    const int lane = threadIdx.x & (WAVE - 1);
+    const bool live = c0 + lane < E;
+    const int c = live ? c0 + lane : E - 1;  // dead lanes shadow the last column (nothing stored)
     const ColParam p = col_param(m, c, false);
-    const int si = m.scaled_index ? m.scaled_index[c] : -1;
-    double* Tc = si >= 0 ? m.T + (int64_t)si * m.n_rows : nullptr;
+    double* const lt = tile[threadIdx.x / WAVE];
+    // the flush's columns: lane l writes rows 2 (l & 7), +1 of wave column 8 k + (l >> 3), k < 8
+    int tsi[8];  // their T columns (-1: not scaled)
+    bool any_t = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int cw = c0 + 8 * k + (lane >> 3);
+        tsi[k] = (m.scaled_index && cw < E) ? m.scaled_index[cw] : -1;
+        any_t |= tsi[k] >= 0;
+    }
+    any_t = __any(any_t);  // wave-uniform
     int64_t r0, r1;
-    // 16 rows per step: each lane writes whole 128-byte lines of its T column (with 8,
-    // half-line partial writes doubled the write traffic: 14 GB for 8 GB of T at C5)
-    row_range(m, r0, r1, 16);
-    const bool t2 = Tc && (((int64_t)si * m.n_rows) & 1) == 0;  // (r0 is even)
-    double tprev = 0.0;
+    row_range(m, r0, r1, 16);  // 16-row groups: whole 128-byte T segments
+    // rows [g0, g0 + nr) of the tile to T (wave-uniform call; every lane takes part)
+    auto flush = [&](int64_t g0, int nr) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const int pr = 2 * (lane & 7);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (tsi[k] < 0) continue;
+            const double* src = lt + (8 * k + (lane >> 3)) * CS_TLD + pr;
+            double* dst = m.T + (int64_t)tsi[k] * m.n_rows + g0 + pr;
+            if (pr + 1 < nr && ((uintptr_t)dst & 15) == 0) {
+                *reinterpret_cast<double2*>(dst) = *reinterpret_cast<const double2*>(src);
+            } else {
+                if (pr < nr) dst[0] = src[0];
+                if (pr + 1 < nr) dst[1] = src[1];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    };
     acc2 sr, srx, sx;
     constexpr bool eqw = EQW;
     double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
@@ -464,24 +500,17 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     // EQW: every weight is 1 / N (k_rep_local), so the largest one is the first present row's:
     // no weight loads, and the argmax is that row's index, converted once at the end
     int64_t first_row = -1;
-    rows_pipelined<16>(  // 16: whole 128-byte lines of T per lane
+    rows_pipelined<PIPE_U>(
         r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], eqw ? 0.0 : m.rep[i]}; },
         [&](int64_t i, XW v) {
             const double x = rescale(v.x, p, m.int_dtype);
             const bool isn = __builtin_isnan(x);
             const bool z = x == 0.0;
-            if (Tc) {
-                const double tv = (isn || z) ? __builtin_nan("") : x;
-                // pairs of rows as one 16-byte store (T's column start even): half the store
-                // instructions, each touching 64 lines (the T writes cost ~3.8 of 10.7 ms at C5)
-                if (!t2)
-                    Tc[i] = tv;
-                else if ((i & 1) == 0)
-                    tprev = tv;
-                else
-                    *reinterpret_cast<double2*>(Tc + i - 1) = double2{tprev, tv};
+            if (any_t) {
+                lt[lane * CS_TLD + (i & 15)] = (isn || z) ? __builtin_nan("") : x;
+                if ((i & 15) == 15) flush(i - 15, 16);
             }
-            nz += z ? 1.0 : 0.0;
+    nz += z ? 1.0 : 0.0;
             if (isn || z) return;
             cnt += 1.0;
             if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
@@ -500,7 +529,8 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             mx_x = fmax(mx_x, x);
             offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);
         });
-    if (t2 && r1 > r0 && (r1 & 1)) Tc[r1 - 1] = tprev;  // an odd end: the last (even) row alone
+    if (any_t && r1 > r0 && (r1 & 15)) flush(r1 & ~(int64_t)15, (int)(r1 & 15));  // the last, partial group
+    if (!live) return;
     if (eqw && first_row >= 0) {
         mx = 1.0 / (double)m.n_total;  // = m.rep[i] (k_rep_local)
         arg = (double)(m.row_offset + first_row);
