@@ -12,6 +12,7 @@
 #                into pmc_traffic.json (tools/pmc_summary.py) and kernel_stats.csv
 #   pmc_c5       PMC passes over one C5 consensus, per kernel (k_gemm_i8 split into grid / mixed)
 #   shard        one 8-GPU C5 shard (125k x 4096) as a one-rank consensus (tools/c5_shard_latency.py)
+#   shard_prof   rocprofv3 kernel trace of the shard run (per-launch times: shard_kt/)
 #   dist         the 2-process tests and bench.py as the driver launches N=2 (gloo: both ranks on cuda:0)
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
@@ -53,7 +54,7 @@ for STEP in "$@"; do
         timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/$C -o pmc -- python3 bench.py $ARGS > $O/$C.log 2>&1 || { echo "pmc $C rc=$?"; tail -5 $O/$C.log; exit 15; }
       done
       KS=$(find $O/kt -name "kt_kernel_stats.csv" | head -1)
-      python3 tools/pmc_summary.py --stats "$KS" --fetch "$(find $O/FETCH_SIZE -name 'pmc_counter_collection.csv' | head -1)" \
+      python3 tools/pmc_summary.py --stats "$KS" --trace "$(find $O/kt -name 'kt_kernel_trace.csv' | head -1)" --fetch "$(find $O/FETCH_SIZE -name 'pmc_counter_collection.csv' | head -1)" \
           --write "$(find $O/WRITE_SIZE -name 'pmc_counter_collection.csv' | head -1)" \
           --valu "$(find $O/SQ_INSTS_VALU -name 'pmc_counter_collection.csv' | head -1)" --out $O/pmc_traffic.json \
           --note "bench.py $ARGS (C3 65536 x 50x20 with every output + one C5 1M x 4k), MI355X" > $O/summary.log 2>&1 || { echo summary failed; tail -5 $O/summary.log; exit 16; }
@@ -73,6 +74,9 @@ for STEP in "$@"; do
     shard)
       timeout -k 10 200 python -u tools/c5_shard_latency.py 8 5 > $O/w8.json 2> $O/w8.err || { echo "shard rc=$?"; tail -20 $O/w8.err; exit 19; }
       python3 -c "import json; d=json.load(open('$O/w8.json')); print('shard', round(d['latency_ms'],2), 'ms;', ' '.join('%s %.2f' % (k[2:], v) for k, v in list(d.get('stage_ms', {}).items())[:10]))" ;;
+    shard_prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard_kt -o kt -- python3 tools/c5_shard_latency.py 8 3 > $O/shard_kt.log 2>&1 || { echo "shard kernel-trace rc=$?"; tail -5 $O/shard_kt.log; exit 27; }
+      echo shard_prof ok ;;
     dist)
       timeout -k 10 240 python -u -m pytest tests/test_dist_gpu.py -x -v --timeout 200 --timeout-method thread > $O/pytest_dist.log 2>&1 || { echo "pytest dist rc=$?"; tail -40 $O/pytest_dist.log; exit 20; }
       tail -1 $O/pytest_dist.log

@@ -33,14 +33,36 @@ def ours(full):
     return "pcx::" in full
 
 
+class GemmSplit:
+    """The int8 GEMM's launches alternate: the grid x grid block, then the mixed block."""
+
+    def __init__(self):
+        self.n = {}
+
+    def __call__(self, name, key=None):
+        if name != "k_gemm_i8":
+            return name
+        self.n[key] = self.n.get(key, -1) + 1
+        return name + ("_grid" if self.n[key] % 2 == 0 else "_mixed")
+
+
 def per_kernel(path, counter):
-    out = {}
-    for r in csv.DictReader(open(path)):
-        if r.get("Counter_Name") != counter or not ours(r["Kernel_Name"]):
-            continue
-        name = kname(r["Kernel_Name"])
+    out, split = {}, GemmSplit()
+    rows = [r for r in csv.DictReader(open(path)) if r.get("Counter_Name") == counter and ours(r["Kernel_Name"])]
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        name = split(kname(r["Kernel_Name"]))
         out.setdefault(name, []).append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in out.items()}
+
+
+def per_kernel_times(path):
+    """Average duration (ns) and launch count per kernel from a kernel_trace.csv."""
+    out, split = {}, GemmSplit()
+    rows = [r for r in csv.DictReader(open(path)) if ours(r["Kernel_Name"])]
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        name = split(kname(r["Kernel_Name"]))
+        out.setdefault(name, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in out.items()}
 
 
 def per_kernel_passes(d, pattern="p*"):
@@ -52,7 +74,7 @@ def per_kernel_passes(d, pattern="p*"):
                 continue
             m = re.search(r"(k_[a-z0-9_]+(<[^>]*>)?)", n)
             k = m.group(1) if m else kname(n)
-            if k == "k_gemm_i8<16, true>" and pattern == "p*":  # launches alternate: grid x grid, then the mixed block
+            if k.startswith("k_gemm_i8<") and pattern == "p*":  # launches alternate: grid x grid, then the mixed block
                 key = (f, r["Counter_Name"])
                 seen[key] = seen.get(key, -1) + 1
                 k += "_grid" if seen[key] % 2 == 0 else "_mixed"
@@ -70,6 +92,7 @@ def main():
     ap.add_argument("--per-kernel", help="directory of --pmc passes p1, p2, ...: print per-kernel medians")
     ap.add_argument("--glob", default="p*", help="--per-kernel: the pass directories' pattern")
     ap.add_argument("--stats")
+    ap.add_argument("--trace", help="kernel_trace.csv: per-launch durations (the int8 GEMM split grid / mixed)")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--valu", help="pmc_counter_collection.csv of an SQ_INSTS_VALU pass")
@@ -92,7 +115,11 @@ def main():
     if a.valu:
         for k, v in per_kernel(a.valu, "SQ_INSTS_VALU").items():
             res.setdefault(k, {})["insts_valu_per_launch"] = v
-    if a.stats:
+    if a.trace:
+        for k, (avg, n) in per_kernel_times(a.trace).items():
+            res.setdefault(k, {})["avg_ns"] = avg
+            res[k]["calls"] = n
+    elif a.stats:
         for r in csv.DictReader(open(a.stats)):
             if not ours(r["Name"]):
                 continue
