@@ -51,7 +51,7 @@ constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
 
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
-               EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE };
+               EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE, EV_LDP, EV_K };  // (pcx_runner.cpp: EV_SLOTS)
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
@@ -860,6 +860,9 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
 // consensus entry's "original" / "filled" matrices are written here too (no M_MATRICES
 // pass over the reports).
 constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread)
+// 4096 blocks, halved until each has at least WCD_MIN_ROWS rows: a C5 shard (125k rows) on ~1k
+// blocks of ~1k rows ran k_wcd 3.49 -> 3.30 ms against 4096 of 256 (1M rows: 4096 either way)
+constexpr int64_t WCD_MIN_ROWS = 768;
 
 // Blocks own a contiguous row range (a multiple of 64 rows) of a 512-event block; each
 // wave also counts the NaN / zero rescaled reports of its 128 events per row (ballots),
@@ -1579,22 +1582,42 @@ __global__ void __launch_bounds__(BT) k_scores_wcd(pcx_mat m) {
     }
 }
 
+// k_scores_grid's per-call constants, once (one wave): the loading in wcd position order
+// (ev[EV_LDP]) and K = sum_{q >= gb} c_q ld_q (ev[EV_K]).  Computed in every wave before, K's
+// dependent gathers cost ~0.1 ms per wave -- the whole pass at a C5 shard's one group per wave.
+__global__ void __launch_bounds__(WAVE) k_scores_prep(pcx_mat m) {
+    const int lane = threadIdx.x;
+    const int E = (int)m.n_events;
+    const double* LD = m.ev + (m.algorithm == 0 ? EV_LD : EV_SPARE) * E;
+    double* LDp = m.ev + EV_LDP * E;
+    const int gb = m.cov_jb * CT, ng = E - gb;
+    for (int q = lane; q < gb && q < E; q += WAVE) {
+        const int c = m.cov_perm[q];
+        LDp[q] = c >= 0 ? LD[c] : 0.0;
+    }
+    double kk = 0.0;
+    for (int q = lane; q < ng; q += WAVE) {
+        const int c = m.cov_perm[gb + q];
+        const double l = LD[c];
+        LDp[gb + q] = l;
+        kk = fma(1.0 - m.ev[EV_MU * E + c], l, kk);
+    }
+    const double K = wave_sum_d(kk);
+    if (lane == 0) m.ev[EV_K * E] = K;
+}
+
 // PCX_M_SCORES with mixed_int8 (wcd holds only the general positions): one wave per 16-row
 // group; general positions from wcd, grid positions from the int8 codes, F - mu = c + z / 2:
 //   s_i = sum_{q < gb} wcd_iq ld_q + K + (1/2) sum_{q >= gb} z_iq ld_q,  K = sum_{q >= gb} c_q ld_q
+// (ld in position order and K from k_scores_prep)
 __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
     const int lane = threadIdx.x % WAVE, wv = threadIdx.x / WAVE;
     const int64_t ld = m.wcd_ld;
     const int ncb = (int)((ld + WCD_COLS - 1) / WCD_COLS);
     const int E = (int)m.n_events;
-    const double* LD = m.ev + (m.algorithm == 0 ? EV_LD : EV_SPARE) * E;
+    const double* LDp = m.ev + EV_LDP * E;
     const int gb = m.cov_jb * CT, ng = E - gb;
-    double kk = 0.0;
-    for (int q = lane; q < ng; q += WAVE) {
-        const int c = m.cov_perm[gb + q];
-        kk = fma(1.0 - m.ev[EV_MU * E + c], LD[c], kk);
-    }
-    const double K = wave_sum_d(kk);
+    const double K = m.ev[EV_K * E];
     uint64_t kmin = ~0ull, kmax = 0;
     bool anynan = false;
     const int64_t ngrp = (m.n_rows + 15) / 16;
@@ -1603,7 +1626,7 @@ __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
 #pragma unroll
         for (int r = 0; r < 16; r++) a[r] = 0.0;
         for (int q = lane; q < gb; q += WAVE) {
-            const double l = LD[m.cov_perm[q]];
+            const double l = LDp[q];
             const double* w = m.wcd + g * 16 * ld + q;
 #pragma unroll
             for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
@@ -1612,7 +1635,7 @@ __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
 #pragma unroll
         for (int r = 0; r < 16; r++) z[r] = 0.0;
         for (int q = lane; q < ng; q += WAVE) {
-            const double l = LD[m.cov_perm[gb + q]];
+            const double l = LDp[gb + q];
             const uint32_t P = zb_packed(m)[g * m.zq + q];
 #pragma unroll
             for (int r = 0; r < 16; r++) z[r] = fma((double)zpack_get(P, r), l, z[r]);
@@ -4543,8 +4566,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             }
             if (stage == M_WCD) {
                 const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
-                hipLaunchKernelGGL(k_wcd,
-                                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(m.wcd_rows, 4096 / ncb)), ncb),
+                int64_t rb = std::max(1, 4096 / ncb);
+                while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS) rb /= 2;
+                hipLaunchKernelGGL(k_wcd, dim3((unsigned)rb, ncb),
                                    dim3(BT), 0, st, m);
                 break;
             }
@@ -4582,6 +4606,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd && m.rowpart &&
                 m.cov_perm && m.cov_mixed)
             {
+                hipLaunchKernelGGL(k_scores_prep, dim3(1), dim3(WAVE), 0, st, m);
                 hipLaunchKernelGGL(k_scores_grid, dim3(grid_rows((m.n_rows + 15) / 16, BT / WAVE)), dim3(BT), 0, st, m);
             }
             else if ((m.algorithm == 0 || m.algorithm == 2 || m.algorithm == 3) && !m.scores_given && m.wcd &&

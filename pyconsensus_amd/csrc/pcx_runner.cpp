@@ -27,6 +27,7 @@ namespace {
 constexpr int BT = 256;
 constexpr int CS = 16;  // dd slots per column in cstat
 constexpr int CM = 8;   // doubles per column in mpart / cmax
+constexpr int EV_SLOTS = 18;  // E-sized rows of ev (pcx_matrix.hip ev_slot)
 constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
@@ -246,7 +247,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->zsum, (size_t)E * 8, true},
         {(void**)&w->scal, (size_t)(world * SS * 2) * 8, true},
         {(void**)&w->spart, (size_t)(4096 * 8) * 8, true},
-        {(void**)&w->ev, (size_t)(16 * E) * 8, true},
+        {(void**)&w->ev, (size_t)(EV_SLOTS * E) * 8, true},
         {(void**)&w->pvec, (size_t)(4 * (E + 64)) * 8, true},
         {(void**)&w->rowv, (size_t)(6 * n_rows) * 8, true},
         {(void**)&w->rowstat, (size_t)(2 * n_rows) * 4, true},

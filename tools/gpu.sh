@@ -16,6 +16,7 @@
 #   dist         the 2-process tests and bench.py as the driver launches N=2 (gloo: both ranks on cuda:0)
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
+#   ab_shard=L1,L2  one C5 shard's latency of several libpcx builds, alternating twice
 #   i8bench      the int8 covariance GEMM variants at the C5 shapes (tools/i8bench, built on the CPU)
 #   i8pmc=V      SQ / LDS / cache PMC passes over the mixed-block GEMM, reference kernel and variant V
 set -o pipefail
@@ -95,6 +96,12 @@ for STEP in "$@"; do
       for i in 1 2; do for L in "${LIBS[@]}"; do
         PCX_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-c4 --c5-steps 3 --steps 3 > $O/ab.json 2> $O/ab.err || { echo "ab rc=$? ($L)"; tail -3 $O/ab.err; exit 23; }
         c5_line $O/ab.json "$L"
+      done; done ;;
+    ab_shard=*)
+      IFS=, read -ra LIBS <<< "${STEP#ab_shard=}"
+      for i in 1 2; do for L in "${LIBS[@]}"; do
+        PCX_LIB=$L timeout -k 10 200 python -u tools/c5_shard_latency.py 8 5 > $O/abs.json 2> $O/abs.err || { echo "ab_shard rc=$? ($L)"; tail -3 $O/abs.err; exit 28; }
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('%-24s shard %.2f ms; ' % (sys.argv[2], d['latency_ms']) + ' '.join('%s %.2f' % (k[2:], v) for k, v in list(d.get('stage_ms', {}).items())[:10]))" $O/abs.json "$L"
       done; done ;;
     i8bench)
       timeout -k 10 300 tools/i8bench/i8bench 5 > $O/i8bench.txt 2>&1 || { echo "i8bench rc=$?"; tail -20 $O/i8bench.txt; exit 24; }
