@@ -46,6 +46,11 @@ constexpr size_t G_PANEL = (size_t)4 * GT * 16;      // one int8 operand's 64-ro
 constexpr int G_BSWZ = 16;
 constexpr size_t G_PANEL_PK = (size_t)4 * GT * 4;    // a packed one: 4 KB
 constexpr int G_KS = PCX_GEMM_KS;  // MFMA k-steps (64 rows each) per ring stage and barrier
+// workgroups of a launch: one per (k-slice, tile) item
+__host__ __device__ inline int64_t gemm_i8_items(int tp, int tq, int lower, int kslices) {
+    return (int64_t)(lower ? tp * (tp + 1) / 2 : tp * tq) * kslices;
+}
+
 struct GemmI8 {
     const int8_t* A;
     int64_t lda;  // positions per row group
@@ -76,11 +81,22 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
     static_assert(NBUF >= 2 && NBUF * STAGE <= 163840, "int8 GEMM ring (160 KB of LDS)");
     constexpr int LOADS = 2 * KS * LPP;  // vector-memory ops per wave per stage (A chunks + packed B pieces)
     extern __shared__ __attribute__((aligned(16))) char glds[];
-    const int ntiles = g.tp * g.tq;
+    // lower: only the tp (tp + 1) / 2 tiles on and below the diagonal are items (with the upper
+    // tiles in the grid as empty workgroups, the XCDs' shares of real items differed by up to a
+    // third: C5's grid block 5.3 ms at 13 k-slices)
+    const int ntiles = g.lower ? g.tp * (g.tp + 1) / 2 : g.tp * g.tq;
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / ntiles, tl = item % ntiles;
-    const int ip = tl / g.tq, iq = tl % g.tq;
-    if (g.lower && iq > ip) return;  // above the diagonal (square tiles)
+    int ip, iq;
+    if (g.lower) {  // tl = ip (ip + 1) / 2 + iq, iq <= ip
+        ip = (int)((__builtin_sqrtf(8.0f * (float)tl + 1.0f) - 1.0f) * 0.5f);
+        while (ip * (ip + 1) / 2 > tl) ip--;
+        while ((ip + 1) * (ip + 2) / 2 <= tl) ip++;
+        iq = tl - ip * (ip + 1) / 2;
+    } else {
+        ip = tl / g.tq;
+        iq = tl % g.tq;
+    }
     const int64_t nst = g.rg / (4 * KS);  // (rg is a multiple of 4 KS)
     const int64_t per = (nst + g.kslices - 1) / g.kslices;
     const int64_t s0 = ks * per < nst ? ks * per : nst;

@@ -109,10 +109,10 @@ typedef struct {
     double*  Fg;                  /* [wcd_rows][128 cov_jb] the filled F of the general positions (or NULL) */
     uint16_t* nam;                /* [wcd_rows/16][wcd_ld] missing-report bits of 16 rows per position */
     int32_t  compact;             /* M_GEMV2 / M_OUTCOMES read Fg, zB and nam, not the reports      */
-    int32_t  tokpos;              /* local int8 position of the token column: E - 128 cov_jb          */
     /* mixed pairs: w of the general positions (< 128 cov_jb) in 8 balanced int8 digits of 7 bits,
        fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */
-    int8_t*  zD;                  /* [wcd_rows/16][8 * 128 cov_jb][16] digit s of position q at s * 128 cov_jb + q */
+    int8_t*  zD;                  /* [wcd_rows/16][zd_ld][16] digit s of position q at s * 128 cov_jb + q */
+    int64_t* dtok;                /* [PCX_NDIG][128 cov_jb] sum of each digit over this rank's rows (k_digits) */
     double*  dscale;              /* [wcd_ld] 2^-e per general position                               */
     int32_t* Pgg;                 /* [ks_gg][zq][zq] int32 zA^T zB per k-slice (lower part)           */
     int32_t* Pmx;                 /* [ks_mx][zq][PCX_NDIG * 128 cov_jb] int32 zA^T zD per k-slice            */
@@ -139,6 +139,7 @@ typedef struct {
 // 256-position tile, so the last p-tile's loads stay inside the row group (NDIG * 128 * odd
 // general tiles need not be a multiple of 256); the pad positions only feed discarded rows
 __host__ __device__ inline int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }
+
 
 namespace pcx {
 

@@ -1131,28 +1131,13 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
             }
 }
 
-// the token column of the int8 operands: zA = tok (<= 63), zB = 1 on live rows (packed)
-__global__ void __launch_bounds__(BT) k_tokcol(pcx_mat m) {
-    const int64_t grp = blockIdx.x * (int64_t)BT + threadIdx.x;
-    if (grp >= m.wcd_rows / 16) return;
-    uint32_t ta[4] = {0, 0, 0, 0}, tb = 0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const int64_t i = grp * 16 + r;
-        if (i < m.n_rows) {
-            ta[r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)m.tok[i] << (8 * (r & 3));
-            tb |= zpack_bit(r);
-        }
-    }
-    *(uint4*)(m.zA + (grp * m.zq + m.tokpos) * 16) = uint4{ta[0], ta[1], ta[2], ta[3]};
-    zb_packed(m)[grp * m.zq + m.tokpos] = tb;
-}
-
 // tok * w of the general positions q < gb (the exact product, as a double-double) as PCX_NDIG
 // balanced base-254 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 254 v (the double-double
 // product, its rounding below 2^-95), d = rint(t_hi), v = t - d -- |d| <= 127, the widest balanced
 // digit int8 holds.  PCX_NDIG digits leave a residue <= 254^-NDIG / 2 of 2^e (6: 2^-48.9 of the
-// column's bound on |tok w|, 3.7e-15 relative)
+// column's bound on |tok w|, 3.7e-15 relative).  Each chunk of rows (blockIdx.y) also adds the
+// sum of every digit over its rows to dtok (int64 atomics: exact, order-free): S_q = sum tok w_q
+// from the same digits (k_cov_tokrow), so neither int8 product carries a token column.
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
@@ -1162,6 +1147,9 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
     const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
     const int64_t ldd = zd_ld(gb);
+    int32_t dsum[PCX_NDIG];  // |d| <= 127: int32-exact for any chunk under 16M rows
+#pragma unroll
+    for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
     for (int64_t grp = g0; grp < g1; grp++) {
         uint32_t d[PCX_NDIG][4];
 #pragma unroll
@@ -1181,12 +1169,16 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
                 const double bv = hi - e;
                 lo = (e - (hi - bv)) + (l - bv);
                 d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
+                dsum[k] += (int)di;
             }
         }
 #pragma unroll
         for (int k = 0; k < PCX_NDIG; k++)
             *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
     }
+#pragma unroll
+    for (int k = 0; k < PCX_NDIG; k++)
+        if (dsum[k]) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)dsum[k]);
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -1275,11 +1267,15 @@ __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t 
     return dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q])));  // 2^e
 }
 
-// the token column's S_q = sum tok w_q of every general position (shared by all grid rows)
+// S_q = sum tok w_q of every general position (shared by all grid rows): k_digits' digit sums
+// (exact), recombined like mixed_comb
 __global__ void __launch_bounds__(BT) k_cov_tokrow(pcx_mat m, double* S) {
     const int64_t q = blockIdx.x * (int64_t)BT + threadIdx.x;
-    if (q >= (int64_t)m.cov_jb * CT) return;
-    st_dd(S + 2 * q, mixed_comb(m, m.tokpos, q));
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    if (q >= gb) return;
+    dd a{(double)m.dtok[(PCX_NDIG - 1) * gb + q], 0.0};
+    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)m.dtok[d * gb + q], 0.0});
+    st_dd(S + 2 * q, dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q]))));  // 2^e
 }
 
 // entry (p, q), q <= p, of the position-space lower triangle of this rank's unnormalised C
@@ -4512,10 +4508,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int nb = (int)(m.wcd_ld / CT);
             if (m.cov_jb >= nb && m.zq == 0) break;  // no grid events
             const int gb = m.cov_jb * CT;
-            const int np = (int)(m.n_events - gb) + 1;  // grid positions + the token column
+            const int np = (int)(m.n_events - gb);  // grid positions
             if (!m.zA || !m.zB || !m.zsum || !m.Pgg || m.cov_jb < 0 || m.cov_jb > nb || m.zq < np || m.ks_gg < 1 ||
-                (m.cov_mixed && m.ks_mx < 1) ||
-                m.zq % GT || m.tokpos != np - 1 || m.wcd_rows % (64 * G_KS) || (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale))) {
+                (m.cov_mixed && m.ks_mx < 1) || m.zq % GT || m.wcd_rows % (64 * G_KS) ||
+                (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale || !m.dtok))) {
                 err = "M_COV_I8: int8 operands missing or plan inconsistent";
                 return hipErrorInvalidValue;
             }
@@ -4527,18 +4523,20 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             });
             if (g_err != hipSuccess) return g_err;
             const int64_t rg = m.wcd_rows / 16;
-            // both products take z (zB, 2-bit packed) as the B operand
-            hipLaunchKernelGGL(k_tokcol, dim3((unsigned)((rg + BT - 1) / BT)), dim3(BT), 0, st, m);
+            // both products take z (zB, 2-bit packed) as the B operand; the token sums they once
+            // carried as an extra position come from k_wcd (Z_j) and k_digits (S_q): a 3,073rd
+            // position cost a 13th tile row and column (C5: grid 4.4 ms, mixed 15.3 ms before)
             {  // grid x grid (lower tiles): P = (tok z)^T z, |tok z z| <= 252 per row
                 GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg, 0};
                 g.tp = g.tq = (np + GT - 1) / GT;
-                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(16 * 64),
                                    GEMM_I8_LDS, st, g);
             }
             if (m.cov_mixed) {
                 // general digits x grid: digits of tok w (A, PCX_NDIG per general position) times z (B);
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
+                if (hipMemsetAsync(m.dtok, 0, (size_t)PCX_NDIG * gb * 8, st) != hipSuccess) return hipGetLastError();
                 hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
                 GemmI8 g{m.zD, zd_ld(gb), m.zB, m.zq, m.Pmx, (int64_t)PCX_NDIG * gb, m.zq * PCX_NDIG * gb, PCX_NDIG * gb, np,
                          0, 0, 0, m.ks_mx, rg, 1};
@@ -4548,7 +4546,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                     err = "M_COV_I8: operand row groups narrower than the tiles";
                     return hipErrorInvalidValue;
                 }
-                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)(g.tp * g.tq * g.kslices)), dim3(16 * 64),
+                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(16 * 64),
                                    GEMM_I8_LDS, st, g);
             }
             break;

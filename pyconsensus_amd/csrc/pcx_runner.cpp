@@ -75,7 +75,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx, clw, fg, nam;
+    } pgg, zd, pmx, clw, fg, nam, dtok;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -89,7 +89,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -872,10 +872,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 const int64_t nb = w->wcd_ld / COV_TILE;
                 const int64_t jb = (n_general + COV_TILE - 1) / COV_TILE, gb = jb * COV_TILE;
                 m.cov_jb = (int32_t)jb;
-                const int64_t np = gb < E ? E - gb + 1 : 0;  // grid positions + the token column
+                const int64_t np = gb < E ? E - gb : 0;  // grid positions
                 m.zq = (np + 255) / 256 * 256;
-                m.tokpos = (int32_t)(np - 1);
-                r->grid_events = (int32_t)(np > 0 ? E - gb : 0);  // grid events past the general tiles
+                r->grid_events = (int32_t)np;  // grid events past the general tiles
                 // k-slices of the int8 products: int32-exact row ranges (|tok z z| <= 252,
                 // |z d| <= 254 per row) and at least two WGs per CU
                 const int64_t nst = w->wcd_rows / 64, tp = (np + 255) / 256, tq = (PCX_NDIG * gb + 255) / 256;
@@ -913,11 +912,13 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.Pgg = (int32_t*)w->pgg.p;
                 // mixed pairs on int8 digits when the bounds are finite and the memory is there
                 m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * zd_ld(gb))) &&
-                                      w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4))
+                                      w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4)) &&
+                                      w->grow(w->dtok, (size_t)(PCX_NDIG * gb * 8))
                                   ? 1
                                   : 0;
                 r->mixed_int8 = m.cov_mixed;
                 m.zD = (int8_t*)w->zd.p;
+                m.dtok = (int64_t*)w->dtok.p;
                 // mixed: the later full passes (M_GEMV2, M_OUTCOMES) read F compactly -- the general
                 // positions' filled values (Fg, written by k_wcd), the grid ones from the 2-bit codes
                 // and the missing bits (nam) -- instead of the reports (a quarter of the bytes at C5)

@@ -18,6 +18,7 @@
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
 #   ab_shard=L1,L2  one C5 shard's latency of several libpcx builds, alternating twice
 #   i8bench      the int8 covariance GEMM variants at the C5 shapes (tools/i8bench, built on the CPU)
+#   i8ks=S:K,..  the product int8 GEMM on shape S (mixed | grid) at each k-slice count K
 #   i8pmc=V      SQ / LDS / cache PMC passes over the mixed-block GEMM, reference kernel and variant V
 set -o pipefail
 export TMPDIR=/tmp
@@ -106,6 +107,10 @@ for STEP in "$@"; do
     i8bench)
       timeout -k 10 300 tools/i8bench/i8bench 5 > $O/i8bench.txt 2>&1 || { echo "i8bench rc=$?"; tail -20 $O/i8bench.txt; exit 24; }
       cat $O/i8bench.txt ;;
+    i8ks=*)  # i8ks=SHAPE:K1,K2,...  the product kernel at each k-slice count (SHAPE: mixed | grid)
+      A=${STEP#i8ks=}
+      timeout -k 10 300 tools/i8bench/i8bench 3 1000064 product "${A%%:*}" "${A#*:}" > $O/i8ks_${A%%:*}.txt 2>&1 || { echo "i8ks rc=$?"; tail -20 $O/i8ks_${A%%:*}.txt; exit 29; }
+      grep -v "small check" $O/i8ks_${A%%:*}.txt ;;
     i8pmc=*)
       V=${STEP#i8pmc=}
       i=0

@@ -2,9 +2,9 @@
 // at the C5 shapes (1M rows: 62,504 groups of 16), every configuration checked against the
 // product's (k_gemm_i8<16, GEMM_I8_NBUF>) as the int64 sum of its k-slice slabs, and all of them
 // against a CPU reference on a small case.
-//   mixed: A = PCX_NDIG int8 digits x 1,024 general positions, B = z of 3,072 grid events +
-//          the token column (packed 2 bits, ldb 3,328), stored transposed;
-//   grid:  A = tok z (int8, lda 3,328), B = z packed, lower tiles.
+//   mixed: A = PCX_NDIG int8 digits x 1,024 general positions, B = z of 3,072 grid events
+//          (packed 2 bits), stored transposed;
+//   grid:  A = tok z (int8, 3,072 positions), B = z packed, lower tiles.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/i8bench/i8bench.hip -o tools/i8bench/i8bench
 // usage: i8bench [reps=5] [rows=1000064] [variant substring] [shape substring]
 #include <hip/hip_runtime.h>
@@ -103,6 +103,14 @@ int main(int argc, char** argv) {
     const int64_t rows = argc > 2 ? atoll(argv[2]) : 1000064;
     const char* vsel = argc > 3 ? argv[3] : "";
     const char* ssel = argc > 4 ? argv[4] : "";
+    // optional: comma-separated k-slice counts to sweep (product configuration only)
+    std::vector<int> ks_list;
+    if (argc > 5)
+        for (const char* p = argv[5]; *p;) {
+            ks_list.push_back(atoi(p));
+            while (*p && *p != ',') p++;
+            if (*p == ',') p++;
+        }
     const int64_t rg = rows / 16;
     int ncu = 256;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -151,7 +159,7 @@ int main(int argc, char** argv) {
             g.tp = (np + GT - 1) / GT;
             g.tq = (nq + GT - 1) / GT;
             CK(hipMemset(dP, 0, (size_t)4 * nq * np * 4));
-            hipLaunchKernelGGL(v.f, dim3(g.tp * g.tq * g.kslices), dim3(v.threads), v.lds, 0, g);
+            hipLaunchKernelGGL(v.f, dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(v.threads), v.lds, 0, g);
             CK(hipGetLastError());
             hipLaunchKernelGGL(k_slabsum, dim3(256), dim3(256), 0, 0, dP, g.kslices, g.slab, (int64_t)nq * np, dS);
             std::vector<long long> got((size_t)nq * np);
@@ -168,8 +176,8 @@ int main(int argc, char** argv) {
     }
 
     const Shape shapes[] = {
-        {"mixed", PCX_NDIG * 1024, 3328, PCX_NDIG * 1024, 3073, 0, 1},
-        {"grid", 3328, 3328, 3073, 3073, 1, 0},
+        {"mixed", PCX_NDIG * 1024, 3072, PCX_NDIG * 1024, 3072, 0, 1},
+        {"grid", 3072, 3072, 3072, 3072, 1, 0},
     };
     for (const Shape& sh : shapes) {
         if (!strstr(sh.name, ssel)) continue;
@@ -188,10 +196,12 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&dSum, outn * 8));
         CK(hipMalloc(&dBad, 8));
         const double ops = 2.0 * (double)rg * 16 * sh.np * (double)sh.nq * (sh.lower ? 0.5 : 1.0);
-        for (size_t vi = 0; vi < vs.size(); vi++) {
+        const size_t nrun = ks_list.empty() ? vs.size() : 1 + ks_list.size();
+        for (size_t ri = 0; ri < nrun; ri++) {
+            const size_t vi = ks_list.empty() ? ri : 0;
             const Variant& v = vs[vi];
-            if (vi > 0 && !strstr(v.name, vsel)) continue;
-            const int ks = ks_for(tiles, rg / (4 * PCX_GEMM_KS), ncu);
+            if (ri > 0 && ks_list.empty() && !strstr(v.name, vsel)) continue;
+            const int ks = (ri > 0 && !ks_list.empty()) ? ks_list[ri - 1] : ks_for(tiles, rg / (4 * PCX_GEMM_KS), ncu);
             int32_t* dP;
             CK(hipMalloc(&dP, (size_t)ks * outn * 4));
             CK(hipMemset(dP, 0, (size_t)ks * outn * 4));
@@ -200,13 +210,13 @@ int main(int argc, char** argv) {
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0));
             CK(hipEventCreate(&e1));
-            hipLaunchKernelGGL(v.f, dim3(tp * tq * ks), dim3(v.threads), v.lds, 0, g);  // warm
+            hipLaunchKernelGGL(v.f, dim3((unsigned)gemm_i8_items(tp, tq, sh.lower, ks)), dim3(v.threads), v.lds, 0, g);  // warm
             CK(hipGetLastError());
             CK(hipDeviceSynchronize());
             std::vector<float> ms;
             for (int r = 0; r < reps; r++) {
                 CK(hipEventRecord(e0, 0));
-                hipLaunchKernelGGL(v.f, dim3(tp * tq * ks), dim3(v.threads), v.lds, 0, g);
+                hipLaunchKernelGGL(v.f, dim3((unsigned)gemm_i8_items(tp, tq, sh.lower, ks)), dim3(v.threads), v.lds, 0, g);
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
                 float t = 0;
@@ -214,16 +224,16 @@ int main(int argc, char** argv) {
                 ms.push_back(t);
             }
             std::sort(ms.begin(), ms.end());
-            hipLaunchKernelGGL(k_slabsum, dim3(4096), dim3(256), 0, 0, dP, ks, outn, outn, vi == 0 ? dRef : dSum);
+            hipLaunchKernelGGL(k_slabsum, dim3(4096), dim3(256), 0, 0, dP, ks, outn, outn, ri == 0 ? dRef : dSum);
             unsigned long long bad = 0;
-            if (vi > 0) {
+            if (ri > 0) {
                 CK(hipMemset(dBad, 0, 8));
                 hipLaunchKernelGGL(k_cmp, dim3(4096), dim3(256), 0, 0, dRef, dSum, outn, dBad);
                 CK(hipMemcpy(&bad, dBad, 8, hipMemcpyDeviceToHost));
             }
             CK(hipDeviceSynchronize());
             printf("%-6s %-24s ks %2d  %8.3f ms (min %8.3f)  %7.1f TOP/s  %s\n", sh.name, v.name, ks, ms[ms.size() / 2],
-                   ms[0], ops / (ms[ms.size() / 2] * 1e-3) / 1e12, vi == 0 ? "reference" : (bad ? "MISMATCH" : "equal"));
+                   ms[0], ops / (ms[ms.size() / 2] * 1e-3) / 1e12, ri == 0 ? "reference" : (bad ? "MISMATCH" : "equal"));
             fflush(stdout);
             CK(hipFree(dP));
             if (bad) return 3;
