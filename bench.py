@@ -141,10 +141,10 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     cov_ms = prof.get("M_COV", float("nan"))
     i8_ms = prof.get("M_COV_I8", float("nan"))
     # unique (j, k<=j) covariance pairs: those with a general event on fp64 MFMA (k_syrk),
-    # the grid-grid pairs on int8 MFMA (k_syrk_i8); one multiply-add per pair per row
-    # with mixed_int8 the general x grid pairs run on int8 too, as D digit slices of w (and
-    # the token column; D = pcx_mixed_digits(), a build parameter): int8 work = grid pairs +
-    # D x general x (grid + 1) per row
+    # the grid-grid pairs on int8 MFMA (k_gemm_i8); one multiply-add per pair per row
+    # with mixed_int8 the general x grid pairs run on int8 too, as D digit slices of tok w
+    # (D = pcx_mixed_digits(), a build parameter): int8 work = grid pairs + D x general x grid
+    # per row (the digit pass k_digits is in the stage time, not in the count)
     from pyconsensus_amd import _lib
 
     ng = meta["grid_events"]
@@ -152,7 +152,7 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     mixed = meta.get("mixed_int8", 0)
     digits = int(_lib.lib().pcx_mixed_digits())
     fp_pairs = G * (G + 1) // 2 + (0 if mixed else G * ng)
-    i8_pairs = ng * (ng + 1) // 2 + (digits * G * (ng + 1) if mixed else 0)
+    i8_pairs = ng * (ng + 1) // 2 + (digits * G * ng if mixed else 0)
     cov_flops_rank = 2.0 * cnt * fp_pairs
     i8_ops_rank = 2.0 * cnt * i8_pairs
     tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms and fp_pairs else None
@@ -169,10 +169,11 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
                              "flops_per_launch": cov_flops_rank, "traffic": load_traffic("k_syrk"),
                              "pairs": ("fp64: pairs inside the general tiles (%d positions; %d grid events on int8; mixed pairs "
                                        "on int8 slices: %s)" % (G, ng, bool(mixed)))},
-            "roofline_cov_i8": {"bound": "mfma", "kernel": "k_syrk_i8", "achieved": tops, "peak": I8_MFMA_PEAK_TOPS,
+            "roofline_cov_i8": {"bound": "mfma", "kernel": "k_gemm_i8 (grid + mixed launches) + k_digits",
+                                "achieved": tops, "peak": I8_MFMA_PEAK_TOPS,
                                 "unit": "TOP/s", "frac": (tops / I8_MFMA_PEAK_TOPS) if tops else None,
                                 "ops_per_launch": i8_ops_rank, "mixed_digits": digits,
-                                "traffic": load_traffic("k_syrk_i8")},
+                                "traffic": _sum_traffic(("k_gemm_i8_grid", "k_gemm_i8_mixed", "k_digits"))},
             "grid_events": ng, "mixed_int8": mixed,
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}
@@ -250,9 +251,14 @@ def bench_c4(dev, steps=3, oracle=True):
     return out
 
 
+def _sum_traffic(kernels, key="bytes_per_launch"):
+    vals = [load_traffic(k, key) for k in kernels]
+    return None if any(v is None for v in vals) else sum(vals)
+
+
 def load_traffic(kernel="batched_round_kernel", key="bytes_per_launch"):
     """Per-launch PMC figure of `kernel` (HBM bytes, VALU instructions) from the committed
-    rocprofv3 passes (profiles/pmc_traffic.json, tools/gpu_profile.sh), or None."""
+    rocprofv3 passes (profiles/pmc_traffic.json, `tools/gpu.sh TAG profile`), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
