@@ -683,7 +683,9 @@ __device__ PCX_OUTLINE void square_scaled(double* M, int ES, int E) {
         if (two) {
             const double a1 = (ok && 16 + ml < E) ? M[sym_at<PK>(16 + ml, mm, ES)] : 0.0;
             const double b1 = a1;
-            t01 = mfma_f64(a0, b1, t01);
+            // PK: the upper tile t01 = t10^T bit for bit (the same products in the same m
+            // order), neither stored nor needed for the maximum (C3: 1.826 -> 1.786 ms)
+            if (!PK) t01 = mfma_f64(a0, b1, t01);
             t10 = mfma_f64(a1, b0, t10);
             t11 = mfma_f64(a1, b1, t11);
         }
@@ -693,7 +695,7 @@ __device__ PCX_OUTLINE void square_scaled(double* M, int ES, int E) {
     for (int r = 0; r < 4; r++) {
         const int j0 = kq + 4 * r, j1 = 16 + kq + 4 * r, k0 = ml, k1 = 16 + ml;
         if (j0 < E && k0 < E) mx = fmax(mx, fabs(t00[r]));
-        if (j0 < E && k1 < E) mx = fmax(mx, fabs(t01[r]));
+        if (!PK && j0 < E && k1 < E) mx = fmax(mx, fabs(t01[r]));
         if (j1 < E && k0 < E) mx = fmax(mx, fabs(t10[r]));
         if (j1 < E && k1 < E) mx = fmax(mx, fabs(t11[r]));
     }
