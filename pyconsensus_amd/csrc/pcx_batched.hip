@@ -122,6 +122,26 @@ __device__ __forceinline__ double tree_sum(double v) {
     return (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
 }
 
+// inclusive prefix sum over the lanes in lane order (row_shr DPP inside each 16-lane row, then the
+// rows' totals by readlane): a fixed tree order, deterministic, within ~6 u of the exact sums
+template <int D>
+__device__ __forceinline__ double shr_lane(double v) {  // lane l <- lane l - D of its row, else +0.0
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x110 + D, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x110 + D, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_scan_d(double v) {
+    v = v + shr_lane<1>(v);
+    v = v + shr_lane<2>(v);
+    v = v + shr_lane<4>(v);
+    v = v + shr_lane<8>(v);
+    const double r0 = lane_value(v, 15), r1 = lane_value(v, 31), r2 = lane_value(v, 47);
+    const int row = threadIdx.x >> 4;
+    const double r01 = r0 + r1;
+    return row == 0 ? v : v + (row == 1 ? r0 : row == 2 ? r01 : r01 + r2);
+}
+
 __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, xor_lane<1>(v));
     v = fmax(v, xor_lane<2>(v));
@@ -458,7 +478,32 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     double v[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) v[q] = ow[q];
+    bool walked = false;
     if (!ballot(sel && !(w >= 0.0))) {
+        // non-negative weights.  First the prefix sums of the sorted weights in a tree order
+        // (slot l on lane l; slots past n hold +0.0): they differ from the walk's sequential
+        // sums by < (n + 6) u W, so when the tree sum crossing mid lies more than 2^-44 W above
+        // it and its predecessor more than 2^-44 W + DBL_EPS below, the sequential walk crosses
+        // at the same slot and the half test below fails -- decided without the serial chain.
+        // Otherwise (a near tie) the walk runs.
+        const double ps = wave_scan_d(ow[l]);  // (ow holds med_ow(NR) >= 64 slots)
+        const double W = lane_value(ps, 63);
+        const double margin = 0x1p-44 * W;
+        const uint64_t above = ballot(ps > mid);
+        if (above) {
+            const int j = __builtin_ctzll(above);
+            const double sj = bcast(ps, j), sp = j > 0 ? bcast(ps, j - 1) : 0.0;
+            if (j < n && sj - mid > margin && (j == 0 || mid - sp > margin + DBL_EPS)) {
+                k = j + 1;
+                before = j == 0 ? 0.0 : sp;  // j = 0: the walk's c_0 - w_0 = 0 exactly
+                walked = true;
+            }
+        } else if (mid - W > margin) {
+            walked = true;  // no crossing: k = 0
+        }
+    }
+    if (walked) {
+    } else if (!ballot(sel && !(w >= 0.0))) {
         // non-negative weights: the running sums only grow (slots past n add +0.0), so a
         // group holds the first cum > mid iff its last sum exceeds mid
         for (int t = 0; t < n; t += 8) {
