@@ -397,21 +397,46 @@ __device__ __forceinline__ uint32_t key_hi32(double x) {
 
 // use_rank (wave-uniform): `rank` is already each selected lane's count of selected keys below
 // its own (the rank loop is skipped); rank_out: when the rank loop runs, each lane's count
+// wlazy: Wtot is not given; weightedstats' total (the selected weights summed in row order, an
+// absent row adding +0.0) is formed only where a decision needs it.  A tree-order total Wt differs
+// from it by < (N + 6) u Wt, so every comparison against mid = Wt / 2 that clears the slack
+// 2^-45 Wt is the one the exact total would make.
 template <int NR>
 __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, double Wtot, int N, double* scr,
                                                     long long* prof = nullptr, bool use_rank = false, int rank = 0,
-                                                    int* rank_out = nullptr) {
+                                                    int* rank_out = nullptr, bool wlazy = false) {
     const int l = lane_id();
     double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
     int* cnt = reinterpret_cast<int*>(scr + 3 * NR + med_ow(NR));
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    const double mid = 0.5 * Wtot;
+    double slack = 0.0;
+    // the exact total, through sx (free before the rank loop and after the scatter)
+    auto exact_total = [&]() {
+        wsync();
+        if (l < N) sx[l] = sel ? w : 0.0;
+        wsync();
+        double t = 0.0;
+#pragma unroll 8
+        for (int i = 0; i < N; i++) t = t + sx[i];
+        wsync();
+        slack = 0.0;
+        return t;
+    };
+    if (wlazy) {
+        Wtot = tree_sum(sel ? w : 0.0);
+        slack = 0x1p-45 * Wtot;
+        if (!(slack < __builtin_inf()) || ballot(sel && fabs(w - 0.5 * Wtot) <= slack)) Wtot = exact_total();
+    }
+    double mid = 0.5 * Wtot;
     if (ballot(sel && w > mid)) {  // weightedstats: a weight above half the total wins outright
         const double mx = wave_max(sel ? w : -__builtin_inf());
         return bcast(x, __builtin_ctzll(ballot(sel && w == mx)));  // first maximal weight
     }
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
-    if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) return wave_wmedian(x, w, sel, Wtot, sx, sw);
+    if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) {
+        if (slack != 0.0) Wtot = exact_total();
+        return wave_wmedian(x, w, sel, Wtot, sx, sw);
+    }
     const int n = popc(ballot(sel));
     // rank by the top 32 bits of x's order-preserving key (one 32-bit compare per row,
     // four keys per LDS read; unselected rows hold the largest key, below no selected
@@ -488,7 +513,7 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
         // Otherwise (a near tie) the walk runs.
         const double ps = wave_scan_d(ow[l]);  // (ow holds med_ow(NR) >= 64 slots)
         const double W = lane_value(ps, 63);
-        const double margin = 0x1p-44 * W;
+        const double margin = 0x1p-44 * W + slack;
         const uint64_t above = ballot(ps > mid);
         if (above) {
             const int j = __builtin_ctzll(above);
@@ -501,6 +526,10 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
         } else if (mid - W > margin) {
             walked = true;  // no crossing: k = 0
         }
+    }
+    if (!walked && slack != 0.0) {  // a near tie: the walk needs the exact total
+        Wtot = exact_total();
+        mid = 0.5 * Wtot;
     }
     if (walked) {
     } else if (!ballot(sel && !(w >= 0.0))) {
@@ -1396,13 +1425,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             const double tot = S.mu[j];
             x = row ? S.F[l * ES + j] : 0.0;
             w = present ? S.rep[l] / tot : 0.0;
-            double* ws = S.M;  // median scratch, dead until the covariance
-            wsync();
-            ws[l] = w;
-            wsync();
-            Wsum = 0.0;
-#pragma unroll 8
-            for (int i = 0; i < N; i++) Wsum = Wsum + ws[i];
+            Wsum = 0.0;  // (formed inside the median only where a decision needs it: wlazy)
         };
         auto finish = [&](int j, double g) {
             if (a.int_dtype) g = trunc(g);
@@ -1419,7 +1442,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             pair_of(j, x0, w0, p0, W0);
             int rk = -1;
             finish(j, wave_wmedian_rank<(NT > 0 ? NT : 64)>(x0, w0, p0, W0, N, S.M, a.stamps ? mprof : nullptr,
-                                                            false, 0, &rk));
+                                                            false, 0, &rk, true));
             if (ballot(rk >= 0)) {  // the rank loop ran (no dominant weight, no NaN)
                 rk_valid |= 1u << j;
                 const int sh = 8 * (j & 3);
