@@ -112,6 +112,10 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
     std::mutex retry_mu;
     std::vector<int64_t> retry;
     std::atomic<int> alive{K};
+    // test hook: PCX_FAULT_ENOMEM_WORKER=k makes worker k's first round report PCX_ENOMEM
+    // without running, exercising the hand-back below (tests/test_rounds_gpu.py)
+    const char* fault_env = getenv("PCX_FAULT_ENOMEM_WORKER");
+    const int fault_k = fault_env ? atoi(fault_env) : -1;
     auto one = [&](pcx_ctx* w, int64_t b, std::string& werr) -> int {
             pcx_problem p{};
             p.n_rows = N;
@@ -169,10 +173,12 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
     };
     auto worker = [&](int k) {
         pcx_ctx* w = c->pool[k];
+        bool fault = k == fault_k;
         for (;;) {
             const int64_t b = next.fetch_add(1);
             if (b >= B || failed.load()) return;
-            const int rc = one(w, b, errs[k]);
+            const int rc = fault ? PCX_ENOMEM : one(w, b, errs[k]);
+            fault = false;
             if (rc == PCX_ENOMEM && alive.fetch_sub(1) > 1) {
                 workspace_free(w);
                 std::lock_guard<std::mutex> lk(retry_mu);
