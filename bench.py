@@ -223,14 +223,18 @@ def bench_c4(dev, steps=3, oracle=True):
     args = (Rd, torch.from_numpy(rep).to(dev), torch.from_numpy(sc.astype(np.uint8)).to(dev),
             torch.from_numpy(lo).to(dev), torch.from_numpy(hi).to(dev))
     consensus_matrix(*args, device=dev, matrices=True)  # warm (workspace)
-    times = []
+    times, prof = [], {}
     for _ in range(steps):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        ev, ag, meta = consensus_matrix(*args, device=dev, matrices=True)
+        p1 = {}
+        ev, ag, meta = consensus_matrix(*args, device=dev, matrices=True, profile=p1)
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
+        for k, v in p1.items():
+            prof[k] = prof.get(k, 0.0) + v / steps
     out = {"metric": "100k x 1k consensus latency", "latency_ms": 1e3 * sorted(times)[len(times) // 2],
+           "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
            "h2d_ms": 1e3 * h2d, "h2d_gbs": R.nbytes / h2d / 1e9, "branch": meta["branch"],
            "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"],
            "data": "synthetic (SURVEY.md 8(d), seed 2, integer reputations U[1,99])"}

@@ -441,6 +441,19 @@ struct XW {
     double x, w;
 };
 
+// min / max of two non-NaN doubles (fmin / fmax canonicalise both operands first: three more
+// fp64 VALU ops per element in k_colstats)
+__device__ __forceinline__ double min_nn(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double max_nn(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
 // min/max present value; writes the scaled columns (column-major) into T.  A lane owns a column
 // and walks the rows, so its T column is one contiguous run; the lanes' values go through a
@@ -495,7 +508,11 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     };
     acc2 sr, srx, sx;
     constexpr bool eqw = EQW;
-    double cnt = 0.0, nz = 0.0, mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
+    // counts in 32-bit integers and the first present row as an offset (fp64 VALU ops issue at half
+    // the rate of 32-bit ones; this pass is VALU-bound)
+    uint32_t icnt = 0, inz = 0;
+    int32_t fro = -1;
+    double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
     bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
     // EQW: every weight is 1 / N (k_rep_local), so the largest one is the first present row's:
     // no weight loads, and the argmax is that row's index, converted once at the end
@@ -510,12 +527,12 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
                 lt[lane * CS_TLD + (i & 15)] = (isn || z) ? __builtin_nan("") : x;
                 if ((i & 15) == 15) flush(i - 15, 16);
             }
-    nz += z ? 1.0 : 0.0;
+            inz += z ? 1u : 0u;
             if (isn || z) return;
-            cnt += 1.0;
+            icnt++;
             if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
                 sx.add(x);
-                first_row = first_row < 0 ? i : first_row;
+                fro = fro < 0 ? (int32_t)(i - r0) : fro;
             } else {
                 const double r = v.w;
                 sr.add(r);
@@ -525,12 +542,14 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
                     arg = (double)(m.row_offset + i);
                 }
             }
-            mn_x = fmin(mn_x, x);
-            mx_x = fmax(mx_x, x);
-            offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);
+            mn_x = min_nn(mn_x, x);
+            mx_x = max_nn(mx_x, x);
+            if (!p.scaled) offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);  // (read for unscaled events only)
         });
     if (any_t && r1 > r0 && (r1 & 15)) flush(r1 & ~(int64_t)15, (int)(r1 & 15));  // the last, partial group
     if (!live) return;
+    const double cnt = (double)icnt, nz = (double)inz;
+    if (eqw && fro >= 0) first_row = r0 + fro;
     if (eqw && first_row >= 0) {
         mx = 1.0 / (double)m.n_total;  // = m.rep[i] (k_rep_local)
         arg = (double)(m.row_offset + first_row);
