@@ -34,8 +34,8 @@ run_tests() {  # $1: log name, rest: pytest args
   tail -1 $O/$log
 }
 
-c5_line() {  # $1 json, $2 label
-  python3 -c "import json,sys; c=json.load(open(sys.argv[1]))['c5']; s=c['stage_ms']; print('%-24s C5 %.1f ms (mean %.1f) ' % (sys.argv[2], c['latency_ms'], c.get('latency_ms_mean', 0)) + ' '.join('%s %.1f' % (k[2:], v) for k, v in list(s.items())[:10]))" "$1" "$2"
+c5_line() {  # $1 json (the last line starting with '{': gloo prints its connection notes to stdout), $2 label
+  python3 -c "import json,sys; c=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['c5']; s=c['stage_ms']; print('%-24s C5 %.1f ms (mean %.1f) ' % (sys.argv[2], c['latency_ms'], c.get('latency_ms_mean', 0)) + ' '.join('%s %.1f' % (k[2:], v) for k, v in list(s.items())[:10]))" "$1" "$2"
 }
 
 for STEP in "$@"; do
