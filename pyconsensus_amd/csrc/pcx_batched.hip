@@ -446,8 +446,6 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     const uint32_t key = sel ? key_hi32(x) : 0xffffffffu;
     wsync();
     if (l < NR) {
-        sx[l] = sel ? x : __builtin_inf();
-        sw[l] = sel ? w : __builtin_inf();
         cnt[l] = 0;
         kx[l] = key;
     }
@@ -472,18 +470,14 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     const bool tied = sel && cnt[r] > 1;
     uint64_t T = ballot(tied);
     int sub = 0;
-    if (T) {
-        int* rk = reinterpret_cast<int*>(kx);  // the keys are dead
-        rk[l] = r;
-        wsync();
-        while (T) {
-            const int m = __builtin_ctzll(T);
-            T &= T - 1;
-            const double xm = sx[m], wm = sw[m];
-            const bool before = (xm < x) | ((xm == x) & ((wm < w) | ((wm == w) & (m < l))));
-            sub += (tied && rk[m] == r && before) ? 1 : 0;
-        }
-        wsync();
+    // (the tied rows' x, w and rank read from their lanes' registers: no LDS round trip per row)
+    while (T) {
+        const int m = __builtin_ctzll(T);
+        T &= T - 1;
+        const double xm = bcast(x, m), wm = bcast(w, m);
+        const int rm = __builtin_amdgcn_readlane(r, m);
+        const bool before = (xm < x) | ((xm == x) & ((wm < w) | ((wm == w) & (m < l))));
+        sub += (tied && rm == r && before) ? 1 : 0;
     }
     if (sel) {
         ox[r + sub] = x;
