@@ -1327,12 +1327,15 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
 
     STAMP(1);
     // ---- a2: rescale (:266-269) + NA masks (:278) -------------------------
+    // (the next column's value is loaded before this column's stores: a load after a store to
+    // the same LDS array would otherwise wait for it)
+    double xnext = row ? S.F[l * ES] : 0.0;
     for (int j = 0; j < E; j++) {
         const bool sc = (scaled_mask >> j) & 1;
         const double lo = bcast(loj, j), hi = bcast(hij, j);
-        double x = 0.0;
+        double x = xnext;
+        if (j + 1 < E) xnext = row ? S.F[l * ES + j + 1] : 0.0;
         if (row) {
-            x = S.F[l * ES + j];
             if (sc) {
                 x = (x - lo) / (hi - lo);
                 if (a.int_dtype) x = trunc(x);
@@ -1447,11 +1450,18 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     }
     wsync();
     STAMP(14);
-    // fill (row phase)
+    // fill (row phase; the next column's masks and fill loaded ahead of this column's store)
     if (row) {
+        uint64_t mn = S.nanm[0] | S.zerm[0];
+        double gn = S.guess[0];
         for (int j = 0; j < E; j++) {
-            const uint64_t mj = S.nanm[j] | S.zerm[j];
-            if ((mj >> l) & 1) S.F[l * ES + j] = S.guess[j];
+            const uint64_t mj = mn;
+            const double g = gn;
+            if (j + 1 < E) {
+                mn = S.nanm[j + 1] | S.zerm[j + 1];
+                gn = S.guess[j + 1];
+            }
+            if ((mj >> l) & 1) S.F[l * ES + j] = g;
         }
     }
     wsync();
@@ -1804,8 +1814,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     double certj = 0.0;
     {
         uint64_t* hitm = reinterpret_cast<uint64_t*>(S.M);  // [E]; M is dead after the medians
+        double fn = row ? S.F[l * ES] : 0.0, an = S.adj[0];  // (next column's loads ahead of this column's store)
         for (int j = 0; j < E; j++) {
-            const uint64_t hm = ballot(row && S.F[l * ES + j] == S.adj[j]);
+            const double f = fn, av = an;
+            if (j + 1 < E) {
+                fn = row ? S.F[l * ES + j + 1] : 0.0;
+                an = S.adj[j + 1];
+            }
+            const uint64_t hm = ballot(row && f == av);
             if (l == 0) hitm[j] = hm;
         }
         wsync();
