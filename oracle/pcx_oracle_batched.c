@@ -991,6 +991,15 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
     double meanrep = pw_sum(rep, N) / (double)N;
     double u[NMAX], this_[NMAX], smooth[NMAX];
     for (int i = 0; i < N; i++) u[i] = nc[i] * (rep[i] / meanrep);
+    /* PCA path: this_rep (then smooth_rep) is a MaskedArray, and a NaN total of |u| leaves it
+     * fully MASKED (numpy.ma masks the NaN quotient): participation_columns is then
+     * 1 - (a fully masked dot) whose data is the 1, and reporter_bonus / author_bonus are fully
+     * masked sums whose data is their first operand's -- normalize(participation_rows) and
+     * |participation_columns.data| = 1 (__init__.py:460-472, 559-581; golden
+     * q_all_missing_scaled_col); percent_na stays masked (participation NaN) */
+    int rep_masked = 0;
+    if (alg == PCX_ALG_PCA)
+        for (int i = 0; i < N; i++) rep_masked |= isnan(u[i]);
     normalize_(u, N, this_);
     const double a = in->alpha, oma = 1.0 - in->alpha;
     for (int i = 0; i < N; i++) smooth[i] = a * this_[i] + oma * rep[i];
@@ -1074,7 +1083,7 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         OUT(out->na_row, o, narow[i]);
         OUT(out->participation_rows, o, pr[i]);
         OUT(out->relative_part, o, rel[i]);
-        OUT(out->reporter_bonus, o, rowmasked[i] ? rel[i] : rel[i] * pna + smooth[i] * (1.0 - pna));
+        OUT(out->reporter_bonus, o, (rowmasked[i] || rep_masked) ? rel[i] : rel[i] * pna + smooth[i] * (1.0 - pna));
     }
     for (int j = 0; j < E; j++) {
         const int64_t o = b * E + j;
@@ -1084,8 +1093,8 @@ static void one_round(const pcx_batch* in, pcx_batch_result* out, int64_t b) {
         OUT(out->outcomes_final, o, fin[j]);
         OUT(out->certainty, o, cert[j]);
         OUT(out->consensus_reward, o, reward[j]);
-        OUT(out->participation_columns, o, pc[j]);
-        OUT(out->author_bonus, o, relc[j] * pna + reward[j] * (1.0 - pna));
+        OUT(out->participation_columns, o, rep_masked ? 1.0 : pc[j]);
+        OUT(out->author_bonus, o, rep_masked ? 1.0 : relc[j] * pna + reward[j] * (1.0 - pna));
     }
     OUT(out->participation, b, 1.0 - pna);
     OUT(out->avg_certainty, b, avg_cert);

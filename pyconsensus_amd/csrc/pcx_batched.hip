@@ -1742,6 +1742,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     const double meanrep = wave_pw_sum(rep, row) / (double)N;
     double u = fabs(nc_i * (rep / meanrep));
     double Su = wave_pw_sum(u, row);
+    // PCA: a NaN total leaves the reference's this_rep / smooth_rep fully MASKED (SPEC
+    // rep_masked: participation_columns, reporter_bonus and author_bonus are numpy.ma's data)
+    const bool rep_masked = alg == 0 && __builtin_isnan(Su);
     if (Su == 0) {
         u += 1.0;
         Su = wave_pw_sum(u, row);
@@ -1930,7 +1933,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         if (a.na_row) a.na_row[o] = narow;
         if (a.participation_rows) a.participation_rows[o] = pr;
         if (a.relative_part) a.relative_part[o] = rel;
-        if (a.reporter_bonus) a.reporter_bonus[o] = rowmasked ? rel : rel * pna + smooth_i * (1.0 - pna);
+        if (a.reporter_bonus) a.reporter_bonus[o] = (rowmasked || rep_masked) ? rel : rel * pna + smooth_i * (1.0 - pna);
     }
     if (col) {
         const int64_t o = b * E + l;
@@ -1941,8 +1944,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         if (a.certainty) a.certainty[o] = certj;
         if (a.consensus_reward) a.consensus_reward[o] = reward;
         if (a.nas_filled) a.nas_filled[o] = nzj;
-        if (a.participation_columns) a.participation_columns[o] = pcj;
-        if (a.author_bonus) a.author_bonus[o] = relc * pna + reward * (1.0 - pna);
+        if (a.participation_columns) a.participation_columns[o] = rep_masked ? 1.0 : pcj;
+        if (a.author_bonus) a.author_bonus[o] = rep_masked ? 1.0 : relc * pna + reward * (1.0 - pna);
     }
     if (l == 0) {
         if (a.participation) a.participation[b] = 1.0 - pna;

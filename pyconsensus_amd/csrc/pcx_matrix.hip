@@ -3554,6 +3554,13 @@ __global__ void __launch_bounds__(BT) k_scaled_cert(pcx_mat m) {
     }
 }
 
+// PCA: a NaN total of |u| leaves the reference's this_rep / smooth_rep fully MASKED, and
+// participation_columns, reporter_bonus and author_bonus are then numpy.ma's data of fully masked
+// results (oracle/pcx_oracle_batched.c rep_masked)
+__device__ __forceinline__ bool rep_fully_masked(const pcx_mat& m) {
+    return m.algorithm == 0 && __builtin_isnan(dd_to_double(scl(m, SC_U)));
+}
+
 // PCX_M_FINAL: certainty of scaled events, consensus_reward, participation, author bonus
 __global__ void __launch_bounds__(1024) k_final(pcx_mat m) {
     __shared__ dd lds[16];
@@ -3597,6 +3604,7 @@ __global__ void __launch_bounds__(1024) k_final(pcx_mat m) {
     }
     __syncthreads();
     const double pna = m.pvec[3 * (m.n_events + 64) + 4];
+    const bool rep_masked = rep_fully_masked(m);
     for (int c = threadIdx.x; c < E; c += 1024) {
         const double cert = m.ev[EV_CERT * E + c];
         const double reward = nweight(fabs(cert), sh[0], sh[1]);
@@ -3609,8 +3617,8 @@ __global__ void __launch_bounds__(1024) k_final(pcx_mat m) {
         if (m.certainty) m.certainty[c] = cert;
         if (m.consensus_reward) m.consensus_reward[c] = reward;
         if (m.nas_filled) m.nas_filled[c] = m.ev[EV_NZERO * E + c];
-        if (m.participation_columns) m.participation_columns[c] = pc;
-        if (m.author_bonus) m.author_bonus[c] = relc * pna + reward * (1.0 - pna);
+        if (m.participation_columns) m.participation_columns[c] = rep_masked ? 1.0 : pc;
+        if (m.author_bonus) m.author_bonus[c] = rep_masked ? 1.0 : relc * pna + reward * (1.0 - pna);
     }
 }
 
@@ -3639,6 +3647,7 @@ __global__ void __launch_bounds__(BT) k_agents(pcx_mat m) {
     const int E = (int)m.n_events;
     const double S = dd_to_double(scl(m, SC_AR)), Sp = dd_to_double(scl(m, SC_ARP));
     const double pna = m.pvec[3 * (m.n_events + 64) + 4];
+    const bool rep_masked = rep_fully_masked(m);
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         const bool masked = (int)m.rowstat[2 * i] == E;
         const double narow = (double)m.rowstat[2 * i + 1];
@@ -3652,7 +3661,7 @@ __global__ void __launch_bounds__(BT) k_agents(pcx_mat m) {
         if (m.na_row) m.na_row[i] = narow;
         if (m.participation_rows) m.participation_rows[i] = pr;
         if (m.relative_part) m.relative_part[i] = rel;
-        if (m.reporter_bonus) m.reporter_bonus[i] = masked ? rel : rel * pna + sm * (1.0 - pna);
+        if (m.reporter_bonus) m.reporter_bonus[i] = (masked || rep_masked) ? rel : rel * pna + sm * (1.0 - pna);
     }
 }
 

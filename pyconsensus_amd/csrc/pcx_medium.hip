@@ -1313,6 +1313,9 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
     }
     __syncthreads();
     const double pna = scal[8];
+    // PCA: a NaN total of |u| (scal[5]) leaves the reference's this_rep / smooth_rep fully MASKED
+    // (SPEC rep_masked: participation_columns, reporter_bonus, author_bonus are numpy.ma's data)
+    const bool rep_masked = alg == PCX_ALG_PCA && __builtin_isnan(scal[5]);
     for (int i = tid; i < N; i += MT) {
         const bool masked = rmask[i] != 0.0;
         const double ai = masked ? 0.0 : fabs(pr[i]) + (scal[10] != 0.0 ? 1.0 : 0.0);
@@ -1325,7 +1328,7 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
         if (a.na_row) a.na_row[o] = narow[i];
         if (a.participation_rows) a.participation_rows[o] = pr[i];
         if (a.relative_part) a.relative_part[o] = rel[i];
-        if (a.reporter_bonus) a.reporter_bonus[o] = masked ? rel[i] : rel[i] * pna + smooth[i] * (1.0 - pna);
+        if (a.reporter_bonus) a.reporter_bonus[o] = (masked || rep_masked) ? rel[i] : rel[i] * pna + smooth[i] * (1.0 - pna);
     }
     for (int j = tid; j < E; j += MT) {
         const int64_t o = b * E + j;
@@ -1335,8 +1338,8 @@ __global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_
         if (a.outcomes_final) a.outcomes_final[o] = fin[j];
         if (a.certainty) a.certainty[o] = cert[j];
         if (a.consensus_reward) a.consensus_reward[o] = reward[j];
-        if (a.participation_columns) a.participation_columns[o] = pc[j];
-        if (a.author_bonus) a.author_bonus[o] = relc[j] * pna + reward[j] * (1.0 - pna);
+        if (a.participation_columns) a.participation_columns[o] = rep_masked ? 1.0 : pc[j];
+        if (a.author_bonus) a.author_bonus[o] = rep_masked ? 1.0 : relc[j] * pna + reward[j] * (1.0 - pna);
     }
     MSTAMP(15);
     if (a.stamps && tid == 0)

@@ -47,11 +47,11 @@ def test_synth_50x20():
     P.assert_known("exact", *_suite(("s%03d" % b, G.unstack(st, b)) for b in range(st["branch"].shape[0])))
 
 
-@pytest.mark.parametrize("name", sorted(P.MASKED_DATA))
-def test_masked_data_case_keywise(name):
-    """The SPEC on the reference's degenerate all-missing scaled column (parity.MASKED_DATA):
-    every output but the masked-data ones, and the branch, as the reference."""
-    P.assert_keywise(name, G.kat()[name], run_c(G.kat()[name]))
+@pytest.mark.parametrize("name", P.DEGENERATE_MASKED)
+def test_masked_data_case(name):
+    """The SPEC on the reference's degenerate all-missing scaled column (parity.DEGENERATE_MASKED):
+    every output, numpy.ma's masked-data ones included, and the branch, as the reference."""
+    P.assert_full(name, G.kat()[name], run_c(G.kat()[name]))
 
 
 def test_threads_deterministic():

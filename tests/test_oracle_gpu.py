@@ -46,11 +46,11 @@ def test_kat_through_oracle(gpu_lib, name):
     assert kind == P.KNOWN_MISMATCH[path].get(name, (None,))[0], (path, kind, bad)
 
 
-@pytest.mark.parametrize("name", sorted(P.MASKED_DATA))
-def test_masked_data_case_keywise(gpu_lib, name):
-    """The degenerate all-missing scaled column (parity.MASKED_DATA) through the drop-in
-    Oracle (batched kernel) and forced through the single-matrix pipeline: every output but
-    the numpy.ma masked-data ones, and the branch, as the reference."""
+@pytest.mark.parametrize("name", P.DEGENERATE_MASKED)
+def test_masked_data_case(gpu_lib, name):
+    """The degenerate all-missing scaled column (parity.DEGENERATE_MASKED) through the drop-in
+    Oracle (batched kernel) and forced through the single-matrix pipeline: every output,
+    numpy.ma's masked-data ones included, and the branch, as the reference."""
     from pyconsensus_amd import Oracle
     from test_matrix_gpu import run_matrix
 
@@ -59,8 +59,8 @@ def test_masked_data_case_keywise(gpu_lib, name):
     res = o.consensus()
     ours = {P.ABI_NAME[k]: v for k, v in G.flat_result(res).items() if k in P.ABI_NAME}
     ours["branch"] = np.array(o.last_info["branch"])
-    P.assert_keywise(name, case, ours)
-    P.assert_keywise(name, case, run_matrix(case))
+    P.assert_full(name, case, ours)
+    P.assert_full(name, case, run_matrix(case))
 
 
 def test_caller_array_rescaled_in_place(gpu_lib):
