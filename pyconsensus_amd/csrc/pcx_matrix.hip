@@ -46,6 +46,10 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
+#ifndef PCX_SEL_HC
+#define PCX_SEL_HC 1
+#endif
+constexpr int SEL_HC = PCX_SEL_HC;  // copies of each k_sel_hist bucket
 constexpr int SELS = 40;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
@@ -61,11 +65,34 @@ enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARG
 struct ColParam {
     bool scaled;
     double lo, range, guess, mu;
+    double rr;  // RN(1 / range); NaN when range lies outside [2^-100, 2^100] (quotients then divide)
 };
+
+// d / b correctly rounded from y = RN(1 / b) (Markstein: q0 = RN(d y) is faithful, the residual
+// d - b q0 is exact in one fma, and RN(q0 + r y) = RN(d / b)), in 4 fp64 ops where the IEEE
+// division sequence (div_scale x2, rcp, 5 fma, div_fmas, div_fixup) takes 11 with a quarter-rate
+// rcp.  The theorem assumes no underflow or overflow: with |b| in [2^-100, 2^100] (else y is
+// NaN) and |q0| in [2^-860, 2^1000], |d| >= 2^-960 keeps the residual exact and q finite.  Other
+// cells -- zeros among them, whose sign the fast path can get wrong (-0 / b) -- divide (a branch,
+// skipped when no lane needs it).  NaN d passes: the fast path returns NaN as the division does.
+// tests/test_fastdiv.py checks the sequence and its guard against the division bit for bit.
+__device__ __forceinline__ double div_rn(double d, double b, double y) {
+    const double q0 = d * y;
+    const double r = __builtin_fma(-q0, b, d);
+    double q = __builtin_fma(r, y, q0);
+    const bool slow = __builtin_isnan(y) | (fabs(q0) < 0x1p-860) | (fabs(q0) > 0x1p1000);
+    if (__builtin_expect(slow, 0)) q = d / b;
+    return q;
+}
+
+__device__ __forceinline__ double range_rcp(double range) {
+    const double a = fabs(range);
+    return (a >= 0x1p-100 && a <= 0x1p100) ? 1.0 / range : __builtin_nan("");
+}
 
 __device__ __forceinline__ double rescale(double r, const ColParam& p, int int_dtype) {
     if (!p.scaled) return r;
-    double x = (r - p.lo) / p.range;
+    double x = div_rn(r - p.lo, p.range, p.rr);
     if (int_dtype) x = trunc(x);
     return x;
 }
@@ -79,6 +106,7 @@ __device__ __forceinline__ ColParam col_param(const pcx_mat& m, int c, bool with
     p.range = p.scaled ? (m.hi[c] - m.lo[c]) : 1.0;
     p.guess = with_fill ? m.ev[EV_GUESS * m.n_events + c] : 0.0;
     p.mu = with_fill ? m.ev[EV_MU * m.n_events + c] : 0.0;
+    p.rr = p.scaled ? range_rcp(p.range) : 1.0;
     return p;
 }
 
@@ -463,15 +491,17 @@ __device__ __forceinline__ double max_nn(double a, double b) {
 // 16-row blocks [row / 16][scaled column][16], so a wave's stores form one contiguous run
 // (8.3 ms either way).
 constexpr int CS_TLD = 18;  // doubles per column in the transpose tile (16 rows + pad: 16-byte aligned pairs)
-template <bool EQW>  // EQW: reputation=None (every weight 1/N)
+template <bool EQW, bool INT>  // EQW: reputation=None (every weight 1/N); INT: m.int_dtype
 __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     __shared__ __attribute__((aligned(16))) double tile[BT / WAVE][WAVE * CS_TLD];
     const int E = (int)m.n_events;
-    const int c0 = blockIdx.x * BT + (threadIdx.x & ~(WAVE - 1));  // the wave's first column
-    if (c0 >= E) return;  // wave-uniform
+    // the wave's first column (wave-uniform: a scalar register, so row addresses are scalar too)
+    const int c0 = __builtin_amdgcn_readfirstlane(blockIdx.x * BT + (threadIdx.x & ~(WAVE - 1)));
+    if (c0 >= E) return;
     const int lane = threadIdx.x & (WAVE - 1);
     const bool live = c0 + lane < E;
     const int c = live ? c0 + lane : E - 1;  // dead lanes shadow the last column (nothing stored)
+    const int cl = c - c0;                    // the lane's column within the wave's run
     const ColParam p = col_param(m, c, false);
     double* const lt = tile[threadIdx.x / WAVE];
     // the flush's columns: lane l writes rows 2 (l & 7), +1 of wave column 8 k + (l >> 3), k < 8
@@ -486,7 +516,9 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     any_t = __any(any_t);  // wave-uniform
     int64_t r0, r1;
     row_range(m, r0, r1, 16);  // 16-row groups: whole 128-byte T segments
-    // rows [g0, g0 + nr) of the tile to T (wave-uniform call; every lane takes part)
+    // rows [g0, g0 + nr) of the tile to T (wave-uniform call; every lane takes part); with an
+    // even row count every segment (an even offset from T's 256-byte aligned base) takes a 16-byte store
+    const bool t_al = (m.n_rows & 1) == 0;
     auto flush = [&](int64_t g0, int nr) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
@@ -496,7 +528,7 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             if (tsi[k] < 0) continue;
             const double* src = lt + (8 * k + (lane >> 3)) * CS_TLD + pr;
             double* dst = m.T + (int64_t)tsi[k] * m.n_rows + g0 + pr;
-            if (pr + 1 < nr && ((uintptr_t)dst & 15) == 0) {
+            if (t_al && pr + 1 < nr) {
                 *reinterpret_cast<double2*>(dst) = *reinterpret_cast<const double2*>(src);
             } else {
                 if (pr < nr) dst[0] = src[0];
@@ -511,16 +543,25 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     // counts in 32-bit integers and the first present row as an offset (fp64 VALU ops issue at half
     // the rate of 32-bit ones; this pass is VALU-bound)
     uint32_t icnt = 0, inz = 0;
-    int32_t fro = -1;
+    uint32_t fro = 0xffffffffu;  // EQW: the first present row's offset from r0 (a running min)
     double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
-    bool offgrid = false;  // a present value outside {1, 1.5, 2} (M_COV_PLAN)
+    // a present value outside {1, 1.5, 2} (M_COV_PLAN): inside [1, 2] (from mn_x / mx_x at the
+    // end) the grid values are those whose mantissa has no bit below its top one -- an OR of
+    // those bits replaces three compares per element
+    uint32_t mant_hi = 0, mant_lo = 0;
     // EQW: every weight is 1 / N (k_rep_local), so the largest one is the first present row's:
     // no weight loads, and the argmax is that row's index, converted once at the end
     int64_t first_row = -1;
     rows_pipelined<PIPE_U>(
-        r0, r1, [&](int64_t i) { return XW{m.reports[i * E + c], eqw ? 0.0 : m.rep[i]}; },
+        r0, r1,
+        [&](int64_t i) {  // (the row's wave-uniform base: a scalar address plus the lane offset)
+            const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double*>(m.reports + i * E + c0), 0, WAVE * 8, 0x00020000);
+            const double x = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row, cl * 8, 0, 0));
+            return XW{x, eqw ? 0.0 : m.rep[i]};
+        },
         [&](int64_t i, XW v) {
-            const double x = rescale(v.x, p, m.int_dtype);
+            const double x = rescale(v.x, p, INT ? 1 : 0);
             const bool isn = __builtin_isnan(x);
             const bool z = x == 0.0;
             if (any_t) {
@@ -532,7 +573,7 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             icnt++;
             if constexpr (eqw) {  // reputation=None: every weight is 1/N -- sum x alone, scale once at the end
                 sx.add(x);
-                fro = fro < 0 ? (int32_t)(i - r0) : fro;
+                fro = min(fro, (uint32_t)(i - r0));
             } else {
                 const double r = v.w;
                 sr.add(r);
@@ -544,12 +585,16 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
             }
             mn_x = min_nn(mn_x, x);
             mx_x = max_nn(mx_x, x);
-            if (!p.scaled) offgrid |= !(x == 1.0 || x == 1.5 || x == 2.0);  // (read for unscaled events only)
+            const uint64_t xb = __double_as_longlong(x);
+            mant_hi |= (uint32_t)(xb >> 32) & 0x7ffffu;  // (mantissa bits 32..50; 51 is 1.5's)
+            mant_lo |= (uint32_t)xb;
         });
     if (any_t && r1 > r0 && (r1 & 15)) flush(r1 & ~(int64_t)15, (int)(r1 & 15));  // the last, partial group
     if (!live) return;
     const double cnt = (double)icnt, nz = (double)inz;
-    if (eqw && fro >= 0) first_row = r0 + fro;
+    // (read for unscaled events only; no present value: not off the grid)
+    const bool offgrid = !p.scaled && icnt > 0 && !(mn_x >= 1.0 && mx_x <= 2.0 && mant_hi == 0 && mant_lo == 0);
+    if (eqw && fro != 0xffffffffu) first_row = r0 + fro;
     if (eqw && first_row >= 0) {
         mx = 1.0 / (double)m.n_total;  // = m.rep[i] (k_rep_local)
         arg = (double)(m.row_offset + first_row);
@@ -902,7 +947,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int k = 0; k < 2; k++) {
         const int c = c0 + k;
         ok[k] = c < E;
-        p[k] = ok[k] ? col_param(m, c, true) : ColParam{false, 0.0, 1.0, 0.0, 0.0};
+        p[k] = ok[k] ? col_param(m, c, true) : ColParam{false, 0.0, 1.0, 0.0, 0.0, 1.0};
         pos[k] = ok[k] ? m.cov_pos[c] : (c < ld ? c : -1);  // padding positions keep their index
         zc[k] = ok[k] && pos[k] >= gb;
     }
@@ -927,8 +972,13 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     const int64_t i = g0 + q0 + 4 * h + u;
                     const bool live = i < m.n_rows;
                     const double* r = m.reports + (live ? i : 0) * E + c0;
+#if PCX_NT_OUT
+                    rv[u][0] = (live && ok[0]) ? __builtin_nontemporal_load(r) : 0.0;
+                    rv[u][1] = (live && ok[1]) ? __builtin_nontemporal_load(r + 1) : 0.0;
+#else
                     rv[u][0] = (live && ok[0]) ? r[0] : 0.0;
                     rv[u][1] = (live && ok[1]) ? r[1] : 0.0;
+#endif
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -971,8 +1021,15 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     if (live && (m.original || m.filled)) {
                         const int64_t o = i * E + c0;
                         if (even_e && ok[1]) {
+#if PCX_NT_OUT
+                            // (written once, never read back here: streaming stores)
+                            typedef double nt2 __attribute__((ext_vector_type(2)));
+                            if (m.original) __builtin_nontemporal_store(nt2{xo[0], xo[1]}, reinterpret_cast<nt2*>(m.original + o));
+                            if (m.filled) __builtin_nontemporal_store(nt2{fo[0], fo[1]}, reinterpret_cast<nt2*>(m.filled + o));
+#else
                             if (m.original) *(double2*)(m.original + o) = double2{xo[0], xo[1]};
                             if (m.filled) *(double2*)(m.filled + o) = double2{fo[0], fo[1]};
+#endif
                         } else {
 #pragma unroll
                             for (int k = 0; k < 2; k++)
@@ -2277,17 +2334,135 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     st_dd(pp + 14, {n2, 0.0});
 }
 
+// A wave of grid positions (all 64 lanes take part, dead ones on a clamped column, nothing
+// stored): outcomes_c_body<true>'s sums with b1 / b15 / b2 and pc from subset tables.  The row
+// weight is the same for every lane, so per 16-row group the wave tabulates, for each byte j of
+// the code word (rows j, j+4, j+8, j+12 at bits 8j + 2b: zpack_get) and each subset of its four
+// rows, the subset's weight sum -- lane l builds quarter l >> 4's entry for subset l & 15 -- and a
+// lane's b1 / b15 / b2 add one entry per byte, indexed by the byte's z == 0 / low / high code
+// bits (the even bits of the byte), in place of a compare, two selects and an add per row each.
+// pc has its own table over rows 4j .. 4j+3 (the missing word's nibble j), built as products so
+// that a NaN weight propagates as np.dot's does.  raw's compensated sum stays per row.
+constexpr int OT_Q = 88;                 // entries per code-table quarter (even-bit bytes <= 0x55)
+constexpr int OT_LD = 4 * OT_Q + WAVE;   // + the missing-word table [4][16]
+__device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S,
+                                                   double* tab) {
+    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
+    const int E = (int)m.n_events;
+    const bool live = q < E;
+    const int qc = live ? q : E - 1;  // (>= gb: the wave's first position is)
+    const int c = m.cov_perm[qc];
+    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
+    const uint32_t* zb = zb_packed(m) + (qc - gb);
+    const int l = threadIdx.x & (WAVE - 1), jl = l >> 4, pat = l & 15;
+    const int e = (pat & 1) | ((pat & 2) << 1) | ((pat & 4) << 2) | ((pat & 8) << 3);
+    double* const tw = tab + jl * OT_Q + e;
+    double* const tw2 = tab + 4 * OT_Q + l;
+    bool bs[4];
+    double bd[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        bs[b] = (pat >> b) & 1;
+        bd[b] = bs[b] ? 1.0 : 0.0;
+    }
+    acc2 zs;
+    double pc = 0, b1 = 0, b15 = 0, b2 = 0;
+    uint32_t c15 = 0, c2 = 0;
+    const int64_t g0 = r0 / 16, gf = r1 / 16;
+    uint32_t Pn = 0, Mn = 0;
+    if (g0 < gf) {
+        Pn = zb[g0 * m.zq];
+        Mn = m.nam[g0 * ld + qc];
+    }
+    for (int64_t g = g0; g < gf; g++) {
+        const uint32_t P = Pn, M = Mn;
+        if (g + 1 < gf) {
+            Pn = zb[(g + 1) * m.zq];
+            Mn = m.nam[(g + 1) * ld + qc];
+        }
+        const double* wg = sm + g * 16;
+        double wa[4], wc[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            wa[b] = wg[jl + 4 * b];
+            wc[b] = wg[4 * jl + b];
+        }
+        double t = bs[0] ? wa[0] : 0.0, t2 = wc[0] * bd[0];
+#pragma unroll
+        for (int b = 1; b < 4; b++) {
+            t += bs[b] ? wa[b] : 0.0;
+            t2 = __builtin_fma(wc[b], bd[b], t2);  // (= t2 + wc bd: the product is exact)
+        }
+        // (a wave's LDS accesses complete in order: the previous group's lookups precede these
+        // writes and the writes this group's lookups)
+        __builtin_amdgcn_wave_barrier();
+        *tw = t;
+        *tw2 = t2;
+        __builtin_amdgcn_wave_barrier();
+        c15 += __popc(P & 0x55555555u);
+        c2 += __popc(P & 0xAAAAAAAAu);
+        double w[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) w[r] = wg[r];
+#pragma unroll
+        for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
+        const uint32_t Lo = P & 0x55555555u, Hi = (P >> 1) & 0x55555555u, Zr = ~(P | (P >> 1)) & 0x55555555u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            b1 += tab[j * OT_Q + ((Zr >> (8 * j)) & 0xffu)];
+            b15 += tab[j * OT_Q + ((Lo >> (8 * j)) & 0xffu)];
+            b2 += tab[j * OT_Q + ((Hi >> (8 * j)) & 0xffu)];
+            pc += tab[4 * OT_Q + 16 * j + ((M >> (4 * j)) & 15u)];
+        }
+    }
+    if (r0 < r1 && gf * 16 < r1) {  // the ragged tail, per row (r0 < r1: r0 is 16-aligned)
+        const uint32_t P = zb[gf * m.zq], M = m.nam[gf * ld + qc];
+        for (int64_t i = gf * 16; i < r1; i++) {
+            const int r = (int)(i - gf * 16);
+            const uint32_t z = zpack_get(P, r);
+            const double w = sm[i];
+            c15 += z == 1u;
+            c2 += z == 2u;
+            zs.add(w * (double)z);
+            pc += w * (((M >> r) & 1u) ? 1.0 : 0.0);
+            b1 += z == 0u ? w : 0.0;
+            b15 += z == 1u ? w : 0.0;
+            b2 += z == 2u ? w : 0.0;
+        }
+    }
+    if (!live || c < 0) return;
+    const dd Z = zs.get();
+    const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
+    const double n15 = (double)c15, n2 = (double)c2, n1 = rows - n15 - n2;
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, dd_add(S, dd{0.5 * Z.hi, 0.5 * Z.lo}));
+    st_dd(pp + 2, {pc, 0.0});
+    st_dd(pp + 4, {b1, 0.0});
+    st_dd(pp + 6, {b15, 0.0});
+    st_dd(pp + 8, {b2, 0.0});
+    st_dd(pp + 10, {n1, 0.0});
+    st_dd(pp + 12, {n15, 0.0});
+    st_dd(pp + 14, {n2, 0.0});
+}
+
 // one launch over every position (unlike k_gemv2_c: here the general positions of a scaled event
 // read only their missing bits, and the two ranges' blocks fill the chip together)
 __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
+    __shared__ double otab[BT / WAVE][OT_LD];
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
+    const int qw = __builtin_amdgcn_readfirstlane(q & ~(WAVE - 1));  // the wave's first position
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     // the chunk's weight total for the grid positions, by every lane of a wave holding one
     // (before any lane leaves: the sum is a wave reduction)
     dd S{0.0, 0.0};
     if ((q | (WAVE - 1)) >= gb) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
+    if (qw >= m.n_events) return;
+    if (qw >= gb) {  // a whole wave of grid positions
+        outcomes_grid_wave(m, q, r0, r1, S, otab[threadIdx.x / WAVE]);
+        return;
+    }
     if (q >= m.n_events) return;
     if (q >= gb)
         outcomes_c_body<true>(m, q, r0, r1, S);
@@ -2741,11 +2916,15 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
-    __shared__ unsigned long long ha[NB], hb[NB], hc[NB], hmin[NB], hmax[NB];
+    // SEL_HC copies of every bucket, bucket b's copy c at b SEL_HC + c and a thread binning into
+    // copy threadIdx.x % SEL_HC: lanes of a wave whose keys share a bucket split over the copies
+    // (same-address LDS atomics serialise); the copies merge exactly (integer sums, min, max)
+    constexpr int HC = SEL_HC;
+    __shared__ unsigned long long ha[NB * HC], hb[NB * HC], hc[NB * HC], hmin[NB * HC], hmax[NB * HC];
     typedef unsigned long long hn_t;  // (32-bit LDS counts measured: no faster)
-    __shared__ hn_t hn[NB];
+    __shared__ hn_t hn[NB * HC];
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
-    for (int b = threadIdx.x; b < NB; b += BT) {
+    for (int b = threadIdx.x; b < NB * HC; b += BT) {
         ha[b] = hb[b] = hc[b] = 0;
         hn[b] = 0;
         hmin[b] = ~0ull;
@@ -2824,8 +3003,9 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const bool gather = !from_buf && m.cbuf && st[SW_INRANGE] > 0 && need <= (uint64_t)m.ccap &&
                         8 * need <= st[SW_COUNT];
     uint64_t* cb = m.cbuf ? m.cbuf + (int64_t)s * m.ccap * 2 : nullptr;
+    const int hcp = HC > 1 ? (int)(threadIdx.x % HC) : 0;
     auto bin = [&](uint64_t k, double w) {
-        const int b = (int)((k - lo) >> sh);
+        const int b = (int)((k - lo) >> sh) * HC + hcp;
         if (wmode) {
             const limbs3 L = to_limbs(w);
             atomicAdd(&ha[b], (unsigned long long)L.l0);
@@ -2911,7 +3091,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
                 st[SW_GW1] = f_gb;
                 st[SW_GW2] = f_gc;
                 const uint64_t fk = dkey(m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]]);
-                const int b = (int)((fk - lo) >> sh);
+                const int b = (int)((fk - lo) >> sh) * HC;
                 if (wmode) {
                     atomicAdd(&ha[b], f_ga);
                     atomicAdd(&hb[b], f_gb);
@@ -2924,7 +3104,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         }
     }
     if (gin && threadIdx.x == 0) {
-        const int b = (int)((gk - lo) >> sh);
+        const int b = (int)((gk - lo) >> sh) * HC;
         if (wmode) {
             atomicAdd(&ha[b], (unsigned long long)st[SW_GW0]);
             atomicAdd(&hb[b], (unsigned long long)st[SW_GW1]);
@@ -2946,14 +3126,25 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     }
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += BT) {
-        if (wmode) {
-            m.hist_w[(o + b) * 3 + 0] = ha[b];
-            m.hist_w[(o + b) * 3 + 1] = hb[b];
-            m.hist_w[(o + b) * 3 + 2] = hc[b];
+        unsigned long long sa = 0, sb = 0, sc = 0, mn = ~0ull, mx = 0;
+        uint64_t sn = 0;
+#pragma unroll
+        for (int c = 0; c < HC; c++) {
+            sa += ha[b * HC + c];
+            sb += hb[b * HC + c];
+            sc += hc[b * HC + c];
+            sn += (uint64_t)hn[b * HC + c];
+            mn = hmin[b * HC + c] < mn ? hmin[b * HC + c] : mn;
+            mx = hmax[b * HC + c] > mx ? hmax[b * HC + c] : mx;
         }
-        m.hist_n[o + b] = (uint64_t)hn[b];
-        m.hist_min[o + b] = hmin[b];
-        m.hist_max[o + b] = hmax[b];
+        if (wmode) {
+            m.hist_w[(o + b) * 3 + 0] = sa;
+            m.hist_w[(o + b) * 3 + 1] = sb;
+            m.hist_w[(o + b) * 3 + 2] = sc;
+        }
+        m.hist_n[o + b] = sn;
+        m.hist_min[o + b] = mn;
+        m.hist_max[o + b] = mx;
     }
 }
 
@@ -4514,9 +4705,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_COLSTATS:
             if (m.rep_raw)
-                hipLaunchKernelGGL(k_colstats<false>, colgrid, dim3(BT), 0, st, m);
+                hipLaunchKernelGGL((m.int_dtype ? k_colstats<false, true> : k_colstats<false, false>), colgrid, dim3(BT), 0, st, m);
             else
-                hipLaunchKernelGGL(k_colstats<true>, colgrid, dim3(BT), 0, st, m);
+                hipLaunchKernelGGL((m.int_dtype ? k_colstats<true, true> : k_colstats<true, false>), colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 4, 0, 1);
             break;
         case M_GUESS:
