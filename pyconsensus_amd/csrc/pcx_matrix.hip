@@ -2343,8 +2343,14 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
 // bits (the even bits of the byte), in place of a compare, two selects and an add per row each.
 // pc has its own table over rows 4j .. 4j+3 (the missing word's nibble j), built as products so
 // that a NaN weight propagates as np.dot's does.  raw's compensated sum stays per row.
+#ifndef PCX_OC_DDTAB
+#define PCX_OC_DDTAB 0
+#endif
+// PCX_OC_DDTAB: the code tables hold double-double subset sums, and raw's sum w z = sum_{z=1} w +
+// 2 sum_{z=2} w comes from compensated sums of the b15 / b2 entries instead of a per-row one
 constexpr int OT_Q = 88;                 // entries per code-table quarter (even-bit bytes <= 0x55)
-constexpr int OT_LD = 4 * OT_Q + WAVE;   // + the missing-word table [4][16]
+constexpr int OT_W = PCX_OC_DDTAB ? 2 : 1;  // doubles per code-table entry
+constexpr int OT_LD = 4 * OT_Q * OT_W + WAVE;  // + the missing-word table [4][16]
 __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S,
                                                    double* tab) {
     const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
@@ -2356,8 +2362,8 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
     const uint32_t* zb = zb_packed(m) + (qc - gb);
     const int l = threadIdx.x & (WAVE - 1), jl = l >> 4, pat = l & 15;
     const int e = (pat & 1) | ((pat & 2) << 1) | ((pat & 4) << 2) | ((pat & 8) << 3);
-    double* const tw = tab + jl * OT_Q + e;
-    double* const tw2 = tab + 4 * OT_Q + l;
+    double* const tw = tab + (jl * OT_Q + e) * OT_W;
+    double* const tw2 = tab + 4 * OT_Q * OT_W + l;
     bool bs[4];
     double bd[4];
 #pragma unroll
@@ -2365,7 +2371,7 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
         bs[b] = (pat >> b) & 1;
         bd[b] = bs[b] ? 1.0 : 0.0;
     }
-    acc2 zs;
+    acc2 zs, z15, z2;  // (PCX_OC_DDTAB: z15 / z2 the sums of w over z == 1 / z == 2)
     double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     uint32_t c15 = 0, c2 = 0;
     const int64_t g0 = r0 / 16, gf = r1 / 16;
@@ -2387,32 +2393,53 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
             wa[b] = wg[jl + 4 * b];
             wc[b] = wg[4 * jl + b];
         }
-        double t = bs[0] ? wa[0] : 0.0, t2 = wc[0] * bd[0];
+        double t = bs[0] ? wa[0] : 0.0, tl = 0.0, t2 = wc[0] * bd[0];
 #pragma unroll
         for (int b = 1; b < 4; b++) {
-            t += bs[b] ? wa[b] : 0.0;
+            if constexpr (PCX_OC_DDTAB) {
+                const dd u = two_sum(t, bs[b] ? wa[b] : 0.0);
+                t = u.hi;
+                tl += u.lo;
+            } else {
+                t += bs[b] ? wa[b] : 0.0;
+            }
             t2 = __builtin_fma(wc[b], bd[b], t2);  // (= t2 + wc bd: the product is exact)
         }
         // (a wave's LDS accesses complete in order: the previous group's lookups precede these
         // writes and the writes this group's lookups)
         __builtin_amdgcn_wave_barrier();
-        *tw = t;
+        if constexpr (PCX_OC_DDTAB)
+            *reinterpret_cast<double2*>(tw) = double2{t, tl};
+        else
+            *tw = t;
         *tw2 = t2;
         __builtin_amdgcn_wave_barrier();
         c15 += __popc(P & 0x55555555u);
         c2 += __popc(P & 0xAAAAAAAAu);
-        double w[16];
+        if constexpr (!PCX_OC_DDTAB) {
+            double w[16];
 #pragma unroll
-        for (int r = 0; r < 16; r++) w[r] = wg[r];
+            for (int r = 0; r < 16; r++) w[r] = wg[r];
 #pragma unroll
-        for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
+            for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
+        }
         const uint32_t Lo = P & 0x55555555u, Hi = (P >> 1) & 0x55555555u, Zr = ~(P | (P >> 1)) & 0x55555555u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            b1 += tab[j * OT_Q + ((Zr >> (8 * j)) & 0xffu)];
-            b15 += tab[j * OT_Q + ((Lo >> (8 * j)) & 0xffu)];
-            b2 += tab[j * OT_Q + ((Hi >> (8 * j)) & 0xffu)];
-            pc += tab[4 * OT_Q + 16 * j + ((M >> (4 * j)) & 15u)];
+            const double* tq = tab + j * OT_Q * OT_W;
+            b1 += tq[((Zr >> (8 * j)) & 0xffu) * OT_W];
+            if constexpr (PCX_OC_DDTAB) {
+                const double2 v15 = *reinterpret_cast<const double2*>(tq + ((Lo >> (8 * j)) & 0xffu) * 2);
+                const double2 v2 = *reinterpret_cast<const double2*>(tq + ((Hi >> (8 * j)) & 0xffu) * 2);
+                z15.add(v15.x);
+                z15.c += v15.y;
+                z2.add(v2.x);
+                z2.c += v2.y;
+            } else {
+                b15 += tq[(Lo >> (8 * j)) & 0xffu];
+                b2 += tq[(Hi >> (8 * j)) & 0xffu];
+            }
+            pc += tab[4 * OT_Q * OT_W + 16 * j + ((M >> (4 * j)) & 15u)];
         }
     }
     if (r0 < r1 && gf * 16 < r1) {  // the ragged tail, per row (r0 < r1: r0 is 16-aligned)
@@ -2423,15 +2450,28 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
             const double w = sm[i];
             c15 += z == 1u;
             c2 += z == 2u;
-            zs.add(w * (double)z);
             pc += w * (((M >> r) & 1u) ? 1.0 : 0.0);
             b1 += z == 0u ? w : 0.0;
-            b15 += z == 1u ? w : 0.0;
-            b2 += z == 2u ? w : 0.0;
+            if constexpr (PCX_OC_DDTAB) {
+                z15.add(z == 1u ? w : 0.0);
+                z2.add(z == 2u ? w : 0.0);
+            } else {
+                zs.add(w * (double)z);
+                b15 += z == 1u ? w : 0.0;
+                b2 += z == 2u ? w : 0.0;
+            }
         }
     }
     if (!live || c < 0) return;
-    const dd Z = zs.get();
+    dd Z;
+    if constexpr (PCX_OC_DDTAB) {
+        const dd Z15 = z15.get(), Z2 = z2.get();
+        b15 = dd_to_double(Z15);
+        b2 = dd_to_double(Z2);
+        Z = dd_add(Z15, dd{2.0 * Z2.hi, 2.0 * Z2.lo});
+    } else {
+        Z = zs.get();
+    }
     const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
     const double n15 = (double)c15, n2 = (double)c2, n1 = rows - n15 - n2;
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
