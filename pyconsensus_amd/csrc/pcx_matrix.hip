@@ -1166,6 +1166,10 @@ __device__ __forceinline__ void syrk_tile(const double* W, const double* tok, in
 }
 
 
+#ifndef PCX_DIGITS_INT
+#define PCX_DIGITS_INT 0
+#endif
+
 // one work item = (tile (I,J) of the trapezoid J < cov_jb of the lower triangle, row
 // slice ks) -> cslab[ks] (lower part, wcd positions); the pure-grid tiles are k_syrk_i8's
 __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
@@ -1235,6 +1239,35 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             const double w = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;  // exact (power of two)
             const double tk = m.tokp[grp * 16 + r];                       // 0 past n_rows
             double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
+#if PCX_DIGITS_INT
+            // X = rint((tok w 2^-e) 254^NDIG) (|X| <= 254^NDIG / 2 < 2^48, off by <= 0.52), then
+            // its balanced base-254 digits from the least significant up: q = rint(X / 254) (X / 254
+            // is a multiple of 1/254 within 2^-14 of X * (1/254): the rounding is exact but for the
+            // 1/2 tie, where either neighbour leaves |d| = 127), d = X - 254 q exactly
+            {
+                constexpr double C = [] {
+                    double c = 1.0;
+                    for (int k = 0; k < PCX_NDIG; k++) c *= PCX_DBASE;
+                    return c;
+                }();
+                const double pv = hi * C, pe = fma(hi, C, -pv);
+                double X = rint(pv + fma(lo, C, pe));
+#pragma unroll
+                for (int k = PCX_NDIG - 1; k >= 0; k--) {
+                    double di;
+                    if (k > 0) {
+                        const double q = rint(X * (1.0 / PCX_DBASE));
+                        di = fma(-q, PCX_DBASE, X);
+                        X = q;
+                    } else {
+                        di = X;
+                    }
+                    d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
+                    dsum[k] += (int)di;
+                }
+            }
+            continue;
+#endif
 #pragma unroll
             for (int k = 0; k < PCX_NDIG; k++) {
                 const double t = hi * PCX_DBASE, te = fma(hi, PCX_DBASE, -t);  // hi 254 = t + te exactly
