@@ -47,7 +47,7 @@ constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
 #ifndef PCX_SEL_HC
-#define PCX_SEL_HC 1
+#define PCX_SEL_HC 2
 #endif
 constexpr int SEL_HC = PCX_SEL_HC;  // copies of each k_sel_hist bucket
 constexpr int SELS = 40;         // sel_state words per scaled event
@@ -972,13 +972,8 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     const int64_t i = g0 + q0 + 4 * h + u;
                     const bool live = i < m.n_rows;
                     const double* r = m.reports + (live ? i : 0) * E + c0;
-#if PCX_NT_OUT
-                    rv[u][0] = (live && ok[0]) ? __builtin_nontemporal_load(r) : 0.0;
-                    rv[u][1] = (live && ok[1]) ? __builtin_nontemporal_load(r + 1) : 0.0;
-#else
                     rv[u][0] = (live && ok[0]) ? r[0] : 0.0;
                     rv[u][1] = (live && ok[1]) ? r[1] : 0.0;
-#endif
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1021,15 +1016,8 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     if (live && (m.original || m.filled)) {
                         const int64_t o = i * E + c0;
                         if (even_e && ok[1]) {
-#if PCX_NT_OUT
-                            // (written once, never read back here: streaming stores)
-                            typedef double nt2 __attribute__((ext_vector_type(2)));
-                            if (m.original) __builtin_nontemporal_store(nt2{xo[0], xo[1]}, reinterpret_cast<nt2*>(m.original + o));
-                            if (m.filled) __builtin_nontemporal_store(nt2{fo[0], fo[1]}, reinterpret_cast<nt2*>(m.filled + o));
-#else
                             if (m.original) *(double2*)(m.original + o) = double2{xo[0], xo[1]};
                             if (m.filled) *(double2*)(m.filled + o) = double2{fo[0], fo[1]};
-#endif
                         } else {
 #pragma unroll
                             for (int k = 0; k < 2; k++)
@@ -1168,6 +1156,12 @@ __device__ __forceinline__ void syrk_tile(const double* W, const double* tok, in
 
 #ifndef PCX_DIGITS_INT
 #define PCX_DIGITS_INT 0
+#endif
+#ifndef PCX_GEMV_PF
+#define PCX_GEMV_PF 0
+#endif
+#ifndef PCX_OC_VW
+#define PCX_OC_VW 0
 #endif
 
 // one work item = (tile (I,J) of the trapezoid J < cov_jb of the lower triangle, row
@@ -1947,15 +1941,46 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
         // next group's code word in flight during this group's adds; then the ragged tail
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Pn = g0 < gf ? zb[g0 * m.zq] : 0u;
+#if PCX_GEMV_PF
+        // the next group's weights in flight during this group's adds, as vector loads (a zero
+        // lane offset the compiler cannot see through: 64 scalar registers of weights would spill)
+        int vz;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+        const double* n1v = n1 + vz;
+        const double* n2v = n2 + vz;
+        double w1n[16], w2n[16];
+        if (g0 < gf) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                w1n[r] = n1v[g0 * 16 + r];
+                w2n[r] = n2v[g0 * 16 + r];
+            }
+        }
+#endif
         for (int64_t g = g0; g < gf; g++) {
             const uint32_t P = Pn;
             if (g + 1 < gf) Pn = zb[(g + 1) * m.zq];
             double w1[16], w2[16];
+#if PCX_GEMV_PF
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                w1[r] = w1n[r];
+                w2[r] = w2n[r];
+            }
+            if (g + 1 < gf) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    w1n[r] = n1v[(g + 1) * 16 + r];
+                    w2n[r] = n2v[(g + 1) * 16 + r];
+                }
+            }
+#else
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 w1[r] = n1[g * 16 + r];
                 w2[r] = n2[g * 16 + r];
             }
+#endif
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const double z = (double)zpack_get(P, r);
@@ -2376,14 +2401,10 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
 // bits (the even bits of the byte), in place of a compare, two selects and an add per row each.
 // pc has its own table over rows 4j .. 4j+3 (the missing word's nibble j), built as products so
 // that a NaN weight propagates as np.dot's does.  raw's compensated sum stays per row.
-#ifndef PCX_OC_DDTAB
-#define PCX_OC_DDTAB 0
-#endif
-// PCX_OC_DDTAB: the code tables hold double-double subset sums, and raw's sum w z = sum_{z=1} w +
-// 2 sum_{z=2} w comes from compensated sums of the b15 / b2 entries instead of a per-row one
+// Every load of group g + 1 (code and missing words, the lanes' table weights, the 16 row weights)
+// is issued before group g's work: a group waited on its weights' latency before.
 constexpr int OT_Q = 88;                 // entries per code-table quarter (even-bit bytes <= 0x55)
-constexpr int OT_W = PCX_OC_DDTAB ? 2 : 1;  // doubles per code-table entry
-constexpr int OT_LD = 4 * OT_Q * OT_W + WAVE;  // + the missing-word table [4][16]
+constexpr int OT_LD = 4 * OT_Q + WAVE;   // + the missing-word table [4][16]
 __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S,
                                                    double* tab) {
     const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
@@ -2395,8 +2416,8 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
     const uint32_t* zb = zb_packed(m) + (qc - gb);
     const int l = threadIdx.x & (WAVE - 1), jl = l >> 4, pat = l & 15;
     const int e = (pat & 1) | ((pat & 2) << 1) | ((pat & 4) << 2) | ((pat & 8) << 3);
-    double* const tw = tab + (jl * OT_Q + e) * OT_W;
-    double* const tw2 = tab + 4 * OT_Q * OT_W + l;
+    double* const tw = tab + jl * OT_Q + e;
+    double* const tw2 = tab + 4 * OT_Q + l;
     bool bs[4];
     double bd[4];
 #pragma unroll
@@ -2404,75 +2425,67 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
         bs[b] = (pat >> b) & 1;
         bd[b] = bs[b] ? 1.0 : 0.0;
     }
-    acc2 zs, z15, z2;  // (PCX_OC_DDTAB: z15 / z2 the sums of w over z == 1 / z == 2)
+    acc2 zs;
     double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     uint32_t c15 = 0, c2 = 0;
     const int64_t g0 = r0 / 16, gf = r1 / 16;
     uint32_t Pn = 0, Mn = 0;
-    if (g0 < gf) {
-        Pn = zb[g0 * m.zq];
-        Mn = m.nam[g0 * ld + qc];
-    }
-    for (int64_t g = g0; g < gf; g++) {
-        const uint32_t P = Pn, M = Mn;
-        if (g + 1 < gf) {
-            Pn = zb[(g + 1) * m.zq];
-            Mn = m.nam[(g + 1) * ld + qc];
-        }
-        const double* wg = sm + g * 16;
-        double wa[4], wc[4];
+    double wan[4], wcn[4], wn[16];
+#if PCX_OC_VW
+    int vz;  // (a zero lane offset: the 16 row weights as vector loads, not 32 spilling SGPRs)
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+    const double* smv = sm + vz;
+#else
+    const double* smv = sm;
+#endif
+    auto fetch = [&](int64_t g) {
+        Pn = zb[g * m.zq];
+        Mn = m.nam[g * ld + qc];
+        const double* wg = smv + g * 16;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-            wa[b] = wg[jl + 4 * b];
-            wc[b] = wg[4 * jl + b];
+            wan[b] = wg[jl + 4 * b];
+            wcn[b] = wg[4 * jl + b];
         }
-        double t = bs[0] ? wa[0] : 0.0, tl = 0.0, t2 = wc[0] * bd[0];
+#pragma unroll
+        for (int r = 0; r < 16; r++) wn[r] = wg[r];
+    };
+    if (g0 < gf) fetch(g0);
+    for (int64_t g = g0; g < gf; g++) {
+        const uint32_t P = Pn, M = Mn;
+        double wa[4], wc[4], w[16];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            wa[b] = wan[b];
+            wc[b] = wcn[b];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) w[r] = wn[r];
+        if (g + 1 < gf) fetch(g + 1);
+        double t = bs[0] ? wa[0] : 0.0, t2 = wc[0] * bd[0];
 #pragma unroll
         for (int b = 1; b < 4; b++) {
-            if constexpr (PCX_OC_DDTAB) {
-                const dd u = two_sum(t, bs[b] ? wa[b] : 0.0);
-                t = u.hi;
-                tl += u.lo;
-            } else {
-                t += bs[b] ? wa[b] : 0.0;
-            }
+            t += bs[b] ? wa[b] : 0.0;
             t2 = __builtin_fma(wc[b], bd[b], t2);  // (= t2 + wc bd: the product is exact)
         }
         // (a wave's LDS accesses complete in order: the previous group's lookups precede these
         // writes and the writes this group's lookups)
         __builtin_amdgcn_wave_barrier();
-        if constexpr (PCX_OC_DDTAB)
-            *reinterpret_cast<double2*>(tw) = double2{t, tl};
-        else
-            *tw = t;
+        *tw = t;
         *tw2 = t2;
         __builtin_amdgcn_wave_barrier();
         c15 += __popc(P & 0x55555555u);
         c2 += __popc(P & 0xAAAAAAAAu);
-        if constexpr (!PCX_OC_DDTAB) {
-            double w[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) w[r] = wg[r];
-#pragma unroll
-            for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
-        }
+        for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
         const uint32_t Lo = P & 0x55555555u, Hi = (P >> 1) & 0x55555555u, Zr = ~(P | (P >> 1)) & 0x55555555u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const double* tq = tab + j * OT_Q * OT_W;
-            b1 += tq[((Zr >> (8 * j)) & 0xffu) * OT_W];
-            if constexpr (PCX_OC_DDTAB) {
-                const double2 v15 = *reinterpret_cast<const double2*>(tq + ((Lo >> (8 * j)) & 0xffu) * 2);
-                const double2 v2 = *reinterpret_cast<const double2*>(tq + ((Hi >> (8 * j)) & 0xffu) * 2);
-                z15.add(v15.x);
-                z15.c += v15.y;
-                z2.add(v2.x);
-                z2.c += v2.y;
-            } else {
-                b15 += tq[(Lo >> (8 * j)) & 0xffu];
-                b2 += tq[(Hi >> (8 * j)) & 0xffu];
-            }
-            pc += tab[4 * OT_Q * OT_W + 16 * j + ((M >> (4 * j)) & 15u)];
+            const double* tq = tab + j * OT_Q;
+            b1 += tq[(Zr >> (8 * j)) & 0xffu];
+            b15 += tq[(Lo >> (8 * j)) & 0xffu];
+            b2 += tq[(Hi >> (8 * j)) & 0xffu];
+            pc += tab[4 * OT_Q + 16 * j + ((M >> (4 * j)) & 15u)];
         }
     }
     if (r0 < r1 && gf * 16 < r1) {  // the ragged tail, per row (r0 < r1: r0 is 16-aligned)
@@ -2483,28 +2496,15 @@ __device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int6
             const double w = sm[i];
             c15 += z == 1u;
             c2 += z == 2u;
+            zs.add(w * (double)z);
             pc += w * (((M >> r) & 1u) ? 1.0 : 0.0);
             b1 += z == 0u ? w : 0.0;
-            if constexpr (PCX_OC_DDTAB) {
-                z15.add(z == 1u ? w : 0.0);
-                z2.add(z == 2u ? w : 0.0);
-            } else {
-                zs.add(w * (double)z);
-                b15 += z == 1u ? w : 0.0;
-                b2 += z == 2u ? w : 0.0;
-            }
+            b15 += z == 1u ? w : 0.0;
+            b2 += z == 2u ? w : 0.0;
         }
     }
     if (!live || c < 0) return;
-    dd Z;
-    if constexpr (PCX_OC_DDTAB) {
-        const dd Z15 = z15.get(), Z2 = z2.get();
-        b15 = dd_to_double(Z15);
-        b2 = dd_to_double(Z2);
-        Z = dd_add(Z15, dd{2.0 * Z2.hi, 2.0 * Z2.lo});
-    } else {
-        Z = zs.get();
-    }
+    const dd Z = zs.get();
     const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
     const double n15 = (double)c15, n2 = (double)c2, n1 = rows - n15 - n2;
     double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
