@@ -46,10 +46,7 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
-#ifndef PCX_SEL_HC
-#define PCX_SEL_HC 2
-#endif
-constexpr int SEL_HC = PCX_SEL_HC;  // copies of each k_sel_hist bucket
+constexpr int SEL_HC = 2;  // copies of each k_sel_hist bucket (4: slower, 12.3 vs 9.0 ms at C5)
 constexpr int SELS = 40;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
@@ -1154,16 +1151,6 @@ __device__ __forceinline__ void syrk_tile(const double* W, const double* tok, in
 }
 
 
-#ifndef PCX_DIGITS_INT
-#define PCX_DIGITS_INT 0
-#endif
-#ifndef PCX_GEMV_PF
-#define PCX_GEMV_PF 0
-#endif
-#ifndef PCX_OC_VW
-#define PCX_OC_VW 0
-#endif
-
 // one work item = (tile (I,J) of the trapezoid J < cov_jb of the lower triangle, row
 // slice ks) -> cslab[ks] (lower part, wcd positions); the pure-grid tiles are k_syrk_i8's
 __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
@@ -1206,12 +1193,18 @@ __global__ void __launch_bounds__(256, 3) k_syrk(pcx_mat m) {
 }
 
 // tok * w of the general positions q < gb (the exact product, as a double-double) as PCX_NDIG
-// balanced base-254 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): t = 254 v (the double-double
-// product, its rounding below 2^-95), d = rint(t_hi), v = t - d -- |d| <= 127, the widest balanced
-// digit int8 holds.  PCX_NDIG digits leave a residue <= 254^-NDIG / 2 of 2^e (6: 2^-48.9 of the
-// column's bound on |tok w|, 3.7e-15 relative).  Each chunk of rows (blockIdx.y) also adds the
+// balanced base-254 digits of (tok w) 2^-e (|tok w 2^-e| <= 1/2): the nearest integer X to
+// (tok w 2^-e) 254^NDIG, written in base 254 with digits |d| <= 127, the widest balanced digit
+// int8 holds.  The residue is <= 0.52 254^-NDIG of 2^e (6: 2^-48.8 of the column's bound on
+// |tok w|, 3.8e-15 relative).  (Round 4 extracted the digits greedily from the top in
+// double-double arithmetic, 77 fp64 ops per element against 46 here: M_COV_I8 20.0 -> 19.6 ms.)  Each chunk of rows (blockIdx.y) also adds the
 // sum of every digit over its rows to dtok (int64 atomics: exact, order-free): S_q = sum tok w_q
 // from the same digits (k_cov_tokrow), so neither int8 product carries a token column.
+constexpr double DIG_SCALE = [] {  // 254^NDIG (exact: 6 digits need 48 bits)
+    double c = 1.0;
+    for (int k = 0; k < PCX_NDIG; k++) c *= PCX_DBASE;
+    return c;
+}();
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
@@ -1233,44 +1226,21 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             const double w = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;  // exact (power of two)
             const double tk = m.tokp[grp * 16 + r];                       // 0 past n_rows
             double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
-#if PCX_DIGITS_INT
-            // X = rint((tok w 2^-e) 254^NDIG) (|X| <= 254^NDIG / 2 < 2^48, off by <= 0.52), then
-            // its balanced base-254 digits from the least significant up: q = rint(X / 254) (X / 254
-            // is a multiple of 1/254 within 2^-14 of X * (1/254): the rounding is exact but for the
-            // 1/2 tie, where either neighbour leaves |d| = 127), d = X - 254 q exactly
-            {
-                constexpr double C = [] {
-                    double c = 1.0;
-                    for (int k = 0; k < PCX_NDIG; k++) c *= PCX_DBASE;
-                    return c;
-                }();
-                const double pv = hi * C, pe = fma(hi, C, -pv);
-                double X = rint(pv + fma(lo, C, pe));
+            // X = rint((tok w 2^-e) 254^NDIG) (|X| <= 254^NDIG / 2 < 2^48, within 0.52 of the
+            // exact value), then its balanced base-254 digits from the least significant up:
+            // q = rint(X / 254) -- X / 254 is a multiple of 1/254 and X * (1/254) lies within 2^-14 of
+            // it, so the rounding is exact but for the 1/2 tie, where either neighbour leaves
+            // |d| = 127 -- and d = X - 254 q exactly
+            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv);
+            double X = rint(pv + fma(lo, DIG_SCALE, pe));
 #pragma unroll
-                for (int k = PCX_NDIG - 1; k >= 0; k--) {
-                    double di;
-                    if (k > 0) {
-                        const double q = rint(X * (1.0 / PCX_DBASE));
-                        di = fma(-q, PCX_DBASE, X);
-                        X = q;
-                    } else {
-                        di = X;
-                    }
-                    d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
-                    dsum[k] += (int)di;
+            for (int k = PCX_NDIG - 1; k >= 0; k--) {
+                double di = X;
+                if (k > 0) {
+                    const double qd = rint(X * (1.0 / PCX_DBASE));
+                    di = fma(-qd, PCX_DBASE, X);
+                    X = qd;
                 }
-            }
-            continue;
-#endif
-#pragma unroll
-            for (int k = 0; k < PCX_NDIG; k++) {
-                const double t = hi * PCX_DBASE, te = fma(hi, PCX_DBASE, -t);  // hi 254 = t + te exactly
-                const double di = rint(t);
-                const double e = t - di;               // exact
-                const double l = fma(lo, PCX_DBASE, te);  // lo 254 + te (|l| < 2^-44)
-                hi = e + l;                            // two-sum: (hi, lo) = e + l exactly
-                const double bv = hi - e;
-                lo = (e - (hi - bv)) + (l - bv);
                 d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
                 dsum[k] += (int)di;
             }
@@ -1941,46 +1911,15 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
         // next group's code word in flight during this group's adds; then the ragged tail
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Pn = g0 < gf ? zb[g0 * m.zq] : 0u;
-#if PCX_GEMV_PF
-        // the next group's weights in flight during this group's adds, as vector loads (a zero
-        // lane offset the compiler cannot see through: 64 scalar registers of weights would spill)
-        int vz;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-        const double* n1v = n1 + vz;
-        const double* n2v = n2 + vz;
-        double w1n[16], w2n[16];
-        if (g0 < gf) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                w1n[r] = n1v[g0 * 16 + r];
-                w2n[r] = n2v[g0 * 16 + r];
-            }
-        }
-#endif
         for (int64_t g = g0; g < gf; g++) {
             const uint32_t P = Pn;
             if (g + 1 < gf) Pn = zb[(g + 1) * m.zq];
             double w1[16], w2[16];
-#if PCX_GEMV_PF
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                w1[r] = w1n[r];
-                w2[r] = w2n[r];
-            }
-            if (g + 1 < gf) {
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    w1n[r] = n1v[(g + 1) * 16 + r];
-                    w2n[r] = n2v[(g + 1) * 16 + r];
-                }
-            }
-#else
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 w1[r] = n1[g * 16 + r];
                 w2[r] = n2[g * 16 + r];
             }
-#endif
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const double z = (double)zpack_get(P, r);
@@ -2392,150 +2331,17 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     st_dd(pp + 14, {n2, 0.0});
 }
 
-// A wave of grid positions (all 64 lanes take part, dead ones on a clamped column, nothing
-// stored): outcomes_c_body<true>'s sums with b1 / b15 / b2 and pc from subset tables.  The row
-// weight is the same for every lane, so per 16-row group the wave tabulates, for each byte j of
-// the code word (rows j, j+4, j+8, j+12 at bits 8j + 2b: zpack_get) and each subset of its four
-// rows, the subset's weight sum -- lane l builds quarter l >> 4's entry for subset l & 15 -- and a
-// lane's b1 / b15 / b2 add one entry per byte, indexed by the byte's z == 0 / low / high code
-// bits (the even bits of the byte), in place of a compare, two selects and an add per row each.
-// pc has its own table over rows 4j .. 4j+3 (the missing word's nibble j), built as products so
-// that a NaN weight propagates as np.dot's does.  raw's compensated sum stays per row.
-// Every load of group g + 1 (code and missing words, the lanes' table weights, the 16 row weights)
-// is issued before group g's work: a group waited on its weights' latency before.
-constexpr int OT_Q = 88;                 // entries per code-table quarter (even-bit bytes <= 0x55)
-constexpr int OT_LD = 4 * OT_Q + WAVE;   // + the missing-word table [4][16]
-__device__ __forceinline__ void outcomes_grid_wave(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S,
-                                                   double* tab) {
-    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
-    const int E = (int)m.n_events;
-    const bool live = q < E;
-    const int qc = live ? q : E - 1;  // (>= gb: the wave's first position is)
-    const int c = m.cov_perm[qc];
-    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
-    const uint32_t* zb = zb_packed(m) + (qc - gb);
-    const int l = threadIdx.x & (WAVE - 1), jl = l >> 4, pat = l & 15;
-    const int e = (pat & 1) | ((pat & 2) << 1) | ((pat & 4) << 2) | ((pat & 8) << 3);
-    double* const tw = tab + jl * OT_Q + e;
-    double* const tw2 = tab + 4 * OT_Q + l;
-    bool bs[4];
-    double bd[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        bs[b] = (pat >> b) & 1;
-        bd[b] = bs[b] ? 1.0 : 0.0;
-    }
-    acc2 zs;
-    double pc = 0, b1 = 0, b15 = 0, b2 = 0;
-    uint32_t c15 = 0, c2 = 0;
-    const int64_t g0 = r0 / 16, gf = r1 / 16;
-    uint32_t Pn = 0, Mn = 0;
-    double wan[4], wcn[4], wn[16];
-#if PCX_OC_VW
-    int vz;  // (a zero lane offset: the 16 row weights as vector loads, not 32 spilling SGPRs)
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-    const double* smv = sm + vz;
-#else
-    const double* smv = sm;
-#endif
-    auto fetch = [&](int64_t g) {
-        Pn = zb[g * m.zq];
-        Mn = m.nam[g * ld + qc];
-        const double* wg = smv + g * 16;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            wan[b] = wg[jl + 4 * b];
-            wcn[b] = wg[4 * jl + b];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) wn[r] = wg[r];
-    };
-    if (g0 < gf) fetch(g0);
-    for (int64_t g = g0; g < gf; g++) {
-        const uint32_t P = Pn, M = Mn;
-        double wa[4], wc[4], w[16];
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            wa[b] = wan[b];
-            wc[b] = wcn[b];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) w[r] = wn[r];
-        if (g + 1 < gf) fetch(g + 1);
-        double t = bs[0] ? wa[0] : 0.0, t2 = wc[0] * bd[0];
-#pragma unroll
-        for (int b = 1; b < 4; b++) {
-            t += bs[b] ? wa[b] : 0.0;
-            t2 = __builtin_fma(wc[b], bd[b], t2);  // (= t2 + wc bd: the product is exact)
-        }
-        // (a wave's LDS accesses complete in order: the previous group's lookups precede these
-        // writes and the writes this group's lookups)
-        __builtin_amdgcn_wave_barrier();
-        *tw = t;
-        *tw2 = t2;
-        __builtin_amdgcn_wave_barrier();
-        c15 += __popc(P & 0x55555555u);
-        c2 += __popc(P & 0xAAAAAAAAu);
-#pragma unroll
-        for (int r = 0; r < 16; r++) zs.add(w[r] * (double)zpack_get(P, r));
-        const uint32_t Lo = P & 0x55555555u, Hi = (P >> 1) & 0x55555555u, Zr = ~(P | (P >> 1)) & 0x55555555u;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const double* tq = tab + j * OT_Q;
-            b1 += tq[(Zr >> (8 * j)) & 0xffu];
-            b15 += tq[(Lo >> (8 * j)) & 0xffu];
-            b2 += tq[(Hi >> (8 * j)) & 0xffu];
-            pc += tab[4 * OT_Q + 16 * j + ((M >> (4 * j)) & 15u)];
-        }
-    }
-    if (r0 < r1 && gf * 16 < r1) {  // the ragged tail, per row (r0 < r1: r0 is 16-aligned)
-        const uint32_t P = zb[gf * m.zq], M = m.nam[gf * ld + qc];
-        for (int64_t i = gf * 16; i < r1; i++) {
-            const int r = (int)(i - gf * 16);
-            const uint32_t z = zpack_get(P, r);
-            const double w = sm[i];
-            c15 += z == 1u;
-            c2 += z == 2u;
-            zs.add(w * (double)z);
-            pc += w * (((M >> r) & 1u) ? 1.0 : 0.0);
-            b1 += z == 0u ? w : 0.0;
-            b15 += z == 1u ? w : 0.0;
-            b2 += z == 2u ? w : 0.0;
-        }
-    }
-    if (!live || c < 0) return;
-    const dd Z = zs.get();
-    const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
-    const double n15 = (double)c15, n2 = (double)c2, n1 = rows - n15 - n2;
-    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
-    st_dd(pp + 0, dd_add(S, dd{0.5 * Z.hi, 0.5 * Z.lo}));
-    st_dd(pp + 2, {pc, 0.0});
-    st_dd(pp + 4, {b1, 0.0});
-    st_dd(pp + 6, {b15, 0.0});
-    st_dd(pp + 8, {b2, 0.0});
-    st_dd(pp + 10, {n1, 0.0});
-    st_dd(pp + 12, {n15, 0.0});
-    st_dd(pp + 14, {n2, 0.0});
-}
-
 // one launch over every position (unlike k_gemv2_c: here the general positions of a scaled event
 // read only their missing bits, and the two ranges' blocks fill the chip together)
 __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
-    __shared__ double otab[BT / WAVE][OT_LD];
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
-    const int qw = __builtin_amdgcn_readfirstlane(q & ~(WAVE - 1));  // the wave's first position
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     // the chunk's weight total for the grid positions, by every lane of a wave holding one
     // (before any lane leaves: the sum is a wave reduction)
     dd S{0.0, 0.0};
     if ((q | (WAVE - 1)) >= gb) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
-    if (qw >= m.n_events) return;
-    if (qw >= gb) {  // a whole wave of grid positions
-        outcomes_grid_wave(m, q, r0, r1, S, otab[threadIdx.x / WAVE]);
-        return;
-    }
     if (q >= m.n_events) return;
     if (q >= gb)
         outcomes_c_body<true>(m, q, r0, r1, S);
