@@ -462,31 +462,6 @@ __device__ __forceinline__ void rows_strided(int64_t first, int64_t stride, int6
     for (; i < n; i += stride) proc(i, load(i));
 }
 
-// rows_strided with the next U rows' loads issued before the current U are processed (as
-// rows_pipelined: a wave keeps loads in flight through its compute instead of alternating bursts)
-template <int U, class LOAD, class PROC>
-__device__ __forceinline__ void rows_strided_pipelined(int64_t first, int64_t stride, int64_t n, LOAD load, PROC proc) {
-    int64_t i = first;
-    if (i + (U - 1) * stride < n) {
-        decltype(load(i)) cur[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) cur[u] = load(i + u * stride);
-        for (; i + (2 * U - 1) * stride < n; i += U * stride) {
-            decltype(load(i)) nxt[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) nxt[u] = load(i + (U + u) * stride);
-#pragma unroll
-            for (int u = 0; u < U; u++) proc(i + u * stride, cur[u]);
-#pragma unroll
-            for (int u = 0; u < U; u++) cur[u] = nxt[u];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) proc(i + u * stride, cur[u]);
-        i += U * stride;
-    }
-    for (; i < n; i += stride) proc(i, load(i));
-}
-
 struct XW {
     double x, w;
 };
@@ -2933,17 +2908,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             bin(k, __longlong_as_double(cb[2 * j + 1]));
         }
     } else {
-#ifndef PCX_SEL_PIPE
-#define PCX_SEL_PIPE 0
-#endif
-#if PCX_SEL_PIPE
-        rows_strided_pipelined<PCX_SEL_PIPE>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
-#else
-#ifndef PCX_SEL_UNROLL
-#define PCX_SEL_UNROLL ROW_UNROLL
-#endif
-        rows_strided<PCX_SEL_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
-#endif
+        rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
                                  [&](int64_t, XW v) {
             double x, w;
             if (gties && __builtin_isnan(v.x)) return;  // a filled row
