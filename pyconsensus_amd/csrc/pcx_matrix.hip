@@ -484,9 +484,11 @@ __device__ __forceinline__ double max_nn(double a, double b) {
 // and walks the rows, so its T column is one contiguous run; the lanes' values go through a
 // per-wave LDS tile of 16 rows, and the wave writes them out as 8 whole 128-byte segments per
 // store instruction (lanes 8 k .. 8 k + 7 one column's 16 rows), where a lane-per-column store
-// touched 64 lines with 16 bytes each (C5: 9.1 -> 8.3 ms; 6.9 with no T at all).  Rejected: T in
-// 16-row blocks [row / 16][scaled column][16], so a wave's stores form one contiguous run
-// (8.3 ms either way).
+// touched 64 lines with 16 bytes each (C5: 9.1 -> 8.3 ms; 6.9 with no T at all).  The division
+// by the range as a reciprocal plus one exact correction (div_rn), int_dtype as a template
+// parameter, scalar row addresses and the mantissa-bit off-grid test: 47 -> 26 VALU per element,
+// 8.3 -> 7.4 ms (5.57 TB/s).  Rejected: T in 16-row blocks [row / 16][scaled column][16], so a
+// wave's stores form one contiguous run (8.3 ms either way).
 constexpr int CS_TLD = 18;  // doubles per column in the transpose tile (16 rows + pad: 16-byte aligned pairs)
 template <bool EQW, bool INT>  // EQW: reputation=None (every weight 1/N); INT: m.int_dtype
 __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
@@ -537,8 +539,8 @@ __global__ void __launch_bounds__(BT) k_colstats(pcx_mat m) {
     };
     acc2 sr, srx, sx;
     constexpr bool eqw = EQW;
-    // counts in 32-bit integers and the first present row as an offset (fp64 VALU ops issue at half
-    // the rate of 32-bit ones; this pass is VALU-bound)
+    // counts in 32-bit integers and the first present row as an offset (fewer fp64 VALU ops per
+    // element: the pass was VALU-bound before the division became a reciprocal)
     uint32_t icnt = 0, inz = 0;
     uint32_t fro = 0xffffffffu;  // EQW: the first present row's offset from r0 (a running min)
     double mx = -1.0, arg = -1.0, mn_x = __builtin_inf(), mx_x = -__builtin_inf();
