@@ -103,14 +103,22 @@ struct limbs3 {
     uint64_t l0, l1, l2;
 };
 
+// Each limb is an integer-valued double f in [0, 2^43): f + 2^52 holds f in its mantissa bits, so
+// one add and a mask convert it (the generic double -> uint64 conversion takes ~7 fp64 ops, three
+// times per element in the selection's weight-mode passes).  A NaN weight gives zero limbs, as the
+// generic conversion of NaN does.
+__device__ __forceinline__ uint64_t limb_bits(double f) {
+    return (uint64_t)__double_as_longlong(f + 0x1p52) & 0xFFFFFFFFFFFFFull;
+}
 __device__ __forceinline__ limbs3 to_limbs(double w) {
+    if (__builtin_isnan(w)) w = 0.0;
     const double a = ldexp(w, 35);
     const double f0 = floor(a);
     const double b = ldexp(a - f0, 43);
     const double f1 = floor(b);
     const double c = ldexp(b - f1, 43);
     const double f2 = floor(c);
-    return {(uint64_t)f0, (uint64_t)f1, (uint64_t)f2};
+    return {limb_bits(f0), limb_bits(f1), limb_bits(f2)};
 }
 
 // ---------------------------------------------------------------- reductions
