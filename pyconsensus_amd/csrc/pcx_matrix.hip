@@ -2823,10 +2823,6 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     const bool first = m.sel_first != 0;
     const bool gfirst = first && m.sel_phase == 2;
     uint64_t wlo = ~0ull, whi = 0, ga = 0, gb = 0, gc = 0, gn = 0;
-    // phase 1 with reputation=None: every weight is 1 / N (sel_load), so the extremes are that
-    // weight's bits as soon as one element is present
-    const bool wconst = m.sel_phase == 1 && !m.rep_raw;
-    bool seen = false;
     __shared__ int win_s[2];
     if (first && threadIdx.x == 0) {  // the sampled window (k_sel_sample, all ranks)
         const double* smp = sel_sample_row(m, a);
@@ -2920,13 +2916,9 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
             if (gties && __builtin_isnan(v.x)) return;  // a filled row
             if (!sel_decode(m, s, v, x, w)) return;
             if (first) {
-                if (wconst) {
-                    seen = true;
-                } else {
-                    const uint64_t wb = (uint64_t)__double_as_longlong(w);  // weights >= 0 order like their bits
-                    wlo = wb < wlo ? wb : wlo;
-                    whi = wb > whi ? wb : whi;
-                }
+                const uint64_t wb = (uint64_t)__double_as_longlong(w);  // weights >= 0 order like their bits
+                wlo = wb < wlo ? wb : wlo;
+                whi = wb > whi ? wb : whi;
                 if (gfirst && __builtin_isnan(v.x)) {  // a filled row: summed here, binned once below
                     if (wmode) {
                         const limbs3 L = to_limbs(w);
@@ -2962,7 +2954,6 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         });
     }
     if (first) {
-        if (wconst && seen) wlo = whi = (uint64_t)__double_as_longlong(1.0 / (double)m.n_total);
         atomicMin(&f_wlo, (unsigned long long)wlo);
         atomicMax(&f_whi, (unsigned long long)whi);
         if (gn) {
