@@ -8,6 +8,10 @@ round).  A "step" is one launch of ``batched_round_kernel`` over the resident
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
+``--gpus N > 1`` with no launcher (WORLD_SIZE unset) starts the second form itself as a
+child job before touching the GPU; WORLD_SIZE set and different from ``--gpus`` is an
+error (exit 2), so the line's ``n_gpus`` is always the number of ranks that ran.
+
 Rounds are independent, so ranks shard them with no data-path collective
 (weak scaling: every rank runs its own 65,536 rounds per step).  Rank 0 prints
 ONE JSON line.
@@ -107,6 +111,14 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     R, sc, lo, hi, _ = synthetic.matrix_device(N, E, seed=3, n_shards=8, shards=shards, device=dev)
     comm = Comm.from_env(dev.index)  # RCCL inside libpcx for the nccl backend
     _C5_STATE["comm"], _C5_STATE["dev"] = comm, dev.index
+    from pyconsensus_amd import _lib
+    from pyconsensus_amd.pipeline import RcclComm
+
+    ctx_world = int(_lib.lib().pcx_ctx_world(comm.context(dev.index)))
+    if ctx_world != world:
+        raise RuntimeError("libpcx context spans %d rank(s), the job %d" % (ctx_world, world))
+    comm_info = {"comm": type(comm).__name__, "ctx_world": ctx_world,
+                 "rccl_world": ctx_world if isinstance(comm, RcclComm) else 0}
 
     def run(profile=None):
         return consensus_matrix(R, None, sc, lo, hi, comm=comm, n_total=N, row_offset=off, device=dev,
@@ -158,7 +170,8 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms and fp_pairs else None
     tops = i8_ops_rank / (i8_ms * 1e-3) / 1e12 if i8_ms == i8_ms and i8_pairs else None
     del R
-    return {"metric": "1M x 4k consensus latency (every output, original and filled included)", "n_gpus": world, "rows_per_gpu": cnt, "events": E,
+    return {"metric": "1M x 4k consensus latency (every output, original and filled included)", "n_gpus": world,
+            **comm_info, "rows_per_gpu": cnt, "events": E,
             "latency_ms": 1e3 * sorted(times)[len(times) // 2], "latency_ms_all": [1e3 * x for x in times],
             "latency_ms_mean": 1e3 * sum(times) / len(times), "warmup_steps": warmup,
             "stage_ms_per_step": [{k: round(p.get(k, 0.0), 3) for k in top} for p in step_prof],
@@ -296,6 +309,57 @@ VALU_ISSUE_CYCLES = 4      # a wave64 VALU instruction holds its SIMD 4 cycles
 SIMDS, CLOCK_GHZ = 1024, 2.4
 
 
+LAUNCHER_ENV = "PCX_BENCH_LAUNCHER"  # set by launch_ranks for its children (reported in the line)
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """``bench.py --gpus N`` without a launcher: run the driver's own N-rank command
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) as a CHILD
+    process and return its exit status.  Called before this process touches the GPU (no
+    exec from a process that initialised HIP); rank 0 of the child job prints the line."""
+    import signal
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, **{LAUNCHER_ENV: "bench.py --gpus %d (torch.distributed.run child)" % n})
+    proc = subprocess.Popen(cmd, env=env)  # same process group: a group kill reaches every rank
+    # a SIGTERM to this process alone is passed on (torch.distributed.run forwards it to its ranks)
+    signal.signal(signal.SIGTERM, lambda s, f: proc.send_signal(s))
+    try:
+        return proc.wait()
+    except BaseException:
+        proc.terminate()
+        try:
+            proc.wait(timeout=30)
+        except Exception:  # noqa: BLE001
+            proc.kill()
+        raise
+
+
+def rank_devices(world, dev):
+    """(rank, local device index, PCI bus id) of every rank, gathered to all ranks."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    mine = {"device": dev.index, "pci_bus_id": getattr(p, "pci_bus_id", None), "name": p.name}
+    if world == 1:
+        return [dict(rank=0, **mine)]
+    import torch.distributed as dist
+
+    allv = [None] * world
+    dist.all_gather_object(allv, mine)
+    return [dict(rank=r, **v) for r, v in enumerate(allv)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -306,6 +370,17 @@ def main():
     ap.add_argument("--c5-steps", type=int, default=3, help="timed 1M x 4k consensus runs (0 = skip)")
     ap.add_argument("--no-c4", dest="c4", action="store_false", help="skip the 100k x 1k (C4) entry")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if env_world is None and args.gpus > 1:
+        # no launcher: start one rank per GPU ourselves, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d; refusing to report a different GPU count"
+              % (env_world, args.gpus), file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
 
@@ -327,6 +402,7 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    devices = rank_devices(world, dev)
 
     from pyconsensus_amd import synthetic
     from pyconsensus_amd.batched import consensus_batched
@@ -417,6 +493,8 @@ def main():
                                           "profiles/pmc_traffic.json) at 4 cycles each on 1024 SIMDs at "
                                           "2.4 GHz, over the kernel time"}},
             "vectors_only_kernel_ms": vec_ms,
+            "launcher": os.environ.get(LAUNCHER_ENV, "external (WORLD_SIZE=%d)" % world if world > 1 else "none"),
+            "devices": devices,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()

@@ -209,6 +209,11 @@ pcx_ctx* pcx_create_devices(int n_devices, const int* device_ids);
 
 int pcx_ctx_world(const pcx_ctx* ctx);
 int pcx_ctx_rank(const pcx_ctx* ctx);
+/* 1 if the context's communicators can still exchange, 0 once a failed call aborted them (RCCL:
+ * ncclCommAbort after a rank of a multi-device call failed mid-exchange): destroy and recreate
+ * it then.  An argument error raised before any exchange (PCX_EINVAL from the rank-independent
+ * checks) leaves the context usable. */
+int pcx_ctx_usable(const pcx_ctx* ctx);
 /* Drop the cached scratch of the single-matrix path (it is kept between calls of
  * the same shape: a C5 consensus needs ~50 GB of it). */
 int pcx_release_workspace(pcx_ctx* ctx);
@@ -331,6 +336,25 @@ int pcx_rccl_version(int* runtime, int* compiled);
  * violations (the handle freed other than exactly once, used after it was freed, or used
  * successfully after an abort returned); 0 = pass, -1 = bad arguments.  For the tests. */
 int pcx_selftest_abort_once(int users, int aborters, int iters);
+/* The same abort path when one user is blocked inside its exchange for twice the abort's wait
+ * (an RCCL enqueue stuck on a failed peer): every abort must return after the bounded wait, free
+ * the handle exactly once (overlapping the blocked use: the documented window, counted once) and
+ * fail every later use.  Returns the number of violations; 0 = pass, -1 = bad arguments. */
+int pcx_selftest_abort_slow_holder(int users, int aborters);
+/* CPU self-test of the virtual-rank exchange (pcx_group, as pcx_create_grouped /
+ * pcx_create_devices use it): `world` threads run `steps` slot exchanges; rank `fail_rank`
+ * fails at step `fail_step` (-1: none), the first failure aborts the group and must release
+ * every waiting rank; after a reset a clean run must pass.  Returns the number of violations. */
+int pcx_selftest_group_abort(int world, int steps, int fail_rank, int fail_step);
+/* CPU self-test of the round scheduler's hand-out (pcx_consensus_batched_f64 above 256 x 64):
+ * `workers` threads take `rounds` fake rounds; worker `enomem_worker` reports PCX_ENOMEM on its
+ * first round (-1: none) and must hand it back; round `fail_round` fails (-1: none) and must stop
+ * the batch.  Every round must run exactly once.  Returns the number of violations. */
+int pcx_selftest_rounds_sched(int workers, int64_t rounds, int enomem_worker, int64_t fail_round);
+/* Test hook: the NEXT pcx_consensus_batched_f64 call on `ctx` that takes the round scheduler
+ * makes its worker `worker` report PCX_ENOMEM for its first round without running it (the
+ * hand-back path); -1 clears it.  Consumed by that call.  For the tests only. */
+int pcx_test_inject_enomem(pcx_ctx* ctx, int worker);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,7 @@ def _declare(lib):
         ("pcx_create_devices", vp, [i32, C.POINTER(C.c_int)]),
         ("pcx_ctx_world", i32, [vp]),
         ("pcx_ctx_rank", i32, [vp]),
+        ("pcx_ctx_usable", i32, [vp]),
         ("pcx_release_workspace", i32, [vp]),
         ("pcx_consensus_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
         ("pcx_interpolate_f64", i32, [vp, C.POINTER(_abi.Problem), C.POINTER(_abi.Result)]),
@@ -63,6 +64,10 @@ def _declare(lib):
         ("pcx_mixed_digits", i32, []),
         ("pcx_rccl_version", i32, [C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         ("pcx_selftest_abort_once", i32, [i32, i32, i32]),
+        ("pcx_selftest_abort_slow_holder", i32, [i32, i32]),
+        ("pcx_selftest_group_abort", i32, [i32, i32, i32, i32]),
+        ("pcx_selftest_rounds_sched", i32, [i32, i64, i32, i64]),
+        ("pcx_test_inject_enomem", i32, [vp, i32]),
     ]:
         f = getattr(lib, name)
         f.restype = res

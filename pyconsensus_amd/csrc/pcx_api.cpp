@@ -16,6 +16,7 @@
 
 #include "../../include/pcx.h"
 #include "pcx_internal.h"
+#include "pcx_sync.h"
 #include "pcx_seqsum.h"
 
 namespace {
@@ -163,6 +164,14 @@ int pcx_ctx_world(const pcx_ctx* ctx) {
     return ctx && ctx->comm ? ctx->comm->world : 1;
 }
 int pcx_ctx_rank(const pcx_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }
+
+int pcx_ctx_usable(const pcx_ctx* ctx) {
+    if (!ctx) return 0;
+    if (ctx->comm && ctx->comm->aborted) return 0;
+    for (const pcx_ctx* s : ctx->sub)
+        if (s->comm && s->comm->aborted) return 0;
+    return 1;
+}
 
 int pcx_release_workspace(pcx_ctx* ctx) {
     if (!ctx) return fail(PCX_EINVAL, "pcx_release_workspace: null context");
@@ -407,7 +416,7 @@ int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, co
     std::vector<pcx_problem> ps(n, *p);
     std::vector<pcx_result> rs(n);
     std::vector<std::string> errs(n);
-    std::vector<int> rcs(n, 0);
+    std::vector<int> rcs;
     const int64_t base = N / n, rem = N % n;
     auto at = [](double* a, int64_t off) { return a ? a + off : nullptr; };
     for (int k = 0; k < n; k++) {
@@ -444,23 +453,21 @@ int run_devices(pcx_ctx* ctx, const pcx_problem* p, pcx_result* r, int entry, co
             o.covariance = r->covariance;
         }
     }
-    std::vector<std::thread> th;
-    std::atomic<bool> aborting{false};
-    for (int k = 0; k < n; k++) {
-        const int64_t off = ps[k].row_offset;
-        th.emplace_back([&, k, off] {
-            rcs[k] = pcx::run_matrix(ctx->sub[k], &ps[k], &rs[k], entry, scores ? scores + off : nullptr, rank_rule,
-                                     nc ? nc + off : nullptr, errs[k]);
-            // release the ranks waiting on this one in an exchange: the first failing worker
-            // aborts every other rank's communicator (RCCL: ncclCommAbort), later ones do nothing
-            if (rcs[k] && !aborting.exchange(true)) {
-                if (ctx->group) pcx::group_abort(ctx->group);
-                for (pcx_ctx* o : ctx->sub)
-                    if (o->comm && o != ctx->sub[k]) o->comm->abort();
-            }
-        });
-    }
-    for (auto& t : th) t.join();
+    // the first failing worker releases the ranks waiting on it in an exchange: it aborts every
+    // other rank's communicator (RCCL: ncclCommAbort; group: pcx_group::abort)
+    pcx::run_workers(
+        n,
+        [&](int k) {
+            const int64_t off = ps[k].row_offset;
+            return pcx::run_matrix(ctx->sub[k], &ps[k], &rs[k], entry, scores ? scores + off : nullptr, rank_rule,
+                                   nc ? nc + off : nullptr, errs[k]);
+        },
+        [&](int k) {
+            if (ctx->group) pcx::group_abort(ctx->group);
+            for (pcx_ctx* o : ctx->sub)
+                if (o->comm && o != ctx->sub[k]) o->comm->abort();
+        },
+        rcs);
     if (ctx->group) pcx::group_reset(ctx->group);  // every worker has left the exchange
     int first = -1;
     for (int k = 0; k < n && first < 0; k++)
@@ -552,7 +559,21 @@ int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax) { return pcx::s
 int pcx_mixed_digits(void) { return PCX_NDIG; }
 int pcx_rccl_version(int* runtime, int* compiled) { return pcx::rccl_version(runtime, compiled); }
 int pcx_selftest_abort_once(int users, int aborters, int iters) {
-    return pcx::selftest_abort_once(users, aborters, iters);
+    return pcx::selftest_abort_once(users, aborters, iters, 0);
+}
+int pcx_selftest_abort_slow_holder(int users, int aborters) {
+    return pcx::selftest_abort_once(users, aborters, 1, 1);
+}
+int pcx_selftest_group_abort(int world, int steps, int fail_rank, int fail_step) {
+    return pcx::selftest_group_abort(world, steps, fail_rank, fail_step);
+}
+int pcx_selftest_rounds_sched(int workers, int64_t rounds, int enomem_worker, int64_t fail_round) {
+    return pcx::selftest_rounds_sched(workers, rounds, enomem_worker, fail_round);
+}
+int pcx_test_inject_enomem(pcx_ctx* ctx, int worker) {
+    if (!ctx) return fail(PCX_EINVAL, "pcx_test_inject_enomem: null context");
+    ctx->test_enomem_worker = worker;
+    return PCX_OK;
 }
 
 }  // extern "C"

@@ -22,37 +22,7 @@
 #include <vector>
 
 #include "pcx_internal.h"
-
-struct pcx_group {
-    int world = 1;
-    std::mutex mu;
-    std::condition_variable cv;
-    int arrived = 0;
-    int64_t generation = 0;
-    std::vector<std::vector<char>> slot;  // per rank host staging
-    std::vector<char> result;             // reduced data (written by the last arriver)
-
-    bool aborted = false;                 // a rank failed: every waiting and later exchange fails
-
-    bool barrier() {
-        std::unique_lock<std::mutex> lk(mu);
-        if (aborted) return false;
-        const int64_t g = generation;
-        if (++arrived == world) {
-            arrived = 0;
-            generation++;
-            cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != g || aborted; });
-        }
-        return !aborted;
-    }
-    void abort() {
-        std::lock_guard<std::mutex> lk(mu);
-        aborted = true;
-        cv.notify_all();
-    }
-};
+#include "pcx_sync.h"
 
 namespace pcx {
 namespace {
@@ -85,34 +55,7 @@ int hip_err(hipError_t e, const char* what, std::string& err) {
 }
 
 // ------------------------------------------------------------------ RCCL
-constexpr int ABORT_SELFTEST_WAIT_MS = 100;
-// A communicator handle that many threads use and any of them may abort: `use` loads the
-// handle and runs the enqueue under `mu`; `abort` marks the handle dead (later uses fail),
-// waits for a use in progress a bounded time, then swaps the handle out and frees it exactly
-// once, whatever the number of callers.  No handle is freed between another thread's load and
-// its enqueue.  An enqueue blocked inside RCCL (lazy connection set-up with a peer that failed)
-// is what ncclCommAbort exists to interrupt, hence the bounded wait rather than a plain lock.
-template <class H>
-struct AbortOnce {
-    std::atomic<H> h{H{}};
-    std::timed_mutex mu;
-    std::atomic<bool> dead{false};
-    template <class F>
-    int use(F&& f, int gone_rc) {
-        std::lock_guard<std::timed_mutex> lk(mu);
-        const H c = h.load();
-        if (c == H{} || dead) return gone_rc;
-        return f(c);
-    }
-    template <class F>
-    void abort(F&& free_fn, int wait_ms) {
-        dead = true;  // uses that have not taken `mu` yet fail from here on
-        const bool locked = mu.try_lock_for(std::chrono::milliseconds(wait_ms));
-        if (H c = h.exchange(H{})) free_fn(c);
-        if (locked) mu.unlock();
-    }
-};
-
+// AbortOnce (pcx_sync.h): the handle, its bounded-wait abort and the overlap it may leave.
 struct RcclComm : Comm {
     AbortOnce<ncclComm_t> handle;
     static constexpr int ABORT_WAIT_MS = 2000;
@@ -326,52 +269,6 @@ int comm_rccl_all(int n, const int* devices, std::vector<Comm*>& out, std::strin
     return 0;
 }
 
-// CPU self-test of AbortOnce (the RCCL abort path without RCCL): `users` threads exchange in a
-// loop on a fake handle while `aborters` threads abort it.  Returns the number of violations
-// (a free that ran more or less than once, a use that saw a freed handle, a use that succeeded
-// after abort() returned), or -1 on a setup error.
-int selftest_abort_once(int users, int aborters, int iters) {
-    if (users < 1 || aborters < 1 || iters < 1 || users + aborters > 256) return -1;
-    struct Fake {
-        std::atomic<int> freed{0}, frees{0}, bad{0};
-    };
-    AbortOnce<Fake*> a;
-    Fake f;
-    a.h = &f;
-    std::atomic<bool> go{false}, aborted_done{false};
-    std::atomic<int> ok_after{0};
-    std::vector<std::thread> th;
-    for (int u = 0; u < users; u++)
-        th.emplace_back([&] {
-            while (!go) std::this_thread::yield();
-            for (int i = 0; i < iters; i++) {
-                const bool after = aborted_done;
-                const int rc = a.use(
-                    [&](Fake* p) {
-                        if (p->freed) p->bad++;  // the handle was freed while in use
-                        return 0;
-                    },
-                    1);
-                if (rc == 0 && after) ok_after++;  // a use that started after abort() returned succeeded
-            }
-        });
-    for (int k = 0; k < aborters; k++)
-        th.emplace_back([&, k] {
-            while (!go) std::this_thread::yield();
-            for (int i = 0; i < iters / 4 + k; i++) std::this_thread::yield();
-            a.abort(
-                [](Fake* p) {
-                    p->frees++;
-                    p->freed = 1;
-                },
-                ABORT_SELFTEST_WAIT_MS);
-            aborted_done = true;
-        });
-    go = true;
-    for (auto& t : th) t.join();
-    return (f.frees != 1) + f.bad + ok_after;
-}
-
 pcx_group* group_create(int world) {
     if (world < 1) return nullptr;
     pcx_group* g = new (std::nothrow) pcx_group;
@@ -388,10 +285,7 @@ void group_abort(pcx_group* g) {
 }
 
 void group_reset(pcx_group* g) {
-    if (!g) return;
-    std::lock_guard<std::mutex> lk(g->mu);
-    g->aborted = false;
-    g->arrived = 0;
+    if (g) g->reset();
 }
 
 Comm* comm_group(pcx_group* g, int rank, std::string& err) {

@@ -103,10 +103,16 @@ struct limbs3 {
     uint64_t l0, l1, l2;
 };
 
-// Each limb is an integer-valued double f in [0, 2^43): f + 2^52 holds f in its mantissa bits, so
+// Each limb is an integer-valued double f: f + 2^52 holds f in its mantissa bits while f < 2^52, so
 // one add and a mask convert it (the generic double -> uint64 conversion takes ~7 fp64 ops, three
 // times per element in the selection's weight-mode passes).  A NaN weight gives zero limbs, as the
 // generic conversion of NaN does.
+// Precondition (the caller's): 0 <= w < 2^8.  Then every limb is below 2^43 and sums of 2^21 limbs
+// fit a uint64.  Outside it the limbs are wrong -- f0 = floor(w 2^35) reaches 2^52 at w = 2^17,
+// and a negative w has no limbs at all -- so k_sel_start sends any event whose weights leave
+// [0, 2^8) (a negative reputation, or one above 256 times the total) to the exact replay in the
+// reference's order instead (pcx_matrix.hip, the weight-range test; tests/test_matrix_gpu.py
+// negative / large reputation cases).
 __device__ __forceinline__ uint64_t limb_bits(double f) {
     return (uint64_t)__double_as_longlong(f + 0x1p52) & 0xFFFFFFFFFFFFFull;
 }

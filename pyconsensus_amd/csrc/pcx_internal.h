@@ -281,7 +281,6 @@ struct Comm {
 Comm* comm_rccl(int device, int world, int rank, const pcx_comm_id* id, std::string& err);
 int comm_rccl_unique_id(pcx_comm_id* out, std::string& err);
 int rccl_version(int* runtime, int* compiled);
-int selftest_abort_once(int users, int aborters, int iters);
 Comm* comm_group(pcx_group* g, int rank, std::string& err);
 Comm* comm_custom(int world, int rank, const pcx_comm_ops* ops, std::string& err);
 // one communicator per listed device, all in this process (ncclCommInitAll); 0 = ok
@@ -314,6 +313,9 @@ struct pcx_ctx {
     // (pcx_ctx_progress: a watchdog names the stage a stuck call is in)
     std::atomic<int> progress_stage{-1};
     std::atomic<int> progress_wait{0};   // 1 while the host blocks on the stream
+    // test hook (pcx_test_inject_enomem): the round scheduler's worker k reports PCX_ENOMEM for
+    // its first round of the NEXT batched call, without running it; -1 = off; consumed by that call
+    int test_enomem_worker = -1;
 };
 
 namespace pcx {

@@ -2586,6 +2586,15 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
     }
     if (lane != 0) return;
     const uint64_t wminb = m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
+    // weights outside [0, 2^8) -- a negative reputation (rep / sum(rep) keeps its sign,
+    // __init__.py:142-145; smooth_rep inherits it, :472) or one above 256 times the total: the
+    // exact limbs hold only [0, 2^8) (pcx_device.h to_limbs), so replay in the reference's order.
+    // Over bit patterns (the MAX reduce): a sign bit, or [bits(256), bits(+inf)]; NaN keeps the
+    // limb path (NaN limbs are zero, as the generic conversion gives).
+    if (wsum && ((wmaxb >> 63) || (wmaxb >= 0x4070000000000000ull && wmaxb <= 0x7ff0000000000000ull))) {
+        mark_hard(m, s, st);
+        return;
+    }
     // count mode known up front (equal weights): the total only needs to be nonzero
     const L3 tot = wsum ? l3_norm({ta, tb, tc}) : L3{n && wmaxb ? 1ull : 0ull, 0, 0};
     if (!wsum && wminb != wmaxb) {  // (cannot happen: reputation=None gives one weight) exact replay
@@ -3359,9 +3368,8 @@ constexpr int HARD_TILE = 4096;
 
 __global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
     __shared__ double tile[HARD_TILE];
-    __shared__ double wmax_s;
-    __shared__ unsigned long long first_s;
-    __shared__ int pos_s;
+    __shared__ unsigned long long wkey_s, first_s;
+    __shared__ int pos_s, dom_s;
     const int j = blockIdx.x;
     const int c = h.cols[j];
     const int mode = h.modes[j];
@@ -3399,33 +3407,35 @@ __global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
     }
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     const double mid = 0.5 * block_serial_sum(n, [&](int64_t k) { return W[k]; }, tile, HARD_TILE);
-    // dominance: any(w > mid) -> data[first index of max(w)]; no positive weight -> None
+    // dominance: any(w > mid) -> data[first index of max(w)]; no positive weight -> None.
+    // Weights may be negative (a negative reputation): max over order-preserving keys.
     if (threadIdx.x == 0) {
-        wmax_s = 0.0;  // weights are >= 0: max over their bit patterns
+        wkey_s = 0;
         first_s = ~0ull;
         pos_s = 0;
+        dom_s = 0;
     }
     __syncthreads();
     double wl = -__builtin_inf();
-    int posl = 0;
+    int posl = 0, doml = 0;
     for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
         wl = fmax(wl, W[k]);
         posl |= W[k] > 0.0;
+        doml |= W[k] > mid;
     }
     wl = wave_max_d(wl);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax((unsigned long long*)&wmax_s, (unsigned long long)__double_as_longlong(wl < 0 ? 0.0 : wl));
-    }
+    if ((threadIdx.x & 63) == 0) atomicMax(&wkey_s, (unsigned long long)dkey(wl));
     if (posl) pos_s = 1;
+    if (doml) dom_s = 1;
     __syncthreads();
-    const double wmax = wmax_s;
-    for (int64_t k = threadIdx.x; k < n; k += blockDim.x)
-        if (W[k] == wmax) {
-            atomicMin(&first_s, (unsigned long long)k);
-            break;
-        }
-    __syncthreads();
-    if (wmax > mid) {
+    if (dom_s) {
+        const double wmax = dkey_inv(wkey_s);  // some W[k] > mid: the max is a finite element
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x)
+            if (W[k] == wmax) {
+                atomicMin(&first_s, (unsigned long long)k);
+                break;
+            }
+        __syncthreads();
         if (threadIdx.x == 0) {
             sel_done(st, X[first_s]);
             hs[2] = 0.0;

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "pcx_internal.h"
+#include "pcx_sync.h"
 
 namespace pcx {
 
@@ -103,19 +104,10 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
     for (pcx_ctx* w : c->pool) w->scaled_floor = max_scaled;  // one workspace serves every round's bounds
     std::vector<double> part(B), avg(B);
     std::vector<int32_t> branch(B), flags(B), iters(B), comps(B);
-    std::atomic<int64_t> next{0};
-    std::atomic<int> failed{0};
-    std::vector<std::string> errs(K);
-    std::vector<int> rcs(K, 0);
-    // a worker whose workspace does not fit (PCX_ENOMEM) leaves the pool and hands its round
-    // back: fewer rounds run in flight instead of the batch failing
-    std::mutex retry_mu;
-    std::vector<int64_t> retry;
-    std::atomic<int> alive{K};
-    // test hook: PCX_FAULT_ENOMEM_WORKER=k makes worker k's first round report PCX_ENOMEM
-    // without running, exercising the hand-back below (tests/test_rounds_gpu.py)
-    const char* fault_env = getenv("PCX_FAULT_ENOMEM_WORKER");
-    const int fault_k = fault_env ? atoi(fault_env) : -1;
+    // test hook (pcx_test_inject_enomem): worker k's first round reports PCX_ENOMEM without
+    // running, exercising the hand-back below (tests/test_rounds_gpu.py); one call only
+    const int fault_k = c->test_enomem_worker;
+    c->test_enomem_worker = -1;
     auto one = [&](pcx_ctx* w, int64_t b, std::string& werr) -> int {
             pcx_problem p{};
             p.n_rows = N;
@@ -171,37 +163,22 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
             comps[b] = r.components;
             return 0;
     };
-    auto worker = [&](int k) {
-        pcx_ctx* w = c->pool[k];
-        bool fault = k == fault_k;
-        for (;;) {
-            const int64_t b = next.fetch_add(1);
-            if (b >= B || failed.load()) return;
-            const int rc = fault ? PCX_ENOMEM : one(w, b, errs[k]);
-            fault = false;
-            if (rc == PCX_ENOMEM && alive.fetch_sub(1) > 1) {
-                workspace_free(w);
-                std::lock_guard<std::mutex> lk(retry_mu);
-                retry.push_back(b);
-                errs[k].clear();
-                return;
+    // a worker whose workspace does not fit (PCX_ENOMEM) leaves the pool and hands its round
+    // back: fewer rounds run in flight instead of the batch failing (pcx_sync.h)
+    std::vector<char> faulted(K, 0);
+    std::vector<int64_t> retry;
+    const int rc = schedule_rounds(
+        K, B, PCX_ENOMEM,
+        [&](int k, int64_t b, std::string& werr) -> int {
+            if (k == fault_k && !faulted[k]) {
+                faulted[k] = 1;
+                werr = "injected PCX_ENOMEM (pcx_test_inject_enomem)";
+                return PCX_ENOMEM;
             }
-            if (rc) {
-                rcs[k] = rc;
-                errs[k] = "round " + std::to_string(b) + ": " + errs[k];
-                failed.store(1);
-                return;
-            }
-        }
-    };
-    std::vector<std::thread> th;
-    for (int k = 0; k < K; k++) th.emplace_back(worker, k);
-    for (auto& t : th) t.join();
-    for (int k = 0; k < K; k++)
-        if (rcs[k]) {
-            err = errs[k];
-            return rcs[k];
-        }
+            return one(c->pool[k], b, werr);
+        },
+        [&](int k) { workspace_free(c->pool[k]); }, retry, err);
+    if (rc) return rc;
     // the handed-back rounds, one at a time on a context whose workspace is resident
     for (int64_t b : retry) {
         pcx_ctx* w = c->pool[0];
@@ -211,9 +188,9 @@ int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::stri
                 break;
             }
         std::string werr;
-        if (const int rc = one(w, b, werr)) {
+        if (const int rb = one(w, b, werr)) {
             err = "round " + std::to_string(b) + ": " + werr;
-            return rc;
+            return rb;
         }
     }
     (void)hipSetDevice(c->device);

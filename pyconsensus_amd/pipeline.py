@@ -349,9 +349,10 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
         setattr(res, k, outs[k].ctypes.data)
     h = _lib.context(device_index) if devices is None else _lib.devices_context(devices)
     rc = getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res))
-    if rc != 0 and devices is not None:
-        # a failing rank aborts every other rank's communicator, whatever its own status
-        # (ENOMEM, EHIP, a per-rank EINVAL): the context is unusable, so the next call makes a fresh one
+    if rc != 0 and devices is not None and not _lib.lib().pcx_ctx_usable(h):
+        # a rank failed mid-call and aborted every other rank's communicator: the context is
+        # unusable, so the next call makes a fresh one.  An argument error caught before any
+        # exchange leaves it usable (no costly ncclCommInitAll again).
         err = _lib.PcxError("libpcx error %d: %s" % (rc, _lib.lib().pcx_last_error().decode(errors="replace")))
         _lib.drop_devices_context(devices)
         raise err

@@ -147,10 +147,13 @@ def test_devices_context_survives_a_failed_call(gpu_lib):
     from pyconsensus_amd.pipeline import consensus_host
 
     R, sc, lo, hi, rep = synthetic.matrix(500, 40, seed=21)
+    h0 = _lib.devices_context([0, 0])
     with pytest.raises(_lib.PcxError, match="catch_tolerance"):
         consensus_host(R, rep, sc, lo, hi, devices=[0, 0], catch_tolerance=float("nan"))
     with pytest.raises(_lib.PcxError, match="one rank"):
         consensus_host(R, rep, sc, lo, hi, devices=[0, 0], algorithm="hierarchical")
+    # the argument errors came before any exchange: the cached context is kept, not recreated
+    assert _lib.devices_context([0, 0]) == h0 and _lib.lib().pcx_ctx_usable(h0) == 1
     two, m2 = consensus_host(R, rep, sc, lo, hi, devices=[0, 0])
     one, m1 = consensus_host(R, rep, sc, lo, hi)
     assert m2["branch"] == m1["branch"]

@@ -1,0 +1,143 @@
+"""Deterministic replay: the same inputs give the SAME
+bits twice, every output -- `original` and `filled` included -- for the single-matrix pipeline
+(int64 / LDS atomics in the selection and digit passes, split-K covariance slabs, cached
+workspace reused across calls of different shapes) and for both batched kernels.
+
+The outputs are compared on the device as raw 64-bit patterns (torch.equal on an int64 view), so
+a -0.0 / +0.0 flip or a different NaN payload counts as a difference.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_equal(a, b):
+    import torch
+
+    if a.dtype == torch.float64:
+        return torch.equal(a.view(torch.int64), b.view(torch.int64))
+    return torch.equal(a, b)
+
+
+def _assert_same(out1, out2, what):
+    assert out1.keys() == out2.keys()
+    bad = [k for k in out1 if not _bits_equal(out1[k], out2[k])]
+    assert not bad, "%s: outputs not bit-identical across replays: %s" % (what, bad)
+
+
+def _matrix_run(args, **kw):
+    from pyconsensus_amd.pipeline import consensus_matrix
+
+    ev, ag, meta = consensus_matrix(*args, matrices=True, **kw)
+    out = dict(ev)
+    out.update(ag)
+    scalars = {k: meta[k] for k in ("participation", "avg_certainty", "branch", "pi_iters", "flags", "n_hard",
+                                    "sel_passes", "grid_events", "mixed_int8")}
+    return out, scalars
+
+
+def _scalars_same(s1, s2, what):
+    for k in s1:
+        a, b = s1[k], s2[k]
+        same = (a == b) or (isinstance(a, float) and np.isnan(a) and np.isnan(b))
+        assert same, "%s: %s differs across replays (%r vs %r)" % (what, k, a, b)
+
+
+@pytest.mark.timeout(600)
+def test_matrix_replay_c5w_c4(gpu_lib):
+    """C5w (250k x 4096, reputation=None: int8 grid + 6-digit mixed blocks, equal-weight selection)
+    and C4 (100k x 1k, integer reputations: exact weight-limb selection and one hard-event replay)
+    each run twice; the C5w replay comes after C4 has re-used (and dirtied) the cached workspace."""
+    import torch
+
+    from pyconsensus_amd import synthetic
+
+    dev = torch.device("cuda", 0)
+    R, sc, lo, hi, _ = synthetic.matrix_device(250_000, 4096, seed=3, n_shards=8, device=dev)
+    c5w = (R, None, sc, lo, hi)
+    a1, s1 = _matrix_run(c5w, device=dev)
+    torch.cuda.synchronize(dev)
+
+    R4, sc4, lo4, hi4, rep4 = synthetic.matrix(100_000, 1000, seed=2)
+    t = lambda x, dt=torch.float64: torch.as_tensor(x, dtype=dt).to(dev)
+    c4 = (t(R4), t(rep4), t(sc4, torch.uint8), t(lo4), t(hi4))
+    b1, u1 = _matrix_run(c4, device=dev)
+    b2, u2 = _matrix_run(c4, device=dev)
+    torch.cuda.synchronize(dev)
+    _assert_same(b1, b2, "C4")
+    _scalars_same(u1, u2, "C4")
+    assert u1["n_hard"] >= 1  # the hard-event replay ran (and replayed identically)
+    del b1, b2
+
+    a2, s2 = _matrix_run(c5w, device=dev)
+    torch.cuda.synchronize(dev)
+    _assert_same(a1, a2, "C5w")
+    _scalars_same(s1, s2, "C5w")
+    assert s1["mixed_int8"] == 1 and s1["grid_events"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_matrix_replay_sharded(gpu_lib):
+    """Two virtual row shards (host-memory exchange): the per-rank partials and the rank-order
+    combination give the same bits on every replay."""
+    import threading
+
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.pipeline import ThreadComm, ThreadGroup, consensus_matrix, shard_rows
+
+    N, E, world = 40_000, 600, 2
+    R, sc, lo, hi, rep = synthetic.matrix(N, E, seed=5)
+    grp = ThreadGroup(world)
+    comms = [ThreadComm(grp, r) for r in range(world)]
+
+    def once():
+        res, errs = [None] * world, []
+
+        def worker(r):
+            try:
+                torch.cuda.set_device(0)
+                off, cnt = shard_rows(N, world, r)
+                ev, ag, meta = consensus_matrix(R[off:off + cnt], rep, sc, lo, hi, comm=comms[r], n_total=N,
+                                                row_offset=off, matrices=True)
+                torch.cuda.synchronize()
+                out = dict(ev)
+                out.update(ag)
+                res[r] = out
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+                grp.barrier.abort()
+
+        th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+        [x.start() for x in th]
+        [x.join() for x in th]
+        assert not errs, errs
+        return res
+
+    first, second = once(), once()
+    for r in range(world):
+        _assert_same(first[r], second[r], "rank %d" % r)
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("shape", [(50, 20, 65536), (100, 50, 2048)], ids=["C3_50x20_wave", "100x50_workgroup"])
+def test_batched_replay(gpu_lib, shape):
+    """The one-wave kernel over the full C3 batch and the workgroup-per-round kernel: every
+    output (original and filled included) bit-identical across two launches."""
+    import torch
+
+    from pyconsensus_amd import synthetic
+    from pyconsensus_amd.batched import consensus_batched
+
+    N, E, B = shape
+    dev = torch.device("cuda", 0)
+    R, sc, lo, hi, rep = synthetic.rounds(B, N, E, seed=11)
+    args = [torch.as_tensor(x).to(dev) for x in (R, rep, sc.astype(np.uint8), lo, hi)]
+    o1 = consensus_batched(*args, device=dev, filled=True, original=True)
+    o2 = consensus_batched(*args, device=dev, filled=True, original=True)
+    torch.cuda.synchronize(dev)
+    _assert_same(o1, o2, "batched %dx%d" % (N, E))

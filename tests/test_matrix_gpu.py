@@ -104,12 +104,31 @@ def _big_case(name):
         # binary events take the int8 covariance and the compact passes (k_gemv2_c / k_outcomes_c)
         N, E = name[:2]
         R, sc, lo, hi, rep = synthetic.matrix(N, E, seed=N + E)
-        if len(name) == 3:
+        if len(name) == 3 and name[2] is None:
             rep = None
+        elif len(name) == 3:
+            rep = _signed_reputation(rep, name[2], seed=N)
     b = synthetic.bounds_list(sc, lo, hi)
     ref = G.flat_result(OracleCPU(reports=R, event_bounds=b, reputation=rep).consensus())
     _REF[name] = (R, sc, lo, hi, rep, ref)
     return _REF[name]
+
+
+def _signed_reputation(rep, kind, seed):
+    """Reputations with negative entries (the reference takes any numbers: rep / sum(rep) keeps
+    the signs, __init__.py:142-145, and smooth_rep inherits them, :472), so the weighted medians'
+    weights leave [0, 1]: "neg" flips 10% of them; "big" balances the signs so that the total is
+    small and |rep / total| reaches the hundreds -- both beyond the exact weight limbs' [0, 2^8)
+    range, so the selection must replay those events in the reference's order."""
+    rng = np.random.default_rng(seed)
+    r = np.asarray(rep, dtype=np.float64).copy()
+    flip = rng.random(r.size) < 0.1
+    r[flip] = -r[flip]
+    if kind == "big":
+        r[: r.size // 2] = np.abs(r[: r.size // 2])
+        r[r.size // 2:] = -np.abs(r[r.size // 2:])
+        r[-1] += -r.sum() + 0.02 * np.abs(r).max()  # total = 2% of the largest entry
+    return r
 
 
 def _record(name, world, info):
@@ -180,10 +199,11 @@ def _abi_events():
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), "C4", "C5r", "C5r_1M",
-                                  "C5w"],
+@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), (20000, 80, "neg"),
+                                  (12000, 60, "big"), "C4", "C5r", "C5r_1M", "C5w"],
                          ids=["3000x150", "20000x400", "20008x400_ragged16",
-                              "16648x2048_repNone_ragged16_empty_chunks", "C4_100k_x_1k_intrep",
+                              "16648x2048_repNone_ragged16_empty_chunks", "20000x80_negative_rep",
+                              "12000x60_large_signed_rep", "C4_100k_x_1k_intrep",
                               "C5recipe_250k_x_1024_repNone",
                               "C5r_1M_x_1024_repNone", "C5width_250k_x_4096_repNone"])
 @pytest.mark.parametrize("world", [1, 2])

@@ -14,6 +14,7 @@
 #   shard        one 8-GPU C5 shard (125k x 4096) as a one-rank consensus (tools/c5_shard_latency.py)
 #   shard_prof   rocprofv3 kernel trace of the shard run (per-launch times: shard_kt/)
 #   dist         the 2-process tests and bench.py as the driver launches N=2 (gloo: both ranks on cuda:0)
+#   selfdist     bench.py --gpus 2 with no launcher (bench.py starts the ranks itself; gloo on cuda:0)
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
 #   ab_shard=L1,L2  one C5 shard's latency of several libpcx builds, alternating twice
@@ -86,6 +87,11 @@ for STEP in "$@"; do
           --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 1 --c5-steps 2 \
           --no-cpu-baseline > $O/bench2.json 2> $O/bench2.err || { echo "bench2 rc=$?"; tail -30 $O/bench2.err; exit 21; }
       c5_line $O/bench2.json "N=2 gloo" ;;
+    selfdist)  # bench.py --gpus 2 with NO launcher: it must start the 2 ranks itself (gloo: both on cuda:0)
+      PCX_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 1 --c5-steps 2 \
+          --no-cpu-baseline > $O/bench_self2.json 2> $O/bench_self2.err || { echo "selfdist rc=$?"; tail -30 $O/bench_self2.err; exit 30; }
+      python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); c=d['c5']; print('self-launched: n_gpus', d['n_gpus'], 'launcher', d['launcher'], 'devices', [x['device'] for x in d['devices']], '| C5 n_gpus', c['n_gpus'], 'comm', c['comm'], 'ctx_world', c['ctx_world'], 'rccl_world', c['rccl_world'])" $O/bench_self2.json
+      c5_line $O/bench_self2.json "N=2 self gloo" ;;
     ab_c3=*)
       IFS=, read -ra LIBS <<< "${STEP#ab_c3=}"
       for i in 1 2; do for L in "${LIBS[@]}"; do
