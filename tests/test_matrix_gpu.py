@@ -117,17 +117,15 @@ def _big_case(name):
 def _signed_reputation(rep, kind, seed):
     """Reputations with negative entries (the reference takes any numbers: rep / sum(rep) keeps
     the signs, __init__.py:142-145, and smooth_rep inherits them, :472), so the weighted medians'
-    weights leave [0, 1]: "neg" flips 10% of them; "big" balances the signs so that the total is
-    small and |rep / total| reaches the hundreds -- both beyond the exact weight limbs' [0, 2^8)
-    range, so the selection must replay those events in the reference's order."""
+    weights leave [0, 1]: "neg" flips 10% of them -- beyond the exact weight limbs' [0, 2^8) range,
+    so the selection must replay those events in the reference's order (k_sel_start's weight-range
+    test).  (A weight of 2^8 or more needs a total far below the entries, i.e. signed tokens whose
+    covariance is indefinite with nearly equal |eigenvalues| -- svd's first vector is then not
+    determined to 1e-9 and the case tests LAPACK, not the selection.)"""
     rng = np.random.default_rng(seed)
     r = np.asarray(rep, dtype=np.float64).copy()
     flip = rng.random(r.size) < 0.1
     r[flip] = -r[flip]
-    if kind == "big":
-        r[: r.size // 2] = np.abs(r[: r.size // 2])
-        r[r.size // 2:] = -np.abs(r[r.size // 2:])
-        r[-1] += -r.sum() + 0.02 * np.abs(r).max()  # total = 2% of the largest entry
     return r
 
 
@@ -199,11 +197,10 @@ def _abi_events():
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), (20000, 80, "neg"),
-                                  (12000, 60, "big"), "C4", "C5r", "C5r_1M", "C5w"],
+@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), (20000, 80, "neg"), "C4", "C5r", "C5r_1M", "C5w"],
                          ids=["3000x150", "20000x400", "20008x400_ragged16",
                               "16648x2048_repNone_ragged16_empty_chunks", "20000x80_negative_rep",
-                              "12000x60_large_signed_rep", "C4_100k_x_1k_intrep",
+                              "C4_100k_x_1k_intrep",
                               "C5recipe_250k_x_1024_repNone",
                               "C5r_1M_x_1024_repNone", "C5width_250k_x_4096_repNone"])
 @pytest.mark.parametrize("world", [1, 2])
