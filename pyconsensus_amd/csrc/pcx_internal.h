@@ -75,6 +75,7 @@ typedef struct {
     uint64_t* sel_arg;            /* [2][n_scaled] first dominant row (MIN), its value key (MAX) */
     int32_t*  sel_act;            /* [n_scaled] active scaled events, compacted in event order */
     int32_t*  hard;               /* [E] 0 / hard-replay mode per event (binary fill mean, median) */
+    int32_t *hard_cols, *hard_modes; /* [E] the marked events in event order (k_sel_compact / k_hard_list) */
     uint64_t* cbuf;               /* [n_scaled][ccap][2] compacted (key, weight bits) of the range (k_sel_hist) */
     int64_t*  ccount;             /* [n_scaled] compacted elements of this rank                    */
     int64_t   ccap;               /* compaction capacity per event (0: none)                       */

@@ -1269,8 +1269,16 @@ struct GramLoader {
     }
 };
 
+// the power iteration's mode from the covariance flags of M_COV_REDUCE / M_COV_FINISH, read on the
+// device so that M_POWER needs no host read before it launches: 0 iterate, 1 non-finite
+// covariance (LAPACK raises, H = ones, :331-333), 2 zero covariance (svd(0): U = I)
+__device__ __forceinline__ int pi_mode_of(int64_t flags) { return (flags & 2) ? 1 : (!(flags & 8) ? 2 : 0); }
+
 // out = A^T A = A A (A symmetric), lower tiles mirrored; atomically tracks max |out| bits
-__global__ void __launch_bounds__(256) k_gram(const double* A, int E, double* out, unsigned long long* maxbits) {
+// (nothing unless the power iteration runs: `flags` = &info[IN_FLAGS])
+__global__ void __launch_bounds__(256) k_gram(const double* A, int E, double* out, unsigned long long* maxbits,
+                                              const int64_t* flags) {
+    if (pi_mode_of(*flags) != 0) return;
     int I, J;
     tri_index(blockIdx.x, I, J);
     GramLoader ld{A, E};
@@ -1295,7 +1303,9 @@ __global__ void __launch_bounds__(256) k_gram(const double* A, int E, double* ou
     if (lane == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
 }
 
-__global__ void __launch_bounds__(BT) k_scale(double* M, int64_t n, const unsigned long long* maxbits) {
+__global__ void __launch_bounds__(BT) k_scale(double* M, int64_t n, const unsigned long long* maxbits,
+                                              const int64_t* flags) {
+    if (pi_mode_of(*flags) != 0) return;
     const double mx = __longlong_as_double(*maxbits);
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < n; i += (int64_t)gridDim.x * BT)
         M[i] = mx > 0.0 ? M[i] / mx : M[i];
@@ -1468,6 +1478,14 @@ __global__ void __launch_bounds__(1024) k_pi_start(pcx_mat m) {
     __shared__ int si[1024];
     __shared__ dd lds[16];
     const int E = (int)m.n_events;
+    if (pi_mode_of(m.info[IN_FLAGS]) != 0) {  // no iteration: the host's first poll sees "converged"
+        if (threadIdx.x == 0) {
+            pv_s(m)[0] = 0.0;
+            pv_s(m)[1] = 1.0;
+            pv_s(m)[2] = 0.0;
+        }
+        return;
+    }
     double best = -__builtin_inf();
     int bi = 0;
     for (int j = threadIdx.x; j < E; j += 1024) {
@@ -1518,7 +1536,7 @@ __global__ void __launch_bounds__(BT) k_pi_gemv(pcx_mat m, const double* M, int 
     const int E = (int)m.n_events;
     const int row = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
     const int lane = threadIdx.x % WAVE;
-    if (row >= E || (honor_done && pv_s(m)[1] != 0.0)) return;
+    if (row >= E || (honor_done && pv_s(m)[1] != 0.0) || pi_mode_of(m.info[IN_FLAGS]) != 0) return;
     const double* Cr = M + (int64_t)row * E;
     const double* x = pv_x(m);
     double acc = 0.0;
@@ -1534,6 +1552,7 @@ __global__ void __launch_bounds__(1024) k_pi_norm(pcx_mat m, int honor_done) {
     __shared__ double nrm;
     const int E = (int)m.n_events;
     if (honor_done && pv_s(m)[1] != 0.0) return;  // (uniform: every thread reads the same flag)
+    if (pi_mode_of(m.info[IN_FLAGS]) != 0) return;
     acc2 a;
     for (int j = threadIdx.x; j < E; j += 1024) {
         const double y = pv_y(m)[j];
@@ -1562,17 +1581,25 @@ __global__ void __launch_bounds__(1024) k_pi_norm(pcx_mat m, int honor_done) {
 }
 
 // loading (:336): sign rule of the batched SPEC, then v / sqrt(sum v^2)
-__global__ void __launch_bounds__(1024) k_pi_finish(pcx_mat m, int mode) {
+// (also the step count and flags of the result: info[IN_PI_ITERS], info[IN_FLAGS] = svd-fail 2 /
+// zero-covariance 1 / the host's iteration-cap bit 4 -- no host write, no sync after M_POWER)
+__global__ void __launch_bounds__(1024) k_pi_finish(pcx_mat m, int64_t iters, int64_t maxit_flag) {
     __shared__ dd lds[16];
-    __shared__ int first_nz, nnz;
+    __shared__ int first_nz, nnz, mode_s;
     __shared__ double scale;
     const int E = (int)m.n_events;
     double* x = pv_x(m);
     if (threadIdx.x == 0) {
         first_nz = E;
         nnz = 0;
+        mode_s = pi_mode_of(m.info[IN_FLAGS]);
     }
     __syncthreads();
+    const int mode = mode_s;
+    if (threadIdx.x == 0) {  // (every thread has its mode: info[IN_FLAGS] may be rewritten)
+        m.info[IN_PI_ITERS] = mode == 0 ? iters : 0;
+        m.info[IN_FLAGS] = mode == 1 ? 2 : (mode == 2 ? 1 : maxit_flag);
+    }
     for (int j = threadIdx.x; j < E; j += 1024) {
         double v = mode == 1 ? 1.0 : (mode == 2 ? (j == 0 ? 1.0 : 0.0) : x[j]);
         x[j] = v;
@@ -2746,6 +2773,18 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
         m.info[IN_SEL_ACTIVE] = cnt;
         m.info[IN_SEL_WACTIVE] = (int64_t)nw;
     }
+    // and the events marked for the exact replay so far (k_hard_list's list): after the pass that
+    // leaves no event active, the host's one read of info[IN_SEL_ACTIVE ..] also has their count
+    if (m.hard_cols) {
+        __syncthreads();  // (every thread has read block_compact's count before it is reset)
+        const int64_t nh = block_compact(
+            m.n_events, [&](int64_t c) { return m.hard[c] != HARD_NONE; },
+            [&](int64_t c, int64_t pos) {
+                m.hard_cols[pos] = (int32_t)c;
+                m.hard_modes[pos] = m.hard[c];
+            });
+        if (threadIdx.x == 0) m.info[IN_HARD] = nh;
+    }
 }
 
 // The first pass's window: a sample of the column (1 / SEL_SAMPLE of its rows, all ranks'
@@ -3345,18 +3384,63 @@ __global__ void __launch_bounds__(1024) k_hard_gather(pcx_mat m, HardArgs h) {
     if (threadIdx.x == 0) h.send_cnt[j] = n;
 }
 
-// sequential left-to-right fp64 sum of f(k), k in [0, n), by thread 0, fed through LDS
-// tiles loaded by the whole block (the add chain is the limit: ~10 cycles per element)
+// The hard replay's sequential fp64 chains (weightedstats' builtin sums and its walk) run on one
+// lane: a dependent add per element is the floor (~8 cycles).  The lane reads its operands from
+// an LDS tile in 16-element chunks, the next chunk's loads issued before the current chunk's adds,
+// so the LDS latency (~50-60 cycles) hides behind the chain instead of stalling it every 8
+// elements; the tiles are double-buffered: waves 1.. fill tile t+1 while lane 0 chains tile t.
+constexpr int CHAIN = 16;
+
+// acc + t[0] + t[1] + ... + t[len-1], left to right
+__device__ __forceinline__ double chain_add(const double* t, int len, double acc) {
+    double a[CHAIN], b[CHAIN];
+    int k = 0;
+    if (len >= CHAIN) {
+#pragma unroll
+        for (int j = 0; j < CHAIN; j++) a[j] = t[j];
+        for (; k + 2 * CHAIN <= len; k += 2 * CHAIN) {
+#pragma unroll
+            for (int j = 0; j < CHAIN; j++) b[j] = t[k + CHAIN + j];
+#pragma unroll
+            for (int j = 0; j < CHAIN; j++) acc = acc + a[j];
+            if (k + 3 * CHAIN <= len) {
+#pragma unroll
+                for (int j = 0; j < CHAIN; j++) a[j] = t[k + 2 * CHAIN + j];
+            }
+#pragma unroll
+            for (int j = 0; j < CHAIN; j++) acc = acc + b[j];
+        }
+        if (k + CHAIN <= len) {  // a chunk loaded into a[] and not yet added
+#pragma unroll
+            for (int j = 0; j < CHAIN; j++) acc = acc + a[j];
+            k += CHAIN;
+        }
+    }
+    for (; k < len; k++) acc = acc + t[k];
+    return acc;
+}
+
+// sequential left-to-right fp64 sum of f(k), k in [0, n): lane 0 chains, waves 1.. stage the
+// tiles (tile: 2 * TILE doubles of LDS)
 template <class F>
 __device__ double block_serial_sum(int64_t n, F f, double* tile, int TILE) {
     __shared__ double acc_s;
     double acc = 0.0;
-    for (int64_t t0 = 0; t0 < n; t0 += TILE) {
+    const int loaders = (int)blockDim.x - WAVE;
+    for (int k = threadIdx.x; k < TILE && k < n; k += blockDim.x) tile[k] = f(k);
+    __syncthreads();
+    int it = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += TILE, it++) {
         const int len = (int)(n - t0 < TILE ? n - t0 : TILE);
-        for (int k = threadIdx.x; k < len; k += blockDim.x) tile[k] = f(t0 + k);
-        __syncthreads();
-        if (threadIdx.x == 0)
-            for (int k = 0; k < len; k++) acc = acc + tile[k];
+        const double* cur = tile + (it & 1) * TILE;
+        double* nxt = tile + ((it + 1) & 1) * TILE;
+        if (threadIdx.x == 0) {
+            acc = chain_add(cur, len, acc);
+        } else if ((int)threadIdx.x >= WAVE) {
+            const int64_t n0 = t0 + TILE;
+            const int nl = (int)(n - n0 < TILE ? (n - n0 > 0 ? n - n0 : 0) : TILE);
+            for (int k = threadIdx.x - WAVE; k < nl; k += loaders) nxt[k] = f(n0 + k);
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) acc_s = acc;
@@ -3367,9 +3451,9 @@ __device__ double block_serial_sum(int64_t n, F f, double* tile, int TILE) {
 constexpr int HARD_TILE = 4096;
 
 __global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
-    __shared__ double tile[HARD_TILE];
+    __shared__ double tile[2 * HARD_TILE];
     __shared__ unsigned long long wkey_s, first_s;
-    __shared__ int pos_s, dom_s;
+    __shared__ int pos_s, dom_s, neg_s;
     const int j = blockIdx.x;
     const int c = h.cols[j];
     const int mode = h.modes[j];
@@ -3414,15 +3498,18 @@ __global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
         first_s = ~0ull;
         pos_s = 0;
         dom_s = 0;
+        neg_s = 0;
     }
     __syncthreads();
     double wl = -__builtin_inf();
-    int posl = 0, doml = 0;
+    int posl = 0, doml = 0, negl = 0;
     for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
         wl = fmax(wl, W[k]);
         posl |= W[k] > 0.0;
         doml |= W[k] > mid;
+        negl |= W[k] < 0.0;
     }
+    if (negl) neg_s = 1;
     wl = wave_max_d(wl);
     if ((threadIdx.x & 63) == 0) atomicMax(&wkey_s, (unsigned long long)dkey(wl));
     if (posl) pos_s = 1;
@@ -3458,6 +3545,7 @@ __global__ void __launch_bounds__(1024) k_hard_prep(pcx_mat m, HardArgs h) {
         hs[0] = mid;
         hs[1] = (double)n;
         hs[2] = 1.0;  // sort + walk pending
+        hs[3] = neg_s ? 1.0 : 0.0;  // some weight < 0: the walk's partial sums are not monotone
     }
 }
 
@@ -3524,7 +3612,8 @@ __global__ void __launch_bounds__(BT) k_bsort_global(uint64_t* keys, int64_t P, 
 
 // the walk (:weighted_median while loop) over the sorted pairs of each pending event
 __global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
-    __shared__ double tw[HARD_TILE];
+    constexpr int TWS = HARD_TILE + 2 * CHAIN;  // a tile and the padding the chain's prefetch reads
+    __shared__ double tw[2 * TWS];
     __shared__ int done_s;
     __shared__ int64_t k_s;
     __shared__ double cum_s;
@@ -3536,26 +3625,77 @@ __global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
     const uint64_t* keys = h.keys + (int64_t)j * h.P * 2;
     const double mid = hs[0];
     const int64_t n = (int64_t)hs[1];
+    const bool monotone = hs[3] == 0.0;  // every weight >= 0: a chunk's last partial is its largest
     if (threadIdx.x == 0) {
         done_s = 0;
         k_s = 0;
         cum_s = 0.0;
     }
+    for (int k = threadIdx.x; k < HARD_TILE && k < n; k += blockDim.x) tw[k] = dkey_inv(keys[2 * k + 1]);
     __syncthreads();
-    // cum += w while cum <= mid, tile by tile
-    for (int64_t t0 = 0; t0 < n && !done_s; t0 += HARD_TILE) {
+    // cum += w while cum <= mid (weightedstats' walk; mid > 0 here, so the first add always runs):
+    // lane 0 adds a chunk's weights unconditionally -- partial sums up to the first one above mid
+    // are exactly the walk's -- then finds that first one; waves 1.. stage the next tile meanwhile
+    const int loaders = (int)blockDim.x - WAVE;
+    int it = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += HARD_TILE, it++) {
         const int len = (int)(n - t0 < HARD_TILE ? n - t0 : HARD_TILE);
-        for (int k = threadIdx.x; k < len; k += 1024) tw[k] = dkey_inv(keys[2 * (t0 + k) + 1]);
-        __syncthreads();
+        const double* cur = tw + (it & 1) * TWS;
+        double* nxt = tw + ((it + 1) & 1) * TWS;
         if (threadIdx.x == 0) {
-            double cum = cum_s;
-            int k = 0;
-            while (cum <= mid && k < len) cum += tw[k++];
-            cum_s = cum;
-            k_s = t0 + k;
-            if (cum > mid) done_s = 1;
+            // static register indices only (a dynamic p[hit] sends the array to scratch); the tiles
+            // are padded by 2 CHAIN so the next chunk's loads need no bounds test
+            double cum = cum_s, hit_cum = 0.0;
+            int hit_at = -1;
+            double nv[CHAIN];
+#pragma unroll
+            for (int q = 0; q < CHAIN; q++) nv[q] = cur[q];
+            for (int k = 0; k < len; k += CHAIN) {
+                double v[CHAIN], p[CHAIN];
+#pragma unroll
+                for (int q = 0; q < CHAIN; q++) v[q] = k + q < len ? nv[q] : 0.0;  // + 0.0 keeps the sum
+#pragma unroll
+                for (int q = 0; q < CHAIN; q++) nv[q] = cur[k + CHAIN + q];  // the next chunk, in flight
+                double acc = cum;
+#pragma unroll
+                for (int q = 0; q < CHAIN; q++) {
+                    acc = acc + v[q];
+                    p[q] = acc;
+                }
+                if (monotone && !(acc > mid)) {  // no partial of this chunk exceeds mid
+                    cum = acc;
+                    continue;
+                }
+                int h = -1;
+                double hc = 0.0;
+#pragma unroll
+                for (int q = CHAIN - 1; q >= 0; q--)
+                    if (p[q] > mid) {  // (padded partials repeat the last real one)
+                        h = q;
+                        hc = p[q];
+                    }
+                if (h >= 0) {
+                    hit_at = k + h;
+                    hit_cum = hc;
+                    break;
+                }
+                cum = acc;
+            }
+            if (hit_at >= 0) {
+                cum_s = hit_cum;
+                k_s = t0 + hit_at + 1;
+                done_s = 1;
+            } else {
+                cum_s = cum;
+                k_s = t0 + len;
+            }
+        } else if ((int)threadIdx.x >= WAVE) {
+            const int64_t n0 = t0 + HARD_TILE;
+            const int nl = (int)(n - n0 < HARD_TILE ? (n - n0 > 0 ? n - n0 : 0) : HARD_TILE);
+            for (int k = threadIdx.x - WAVE; k < nl; k += loaders) nxt[k] = dkey_inv(keys[2 * (n0 + k) + 1]);
         }
         __syncthreads();
+        if (done_s) break;
     }
     if (threadIdx.x == 0) {
         double res;
@@ -4826,18 +4966,13 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         case M_POWER: {
             // replicated on every rank (C is identical everywhere); host loop with polling.  The
-            // finite / non-zero flags of C come from M_COV_REDUCE (one rank) or M_COV_FINISH
-            int64_t flags = 0;
-            hipError_t e = hipMemcpyAsync(&flags, &m.info[IN_FLAGS], sizeof(flags), hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) return e;
-            int mode = 0;
+            // finite / non-zero flags of C come from M_COV_REDUCE (one rank) or M_COV_FINISH and are
+            // read by the kernels themselves (pi_mode_of): a non-finite or zero covariance makes every
+            // launch below return at once and the first poll see "converged"
             int iters = 0;
-            if (flags & 2) {
-                mode = 1;  // non-finite covariance: LAPACK raises, H = ones (:331-333)
-            } else if (!(flags & 8)) {
-                mode = 2;  // zero covariance: svd(0) -> U = I
-            } else {
+            int64_t maxit_flag = 0;
+            {
+                hipError_t e = hipSuccess;
                 hipLaunchKernelGGL(k_pi_start, dim3(1), dim3(1024), 0, st, m);
                 const int gb = (E + BT / WAVE - 1) / (BT / WAVE);
                 const int nb = (E + CT - 1) / CT;
@@ -4848,11 +4983,12 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 const double* M = m.C;
                 double* Tm = m.Mw;
                 unsigned long long* mxb = (unsigned long long*)&m.info[8];
+                const int64_t* fl = &m.info[IN_FLAGS];
                 auto square = [&]() {
                     (void)hipMemsetAsync(mxb, 0, sizeof(unsigned long long), st);
-                    hipLaunchKernelGGL(k_gram, dim3(ntri), dim3(256), 0, st, M, E, Tm, mxb);
+                    hipLaunchKernelGGL(k_gram, dim3(ntri), dim3(256), 0, st, M, E, Tm, mxb, fl);
                     hipLaunchKernelGGL(k_scale, dim3(grid_rows(nn2, BT)), dim3(BT), 0, st, Tm, nn2,
-                                       (const unsigned long long*)mxb);
+                                       (const unsigned long long*)mxb, fl);
                     const double* sq_out = Tm;
                     Tm = (Tm == m.Mw) ? m.Mw + nn2 : m.Mw;
                     M = sq_out;
@@ -4886,7 +5022,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                         since = 0;
                     }
                 }
-                if (!(ps[0] <= PI_TOL_M)) flags |= 4;
+                if (!(ps[0] <= PI_TOL_M)) maxit_flag = 4;
                 if (sq > 0)  // polish with C itself (after squarings)
                     for (int k = 0; k < 4; k++) {
                         hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m, (const double*)m.C, 0);
@@ -4894,11 +5030,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                     }
                 iters += (sq > 0 ? 4 : 0) + sq;
             }
-            hipLaunchKernelGGL(k_pi_finish, dim3(1), dim3(1024), 0, st, m, mode);
-            int64_t info2[2] = {iters, (int64_t)((mode == 1 ? 2 : 0) | (mode == 2 ? 1 : 0) | (flags & 4))};
-            e = hipMemcpyAsync(&m.info[IN_PI_ITERS], info2, sizeof(info2), hipMemcpyHostToDevice, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_pi_finish, dim3(1), dim3(1024), 0, st, m, (int64_t)iters, maxit_flag);
             break;
         }
         case M_MATRICES:

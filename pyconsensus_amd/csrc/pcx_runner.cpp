@@ -355,11 +355,16 @@ int64_t pow2_at_least(int64_t n) {
 }
 
 // events whose decision is rounding-decided: replay the reference's own float order
-void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
-    R.mark(M_HARD_LIST);
-    R.hip(hard_list(m, w->hard_cols, w->hard_modes, R.st), "k_hard_list");
-    R.mark(-1);
-    const int64_t H = R.read(m.info + INFO_HARD);
+// known_H >= 0: the selection's last read already returned the count (k_sel_compact lists the
+// marked events every pass), so no list launch and no host read here
+void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res, int64_t known_H = -1) {
+    int64_t H = known_H;
+    if (H < 0) {
+        R.mark(M_HARD_LIST);
+        R.hip(hard_list(m, w->hard_cols, w->hard_modes, R.st), "k_hard_list");
+        R.mark(-1);
+        H = R.read(m.info + INFO_HARD);
+    }
     if (H <= 0) return;
     res->n_hard += (int32_t)H;
     const int64_t N = m.n_total, cap = std::max<int64_t>(1, m.n_rows);
@@ -434,6 +439,7 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res) {
 void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
     m.sel_phase = phase;
     const int S = m.n_scaled;
+    int64_t known_H = -1;
     if (!R.comm && m.n_rows <= SEL_EXACT_MAX) {
         // small matrices: replay the reference's float walk directly
         if (S) R.stage(m, M_SEL_EXACT);
@@ -464,6 +470,7 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         R.hip(hipMemcpyAsync(inf5, m.info + INFO_SEL_ACTIVE, sizeof(inf5), hipMemcpyDeviceToHost, R.st), "D2H");
         R.sync();
         int64_t active = inf5[0], wactive = inf5[4];
+        known_H = inf5[3];
         if (inf5[1] > 0) {  // dominant weights: the first row holding the max weight (all ranks)
             R.stage(m, M_SEL_ARGMAX);
             R.allreduce(w->sel_arg, S, PCX_U64, PCX_MIN);
@@ -493,11 +500,12 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
             R.sync();
             active = inf5[0];
             wactive = inf5[4];
+            known_H = inf5[3];
             passes++;
         }
         res->sel_passes += passes;
     }
-    hard_replay(R, m, w, res);
+    hard_replay(R, m, w, res, known_H);
     if (S) R.stage(m, M_SEL_FINISH);
 }
 
@@ -815,6 +823,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.sel_arg = w->sel_arg;
         m.sel_act = w->sel_act;
         m.hard = w->hard;
+        m.hard_cols = w->hard_cols;
+        m.hard_modes = w->hard_modes;
         m.cbuf = w->ccap > 0 ? w->cbuf : nullptr;
         m.ccount = w->ccount;
         m.ccap = w->ccap;
@@ -965,10 +975,13 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 }
                 R.stage(m, M_COV_FINISH);
                 R.stage(m, M_POWER);
-                flags = R.read(m.info + INFO_FLAGS);
                 // big-five / fixed-variance components (:373-390, :429-451); a non-finite
-                // covariance makes the reference's second svd raise (Oracle: LinAlgError)
-                if (entry != 2 && alg != PCX_ALG_PCA && !clustering && !(flags & PCX_FLAG_SVD_FAIL)) R.stage(m, M_EIG);
+                // covariance makes the reference's second svd raise (Oracle: LinAlgError).  (PCA
+                // needs no flags on the host here: no read, no sync)
+                if (entry != 2 && alg != PCX_ALG_PCA && !clustering) {
+                    flags = R.read(m.info + INFO_FLAGS);
+                    if (!(flags & PCX_FLAG_SVD_FAIL)) R.stage(m, M_EIG);
+                }
             } else {
                 R.stage(m, M_ZERO_LOADING);
             }
