@@ -257,7 +257,12 @@ typedef struct {
     /* [E] -- result["events"] (identical on every rank) */
     double *adj_first_loadings, *outcomes_raw, *outcomes_adjusted, *outcomes_final, *certainty,
         *consensus_reward, *nas_filled, *participation_columns, *author_bonus;
-    /* [n_rows][E], optional: result["original"] (rescaled reports), result["filled"] */
+    /* [n_rows][E], optional: result["original"] (rescaled reports), result["filled"].
+     * original == (double*)problem.reports (the same pointer) is the reference's own aliasing
+     * (__init__.py:121, 266-269, 584: `original` IS the caller's array, rescaled in place): the
+     * scaled columns of the reports are then rescaled in place and the other columns are left as
+     * they are, which saves writing a copy of the whole matrix (pcx_consensus_f64 and
+     * pcx_interpolate_f64; the reports buffer must then be writable). */
     double *original, *filled;
     /* wpca intermediates (:317-326), optional: [E] weighted_mean, [E][E] covariance_matrix */
     double *weighted_mean, *covariance;

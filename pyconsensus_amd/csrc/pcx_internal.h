@@ -110,6 +110,10 @@ typedef struct {
     double*  Fg;                  /* [wcd_rows][128 cov_jb] the filled F of the general positions (or NULL) */
     uint16_t* nam;                /* [wcd_rows/16][wcd_ld] missing-report bits of 16 rows per position */
     int32_t  compact;             /* M_GEMV2 / M_OUTCOMES read Fg, zB and nam, not the reports      */
+    int32_t  orig_inplace;        /* result.original aliases the reports: rescale the scaled columns
+                                     in place (k_wcd / k_matrices), nothing else written (Q2)       */
+    int32_t  rescaled;            /* set once that ran: later readers take the scaled columns as
+                                     already rescaled (col_param: identity)                          */
     /* mixed pairs: w of the general positions (< 128 cov_jb) in 8 balanced int8 digits of 7 bits,
        fixed point at 2^e with e from the column's |F - mu| bound (exact, M_COV_PLAN) */
     int8_t*  zD;                  /* [wcd_rows/16][zd_ld][16] digit s of position q at s * 128 cov_jb + q */

@@ -98,7 +98,7 @@ __device__ __forceinline__ bool missing(double x) { return __builtin_isnan(x) ||
 
 __device__ __forceinline__ ColParam col_param(const pcx_mat& m, int c, bool with_fill) {
     ColParam p;
-    p.scaled = m.scaled && m.scaled[c];
+    p.scaled = m.scaled && m.scaled[c] && !m.rescaled;  // (in place already: the identity)
     p.lo = p.scaled ? m.lo[c] : 0.0;
     p.range = p.scaled ? (m.hi[c] - m.lo[c]) : 1.0;
     p.guess = with_fill ? m.ev[EV_GUESS * m.n_events + c] : 0.0;
@@ -1010,6 +1010,15 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                         // block) for k_syrk / k_scores_grid / k_digits (centring the compact Fg on
                         // the fly instead writes 8 GB less at C5, but k_syrk then runs 26 ms, not 18)
                         if (pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb)) m.wcd[i * ld + pos[k]] = w[k];
+                    }
+                    // in place (result["original"] aliases the reports, as the reference's own does,
+                    // __init__.py:121, 266-269, 584): only the scaled columns change -- the rescaled
+                    // value over the report this thread just read
+                    if (live && m.orig_inplace) {
+                        double* rw = const_cast<double*>(m.reports) + i * E + c0;
+#pragma unroll
+                        for (int k = 0; k < 2; k++)
+                            if (ok[k] && p[k].scaled) rw[k] = xo[k];
                     }
                     // result["original"] / result["filled"] (:266-313), event order
                     if (live && (m.original || m.filled)) {
@@ -3902,6 +3911,7 @@ __global__ void __launch_bounds__(BT) k_matrices(pcx_mat m) {
         [&](int64_t i, double v) {
             const double x = rescale(v, p, m.int_dtype);
             if (m.original) m.original[i * E + c] = x;
+            if (m.orig_inplace && p.scaled) const_cast<double*>(m.reports)[i * E + c] = x;
             if (m.filled) m.filled[i * E + c] = missing(x) ? p.guess : x;
         });
 }

@@ -757,7 +757,16 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.nas_filled = cons ? out(r->nas_filled, E) : nullptr;
         m.participation_columns = cons ? out(r->participation_columns, E) : nullptr;
         m.author_bonus = cons ? out(r->author_bonus, E) : nullptr;
-        m.original = (cons || entry == 1) ? out(r->original, n_rows * E) : nullptr;
+        // result.original aliasing the reports (the same pointer): the reference's own `original` is
+        // the caller's array rescaled in place (__init__.py:121, 266-269, 584, Q2) -- rescale the
+        // scaled columns in place instead of writing a copy of every column (host memory: the
+        // device copy of the reports is rescaled and copied back into the caller's array)
+        const bool inplace = (cons || entry == 1) && r->original &&
+                             (const void*)r->original == (const void*)p->reports;
+        m.original = (cons || entry == 1) && !inplace ? out(r->original, n_rows * E) : nullptr;
+        m.orig_inplace = inplace ? 1 : 0;
+        m.rescaled = 0;
+        if (inplace && host) outs.push_back({r->original, const_cast<double*>(reports), n_rows * E});
         m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
         m.weighted_mean = entry == 2 ? out(r->weighted_mean, E) : nullptr;
         m.nc_out = entry == 4 ? out(nc_out, n_rows) : nullptr;
@@ -965,6 +974,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 }
                 R.stage(m, M_WCD);
                 mats_written = true;
+                m.rescaled = m.orig_inplace;  // later stages read the scaled columns rescaled already
                 R.stage(m, M_COV);
                 R.stage(m, M_COV_I8);
                 R.stage(m, M_COV_REDUCE);

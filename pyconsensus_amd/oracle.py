@@ -243,8 +243,11 @@ class Oracle(object):
             ckw = {}
             if self.algorithm in _abi.CLUSTER_ALGORITHMS:  # one GPU (the clusterings do not shard)
                 ckw = dict(hierarchy_threshold=self.hierarchy_threshold)
+            # Q2 without a host copy: when the caller's float64 array is the one the library reads,
+            # `original` aliases it and libpcx rescales its scaled columns in place (else `original`
+            # aliases this Oracle's own float64 copy)
             g, meta = consensus_host(self._data, self._rep_raw, sc, lo, hi, device_index=self._device_index(),
-                                     aux_scores=aux,
+                                     aux_scores=aux, original_inplace=True,
                                      devices=None if self.algorithm in _abi.CLUSTER_ALGORITHMS else self.devices,
                                      **ckw, **{k: v for k, v in kw.items() if k != "device"})
             participation = float(meta["participation"])
@@ -305,8 +308,8 @@ class Oracle(object):
         if self._int_dtype:  # int64 storage truncates (Q3)
             original = original.astype(np.int64)
             filled = filled.astype(np.int64)
-        if self._caller is not None:  # Q2: the caller's float array carries the rescaled values
-            self._caller[...] = g["original"]
+        if self._caller is not None and not np.shares_memory(self._caller, g["original"]):
+            self._caller[...] = g["original"]  # Q2: the caller's float array carries the rescaled values
         self.reports = np.ma.masked_array(original, self.reports.mask)
         ints = self._int_dtype
         cnt = (lambda a: [int(x) for x in a]) if ints else (lambda a: [float(x) for x in a])

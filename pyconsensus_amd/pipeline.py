@@ -235,7 +235,7 @@ def _shape_args(n_rows, comm, n_total, row_offset):
 def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, catch_tolerance=0.1,
                      alpha=0.1, int_dtype=False, algorithm="PCA", comm=None, n_total=None,
                      row_offset=None, device=None, matrices=False, profile=None, max_components=5,
-                     variance_threshold=0.9, aux_scores=None):
+                     variance_threshold=0.9, aux_scores=None, original_inplace=False):
     """Consensus of one report matrix on the GPU(s), device-resident (torch tensors).
 
     reports:    this rank's rows, (n_rows, E) float64 (torch tensor on the GPU, or numpy)
@@ -243,6 +243,10 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     scaled/lo/hi: event bounds (E,), or None (every event binary)
     comm:       :class:`Comm` (default: single GPU); sharded calls also give n_total, row_offset
     matrices:   also return this rank's rescaled ("original") and filled reports
+    original_inplace: with ``matrices``, ``original`` IS ``reports`` rescaled in place -- the
+                reference's own aliasing (__init__.py:121, 266-269, 584) -- instead of a new
+                tensor: only the scaled columns are written.  ``reports`` must then be a
+                contiguous float64 tensor on ``device`` (it is modified)
     profile:    optional dict; receives per-stage device milliseconds (HIP events on the
                 launching stream, pcx_profile_read) under the stage names of libpcx
     algorithm:  "PCA", "absolute", "big-five" (max_components, capped at E), "fixed-variance"
@@ -272,7 +276,12 @@ def consensus_matrix(reports, reputation=None, scaled=None, lo=None, hi=None, ca
     out = {k: z(n_rows) for k in _abi.MAT_OUTPUT_AGENTS}
     out.update({k: z(E) for k in _abi.MAT_OUTPUT_EVENTS})
     if matrices:
-        out["original"], out["filled"] = z(n_rows, E), z(n_rows, E)
+        if original_inplace:
+            if not (isinstance(reports, t.Tensor) and reports.data_ptr() == R.data_ptr()):
+                raise ValueError("original_inplace needs the reports as a contiguous float64 tensor on the device")
+            out["original"], out["filled"] = R, z(n_rows, E)
+        else:
+            out["original"], out["filled"] = z(n_rows, E), z(n_rows, E)
     res = _abi.Result()
     for k, v in out.items():
         setattr(res, k, v.data_ptr())
@@ -311,7 +320,7 @@ def _meta(res, algorithm):
 def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outputs, catch_tolerance=0.1,
                alpha=0.1, int_dtype=False, algorithm="PCA", max_components=5, variance_threshold=0.9,
                aux_scores=None, extra=(), devices=None, hierarchy_threshold=0.5, cluster_threshold=None,
-               kmeans_init=None):
+               kmeans_init=None, original_inplace=False):
     """Call a single-matrix entry point with numpy inputs / outputs (PCX_MEM_HOST: libpcx
     copies in and out).  ``outputs``: {result field: shape}.  ``devices``: a list of device
     ids -- libpcx shards the rows over them (pcx_create_devices), else one GPU."""
@@ -319,6 +328,8 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
     R = np.ascontiguousarray(reports, dtype=np.float64)
     n_rows, E = R.shape
     keep = [R]
+    if original_inplace and R is not reports:
+        raise ValueError("original_inplace needs the reports as a C-contiguous float64 ndarray")
 
     def ptr(a, dt):
         if a is None:
@@ -345,7 +356,9 @@ def _host_call(fn_name, reports, reputation, scaled, lo, hi, device_index, outpu
     res = _abi.Result()
     outs = {}
     for k, shape in outputs.items():
-        outs[k] = np.empty(shape, dtype=np.float64)
+        # original_inplace: `original` is the reports array itself (pcx_result.original aliasing
+        # pcx_problem.reports: the library rescales its scaled columns in place)
+        outs[k] = R if (k == "original" and original_inplace) else np.empty(shape, dtype=np.float64)
         setattr(res, k, outs[k].ctypes.data)
     h = _lib.context(device_index) if devices is None else _lib.devices_context(devices)
     rc = getattr(_lib.lib(), fn_name)(h, C.byref(prob), *extra, C.byref(res))
