@@ -356,6 +356,11 @@ int pcx_selftest_group_abort(int world, int steps, int fail_rank, int fail_step)
  * first round (-1: none) and must hand it back; round `fail_round` fails (-1: none) and must stop
  * the batch.  Every round must run exactly once.  Returns the number of violations. */
 int pcx_selftest_rounds_sched(int workers, int64_t rounds, int enomem_worker, int64_t fail_round);
+/* CPU self-test of the host-memory path's staged large copies (pinned slots, host threads):
+ * `bytes` through `slots` slots of `chunk` bytes by `threads` threads, memcpy standing in for the
+ * DMA; chunk `fail_chunk`'s transfer fails (-1: none) and must stop the copy.  Returns the number
+ * of violations (data, a chunk moved twice or after the failure); 0 = pass, -1 = bad arguments. */
+int pcx_selftest_chunked_copy(int64_t bytes, int64_t chunk, int slots, int threads, int64_t fail_chunk);
 /* Test hook: the NEXT pcx_consensus_batched_f64 call on `ctx` that takes the round scheduler
  * makes its worker `worker` report PCX_ENOMEM for its first round without running it (the
  * hand-back path); -1 clears it.  Consumed by that call.  For the tests only. */

@@ -67,6 +67,7 @@ def _declare(lib):
         ("pcx_selftest_abort_slow_holder", i32, [i32, i32]),
         ("pcx_selftest_group_abort", i32, [i32, i32, i32, i32]),
         ("pcx_selftest_rounds_sched", i32, [i32, i64, i32, i64]),
+        ("pcx_selftest_chunked_copy", i32, [i64, i64, i32, i32, i64]),
         ("pcx_test_inject_enomem", i32, [vp, i32]),
     ]:
         f = getattr(lib, name)

@@ -188,6 +188,7 @@ void pcx_destroy(pcx_ctx* ctx) {
     if (ctx->group) pcx::group_destroy(ctx->group);
     pcx::rounds_free(ctx);
     if (ctx->mscr) (void)hipFree(ctx->mscr);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
     delete ctx->comm;
@@ -293,6 +294,7 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
             const size_t need = per * (size_t)chunk;
             if (ctx->mscr_bytes < need) {
                 if (ctx->mscr) (void)hipFree(ctx->mscr);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
                 ctx->mscr = nullptr;
                 ctx->mscr_bytes = 0;
                 e = hipMalloc(&ctx->mscr, need);
@@ -569,6 +571,9 @@ int pcx_selftest_group_abort(int world, int steps, int fail_rank, int fail_step)
 }
 int pcx_selftest_rounds_sched(int workers, int64_t rounds, int enomem_worker, int64_t fail_round) {
     return pcx::selftest_rounds_sched(workers, rounds, enomem_worker, fail_round);
+}
+int pcx_selftest_chunked_copy(int64_t bytes, int64_t chunk, int slots, int threads, int64_t fail_chunk) {
+    return pcx::selftest_chunked_copy(bytes, chunk, slots, threads, fail_chunk);
 }
 int pcx_test_inject_enomem(pcx_ctx* ctx, int worker) {
     if (!ctx) return fail(PCX_EINVAL, "pcx_test_inject_enomem: null context");

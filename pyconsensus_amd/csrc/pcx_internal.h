@@ -321,6 +321,9 @@ struct pcx_ctx {
     // test hook (pcx_test_inject_enomem): the round scheduler's worker k reports PCX_ENOMEM for
     // its first round of the NEXT batched call, without running it; -1 = off; consumed by that call
     int test_enomem_worker = -1;
+    // pinned staging slots of the host-memory path's large output copies (pcx_runner.cpp)
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
 };
 
 namespace pcx {

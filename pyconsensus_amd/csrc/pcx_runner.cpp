@@ -16,12 +16,15 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "pcx_internal.h"
+#include "pcx_sync.h"
 
 namespace {
 constexpr int BT = 256;
@@ -347,6 +350,62 @@ struct Io {
         return (double*)p;
     }
 };
+
+// Device -> pageable host copy of a large output (the host-memory path's `filled` / `original`,
+// 33 GB each at C5).  A plain hipMemcpy stages it through the runtime's pinned buffer on one
+// thread, where the destination's first-touch page faults also land: 17-26 GB/s measured for C5's
+// outputs (tools/c5_host_latency.py).  Here the DMA of chunk k+1 runs into a pinned slot while
+// host threads move chunk k into place (chunked_copy, pcx_sync.h), so PCIe and the page faults
+// overlap and the faults spread over the threads.
+constexpr size_t STAGE_CHUNK = (size_t)64 << 20;
+constexpr int STAGE_SLOTS = 3;
+constexpr size_t STAGE_MIN = (size_t)256 << 20;  // smaller copies: one hipMemcpyAsync
+
+int host_threads() {
+    int t = 0;
+    if (const char* e = getenv("OMP_NUM_THREADS")) t = atoi(e);  // the job's host-core share (16 per GPU on the pool)
+    if (t < 1) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 16));
+}
+
+void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
+    pcx_ctx* c = R.c;
+    const size_t need = STAGE_CHUNK * STAGE_SLOTS;
+    if (c->pinned_bytes < need) {
+        if (c->pinned) (void)hipHostFree(c->pinned);
+        c->pinned = nullptr;
+        c->pinned_bytes = 0;
+        R.hip(hipHostMalloc(&c->pinned, need, hipHostMallocDefault), "hipHostMalloc(staging)");
+        c->pinned_bytes = need;
+    }
+    hipEvent_t ev[STAGE_SLOTS];
+    for (int k = 0; k < STAGE_SLOTS; k++) R.hip(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
+    struct Evs {
+        hipEvent_t* e;
+        ~Evs() {
+            for (int k = 0; k < STAGE_SLOTS; k++) (void)hipEventDestroy(e[k]);
+        }
+    } evs{ev};
+    char* pin = static_cast<char*>(c->pinned);
+    const char* s = static_cast<const char*>(src);
+    char* d = static_cast<char*>(dst);
+    const int64_t nchunks = (int64_t)((bytes + STAGE_CHUNK - 1) / STAGE_CHUNK);
+    auto len_of = [&](int64_t k) { return std::min(STAGE_CHUNK, bytes - (size_t)k * STAGE_CHUNK); };
+    const int rc = chunked_copy(
+        nchunks, STAGE_SLOTS, host_threads(),
+        [&](int64_t k, int slot) -> int {
+            hipError_t e = hipMemcpyAsync(pin + slot * STAGE_CHUNK, s + k * STAGE_CHUNK, len_of(k),
+                                          hipMemcpyDeviceToHost, R.st);
+            if (e == hipSuccess) e = hipEventRecord(ev[slot], R.st);
+            return e == hipSuccess ? 0 : PCX_EHIP;
+        },
+        [&](int slot) { return hipEventSynchronize(ev[slot]) == hipSuccess ? 0 : PCX_EHIP; },
+        [&](int64_t k, int slot, int t, int T) {
+            const size_t len = len_of(k), a = len * t / T, b = len * (t + 1) / T;
+            if (b > a) memcpy(d + k * STAGE_CHUNK + a, pin + slot * STAGE_CHUNK + a, b - a);
+        });
+    if (rc) R.hip(hipErrorUnknown, "staged D2H of an output");
+}
 
 int64_t pow2_at_least(int64_t n) {
     int64_t p = 2;
@@ -1052,7 +1111,10 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         R.hip(hipMemcpyAsync(sc2, w->scalars, sizeof(sc2), hipMemcpyDeviceToHost, R.st), "D2H scalars");
         R.mark(M_D2H);
         for (auto& o : outs)
-            R.hip(hipMemcpyAsync(o.user, o.dev, o.n * 8, hipMemcpyDeviceToHost, R.st), "D2H output");
+            if ((size_t)o.n * 8 < STAGE_MIN)
+                R.hip(hipMemcpyAsync(o.user, o.dev, o.n * 8, hipMemcpyDeviceToHost, R.st), "D2H output");
+        for (auto& o : outs)
+            if ((size_t)o.n * 8 >= STAGE_MIN) d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
         R.mark(-1);
         R.sync();
         r->participation = sc2[0];

@@ -2,8 +2,10 @@
 // no HIP, no RCCL.  Compiled into libpcx (exported as pcx_selftest_*, run by tests/test_abi.py)
 // and, with the same sources, into tests/c/host_selftest.cpp's sanitizer builds
 // (tests/test_sanitizers.py: -fsanitize=thread and -fsanitize=address,undefined).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -212,6 +214,40 @@ int selftest_rounds_sched(int K, int64_t B, int enomem_worker, int64_t fail_roun
     const bool expect_handback = faulted_any;
     for (int k = 0; k < K; k++) violations += released[k] != (expect_handback && k == enomem_worker ? 1 : 0);
     violations += (int64_t)retry.size() != (expect_handback ? 1 : 0);
+    return violations;
+}
+
+int selftest_chunked_copy(int64_t bytes, int64_t chunk, int nslots, int T, int64_t fail_chunk) {
+    if (bytes < 0 || bytes > (1ll << 30) || chunk < 1 || nslots < 1 || nslots > 8 || T < 1 || T > 64) return -1;
+    std::vector<unsigned char> src((size_t)bytes), dst((size_t)bytes, 0), slots((size_t)(nslots * chunk));
+    for (int64_t i = 0; i < bytes; i++) src[(size_t)i] = (unsigned char)(i * 131 + 7);
+    const int64_t nchunks = (bytes + chunk - 1) / chunk;
+    std::vector<std::atomic<int>> moved((size_t)nchunks);
+    const int rc = chunked_copy(
+        nchunks, nslots, T,
+        [&](int64_t k, int slot) -> int {
+            if (k == fail_chunk) return PCX_EHIP;
+            if (k % 3 == 1) std::this_thread::sleep_for(std::chrono::microseconds(200));
+            const int64_t len = std::min(chunk, bytes - k * chunk);
+            std::memcpy(&slots[(size_t)(slot * chunk)], &src[(size_t)(k * chunk)], (size_t)len);
+            return 0;
+        },
+        [&](int) { return 0; },
+        [&](int64_t k, int slot, int t, int nt) {
+            const int64_t len = std::min(chunk, bytes - k * chunk);
+            const int64_t a = len * t / nt, b = len * (t + 1) / nt;
+            if (b > a) std::memcpy(&dst[(size_t)(k * chunk + a)], &slots[(size_t)(slot * chunk + a)], (size_t)(b - a));
+            moved[(size_t)k]++;
+        });
+    int violations = 0;
+    if (fail_chunk >= 0 && fail_chunk < nchunks) {
+        violations += rc != PCX_EHIP;
+        for (int64_t k = fail_chunk; k < nchunks; k++) violations += moved[(size_t)k] != 0;  // nothing after the failure
+        return violations;
+    }
+    violations += rc != 0;
+    for (int64_t k = 0; k < nchunks; k++) violations += moved[(size_t)k] != T;
+    violations += std::memcmp(src.data(), dst.data(), (size_t)bytes) != 0;
     return violations;
 }
 

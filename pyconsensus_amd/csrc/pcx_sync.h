@@ -184,6 +184,68 @@ int schedule_rounds(int K, int64_t B, int enomem, Run&& run, Release&& release, 
     return 0;
 }
 
+// A large copy through `nslots` staging slots: the main thread issues chunk k's transfer into slot
+// k % nslots (issue(k, slot), e.g. a DMA into pinned memory) as soon as that slot's previous chunk
+// has been moved out; T worker threads wait for the chunk (wait(slot)) and each move their share
+// out of the slot (part(k, slot, t, T), e.g. a memcpy into pageable memory, whose first-touch page
+// faults then spread over T threads).  Returns 0, or the first non-zero status of issue / wait
+// (the copy then stops; every thread is joined before the return).
+template <class Issue, class Wait, class Part>
+int chunked_copy(int64_t nchunks, int nslots, int T, Issue&& issue, Wait&& wait, Part&& part) {
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t issued = -1;                        // last chunk issued (under mu)
+    std::vector<int64_t> consumed(nslots, -1);  // last chunk moved out of each slot (under mu)
+    std::vector<int> left(nslots, 0);           // workers still moving the slot's chunk (under mu)
+    std::atomic<int> rc{0};
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (int64_t k = 0; k < nchunks; k++) {
+                const int slot = (int)(k % nslots);
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    // (every chunk is marked issued, also after a failure -- a worker must not run
+                    // ahead of that: its count on the slot would precede the slot's reset)
+                    cv.wait(lk, [&] { return issued >= k; });
+                }
+                if (rc.load() == 0) {
+                    const int w = wait(slot);
+                    if (w) {
+                        int z = 0;
+                        rc.compare_exchange_strong(z, w);
+                    } else {
+                        part(k, slot, t, T);
+                    }
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                if (--left[slot] == 0) {
+                    consumed[slot] = k;
+                    cv.notify_all();
+                }
+            }
+        });
+    for (int64_t k = 0; k < nchunks; k++) {
+        const int slot = (int)(k % nslots);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return consumed[slot] >= k - nslots; });
+        }
+        const int r = rc.load() == 0 ? issue(k, slot) : 1;
+        std::lock_guard<std::mutex> lk(mu);
+        if (r) {
+            int z = 0;
+            rc.compare_exchange_strong(z, r);
+        }
+        left[slot] = T;
+        issued = k;
+        cv.notify_all();
+    }
+    for (auto& t : th) t.join();
+    return rc.load();
+}
+
 // CPU self-tests (pcx_selftest.cpp); each returns the number of violations, -1 on bad arguments.
 // mode 0: users race aborters on a fast handle; mode 1: one user holds the handle longer than
 // the abort's wait (the timed-out path)
@@ -194,5 +256,8 @@ int selftest_group_abort(int world, int steps, int fail_rank, int fail_step);
 // K workers, B rounds; worker `enomem_worker` reports ENOMEM on its first round (-1: none),
 // round `fail_round` fails hard (-1: none)
 int selftest_rounds_sched(int K, int64_t B, int enomem_worker, int64_t fail_round);
+// chunked_copy of `bytes` through `nslots` slots of `chunk` bytes by T threads (memcpy as the
+// transfer, a slow `issue` every 3rd chunk); chunk `fail_chunk`'s issue fails (-1: none)
+int selftest_chunked_copy(int64_t bytes, int64_t chunk, int nslots, int T, int64_t fail_chunk);
 
 }  // namespace pcx

@@ -22,6 +22,7 @@ void expect(const char* what, int violations) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // (a hang shows its last self-test)
     const int scale = argc > 1 ? std::atoi(argv[1]) : 1;  // iterations multiplier
     char name[128];
     // AbortOnce: users racing aborters, then one holder blocked past the abort's wait
@@ -48,6 +49,14 @@ int main(int argc, char** argv) {
                 expect(name, pcx::selftest_rounds_sched(K, 64 * scale, enw, fail));
             }
         }
+    // the staged large copy of the host-memory path (chunked_copy): slots, threads, ragged tail, failure
+    for (int slots : {1, 2, 3})
+        for (int T : {1, 4, 16}) {
+            std::snprintf(name, sizeof name, "chunked_copy slots=%d T=%d", slots, T);
+            expect(name, pcx::selftest_chunked_copy(1000003 * scale, 65536, slots, T, -1));
+        }
+    expect("chunked_copy failure at chunk 5", pcx::selftest_chunked_copy(1 << 20, 65536, 2, 8, 5));
+    expect("chunked_copy failure at chunk 0", pcx::selftest_chunked_copy(1 << 20, 65536, 2, 8, 0));
     std::printf("%s (%d failure(s))\n", failures ? "FAILED" : "PASSED", failures);
     return failures ? 1 : 0;
 }

@@ -55,5 +55,7 @@ def test_selftests_in_libpcx():
     for world, fr, fs in [(1, -1, -1), (2, 0, 0), (2, 1, 3), (4, 2, 1), (8, 7, 4)]:
         assert h.pcx_selftest_group_abort(world, 5, fr, fs) == 0, (world, fr, fs)
     assert h.pcx_selftest_group_abort(2, 5, 2, 0) == -1
+    for slots, T, fail in [(3, 16, -1), (1, 1, -1), (2, 8, 4)]:
+        assert h.pcx_selftest_chunked_copy(C.c_int64(5_000_011), C.c_int64(1 << 18), slots, T, C.c_int64(fail)) == 0
     for K, enw, fail in [(1, -1, -1), (4, 0, -1), (4, 3, -1), (16, 2, 9), (1, 0, -1)]:
         assert h.pcx_selftest_rounds_sched(K, C.c_int64(200), enw, C.c_int64(fail)) == 0, (K, enw, fail)

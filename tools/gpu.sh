@@ -79,7 +79,7 @@ for STEP in "$@"; do
       timeout -k 10 200 python -u tools/c5_shard_latency.py 8 5 > $O/w8.json 2> $O/w8.err || { echo "shard rc=$?"; tail -20 $O/w8.err; exit 19; }
       python3 -c "import json; d=json.load(open('$O/w8.json')); print('shard', round(d['latency_ms'],2), 'ms;', ' '.join('%s %.2f' % (k[2:], v) for k, v in list(d.get('stage_ms', {}).items())[:10]))" ;;
     host)  # the drop-in's host-memory path at C5: copies in and out + consensus (tools/c5_host_latency.py)
-      timeout -k 10 900 python -u tools/c5_host_latency.py 2 > $O/host.json 2> $O/host.err || { echo "host rc=$?"; tail -20 $O/host.err; exit 31; }
+      timeout -k 10 900 python -u tools/c5_host_latency.py 3 > $O/host.json 2> $O/host.err || { echo "host rc=$?"; tail -20 $O/host.err; exit 31; }
       grep '"mode"' $O/host.err ;;
     shard_prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard_kt -o kt -- python3 tools/c5_shard_latency.py 8 3 > $O/shard_kt.log 2>&1 || { echo "shard kernel-trace rc=$?"; tail -5 $O/shard_kt.log; exit 27; }
