@@ -1312,6 +1312,57 @@ __global__ void __launch_bounds__(256) k_gram(const double* A, int E, double* ou
     if (lane == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
 }
 
+// The same product split over the K (row) range for large E: tile t of the lower triangle, slice z
+// of the rows -> slab[z] (a tile's own entries), then k_gram_reduce sums the slices in slice order.
+// At E = 1000 the single-pass k_gram is 36 workgroups on 256 CUs (0.24 ms per squaring, three
+// squarings per consensus); split 8 ways it fills the chip.
+__global__ void __launch_bounds__(256) k_gram_part(const double* A, int E, double* slab, int ks,
+                                                   const int64_t* flags) {
+    if (pi_mode_of(*flags) != 0) return;
+    const int t = blockIdx.x / ks, z = blockIdx.x % ks;
+    int I, J;
+    tri_index(t, I, J);
+    const int64_t per = ((E + ks - 1) / ks + KB - 1) / KB * KB;
+    const int64_t rb = (int64_t)z * per, re = rb + per < E ? rb + per : E;
+    GramLoader ld{A, E};
+    d4 acc[4][4];
+    mfma_tile(ld, I, J, rb < E ? rb : E, re, acc);
+    store_tile(slab + (int64_t)z * E * E, E, E, I, J, acc);
+}
+
+// 32 x 32 tiles of the lower triangle: the slices summed in order (coalesced over q), the tile
+// mirrored through LDS so the upper half's stores are coalesced too
+constexpr int GR_T = 32;
+__global__ void __launch_bounds__(256) k_gram_reduce(const double* slab, int ks, int E, double* out,
+                                                     unsigned long long* maxbits, const int64_t* flags) {
+    if (pi_mode_of(*flags) != 0) return;
+    __shared__ double t[GR_T][GR_T + 1];
+    int I, J;
+    tri_index(blockIdx.x, I, J);
+    const int tx = threadIdx.x % GR_T, ty = threadIdx.x / GR_T;  // 32 x 8
+    const int64_t n2 = (int64_t)E * E;
+    double mx = 0.0;
+    for (int r = ty; r < GR_T; r += 256 / GR_T) {
+        const int64_t p = (int64_t)I * GR_T + r, q = (int64_t)J * GR_T + tx;
+        double v = 0.0;
+        if (p < E && q <= p) {
+            const int64_t o = p * E + q;
+            v = slab[o];
+            for (int z = 1; z < ks; z++) v += slab[(int64_t)z * n2 + o];
+            out[o] = v;
+            mx = fmax(mx, fabs(v));
+        }
+        t[r][tx] = v;
+    }
+    __syncthreads();
+    for (int r = ty; r < GR_T; r += 256 / GR_T) {  // out[q][p] = out[p][q], coalesced over p
+        const int64_t q = (int64_t)J * GR_T + r, p = (int64_t)I * GR_T + tx;
+        if (p < E && q < p) out[q * E + p] = t[tx][r];
+    }
+    mx = wave_max_d(mx);
+    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, (unsigned long long)__double_as_longlong(mx));
+}
+
 __global__ void __launch_bounds__(BT) k_scale(double* M, int64_t n, const unsigned long long* maxbits,
                                               const int64_t* flags) {
     if (pi_mode_of(*flags) != 0) return;
@@ -3378,6 +3429,27 @@ __global__ void __launch_bounds__(1024) k_hard_gather(pcx_mat m, HardArgs h) {
     double* out = h.send + (int64_t)j * h.cap * 2;
     const double* wsrc = m.sel_phase == 1 ? m.rep : m.rowv + RV_SMOOTH * m.n_rows;
     const int64_t E = m.n_events;
+    const int sidx = m.scaled_index ? m.scaled_index[c] : -1;
+    if (h.modes[j] == HARD_MEDIAN && sidx >= 0) {
+        // a median's values come from T (k_colstats: the rescaled present value, NaN where missing,
+        // one contiguous column) instead of a strided column of the row-major reports
+        const double* Tc = m.T + (int64_t)sidx * m.n_rows;
+        const double g = p.guess;
+        const int64_t nt = block_compact(
+            m.n_rows,
+            [&](int64_t i) {
+                const double v = Tc[i];
+                if (m.sel_phase == 1) return !__builtin_isnan(v);
+                return !__builtin_isnan(__builtin_isnan(v) ? g : v);
+            },
+            [&](int64_t i, int64_t pos) {
+                const double v = Tc[i];
+                out[pos * 2 + 0] = __builtin_isnan(v) ? g : v;
+                out[pos * 2 + 1] = wsrc[i];
+            });
+        if (threadIdx.x == 0) h.send_cnt[j] = nt;
+        return;
+    }
     const int64_t n = block_compact(
         m.n_rows,
         [&](int64_t i) {
@@ -4825,7 +4897,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (stage == M_WCD) {
                 const int ncb = (int)((m.wcd_ld + WCD_COLS - 1) / WCD_COLS);
                 int64_t rb = std::max(1, 4096 / ncb);
-                while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS) rb /= 2;
+                // (but keep >= 1,024 workgroups: at C4's 1,000 events -- two column blocks -- the
+                // 768-row floor left 256 workgroups, one per CU: k_wcd 1.03 ms at 2.5 TB/s)
+                while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS && (rb / 2) * ncb >= 1024) rb /= 2;
                 hipLaunchKernelGGL(k_wcd, dim3((unsigned)rb, ncb),
                                    dim3(BT), 0, st, m);
                 break;
@@ -4994,9 +5068,21 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 double* Tm = m.Mw;
                 unsigned long long* mxb = (unsigned long long*)&m.info[8];
                 const int64_t* fl = &m.info[IN_FLAGS];
+                // split-K squaring for E >= 512 when the slabs fit the covariance's (free by now);
+                // smaller E keeps the single pass (the goldens' arithmetic)
+                const int gks = E >= 512 ? (int)std::min<int64_t>(std::min<int64_t>(8, m.cov_kslices),
+                                                                   std::max(1, 1024 / ntri))
+                                         : 1;
                 auto square = [&]() {
                     (void)hipMemsetAsync(mxb, 0, sizeof(unsigned long long), st);
-                    hipLaunchKernelGGL(k_gram, dim3(ntri), dim3(256), 0, st, M, E, Tm, mxb, fl);
+                    if (gks > 1 && m.cslab) {
+                        hipLaunchKernelGGL(k_gram_part, dim3(ntri * gks), dim3(256), 0, st, M, E, m.cslab, gks, fl);
+                        const int n32 = (E + GR_T - 1) / GR_T;
+                        hipLaunchKernelGGL(k_gram_reduce, dim3(n32 * (n32 + 1) / 2), dim3(256), 0, st,
+                                           (const double*)m.cslab, gks, E, Tm, mxb, fl);
+                    } else {
+                        hipLaunchKernelGGL(k_gram, dim3(ntri), dim3(256), 0, st, M, E, Tm, mxb, fl);
+                    }
                     hipLaunchKernelGGL(k_scale, dim3(grid_rows(nn2, BT)), dim3(BT), 0, st, Tm, nn2,
                                        (const unsigned long long*)mxb, fl);
                     const double* sq_out = Tm;
