@@ -2900,7 +2900,10 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
 // the pass that reads the whole column also compacts this rank's in-range (key, weight)
 // pairs into cbuf; later passes read only those (the histogram is a set of exact integer
 // sums / minima / maxima, so the compacted order does not matter).
-__global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
+// NT threads per event: 256, or 1,024 when the active events leave CUs idle (C4: 250 events on 256
+// CUs -- one 256-thread workgroup per CU kept four waves streaming each column)
+template <int NT>
+__global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
@@ -2913,7 +2916,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     typedef unsigned long long hn_t;  // (32-bit LDS counts measured: no faster)
     __shared__ hn_t hn[NB * HC];
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
-    for (int b = threadIdx.x; b < NB * HC; b += BT) {
+    for (int b = threadIdx.x; b < NB * HC; b += NT) {
         ha[b] = hb[b] = hc[b] = 0;
         hn[b] = 0;
         hmin[b] = ~0ull;
@@ -3012,13 +3015,13 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
     };
     if (from_buf) {
         const int64_t nc = m.ccount[s];
-        for (int64_t j = threadIdx.x; j < nc; j += BT) {
+        for (int64_t j = threadIdx.x; j < nc; j += NT) {
             const uint64_t k = cb[2 * j];
             if (k < lo || k > hi) continue;
             bin(k, __longlong_as_double(cb[2 * j + 1]));
         }
     } else {
-        rows_strided<ROW_UNROLL>(threadIdx.x, BT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
+        rows_strided<ROW_UNROLL>(threadIdx.x, NT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
                                  [&](int64_t, XW v) {
             double x, w;
             if (gties && __builtin_isnan(v.x)) return;  // a filled row
@@ -3114,7 +3117,7 @@ __global__ void __launch_bounds__(BT) k_sel_hist(pcx_mat m) {
         st[SW_CMODE] = fits ? 2 : 0;
     }
     const int64_t o = (int64_t)a * NB;
-    for (int b = threadIdx.x; b < NB; b += BT) {
+    for (int b = threadIdx.x; b < NB; b += NT) {
         unsigned long long sa = 0, sb = 0, sc = 0, mn = ~0ull, mx = 0;
         uint64_t sn = 0;
 #pragma unroll
@@ -3712,7 +3715,8 @@ __global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
         k_s = 0;
         cum_s = 0.0;
     }
-    for (int k = threadIdx.x; k < HARD_TILE && k < n; k += blockDim.x) tw[k] = dkey_inv(keys[2 * k + 1]);
+    // (a partial tile is followed by zeros: a chunk that runs past the last weight adds + 0.0)
+    for (int k = threadIdx.x; k < TWS; k += blockDim.x) tw[k] = k < n && k < HARD_TILE ? dkey_inv(keys[2 * k + 1]) : 0.0;
     __syncthreads();
     // cum += w while cum <= mid (weightedstats' walk; mid > 0 here, so the first add always runs):
     // lane 0 adds a chunk's weights unconditionally -- partial sums up to the first one above mid
@@ -3734,7 +3738,7 @@ __global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
             for (int k = 0; k < len; k += CHAIN) {
                 double v[CHAIN], p[CHAIN];
 #pragma unroll
-                for (int q = 0; q < CHAIN; q++) v[q] = k + q < len ? nv[q] : 0.0;  // + 0.0 keeps the sum
+                for (int q = 0; q < CHAIN; q++) v[q] = nv[q];  // (past len: the tile's zero padding)
 #pragma unroll
                 for (int q = 0; q < CHAIN; q++) nv[q] = cur[k + CHAIN + q];  // the next chunk, in flight
                 double acc = cum;
@@ -3773,7 +3777,7 @@ __global__ void __launch_bounds__(1024) k_hard_walk(pcx_mat m, HardArgs h) {
         } else if ((int)threadIdx.x >= WAVE) {
             const int64_t n0 = t0 + HARD_TILE;
             const int nl = (int)(n - n0 < HARD_TILE ? (n - n0 > 0 ? n - n0 : 0) : HARD_TILE);
-            for (int k = threadIdx.x - WAVE; k < nl; k += loaders) nxt[k] = dkey_inv(keys[2 * (n0 + k) + 1]);
+            for (int k = threadIdx.x - WAVE; k < TWS; k += loaders) nxt[k] = k < nl ? dkey_inv(keys[2 * (n0 + k) + 1]) : 0.0;
         }
         __syncthreads();
         if (done_s) break;
@@ -5154,7 +5158,17 @@ hipError_t hard_list(pcx_mat& m, int32_t* cols, int32_t* modes, hipStream_t st) 
 
 hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st) {
     if (n_active <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sel_hist, dim3(n_active), dim3(BT), 0, st, m);
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            ncu = n;
+        if (ncu <= 0) ncu = 256;
+    }
+    if (n_active <= ncu)
+        hipLaunchKernelGGL(k_sel_hist<1024>, dim3(n_active), dim3(1024), 0, st, m);
+    else
+        hipLaunchKernelGGL(k_sel_hist<BT>, dim3(n_active), dim3(BT), 0, st, m);
     return hipGetLastError();
 }
 
