@@ -8,6 +8,10 @@
 #ifndef PCX_GEMM_KS
 #define PCX_GEMM_KS 2
 #endif
+// balanced base-254 digits per general position (pcx_internal.h, k_digits)
+#ifndef PCX_NDIG
+#define PCX_NDIG 6
+#endif
 
 namespace pcx {
 
@@ -70,7 +74,7 @@ struct GemmI8 {
 // offset, the ring slot rotates as a scalar and the fragment offsets are loop-invariant -- with
 // 64-bit per-lane address math (~3.3 VALU per MFMA; an MFMA holds its SIMD's vector issue for
 // 8 of its 16 cycles) the same loop ran 3-5 % slower.  The product launches
-// <16, 3>.
+// <8, 3> (two waves per SIMD: half the B unpacking per MFMA of <16, 3>).
 template <int WAVES, int NBUF>
 __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
     static_assert(WAVES == 16 || WAVES == 8, "4 x 4 or 2 x 4 waves");
@@ -139,47 +143,78 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
 #pragma unroll
     for (int b = 0; b < 4; b++)
         bfr[b] = (uint32_t)(KS * G_PANEL + (lg * GT + wc * 64 + lc + ((b * 16) ^ (G_BSWZ * lg))) * 4);
+    struct Frag {  // one k-step's fragments: AF A blocks, four packed B dwords
+        v4i a[AF];
+        uint32_t b[4];
+    };
+    auto read = [&](int buf, int kk, Frag& f) {
+        const char* sb = glds + (size_t)buf * STAGE;
+#pragma unroll
+        for (int a = 0; a < AF; a++) f.a[a] = *reinterpret_cast<const v4i*>(sb + kk * G_PANEL + afr + a * 256);
+#pragma unroll
+        for (int b = 0; b < 4; b++) f.b[b] = *reinterpret_cast<const uint32_t*>(sb + kk * G_PANEL_PK + bfr[b]);
+    };
     v4i acc[AF][4];
 #pragma unroll
     for (int a = 0; a < AF; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
-    const int64_t n = s1 - s0;
+    auto mma = [&](const Frag& f) {
+        constexpr uint32_t M2 = 0x03030303u;
 #pragma unroll
-    for (int k = 0; k < NBUF - 1; k++)
-        if (k < n) issue(k, k);
-    int buf = 0, ibuf = NBUF - 1;  // ring slot of stage t, and of stage t + NBUF - 1
-    for (int64_t t = 0; t < n; t++) {
-        if (t + NBUF - 2 < n)
-            wait_vmcnt<LOADS * (NBUF - 2)>();  // stage t landed, t+1 .. t+NBUF-2 may be in flight
+        for (int b = 0; b < 4; b++) {
+            const uint32_t P = f.b[b];
+            const v4i bf = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
+#pragma unroll
+            for (int a = 0; a < AF; a++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[a], bf, acc[a][b], 0, 0, 0);
+        }
+    };
+    // The fragment reads are software-pipelined across the ring's barrier (round 5; reading a
+    // k-step's fragments and then running its MFMAs left every SIMD's MFMA pipe empty after each
+    // barrier while all waves read LDS at once): k-step 1's fragments are read under k-step 0's
+    // MFMAs, and k-step 1's MFMAs wait until after the barrier that publishes the next stage, whose
+    // first fragments are then read under them.  Every wave has its fragments of stage t in registers
+    // when it reaches that barrier, so stage t's slot takes stage t + NBUF right after it (all NBUF
+    // slots filled up front: NBUF - 1 stages stay in flight, as before).  C5 mixed block 14.06 ->
+    // 13.40 ms, grid block 4.00 -> 3.71 ms with 8 waves (tools/i8bench).
+    static_assert(KS == 2, "the pipelined loop alternates two k-steps per stage");
+    const int64_t n = s1 - s0;
+    if (n > 0) {
+#pragma unroll
+        for (int k = 0; k < NBUF; k++)
+            if (k < n) issue(k, k);
+        if (NBUF - 1 < n)
+            wait_vmcnt<LOADS * (NBUF - 1)>();
         else
             wait_vmcnt<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + NBUF - 1 < n) issue(t + NBUF - 1, ibuf);
-        const char* sb = glds + (size_t)buf * STAGE;
-#pragma unroll
-        for (int kk = 0; kk < KS; kk++) {
-            const char* sk = sb + kk * G_PANEL;
-            v4i af[AF], bf[4];
-#pragma unroll
-            for (int a = 0; a < AF; a++) af[a] = *reinterpret_cast<const v4i*>(sk + afr + a * 256);
-            constexpr uint32_t M2 = 0x03030303u;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const uint32_t P = *reinterpret_cast<const uint32_t*>(sb + kk * G_PANEL_PK + bfr[b]);
-                bf[b] = v4i{(int)(P & M2), (int)((P >> 2) & M2), (int)((P >> 4) & M2), (int)((P >> 6) & M2)};
-            }
-#pragma unroll
-            for (int a = 0; a < AF; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+        Frag F, G;  // a stage's first k-step in F, its second in G
+        read(0, 0, F);
+        int buf = 0;
+        for (int64_t t = 0; t + 1 < n; t++) {  // (the last stage peeled: no join before its mma(G))
+            read(buf, 1, G);
+            mma(F);
+            if (t + NBUF - 1 < n)
+                wait_vmcnt<LOADS * (NBUF - 2)>();  // stage t + 1 landed (this wave's pieces)
+            else
+                wait_vmcnt<0>();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) as a builtin (an asm one is opaque to
+                                                 // the compiler, which then waited for F's reads too
+                                                 // before mma(G) below)
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + NBUF < n) issue(t + NBUF, buf);
+            buf = buf + 1 == NBUF ? 0 : buf + 1;
+            read(buf, 0, F);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(G);
         }
-        asm volatile("" ::: "memory");
-        buf = buf + 1 == NBUF ? 0 : buf + 1;
-        ibuf = ibuf + 1 == NBUF ? 0 : ibuf + 1;
+        read(buf, 1, G);
+        mma(F);
+        mma(G);
     }
     // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
     const int p0 = ip * GT + wr * TM + 4 * lg, q0 = iq * GT + wc * 64 + lc;
@@ -207,8 +242,183 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
         }
 }
 
+// General x general pairs on int8 (k_gemm_i8x): both operands are PCX_NDIG balanced base-254 digit
+// slices in the A layout above -- A the digits of tok w (zD), B those of w (zE), digit i of general
+// position q at position i gb + q -- and the product of digit i of p with digit j of q is weighted
+// 254^-(i + j + 2).  Only the digit pairs with i + j <= smax matter at fp64's level and only the
+// lower event tiles (p >= q) are needed.  Items run k-slice major, then by A panel (digit i, tile
+// a), then (digit j, tile b <= a), so the workgroups resident on one XCD at a time share their A
+// panels in its L2; each writes its whole 256 x 256 int32 tile to its own slab,
+// out[ks][i][j][tile (a, b)][256][256] (row: the position of p in the tile, column: that of q).
+struct GemmX {
+    const int8_t* A;  // [rg][lda][16]
+    const int8_t* B;  // [rg][ldb][16]
+    int64_t lda, ldb;
+    int32_t* out;
+    int64_t rg;  // row groups, a multiple of 4 KS
+    int gb;      // positions per digit slice, a multiple of 256
+    int nt;      // gb / 256 event tiles per side
+    int smax, kslices;
+};
+__host__ __device__ inline int gemm_i8x_pairs(int smax) {  // digit pairs (i, j), i, j < NDIG, i + j <= smax
+    int n = 0;
+    for (int i = 0; i < PCX_NDIG; i++) n += smax - i >= 0 ? (smax - i < PCX_NDIG ? smax - i + 1 : PCX_NDIG) : 0;
+    return n;
+}
+__host__ __device__ inline int64_t gemm_i8x_items(const GemmX& g) {
+    return (int64_t)g.kslices * gemm_i8x_pairs(g.smax) * (g.nt * (g.nt + 1) / 2);
+}
+// slab of (k-slice, i, j, lower tile)
+__host__ __device__ inline int64_t gemm_i8x_slab(int ks, int i, int j, int tl, int nt) {
+    return (((int64_t)ks * PCX_NDIG + i) * PCX_NDIG + j) * (nt * (nt + 1) / 2) + tl;
+}
+
+// 16-byte fragments of both operands straight from the LDS ring (no unpacking); the fragment reads
+// are software-pipelined across the ring's barrier: a stage's last k-step keeps its MFMAs until after
+// the barrier that publishes the next stage, whose first fragments are then read under them (every
+// wave has its fragments of the stage in registers before it arrives, so that stage's slot is
+// refilled right after the barrier: stage t + NBUF into stage t's slot).  WAVES = 8: 2 x 4 waves of
+// 128 x 64; 16: 4 x 4 of 64 x 64.
+template <int WAVES, int NBUF>
+__global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8x(GemmX g) {
+    static_assert(WAVES == 16 || WAVES == 8, "4 x 4 or 2 x 4 waves");
+    constexpr int KS = 2, WR = WAVES == 16 ? 4 : 2, TM = GT / WR, AF = TM / 16;
+    constexpr int LPP = 16 / WAVES;       // DMA pieces per wave per operand per k-step
+    constexpr size_t STAGE = KS * 2 * G_PANEL;
+    static_assert(NBUF >= 2 && NBUF * STAGE <= 163840, "int8 GEMM ring (160 KB of LDS)");
+    constexpr int LOADS = 2 * KS * LPP;  // vector-memory ops per wave per stage
+    extern __shared__ __attribute__((aligned(16))) char glds[];
+    const int ntri = g.nt * (g.nt + 1) / 2, npair = gemm_i8x_pairs(g.smax);
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int ks = item / (npair * ntri);
+    int r = item % (npair * ntri), i = 0;
+    for (;; i++) {  // digit i of the A panel: (min(smax - i, NDIG - 1) + 1) digits j x ntri tiles each
+        const int nj = (g.smax - i < PCX_NDIG - 1 ? g.smax - i : PCX_NDIG - 1) + 1;
+        if (r < nj * ntri) break;
+        r -= nj * ntri;
+    }
+    const int nj = (g.smax - i < PCX_NDIG - 1 ? g.smax - i : PCX_NDIG - 1) + 1;
+    int ta = 0;
+    while (r >= nj * (ta + 1)) {  // tile row a holds nj (a + 1) items (j, b <= a)
+        r -= nj * (ta + 1);
+        ta++;
+    }
+    const int j = r / (ta + 1), tb = r % (ta + 1), tl = ta * (ta + 1) / 2 + tb;
+    const int64_t nst = g.rg / (4 * KS);
+    const int64_t per = (nst + g.kslices - 1) / g.kslices;
+    const int64_t s0 = ks * per < nst ? ks * per : nst;
+    const int64_t s1 = s0 + per < nst ? s0 + per : nst;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wv >> 2, wc = wv & 3;
+    const int lc = lane & 15, lg = lane >> 4;
+    const int8_t* const abase = g.A + ((int64_t)i * g.gb + (int64_t)ta * GT) * 16;
+    const int8_t* const bbase = g.B + ((int64_t)j * g.gb + (int64_t)tb * GT) * 16;
+    const int64_t astep = 4 * g.lda * 16, bstep = 4 * g.ldb * 16;  // bytes per k-step
+    uint32_t aoff[LPP], boff[LPP], dst[LPP];
+#pragma unroll
+    for (int u = 0; u < LPP; u++) {
+        const int ch = wv + u * WAVES, mg = ch & 3, mh = ch >> 2;
+        aoff[u] = (uint32_t)(((int64_t)mg * g.lda + mh * 64 + lane) * 16);
+        boff[u] = (uint32_t)(((int64_t)mg * g.ldb + mh * 64 + lane) * 16);
+        dst[u] = (uint32_t)((mg * GT + mh * 64) * 16);
+    }
+    auto issue = [&](int64_t st, int buf) {
+        char* sb = glds + (size_t)buf * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < KS; kk++) {
+            const int64_t k = (s0 + st) * KS + kk;
+#pragma unroll
+            for (int u = 0; u < LPP; u++) {
+                __builtin_amdgcn_global_load_lds((const void*)(abase + k * astep + aoff[u]),
+                                                 (lds_ptr_t)(sb + kk * G_PANEL + dst[u]), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(bbase + k * bstep + boff[u]),
+                                                 (lds_ptr_t)(sb + (KS + kk) * G_PANEL + dst[u]), 16, 0, 0);
+            }
+        }
+    };
+    const uint32_t afr = (uint32_t)((lg * GT + wr * TM + lc) * 16);
+    const uint32_t bfr = (uint32_t)(KS * G_PANEL + (lg * GT + wc * 64 + lc) * 16);
+    struct Frag {
+        v4i a[AF], b[4];
+    };
+    auto read = [&](int buf, int kk, Frag& f) {
+        const char* sb = glds + (size_t)buf * STAGE + kk * G_PANEL;
+#pragma unroll
+        for (int a = 0; a < AF; a++) f.a[a] = *reinterpret_cast<const v4i*>(sb + afr + a * 256);
+#pragma unroll
+        for (int b = 0; b < 4; b++) f.b[b] = *reinterpret_cast<const v4i*>(sb + bfr + b * 256);
+    };
+    v4i acc[AF][4];
+#pragma unroll
+    for (int a = 0; a < AF; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = v4i{0, 0, 0, 0};
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int a = 0; a < AF; a++) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[a], f.b[b], acc[a][b], 0, 0, 0);
+    };
+    const int64_t n = s1 - s0;
+    if (n > 0) {
+#pragma unroll
+        for (int k = 0; k < NBUF; k++)
+            if (k < n) issue(k, k);
+        if (NBUF - 1 < n)
+            wait_vmcnt<LOADS * (NBUF - 1)>();
+        else
+            wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // stage t + 1 published: every wave's pieces landed and every wave's fragments of stage t are in
+        // registers (the lgkmcnt wait is a builtin, so the compiler's own wait before the next MFMAs
+        // knows they have landed); stage t's slot then takes stage t + NBUF
+        auto publish = [&](int64_t t, int slot) {
+            if (t + NBUF - 1 < n)
+                wait_vmcnt<LOADS * (NBUF - 2)>();  // stage t + 1 landed (this wave's pieces)
+            else
+                wait_vmcnt<0>();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + NBUF < n) issue(t + NBUF, slot);
+        };
+        Frag F, G;
+        read(0, 0, F);
+        int buf = 0;
+        // a stage's first k-step in F, its second in G (one k-step per stage, alternating stages
+        // between F and G, spilled 175 VGPRs at 8 waves)
+        for (int64_t t = 0; t + 1 < n; t++) {  // (the last stage peeled: no join before its mma(G))
+            read(buf, 1, G);
+            mma(F);
+            publish(t, buf);
+            buf = buf + 1 == NBUF ? 0 : buf + 1;
+            read(buf, 0, F);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(G);
+        }
+        read(buf, 1, G);
+        mma(F);
+        mma(G);
+    }
+    // D layout (i32 16x16): col = lane & 15, row = 4 * (lane >> 4) + r
+    int32_t* out = g.out + gemm_i8x_slab(ks, i, j, tl, g.nt) * (GT * GT);
+#pragma unroll
+    for (int a = 0; a < AF; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                out[(wr * TM + a * 16 + 4 * lg + e) * GT + wc * 64 + b * 16 + lc] = acc[a][b][e];
+}
+constexpr int GEMM_I8X_WAVES = 8, GEMM_I8X_NBUF = 2;
+constexpr size_t GEMM_I8X_LDS = (size_t)GEMM_I8X_NBUF * 2 * 2 * G_PANEL;  // 128 KB
+
 // the product's configuration (pcx_matrix.hip M_COV_I8)
-constexpr int GEMM_I8_NBUF = 3;
+constexpr int GEMM_I8_WAVES = 8, GEMM_I8_NBUF = 3;
 constexpr size_t GEMM_I8_LDS = (size_t)GEMM_I8_NBUF * G_KS * (G_PANEL + G_PANEL_PK);  // 120 KB
 static_assert(GEMM_I8_LDS <= 163840, "int8 GEMM ring (160 KB of LDS)");
 

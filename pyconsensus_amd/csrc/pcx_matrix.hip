@@ -4854,7 +4854,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             static std::once_flag g_once;
             static hipError_t g_err = hipSuccess;
             std::call_once(g_once, [] {
-                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<16, GEMM_I8_NBUF>,
+                g_err = hipFuncSetAttribute((const void*)k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8_LDS);
             });
             if (g_err != hipSuccess) return g_err;
@@ -4865,7 +4865,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             {  // grid x grid (lower tiles): P = (tok z)^T z, |tok z z| <= 252 per row
                 GemmI8 g{m.zA, m.zq, m.zB, m.zq, m.Pgg, m.zq, m.zq * m.zq, np, np, 0, 0, 1, m.ks_gg, rg, 0};
                 g.tp = g.tq = (np + GT - 1) / GT;
-                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(16 * 64),
+                hipLaunchKernelGGL((k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(GEMM_I8_WAVES * 64),
                                    GEMM_I8_LDS, st, g);
             }
             if (m.cov_mixed) {
@@ -4882,7 +4882,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                     err = "M_COV_I8: operand row groups narrower than the tiles";
                     return hipErrorInvalidValue;
                 }
-                hipLaunchKernelGGL((k_gemm_i8<16, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(16 * 64),
+                hipLaunchKernelGGL((k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(GEMM_I8_WAVES * 64),
                                    GEMM_I8_LDS, st, g);
             }
             break;

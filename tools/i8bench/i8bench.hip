@@ -1,10 +1,11 @@
 // i8bench.hip -- standalone benchmark of the M_COV_I8 int8 products (pyconsensus_amd/csrc/pcx_gemm_i8.h)
 // at the C5 shapes (1M rows: 62,504 groups of 16), every configuration checked against the
-// product's (k_gemm_i8<16, GEMM_I8_NBUF>) as the int64 sum of its k-slice slabs, and all of them
+// product's (k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>) as the int64 sum of its k-slice slabs, and all of them
 // against a CPU reference on a small case.
 //   mixed: A = PCX_NDIG int8 digits x 1,024 general positions, B = z of 3,072 grid events
 //          (packed 2 bits), stored transposed;
-//   grid:  A = tok z (int8, 3,072 positions), B = z packed, lower tiles.
+//   grid:  A = tok z (int8, 3,072 positions), B = z packed, lower tiles;
+//   gg (shape argument "gg"): the general x general digit pairs (k_gemm_i8x), both operands digits.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/i8bench/i8bench.hip -o tools/i8bench/i8bench
 // usage: i8bench [reps=5] [rows=1000064] [variant substring] [shape substring]
 #include <hip/hip_runtime.h>
@@ -24,6 +25,8 @@
 #endif
 
 using namespace pcx;
+
+static int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }  // (pcx_internal.h)
 
 #define CK(x)                                                                              \
     do {                                                                                   \
@@ -98,6 +101,130 @@ struct Variant {
     size_t lds;
 };
 
+// ---- general x general digit pairs (k_gemm_i8x): A = digits of tok w, B = digits of w, both [rg][ld][16]
+static int run_gg(int reps, int64_t rows, const std::vector<int>& ks_list) {
+    constexpr int ND = PCX_NDIG;
+    auto make = [](int smax, GemmX& g) { g.smax = smax; };
+    CK(hipFuncSetAttribute((const void*)k_gemm_i8x<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8X_LDS));
+    CK(hipFuncSetAttribute((const void*)k_gemm_i8x<16, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8X_LDS));
+    {  // small check against the CPU: gb 512 (two event tiles), 32 row groups, 3 k-slices
+        const int64_t srg = 32, gb = 512, ld = zd_ld(gb);
+        std::vector<int8_t> hA(srg * ld * 16), hB(srg * ld * 16);
+        for (size_t i = 0; i < hA.size(); i++) {
+            hA[i] = (int8_t)((int)((i * 2654435761u) % 255) - 127);
+            hB[i] = (int8_t)((int)((i * 40503u + 7u) % 255) - 127);
+        }
+        GemmX g{};
+        make(ND, g);
+        g.lda = g.ldb = ld;
+        g.rg = srg;
+        g.gb = (int)gb;
+        g.nt = (int)(gb / GT);
+        g.kslices = 3;
+        const int ntri = g.nt * (g.nt + 1) / 2;
+        const size_t outn = (size_t)g.kslices * ND * ND * ntri * GT * GT;
+        int8_t *dA, *dB;
+        int32_t* dP;
+        CK(hipMalloc(&dA, hA.size()));
+        CK(hipMalloc(&dB, hB.size()));
+        CK(hipMalloc(&dP, outn * 4));
+        CK(hipMemcpy(dA, hA.data(), hA.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(dB, hB.data(), hB.size(), hipMemcpyHostToDevice));
+        g.A = dA;
+        g.B = dB;
+        g.out = dP;
+        for (int wv : {8, 16}) {
+            CK(hipMemset(dP, 0, outn * 4));
+            if (wv == 8)
+                hipLaunchKernelGGL((k_gemm_i8x<8, 2>), dim3((unsigned)gemm_i8x_items(g)), dim3(512), GEMM_I8X_LDS, 0, g);
+            else
+                hipLaunchKernelGGL((k_gemm_i8x<16, 2>), dim3((unsigned)gemm_i8x_items(g)), dim3(1024), GEMM_I8X_LDS, 0, g);
+            CK(hipGetLastError());
+            std::vector<int32_t> got(outn);
+            CK(hipMemcpy(got.data(), dP, outn * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0, n = 0;
+            const int64_t nst = srg / 8, per = (nst + g.kslices - 1) / g.kslices;
+            for (int ks = 0; ks < g.kslices; ks++)
+                for (int pr = 0; pr < ND * ND; pr++)
+                    for (int ta = 0; ta < g.nt; ta++)
+                        for (int tb = 0; tb <= ta; tb++) {
+                            const int tl = ta * (ta + 1) / 2 + tb, pi = pr / ND, pj = pr % ND;
+                            if (pi + pj > g.smax) continue;
+                            const int64_t g0 = std::min(nst, ks * per) * 8, g1 = std::min(nst, ks * per + per) * 8;  // 8 groups a stage
+                            for (int r = 0; r < GT; r += 7)
+                                for (int c = 0; c < GT; c += 5) {
+                                    long long ref = 0;
+                                    const int64_t pa = pi * gb + ta * GT + r, pb = pj * gb + tb * GT + c;
+                                    for (int64_t grp = g0; grp < g1; grp++)
+                                        for (int k = 0; k < 16; k++)
+                                            ref += (long long)hA[(grp * ld + pa) * 16 + k] * hB[(grp * ld + pb) * 16 + k];
+                                    const size_t o = (size_t)gemm_i8x_slab(ks, pi, pj, tl, g.nt) * GT * GT + (size_t)r * GT + c;
+                                    bad += got[o] != ref;
+                                    n++;
+                                }
+                        }
+            printf("small check k_gemm_i8x<%d,2>  %s (%zu of %zu differ)\n", wv, bad ? "FAIL" : "ok", bad, n);
+            if (bad) return 2;
+        }
+        CK(hipFree(dA));
+        CK(hipFree(dB));
+        CK(hipFree(dP));
+    }
+    const int64_t rg = rows / 16, gb = 1024, ld = zd_ld(gb);
+    int8_t *dA, *dB;
+    CK(hipMalloc(&dA, (size_t)rg * ld * 16));
+    CK(hipMalloc(&dB, (size_t)rg * ld * 16));
+    hipLaunchKernelGGL(k_fill_a, dim3(4096), dim3(256), 0, 0, dA, rg * ld * 16, 127, 21ull);
+    hipLaunchKernelGGL(k_fill_a, dim3(4096), dim3(256), 0, 0, dB, rg * ld * 16, 127, 23ull);
+    std::vector<int> kl = ks_list.empty() ? std::vector<int>{8, 12, 16} : ks_list;
+    for (int smax : {ND - 1})
+        for (int wv : {8})  // (16 waves spill: 32 VGPRs)
+            for (int ks : kl) {
+                GemmX g{};
+                make(smax, g);
+                g.A = dA;
+                g.B = dB;
+                g.lda = g.ldb = ld;
+                g.rg = rg;
+                g.gb = (int)gb;
+                g.nt = (int)(gb / GT);
+                g.kslices = ks;
+                const size_t outn = (size_t)g.kslices * ND * ND * (g.nt * (g.nt + 1) / 2) * GT * GT;
+                CK(hipMalloc(&g.out, outn * 4));
+                auto launch = [&] {
+                    if (wv == 8)
+                        hipLaunchKernelGGL((k_gemm_i8x<8, 2>), dim3((unsigned)gemm_i8x_items(g)), dim3(512), GEMM_I8X_LDS, 0, g);
+                    else
+                        hipLaunchKernelGGL((k_gemm_i8x<16, 2>), dim3((unsigned)gemm_i8x_items(g)), dim3(1024), GEMM_I8X_LDS, 0, g);
+                };
+                launch();
+                CK(hipGetLastError());
+                CK(hipDeviceSynchronize());
+                hipEvent_t e0, e1;
+                CK(hipEventCreate(&e0));
+                CK(hipEventCreate(&e1));
+                std::vector<float> ms;
+                for (int r = 0; r < reps; r++) {
+                    CK(hipEventRecord(e0, 0));
+                    launch();
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float t = 0;
+                    CK(hipEventElapsedTime(&t, e0, e1));
+                    ms.push_back(t);
+                }
+                std::sort(ms.begin(), ms.end());
+                const double ops = 2.0 * (double)rg * 16 * (double)gemm_i8x_pairs(smax) * (g.nt * (g.nt + 1) / 2) * GT * GT;
+                printf("gg     k_gemm_i8x<%d,2> pairs %d ks %2d  %8.3f ms (min %8.3f)  %7.1f TOP/s\n", wv, gemm_i8x_pairs(smax), ks,
+                       ms[ms.size() / 2], ms[0], ops / (ms[ms.size() / 2] * 1e-3) / 1e12);
+                fflush(stdout);
+                CK(hipFree(g.out));
+            }
+    CK(hipFree(dA));
+    CK(hipFree(dB));
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
     const int64_t rows = argc > 2 ? atoll(argv[2]) : 1000064;
@@ -111,13 +238,14 @@ int main(int argc, char** argv) {
             while (*p && *p != ',') p++;
             if (*p == ',') p++;
         }
+    if (!strcmp(ssel, "gg")) return run_gg(reps, rows, ks_list);
     const int64_t rg = rows / 16;
     int ncu = 256;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     std::vector<Variant> vs = {
-        {"k_gemm_i8<16,3> (product)", k_gemm_i8<16, 3>, 1024, 3 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
-        {"k_gemm_i8<16,4>", k_gemm_i8<16, 4>, 1024, 4 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
-        {"k_gemm_i8<8,3>", k_gemm_i8<8, 3>, 512, 3 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
+        {"k_gemm_i8<8,3> (product)", k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>, GEMM_I8_WAVES * 64, GEMM_I8_LDS},
+        {"k_gemm_i8<16,3>", k_gemm_i8<16, 3>, 1024, 3 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
+        {"k_gemm_i8<8,4>", k_gemm_i8<8, 4>, 512, 4 * PCX_GEMM_KS * (G_PANEL + G_PANEL_PK)},
     };
     for (auto& v : vs) CK(hipFuncSetAttribute((const void*)v.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.lds));
 
