@@ -161,12 +161,16 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
     # per row (the digit pass k_digits is in the stage time, not in the count)
     from pyconsensus_amd import _lib
 
+    # mixed_int8 bit 1: the general x general pairs on int8 as well, digits of tok w against digits
+    # of w, the D (D + 1) / 2 digit pairs i + j < D (k_gemm_i8x): no fp64 tiles left
     ng = meta["grid_events"]
     G = E - ng
     mixed = meta.get("mixed_int8", 0)
+    gg = bool(mixed & 2)
     digits = int(_lib.lib().pcx_mixed_digits())
-    fp_pairs = G * (G + 1) // 2 + (0 if mixed else G * ng)
-    i8_pairs = ng * (ng + 1) // 2 + (digits * G * ng if mixed else 0)
+    fp_pairs = 0 if gg else G * (G + 1) // 2 + (0 if mixed else G * ng)
+    i8_pairs = (ng * (ng + 1) // 2 + (digits * G * ng if mixed else 0) +
+                (digits * (digits + 1) // 2 * (G * (G + 1) // 2) if gg else 0))
     cov_flops_rank = 2.0 * cnt * fp_pairs
     i8_ops_rank = 2.0 * cnt * i8_pairs
     tfs = cov_flops_rank / (cov_ms * 1e-3) / 1e12 if cov_ms == cov_ms and fp_pairs else None
@@ -179,16 +183,18 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
             "stage_ms_per_step": [{k: round(p.get(k, 0.0), 3) for k in top} for p in step_prof],
             "branch": meta["branch"], "pi_iters": meta["pi_iters"], "flags": meta["flags"],
             "stage_ms": {k: round(v, 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1])},
-            "roofline_cov": {"bound": "mfma", "kernel": "k_syrk", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS,
+            "roofline_cov": {"bound": "mfma", "kernel": "k_syrk (none when mixed_int8 & 2)", "achieved": tfs,
+                             "peak": FP64_MFMA_PEAK_TFS,
                              "unit": "TFLOP/s", "frac": (tfs / FP64_MFMA_PEAK_TFS) if tfs else None,
                              "flops_per_launch": cov_flops_rank, "traffic": load_traffic("k_syrk"),
                              "pairs": ("fp64: pairs inside the general tiles (%d positions; %d grid events on int8; mixed pairs "
                                        "on int8 slices: %s)" % (G, ng, bool(mixed)))},
-            "roofline_cov_i8": {"bound": "mfma", "kernel": "k_gemm_i8 (grid + mixed launches) + k_digits",
+            "roofline_cov_i8": {"bound": "mfma", "kernel": "k_gemm_i8 (grid + mixed launches) + k_gemm_i8x (general "
+                                "pairs, when mixed_int8 & 2) + k_digits",
                                 "achieved": tops, "peak": I8_MFMA_PEAK_TOPS,
                                 "unit": "TOP/s", "frac": (tops / I8_MFMA_PEAK_TOPS) if tops else None,
                                 "ops_per_launch": i8_ops_rank, "mixed_digits": digits,
-                                "traffic": _sum_traffic(("k_gemm_i8_grid", "k_gemm_i8_mixed", "k_digits"))},
+                                "traffic": _sum_traffic(("k_gemm_i8_grid", "k_gemm_i8_mixed", "k_gemm_i8x", "k_digits"))},
             "grid_events": ng, "mixed_int8": mixed, "inplace": inplace,
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}

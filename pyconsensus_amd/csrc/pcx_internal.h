@@ -124,6 +124,14 @@ typedef struct {
     int32_t  ks_gg, ks_mx;        /* k-slices of the two int8 products (int32-exact row ranges)       */
     int32_t  fp_ks;               /* k-slices of the fp64 tiles (k_syrk)                              */
     int64_t  fp_ld;               /* row length of one fp64 slab: E, or 128 cov_jb when mixed          */
+    /* general x general pairs on int8 as well (cov_gg8, k_gemm_i8x): the digits of tok w (zD) against
+       PCX_NDIG digits of w (zE, at 2^f from the column's |F - mu| bound), the digit pairs i + j <=
+       PCX_NDIG - 1; k_syrk then runs nothing */
+    int32_t  cov_gg8;
+    int32_t  ks_gx;               /* k-slices of that product (int32-exact: |d e| <= 127^2 per row)   */
+    int8_t*  zE;                  /* [wcd_rows/16][zd_ld][16] digit s of w at s * 128 cov_jb + q       */
+    double*  escale;              /* [wcd_ld] 2^-f per general position                               */
+    int32_t* Pgx;                 /* gemm_i8x_slab(ks, i, j, lower tile) x [256][256] int32            */
     /* algorithms other than PCA (enum pcx_algorithm) */
     int32_t max_components;       /* "big-five" component count                                     */
     int32_t components;           /* out ("fixed-variance"): components used, else -1               */
@@ -140,10 +148,12 @@ typedef struct {
 #define PCX_NDIG 6
 #endif
 #define PCX_DBASE 254.0
-// positions per 16-row group of the digit operand zD: PCX_NDIG * gb rounded up to the GEMM's
-// 256-position tile, so the last p-tile's loads stay inside the row group (NDIG * 128 * odd
-// general tiles need not be a multiple of 256); the pad positions only feed discarded rows
-__host__ __device__ inline int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }
+// positions per 16-row group of the digit operands zD / zE: PCX_NDIG * gb rounded up to the GEMM's
+// 256-position tile plus one more tile, so every tile's loads stay inside the row group -- the
+// mixed block's last p-tile (NDIG * 128 * odd general tiles need not be a multiple of 256) and
+// the general x general tiles (i gb + 256 a .. + 255, a < ceil(gb / 256), reach past digit i into
+// digit i + 1 when gb is an odd multiple of 128); the pad positions only feed discarded entries
+__host__ __device__ inline int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256 + 256; }
 
 
 namespace pcx {

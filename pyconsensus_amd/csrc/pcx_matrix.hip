@@ -905,6 +905,8 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
             }
             if (m.ev[EV_MISS * E + c] > 0.0) bnd = fmax(bnd, fabs(m.ev[EV_GUESS * E + c] - mu));
             if (!__builtin_isfinite(bnd) || __builtin_isnan(mu)) bad = 1;
+            // the general x general product's digits of w itself: |w| 2^-f <= 1/2 likewise
+            if (m.escale) m.escale[q] = bnd > 0.0 && __builtin_isfinite(bnd) ? ldexp(1.0, -(ilogb(bnd) + 2)) : 1.0;
             // the digits are of tok w: |tok w| <= maxtok bnd < 2^(ilogb + 1), so |tok w| 2^-e <= 1/2
             // with e = ilogb + 2 (first digit |d| <= 64)
             bnd *= maxtok;
@@ -1216,11 +1218,36 @@ constexpr double DIG_SCALE = [] {  // 254^NDIG (exact: 6 digits need 48 bits)
     for (int k = 0; k < PCX_NDIG; k++) c *= PCX_DBASE;
     return c;
 }();
+// With cov_gg8 the same pass writes PCX_NDIG digits of w 2^-f (escale) to zE, the other operand of
+// the general x general product (w 2^-f is exact; X = rint(w 2^-f 254^NDIG) from the product and
+// its fma error, as for tok w).  Four lanes share a position's 16-row group, a quarter (4 rows, one
+// byte per row: one dword per digit) each, so a wave stores 16 positions x 16 bytes = 256
+// contiguous bytes per digit and a lane holds two dwords per digit (a lane per position holding
+// all 16 rows -- the round-4 layout -- took 182 VGPRs with both operands: two waves per SIMD,
+// 7.0 ms at C5 against 2.7 ms for the tok w digits alone).
+__device__ __forceinline__ void balanced_digits(double X, uint32_t (&d)[PCX_NDIG], int u, int32_t* dsum) {
+#pragma unroll
+    for (int k = PCX_NDIG - 1; k >= 0; k--) {
+        double di = X;
+        if (k > 0) {
+            const double qd = rint(X * (1.0 / PCX_DBASE));
+            di = fma(-qd, PCX_DBASE, X);
+            X = qd;
+        }
+        d[k] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * u);
+        if (dsum) dsum[k] += (int)di;
+    }
+}
+constexpr int DG_POS = BT / 4;  // positions per k_digits workgroup
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
-    const int q = blockIdx.x * BT + threadIdx.x;
-    if (q >= gb) return;
-    const double sc = m.dscale[q];
+    const int h = threadIdx.x & 3;  // rows 4h .. 4h + 3 of each 16-row group
+    const int q = blockIdx.x * DG_POS + (threadIdx.x >> 2);
+    const bool live = q < gb;
+    const int qq = live ? q : 0;
+    const double sc = m.dscale[qq];
+    const bool gg = m.cov_gg8 != 0;
+    const double esc = gg ? m.escale[qq] : 1.0;
     const int64_t ng = m.wcd_rows / 16;
     const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
     const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
@@ -1228,41 +1255,48 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     int32_t dsum[PCX_NDIG];  // |d| <= 127: int32-exact for any chunk under 16M rows
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
-    for (int64_t grp = g0; grp < g1; grp++) {
-        uint32_t d[PCX_NDIG][4];
+    for (int64_t grp = g0; live && grp < g1; grp++) {
+        uint32_t d[PCX_NDIG], e[PCX_NDIG];
 #pragma unroll
-        for (int k = 0; k < PCX_NDIG; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
+        for (int k = 0; k < PCX_NDIG; k++) d[k] = e[k] = 0;
+        double wr[4], tk[4];
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const double w = m.wcd[(grp * 16 + r) * m.wcd_ld + q] * sc;  // exact (power of two)
-            const double tk = m.tokp[grp * 16 + r];                       // 0 past n_rows
-            double hi = w * tk, lo = fma(w, tk, -hi);                      // tok w exactly
+        for (int u = 0; u < 4; u++) {
+            const int64_t i = grp * 16 + 4 * h + u;
+            wr[u] = m.wcd[i * m.wcd_ld + q];
+            tk[u] = m.tokp[i];  // 0 past n_rows
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const double w = wr[u] * sc;  // exact (power of two)
+            double hi = w * tk[u], lo = fma(w, tk[u], -hi);  // tok w exactly
             // X = rint((tok w 2^-e) 254^NDIG) (|X| <= 254^NDIG / 2 < 2^48, within 0.52 of the
             // exact value), then its balanced base-254 digits from the least significant up:
             // q = rint(X / 254) -- X / 254 is a multiple of 1/254 and X * (1/254) lies within 2^-14 of
             // it, so the rounding is exact but for the 1/2 tie, where either neighbour leaves
             // |d| = 127 -- and d = X - 254 q exactly
             const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv);
-            double X = rint(pv + fma(lo, DIG_SCALE, pe));
-#pragma unroll
-            for (int k = PCX_NDIG - 1; k >= 0; k--) {
-                double di = X;
-                if (k > 0) {
-                    const double qd = rint(X * (1.0 / PCX_DBASE));
-                    di = fma(-qd, PCX_DBASE, X);
-                    X = qd;
-                }
-                d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
-                dsum[k] += (int)di;
+            balanced_digits(rint(pv + fma(lo, DIG_SCALE, pe)), d, u, dsum);
+            if (gg) {
+                const double v = wr[u] * esc, uv = v * DIG_SCALE;
+                balanced_digits(rint(uv + fma(v, DIG_SCALE, -uv)), e, u, nullptr);
             }
         }
+        const int64_t o = (grp * ldd + q) * 16 + 4 * h;
 #pragma unroll
-        for (int k = 0; k < PCX_NDIG; k++)
-            *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
+        for (int k = 0; k < PCX_NDIG; k++) *(uint32_t*)(m.zD + o + (int64_t)k * gb * 16) = d[k];
+        if (gg) {
+#pragma unroll
+            for (int k = 0; k < PCX_NDIG; k++) *(uint32_t*)(m.zE + o + (int64_t)k * gb * 16) = e[k];
+        }
     }
 #pragma unroll
-    for (int k = 0; k < PCX_NDIG; k++)
-        if (dsum[k]) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)dsum[k]);
+    for (int k = 0; k < PCX_NDIG; k++) {  // the position's four quarters summed, one atomic
+        int32_t t = dsum[k];
+        t += __shfl_xor(t, 1, WAVE);
+        t += __shfl_xor(t, 2, WAVE);
+        if (live && h == 0 && t) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)t);
+    }
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -1412,6 +1446,34 @@ __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t 
     return dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q])));  // 2^e
 }
 
+// sum tok w_p w_q (q <= p < gb) from the general x general digit products (256-position tiles over
+// each digit's gb positions: p's tile ta = p / 256): the pairs of each
+// weight 254^-(s + 2) summed exactly in int64 (over the pairs i + j = s and the k-slices), Horner
+// over 1/254 in double-double from the smallest weight up, times 2^(e_p + f_q).  Dropping the pairs
+// i + j >= NDIG leaves < 5.2 254^-NDIG of the two bounds' product per row, beside the digits' own
+// residue (2 x 0.52 x 254^-NDIG x 1/2): ~2e-14 of |tok w_p| |w_q|'s bound, exact sums otherwise
+// (fp64 tiles: a rounding per multiply-add).
+__device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
+    constexpr int SMAX = PCX_NDIG - 1;
+    const int nt = (m.cov_jb * CT + GT - 1) / GT;
+    const int ta = (int)(p / GT), tb = (int)(q / GT), tl = ta * (ta + 1) / 2 + tb;
+    const int64_t within = (p % GT) * GT + (q % GT);
+    const int64_t kstride = gemm_i8x_slab(1, 0, 0, 0, nt) * (GT * GT);  // one k-slice's slabs
+    dd a{0.0, 0.0};
+    for (int sd = SMAX; sd >= 0; sd--) {
+        int64_t t = 0;
+        for (int i = 0; i <= sd && i < PCX_NDIG; i++) {
+            const int j = sd - i;
+            if (j >= PCX_NDIG) continue;
+            t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
+        }
+        a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)t, 0.0});
+    }
+    a = dd_div_base(dd_div_base(a));  // the (s + 2): 254^-2 more
+    // 2^(e_p + f_q) applied to the rounded value: the product of the two scales alone can overflow
+    return ldexp(dd_to_double(a), -ilogb(m.dscale[p]) - ilogb(m.escale[q]));
+}
+
 // S_q = sum tok w_q of every general position (shared by all grid rows): k_digits' digit sums
 // (exact), recombined like mixed_comb
 __global__ void __launch_bounds__(BT) k_cov_tokrow(pcx_mat m, double* S) {
@@ -1429,6 +1491,7 @@ __device__ __forceinline__ double cov_entry(const pcx_mat& m, const double* S, i
     const int64_t E = m.n_events;
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int64_t cp = m.cov_perm[p], cq = m.cov_perm[q];
+    if (m.cov_gg8 && p < gb) return gg_comb(m, p, q);  // general x general on int8 digits
     if (q < gb && (!m.cov_mixed || p < gb)) {  // fp64 tiles: the slabs of k_syrk
         const int64_t ld = m.fp_ld, sl = ld * ld;
         const double* cs = m.cslab + p * ld + q;
@@ -4847,7 +4910,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int np = (int)(m.n_events - gb);  // grid positions
             if (!m.zA || !m.zB || !m.zsum || !m.Pgg || m.cov_jb < 0 || m.cov_jb > nb || m.zq < np || m.ks_gg < 1 ||
                 (m.cov_mixed && m.ks_mx < 1) || m.zq % GT || m.wcd_rows % (64 * G_KS) ||
-                (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale || !m.dtok))) {
+                (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale || !m.dtok)) ||
+                (m.cov_gg8 && (!m.cov_mixed || !m.zE || !m.escale || !m.Pgx || m.ks_gx < 1))) {
                 err = "M_COV_I8: int8 operands missing or plan inconsistent";
                 return hipErrorInvalidValue;
             }
@@ -4873,7 +4937,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
                 if (hipMemsetAsync(m.dtok, 0, (size_t)PCX_NDIG * gb * 8, st) != hipSuccess) return hipGetLastError();
-                hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
+                hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
                 GemmI8 g{m.zD, zd_ld(gb), m.zB, m.zq, m.Pmx, (int64_t)PCX_NDIG * gb, m.zq * PCX_NDIG * gb, PCX_NDIG * gb, np,
                          0, 0, 0, m.ks_mx, rg, 1};
                 g.tp = (PCX_NDIG * gb + GT - 1) / GT;
@@ -4885,6 +4949,20 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 hipLaunchKernelGGL((k_gemm_i8<GEMM_I8_WAVES, GEMM_I8_NBUF>), dim3((unsigned)gemm_i8_items(g.tp, g.tq, g.lower, g.kslices)), dim3(GEMM_I8_WAVES * 64),
                                    GEMM_I8_LDS, st, g);
             }
+            if (m.cov_gg8) {
+                // general x general: digits of tok w (zD) x digits of w (zE), the digit pairs
+                // i + j <= NDIG - 1 over the lower event tiles; |d e| <= 127^2 per row
+                static std::once_flag x_once;
+                static hipError_t x_err = hipSuccess;
+                std::call_once(x_once, [] {
+                    x_err = hipFuncSetAttribute((const void*)k_gemm_i8x<GEMM_I8X_WAVES, GEMM_I8X_NBUF>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8X_LDS);
+                });
+                if (x_err != hipSuccess) return x_err;
+                GemmX g{m.zD, m.zE, zd_ld(gb), zd_ld(gb), m.Pgx, rg, gb, (gb + GT - 1) / GT, PCX_NDIG - 1, m.ks_gx};
+                hipLaunchKernelGGL((k_gemm_i8x<GEMM_I8X_WAVES, GEMM_I8X_NBUF>), dim3((unsigned)gemm_i8x_items(g)),
+                                   dim3(GEMM_I8X_WAVES * 64), GEMM_I8X_LDS, st, g);
+            }
             break;
         }
         case M_WCD:
@@ -4892,8 +4970,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int nb = (int)(m.wcd_ld / CT);
             if (!m.wcd || !m.tokp || !m.rowpart || !m.cov_perm || !m.cov_pos || m.wcd_rows % 64 ||
                 m.wcd_rows < m.n_rows || m.wcd_ld % CT || m.wcd_ld < m.n_events || m.cov_jb < 0 || m.cov_jb > nb ||
-                m.cov_fp_tiles != (m.cov_mixed ? m.cov_jb * (m.cov_jb + 1) / 2
-                                                : m.cov_jb * nb - m.cov_jb * (m.cov_jb - 1) / 2) ||
+                m.cov_fp_tiles != (m.cov_gg8     ? 0
+                                   : m.cov_mixed ? m.cov_jb * (m.cov_jb + 1) / 2
+                                                 : m.cov_jb * nb - m.cov_jb * (m.cov_jb - 1) / 2) ||
                 (m.cov_jb < nb && (!m.zA || !m.zB || !m.zsum))) {
                 err = "M_COV: wcd workspace missing or mis-sized (wcd_rows % 16, wcd_ld % 128) or no plan";
                 return hipErrorInvalidValue;

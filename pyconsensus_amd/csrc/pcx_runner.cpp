@@ -78,7 +78,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx, clw, fg, nam, dtok;
+    } pgg, zd, pmx, clw, fg, nam, dtok, ze, pgx;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -92,7 +92,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok, &ze, &pgx})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -285,7 +285,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
         {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
-        {(void**)&w->dscale, (size_t)w->wcd_ld * 8, false},
+        {(void**)&w->dscale, (size_t)(2 * w->wcd_ld) * 8, false},  // dscale, then escale
     };
     auto align = [](size_t b) { return (b + 255) / 256 * 256; };
     size_t zb = 0;
@@ -941,6 +941,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.zB = w->zB;
                 m.zsum = w->zsum;
                 m.dscale = w->dscale;
+                m.escale = w->dscale + w->wcd_ld;
                 R.stage(m, M_COV_PLAN);
                 int64_t plan[2];  // general events, mixed pairs on int8
                 R.hip(hipMemcpyAsync(plan, m.info + INFO_COV_GENERAL, sizeof(plan), hipMemcpyDeviceToHost, R.st),
@@ -1007,7 +1008,24 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.Fg = m.compact ? (double*)w->fg.p : nullptr;
                 m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
                 m.Pmx = (int32_t*)w->pmx.p;
-                m.cov_fp_tiles = (int32_t)(m.cov_mixed ? jb * (jb + 1) / 2 : jb * nb - jb * (jb - 1) / 2);
+                // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
+                // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
+                if (m.cov_mixed) {
+                    const int64_t nt = (gb + 255) / 256, npair = gemm_i8x_pairs(PCX_NDIG - 1);
+                    // |d e| <= 127^2 per row: int32-exact k-slices of <= 133,143 rows
+                    m.ks_gx = ks_for(npair * nt * (nt + 1) / 2, 133120,
+                                     4.0 * (double)(npair * nt * (nt + 1) / 2) * 256.0 * 256.0);
+                    m.cov_gg8 = w->grow(w->ze, (size_t)(w->wcd_rows * zd_ld(gb))) &&
+                                        w->grow(w->pgx, (size_t)(gemm_i8x_slab(m.ks_gx, 0, 0, 0, (int)nt) * 256 * 256 * 4))
+                                    ? 1
+                                    : 0;
+                    m.zE = (int8_t*)w->ze.p;
+                    m.Pgx = (int32_t*)w->pgx.p;
+                }
+                r->mixed_int8 = m.cov_mixed ? (m.cov_gg8 ? 3 : 1) : 0;
+                m.cov_fp_tiles = (int32_t)(m.cov_gg8     ? 0
+                                           : m.cov_mixed ? jb * (jb + 1) / 2
+                                                         : jb * nb - jb * (jb - 1) / 2);
                 // fp64 slabs: [E][E] for the trapezoid; the mixed triangle's [gb][gb] slabs are
                 // small, so it takes more k-slices (~16 WGs per CU) within the same cslab
                 m.fp_ld = m.cov_mixed ? gb : E;

@@ -3,7 +3,11 @@
 Binary events whose filled values all lie on {1, 1.5, 2} ("grid" events) take the wcd
 positions after the general events; the covariance tiles made only of grid positions are
 P = sum tok z z^T on int8 MFMA with z = 2 (F - 1), combined with the exact T and Z sums;
-the general x grid pairs multiply PCX_NDIG (6) base-254 int8 digit slices of tok w (w = F - mu) with z.
+the general x grid pairs multiply PCX_NDIG (6) base-254 int8 digit slices of tok w (w = F - mu) with z,
+and when the general events fill whole 256-event tiles the general x general pairs multiply those
+digits with PCX_NDIG digit slices of w (k_gemm_i8x; pcx_result.mixed_int8 == 3), over 256-position
+tiles that reach into the next digit's positions when the general events fill an odd number of
+128-event tiles.
 The wpca entry's covariance is checked against the reference formula
 (pyconsensus/__init__.py:317-326) evaluated in numpy: all-general, mixed, all-grid,
 varying tokens (tok * z operand), off-grid values and tokens above 63 (no int8 path).
@@ -46,6 +50,9 @@ CASES = {
     "tokens_above_63": (3000, 300, 0.25, "int", (), False),
     "single_tile": (20000, 100, 0.3, None, (), True),  # general and grid share the one tile: fp64
     "two_tiles": (20000, 200, 0.3, None, (), True),
+    # 256 and 512 general positions (1 and 2 whole 256-position tiles)
+    "gg_int8_one_tile": (40000, 700, 0.33, None, (), True),
+    "gg_int8_int_rep": (40000, 900, 0.5, "int", (), True),
 }
 
 
@@ -61,8 +68,9 @@ def test_wpca_covariance_grid(name):
     n_grid = int(E - sc.sum() - len([c for c in og if not sc[c]]))
     gb = -(-(E - n_grid) // 128) * 128  # general events take the first 128-event tiles
     assert meta["grid_events"] == (max(0, E - gb) if expect else 0), (meta["grid_events"], n_grid)
-    # general x grid pairs on int8 digit slices whenever both kinds of tile are present
-    assert meta["mixed_int8"] == (1 if expect and 0 < gb < E else 0)
+    # general x grid and general x general pairs on int8 digit slices whenever both kinds of tile
+    # are present
+    assert meta["mixed_int8"] == (3 if expect and 0 < gb < E else 0), (meta["mixed_int8"], gb)
     np.testing.assert_allclose(outs["weighted_mean"], mu, rtol=1e-14, atol=0)
     scale = np.abs(cov).max()
     err = np.abs(outs["covariance"] - cov).max() / scale

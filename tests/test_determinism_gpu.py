@@ -76,7 +76,7 @@ def test_matrix_replay_c5w_c4(gpu_lib):
     torch.cuda.synchronize(dev)
     _assert_same(a1, a2, "C5w")
     _scalars_same(s1, s2, "C5w")
-    assert s1["mixed_int8"] == 1 and s1["grid_events"] > 0
+    assert s1["mixed_int8"] & 1 and s1["grid_events"] > 0
 
 
 @pytest.mark.timeout(600)

@@ -228,7 +228,7 @@ def test_matrix_vs_numpy_oracle(gpu_lib, case, world):
     if case in ("C4", "C5w"):
         # C4: integer reputations, tokens int(r / sum(r) 1e6) in [0, 19] -- non-uniform tokens through
         # the int8 blocks (the mixed block's digits of tok * w); C5w: the 3,072-event grid
-        assert info.get("mixed_int8") == 1 and info.get("grid_events", 0) > 0, info
+        assert info.get("mixed_int8", 0) & 1 and info.get("grid_events", 0) > 0, info
 
 
 def test_virtual_shards_match_single(gpu_lib):

@@ -19,6 +19,7 @@
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
 #   ab_shard=L1,L2  one C5 shard's latency of several libpcx builds, alternating twice
+#   kt_c5=L1,L2  rocprofv3 kernel trace of one C5 consensus per libpcx build, per-kernel times (tools/kt_top.py)
 #   i8bench      the int8 covariance GEMM variants at the C5 shapes (tools/i8bench, built on the CPU)
 #   i8ks=S:K,..  the product int8 GEMM on shape S (mixed | grid) at each k-slice count K
 #   i8pmc=V      SQ / LDS / cache PMC passes over the mixed-block GEMM, reference kernel and variant V
@@ -108,6 +109,15 @@ for STEP in "$@"; do
         PCX_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-c4 --c5-steps 3 --steps 3 > $O/ab.json 2> $O/ab.err || { echo "ab rc=$? ($L)"; tail -3 $O/ab.err; exit 23; }
         c5_line $O/ab.json "$L"
       done; done ;;
+    kt_c5=*)
+      IFS=, read -ra LIBS <<< "${STEP#kt_c5=}"
+      i=0
+      for L in "${LIBS[@]}"; do
+        i=$((i+1))
+        PCX_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt$i -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --c5-steps 1 --no-c4 > $O/kt$i.log 2>&1 || { echo "kt_c5 rc=$? ($L)"; tail -5 $O/kt$i.log; exit 30; }
+        echo "== $L"
+        python3 tools/kt_top.py $(find $O/kt$i -name "kt_kernel_trace.csv" | head -1) -1 14 || exit 31
+      done ;;
     ab_shard=*)
       IFS=, read -ra LIBS <<< "${STEP#ab_shard=}"
       for i in 1 2; do for L in "${LIBS[@]}"; do
