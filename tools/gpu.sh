@@ -131,14 +131,16 @@ for STEP in "$@"; do
       A=${STEP#i8ks=}
       timeout -k 10 300 tools/i8bench/i8bench 3 1000064 product "${A%%:*}" "${A#*:}" > $O/i8ks_${A%%:*}.txt 2>&1 || { echo "i8ks rc=$?"; tail -20 $O/i8ks_${A%%:*}.txt; exit 29; }
       grep -v "small check" $O/i8ks_${A%%:*}.txt ;;
-    i8pmc=*)
+    i8pmc=*)  # i8pmc=V or i8pmc=V:SHAPE (SHAPE: mixed (default) | grid | gg)
       V=${STEP#i8pmc=}
+      SH=mixed
+      case $V in *:*) SH=${V#*:}; V=${V%%:*} ;; esac
       i=0
       for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU" \
                "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE" \
                "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i+1))
-        timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/i8p$i -o pmc -- tools/i8bench/i8bench 2 1000064 "$V" mixed > $O/i8p$i.log 2>&1 || { echo "i8pmc pass $i rc=$?"; tail -5 $O/i8p$i.log; exit 25; }
+        timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/i8p$i -o pmc -- tools/i8bench/i8bench 2 1000064 "$V" $SH > $O/i8p$i.log 2>&1 || { echo "i8pmc pass $i rc=$?"; tail -5 $O/i8p$i.log; exit 25; }
       done
       python3 tools/pmc_summary.py --per-kernel "$O" --glob "i8p*" > $O/i8pmc.txt 2>&1 || { echo "i8pmc summary failed"; tail -5 $O/i8pmc.txt; exit 26; }
       cat $O/i8pmc.txt ;;

@@ -26,7 +26,7 @@
 
 using namespace pcx;
 
-static int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256; }  // (pcx_internal.h)
+static int64_t zd_ld(int64_t gb) { return ((int64_t)PCX_NDIG * gb + 255) / 256 * 256 + 256; }  // (pcx_internal.h)
 
 #define CK(x)                                                                              \
     do {                                                                                   \
@@ -143,14 +143,15 @@ static int run_gg(int reps, int64_t rows, const std::vector<int>& ks_list) {
             std::vector<int32_t> got(outn);
             CK(hipMemcpy(got.data(), dP, outn * 4, hipMemcpyDeviceToHost));
             size_t bad = 0, n = 0;
-            const int64_t nst = srg / 8, per = (nst + g.kslices - 1) / g.kslices;
+            const int64_t spg = 8;  // row groups per stage (two k-steps)
+            const int64_t nst = srg / spg, per = (nst + g.kslices - 1) / g.kslices;
             for (int ks = 0; ks < g.kslices; ks++)
                 for (int pr = 0; pr < ND * ND; pr++)
                     for (int ta = 0; ta < g.nt; ta++)
                         for (int tb = 0; tb <= ta; tb++) {
                             const int tl = ta * (ta + 1) / 2 + tb, pi = pr / ND, pj = pr % ND;
                             if (pi + pj > g.smax) continue;
-                            const int64_t g0 = std::min(nst, ks * per) * 8, g1 = std::min(nst, ks * per + per) * 8;  // 8 groups a stage
+                            const int64_t g0 = std::min(nst, ks * per) * spg, g1 = std::min(nst, ks * per + per) * spg;
                             for (int r = 0; r < GT; r += 7)
                                 for (int c = 0; c < GT; c += 5) {
                                     long long ref = 0;
