@@ -278,7 +278,8 @@ typedef struct {
     double  comm_bytes;           /* bytes this rank passed to collectives (all-reduce buffers + all-gather sends) */
     int32_t grid_events;          /* grid events (binary, filled values on {1, 1.5, 2}) past the general 128-event tiles:
                                      their covariance block ran on int8 MFMA */
-    int32_t mixed_int8;           /* 1: general x grid pairs ran on int8 digit slices too (else fp64 MFMA) */
+    int32_t mixed_int8;           /* bit 0: general x grid pairs ran on int8 digit slices too (else fp64 MFMA);
+                                     bit 1: and the general x general pairs (digits of tok w x digits of w) */
 } pcx_result;
 
 /* The whole consensus (__init__.py:502-611) on this rank's rows; collective over
@@ -325,8 +326,8 @@ double  pcx_seqsum_const(double c, int64_t k);
 int64_t pcx_seqsum_first_above(double c, double t, int64_t kmax);
 
 /* Build parameter: balanced base-254 int8 digits per general event in the covariance's mixed block
- * (pcx_result.mixed_int8; the int8 work per row is then grid pairs + digits x general x
- * (grid + 1)).  For roofline accounting. */
+ * (pcx_result.mixed_int8 bit 0; the int8 work per row is then grid pairs + digits x general x grid,
+ * plus digits (digits + 1) / 2 x the general pairs with bit 1).  For roofline accounting. */
 int pcx_mixed_digits(void);
 
 /* The RCCL that serves libpcx's collectives: *runtime = ncclGetVersion() of the librccl the

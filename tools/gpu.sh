@@ -84,7 +84,8 @@ for STEP in "$@"; do
       grep '"mode"' $O/host.err ;;
     shard_prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard_kt -o kt -- python3 tools/c5_shard_latency.py 8 3 > $O/shard_kt.log 2>&1 || { echo "shard kernel-trace rc=$?"; tail -5 $O/shard_kt.log; exit 27; }
-      echo shard_prof ok ;;
+      KT=$(find $O/shard_kt -name "kt_kernel_trace.csv" | head -1)
+      python3 tools/kt_top.py $KT -1 24 && python3 tools/trace_gaps.py $KT -1 15 > $O/shard_gaps.txt && head -12 $O/shard_gaps.txt ;;
     dist)
       timeout -k 10 240 python -u -m pytest tests/test_dist_gpu.py -x -v --timeout 200 --timeout-method thread > $O/pytest_dist.log 2>&1 || { echo "pytest dist rc=$?"; tail -40 $O/pytest_dist.log; exit 20; }
       tail -1 $O/pytest_dist.log
