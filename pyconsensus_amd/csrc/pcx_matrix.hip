@@ -52,7 +52,7 @@ constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
 
 enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ, EV_FIN, EV_CERT, EV_PC,
-               EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE, EV_LDP, EV_K };  // (pcx_runner.cpp: EV_SLOTS)
+               EV_MINX, EV_MAXX, EV_MISS, EV_NZERO, EV_SPARE, EV_LDP, EV_K, EV_MUP };  // (pcx_runner.cpp: EV_SLOTS)
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
@@ -1011,7 +1011,9 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                         // wcd = F - mu of the general positions (all of them without the int8 mixed
                         // block) for k_syrk / k_scores_grid / k_digits (centring the compact Fg on
                         // the fly instead writes 8 GB less at C5, but k_syrk then runs 26 ms, not 18)
-                        if (pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb)) m.wcd[i * ld + pos[k]] = w[k];
+                        // (with cov_gg8 nothing reads wcd: k_digits and k_scores_grid take Fg - mu,
+                        // the same subtraction bit for bit -- 8 GB fewer bytes written at C5)
+                        if (pos[k] >= 0 && (!m.cov_mixed || pos[k] < gb) && !m.cov_gg8) m.wcd[i * ld + pos[k]] = w[k];
                     }
                     // in place (result["original"] aliases the reports, as the reference's own does,
                     // __init__.py:121, 266-269, 584): only the scaled columns change -- the rescaled
@@ -1248,6 +1250,7 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const double sc = m.dscale[qq];
     const bool gg = m.cov_gg8 != 0;
     const double esc = gg ? m.escale[qq] : 1.0;
+    const double mu = gg ? m.ev[EV_MU * m.n_events + m.cov_perm[qq]] : 0.0;  // w = Fg - mu (k_wcd's own op)
     const int64_t ng = m.wcd_rows / 16;
     const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
     const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
@@ -1263,7 +1266,7 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int64_t i = grp * 16 + 4 * h + u;
-            wr[u] = m.wcd[i * m.wcd_ld + q];
+            wr[u] = gg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q];
             tk[u] = m.tokp[i];  // 0 past n_rows
         }
 #pragma unroll
@@ -1815,6 +1818,7 @@ __global__ void __launch_bounds__(WAVE) k_scores_prep(pcx_mat m) {
     for (int q = lane; q < gb && q < E; q += WAVE) {
         const int c = m.cov_perm[q];
         LDp[q] = c >= 0 ? LD[c] : 0.0;
+        m.ev[EV_MUP * E + q] = c >= 0 ? m.ev[EV_MU * E + c] : 0.0;  // mu in position order (cov_gg8: Fg - mu)
     }
     double kk = 0.0;
     for (int q = lane; q < ng; q += WAVE) {
@@ -1846,11 +1850,20 @@ __global__ void __launch_bounds__(BT) k_scores_grid(pcx_mat m) {
         double a[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) a[r] = 0.0;
-        for (int q = lane; q < gb; q += WAVE) {
-            const double l = LDp[q];
-            const double* w = m.wcd + g * 16 * ld + q;
+        if (m.cov_gg8) {  // no wcd written: F - mu from Fg (k_wcd's own subtraction, bit for bit)
+            for (int q = lane; q < gb; q += WAVE) {
+                const double l = LDp[q], mu = m.ev[EV_MUP * E + q];
+                const double* f = m.Fg + g * 16 * gb + q;
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
+                for (int r = 0; r < 16; r++) a[r] = fma(f[r * gb] - mu, l, a[r]);
+            }
+        } else {
+            for (int q = lane; q < gb; q += WAVE) {
+                const double l = LDp[q];
+                const double* w = m.wcd + g * 16 * ld + q;
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = fma(w[r * ld], l, a[r]);
+            }
         }
         double z[16];
 #pragma unroll
@@ -4911,7 +4924,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (!m.zA || !m.zB || !m.zsum || !m.Pgg || m.cov_jb < 0 || m.cov_jb > nb || m.zq < np || m.ks_gg < 1 ||
                 (m.cov_mixed && m.ks_mx < 1) || m.zq % GT || m.wcd_rows % (64 * G_KS) ||
                 (m.cov_mixed && (!m.zD || !m.Pmx || !m.dscale || !m.dtok)) ||
-                (m.cov_gg8 && (!m.cov_mixed || !m.zE || !m.escale || !m.Pgx || m.ks_gx < 1))) {
+                (m.cov_gg8 && (!m.cov_mixed || !m.compact || !m.Fg || !m.zE || !m.escale || !m.Pgx || m.ks_gx < 1))) {
                 err = "M_COV_I8: int8 operands missing or plan inconsistent";
                 return hipErrorInvalidValue;
             }

@@ -30,7 +30,7 @@ namespace {
 constexpr int BT = 256;
 constexpr int CS = 16;  // dd slots per column in cstat
 constexpr int CM = 8;   // doubles per column in mpart / cmax
-constexpr int EV_SLOTS = 18;  // E-sized rows of ev (pcx_matrix.hip ev_slot)
+constexpr int EV_SLOTS = 19;  // E-sized rows of ev (pcx_matrix.hip ev_slot)
 constexpr int SS = 16;  // dd slots in scal
 constexpr int SC_BIGTOK_SLOT = 10;  // scal slot: count of tokens outside [0, 63] (pcx_matrix.hip SC_BIGTOK)
 constexpr int COV_TILE = 128;
@@ -1007,10 +1007,10 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                                 : 0;
                 m.Fg = m.compact ? (double*)w->fg.p : nullptr;
                 m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
-                m.Pmx = (int32_t*)w->pmx.p;
                 // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
                 // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
-                if (m.cov_mixed) {
+                // (it reads the general positions' F - mu from the compact Fg, so k_wcd writes no wcd)
+                if (m.cov_mixed && m.compact) {
                     const int64_t nt = (gb + 255) / 256, npair = gemm_i8x_pairs(PCX_NDIG - 1);
                     // |d e| <= 127^2 per row: int32-exact k-slices of <= 133,143 rows
                     m.ks_gx = ks_for(npair * nt * (nt + 1) / 2, 133120,
@@ -1022,6 +1022,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     m.zE = (int8_t*)w->ze.p;
                     m.Pgx = (int32_t*)w->pgx.p;
                 }
+                m.Pmx = (int32_t*)w->pmx.p;
                 r->mixed_int8 = m.cov_mixed ? (m.cov_gg8 ? 3 : 1) : 0;
                 m.cov_fp_tiles = (int32_t)(m.cov_gg8     ? 0
                                            : m.cov_mixed ? jb * (jb + 1) / 2
