@@ -2,7 +2,8 @@
 (kt_kernel_trace.csv; calls split as in tools/trace_gaps.py): launches, total and mean ms per kernel,
 largest first.
 
-usage: python tools/kt_top.py TRACE.csv [call_index=-1] [top=15]
+usage: python tools/kt_top.py TRACE.csv [call_index=-1] [top=15] [name_prefix]
+(with name_prefix: also every launch of the kernels whose name starts with it, in order)
 """
 import sys
 
@@ -23,6 +24,9 @@ def main():
     print("call %d: span %.3f ms, kernels %.3f ms" % (idx, span, sum(s for _, s in agg.values()) / 1e6))
     for name, (n, s) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         print("  %-48s %4d x  %8.3f ms  (mean %.3f)" % (name, n, s / 1e6, s / 1e6 / n))
+    if len(sys.argv) > 4:
+        print("  launches of %s*: %s" % (sys.argv[4], " ".join("%.3f" % ((t1 - t0) / 1e6) for t0, t1, name in c
+                                                             if name.startswith(sys.argv[4]))))
 
 
 if __name__ == "__main__":
