@@ -246,9 +246,9 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8(GemmI8 g) {
 // slices in the A layout above -- A the digits of tok w (zD), B those of w (zE), digit i of general
 // position q at position i gb + q -- and the product of digit i of p with digit j of q is weighted
 // 254^-(i + j + 2).  Only the digit pairs with i + j <= smax matter at fp64's level and only the
-// lower event tiles (p >= q) are needed.  Items run k-slice major, then by A panel (digit i, tile
-// a), then (digit j, tile b <= a), so the workgroups resident on one XCD at a time share their A
-// panels in its L2; each writes its whole 256 x 256 int32 tile to its own slab,
+// lower event tiles (p >= q) are needed.  Items run k-slice major, then by output tile, then by
+// digit pair, so the workgroups resident on one XCD at a time share their digit panels in its L2;
+// each writes its whole 256 x 256 int32 tile to its own slab,
 // out[ks][i][j][tile (a, b)][256][256] (row: the position of p in the tile, column: that of q).
 struct GemmX {
     const int8_t* A;  // [rg][lda][16]
@@ -291,19 +291,22 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8x(GemmX g) {
     const int ntri = g.nt * (g.nt + 1) / 2, npair = gemm_i8x_pairs(g.smax);
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / (npair * ntri);
+    // tile major: every digit pair of one output tile, then the next tile (a, b + 1) -- the items
+    // resident on one XCD share both operands' digit panels (11.85 vs 12.09 ms at C5 against
+    // ordering by A panel, digit i then tile a, then (j, b))
     int r = item % (npair * ntri), i = 0;
-    for (;; i++) {  // digit i of the A panel: (min(smax - i, NDIG - 1) + 1) digits j x ntri tiles each
+    const int tl = r / npair;
+    r %= npair;
+    for (;; i++) {  // digit i: min(smax - i, NDIG - 1) + 1 digits j
         const int nj = (g.smax - i < PCX_NDIG - 1 ? g.smax - i : PCX_NDIG - 1) + 1;
-        if (r < nj * ntri) break;
-        r -= nj * ntri;
+        if (r < nj) break;
+        r -= nj;
     }
-    const int nj = (g.smax - i < PCX_NDIG - 1 ? g.smax - i : PCX_NDIG - 1) + 1;
-    int ta = 0;
-    while (r >= nj * (ta + 1)) {  // tile row a holds nj (a + 1) items (j, b <= a)
-        r -= nj * (ta + 1);
-        ta++;
-    }
-    const int j = r / (ta + 1), tb = r % (ta + 1), tl = ta * (ta + 1) / 2 + tb;
+    const int j = r;
+    int ta = (int)((__builtin_sqrtf(8.0f * (float)tl + 1.0f) - 1.0f) * 0.5f);  // tl = ta (ta + 1) / 2 + tb
+    while (ta * (ta + 1) / 2 > tl) ta--;
+    while ((ta + 1) * (ta + 2) / 2 <= tl) ta++;
+    const int tb = tl - ta * (ta + 1) / 2;
     const int64_t nst = g.rg / (4 * KS);
     const int64_t per = (nst + g.kslices - 1) / g.kslices;
     const int64_t s0 = ks * per < nst ? ks * per : nst;
