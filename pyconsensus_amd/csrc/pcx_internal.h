@@ -66,11 +66,15 @@ typedef struct {
     /* weighted-median selection: per scaled event (reduced over ranks by SUM / MIN / MAX) */
     uint64_t* sel_state;          /* [n_scaled][SELS] range, sums, mode, result    */
     uint64_t* sel_isum;           /* [n_scaled][4] total weight limbs, count       (SUM) */
-    uint64_t* sel_imin;           /* [n_scaled][2] min key, min weight bits        (MIN) */
+    /* a pass over n_active events reduces over ranks in two collectives: one SUM of hist_w | hist_n
+       and one MAX of hist_min | hist_max (| sel_imin | sel_imax after the first pass) -- hist_n
+       starts right after hist_w's n_active rows, hist_max after hist_min's (the runner moves the
+       two pointers per pass), and every minimum is stored complemented (~min) so that MAX reduces it */
+    uint64_t* sel_imin;           /* [n_scaled][2] ~(min key, min weight bits)     (MAX) */
     uint64_t* sel_imax;           /* [n_scaled][2] max key, max weight bits        (MAX) */
     uint64_t* hist_w;             /* [n_active][256][3] bucket weight limbs (SUM; weight-mode events) */
     uint64_t* hist_n;             /* [n_active][256] bucket element count          (SUM) */
-    uint64_t* hist_min;           /* [n_active][256] bucket min key                (MIN) */
+    uint64_t* hist_min;           /* [n_active][256] ~(bucket min key)             (MAX) */
     uint64_t* hist_max;           /* [n_active][256] bucket max key                (MAX) */
     uint64_t* sel_arg;            /* [2][n_scaled] first dominant row (MIN), its value key (MAX) */
     int32_t*  sel_act;            /* [n_scaled] active scaled events, compacted in event order */

@@ -2734,7 +2734,8 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
             tb += m.hist_w[(o + b) * 3 + 1];
             tc += m.hist_w[(o + b) * 3 + 2];
         }
-        kmin = m.hist_min[o + b] < kmin ? m.hist_min[o + b] : kmin;
+        const uint64_t bmin = ~m.hist_min[o + b];  // (stored complemented: one MAX reduce, pcx_internal.h)
+        kmin = bmin < kmin ? bmin : kmin;
         kmax = m.hist_max[o + b] > kmax ? m.hist_max[o + b] : kmax;
     }
 #pragma unroll
@@ -2748,7 +2749,7 @@ __global__ void __launch_bounds__(BT) k_sel_start(pcx_mat m) {
         kmax = omx > kmax ? omx : kmax;
     }
     if (lane != 0) return;
-    const uint64_t wminb = m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
+    const uint64_t wminb = ~m.sel_imin[s * 2 + 1], wmaxb = m.sel_imax[s * 2 + 1];
     // weights outside [0, 2^8) -- a negative reputation (rep / sum(rep) keeps its sign,
     // __init__.py:142-145; smooth_rep inherits it, :472) or one above 256 times the total: the
     // exact limbs hold only [0, 2^8) (pcx_device.h to_limbs), so replay in the reference's order.
@@ -3151,7 +3152,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            m.sel_imin[s * 2 + 1] = f_wlo;  // all ranks: MIN / MAX before k_sel_start
+            m.sel_imin[s * 2 + 1] = ~f_wlo;  // all ranks: (complemented) MAX before k_sel_start
             m.sel_imax[s * 2 + 1] = f_whi;
             if (f_gn) {  // this rank's filled rows, all at the fill value (inside [lo, hi])
                 st[SW_GN] = f_gn;
@@ -3211,7 +3212,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
             m.hist_w[(o + b) * 3 + 2] = sc;
         }
         m.hist_n[o + b] = sn;
-        m.hist_min[o + b] = mn;
+        m.hist_min[o + b] = ~mn;  // complemented: the ranks' minima and maxima reduce in one MAX
         m.hist_max[o + b] = mx;
     }
 }
@@ -3264,7 +3265,7 @@ __global__ void __launch_bounds__(BT) k_sel_step(pcx_mat m, int n_active) {
         nb[j] = m.hist_n[o + b];
         const uint64_t* hs = m.hist_w + (o + b) * 3;
         hw[j] = (wmode && nb[j]) ? l3_norm({hs[0], hs[1], hs[2]}) : L3{0, 0, 0};
-        kmn[j] = m.hist_min[o + b];
+        kmn[j] = ~m.hist_min[o + b];
         kmx[j] = m.hist_max[o + b];
         sc += nb[j];
         sa += hw[j].a;

@@ -63,7 +63,7 @@ struct pcx_workspace {
     uint32_t* rowstat;
     uint64_t* skey;
     int64_t* info;
-    uint64_t *sel_state, *sel_isum, *sel_imin, *sel_imax, *hist_w, *hist_n, *hist_min, *hist_max, *sel_arg;
+    uint64_t *sel_state, *sel_isum, *hist_w, *hist_min, *sel_arg;
     int32_t *sel_act, *hard, *hard_cols, *hard_modes, *scols, *sidx;
     double *wcd, *tokp, *scalars, *xsend, *xrecv;
     uint32_t* rowpart;
@@ -258,8 +258,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->info, (size_t)16 * 8, true},
         {(void**)&w->sel_state, (size_t)(S * SELS) * 8, true},
         {(void**)&w->sel_isum, (size_t)(S * 4) * 8, true},
-        {(void**)&w->sel_imin, (size_t)(S * 2) * 8, true},
-        {(void**)&w->sel_imax, (size_t)(S * 2) * 8, true},
+
         {(void**)&w->sel_arg, (size_t)(S * 2) * 8, true},
         {(void**)&w->sel_act, (size_t)S * 4, true},
         {(void**)&w->hard, (size_t)E * 4, true},
@@ -270,10 +269,10 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->scols, (size_t)S * 4, false},
         {(void**)&w->sidx, (size_t)E * 4, false},
         {(void**)&w->scalars, (size_t)4 * 8, true},
-        {(void**)&w->hist_w, (size_t)(S * SEL_NB * 3) * 8, false},
-        {(void**)&w->hist_n, (size_t)(S * SEL_NB) * 8, false},
-        {(void**)&w->hist_min, (size_t)(S * SEL_NB) * 8, false},
-        {(void**)&w->hist_max, (size_t)(S * SEL_NB) * 8, false},
+        // hist_w | hist_n (one SUM per pass), hist_min | hist_max | sel_imin | sel_imax (one MAX):
+        // the runner places hist_n / hist_max right after the pass's active rows (select())
+        {(void**)&w->hist_w, (size_t)(S * SEL_NB * 4) * 8, false},
+        {(void**)&w->hist_min, (size_t)(S * SEL_NB * 2 + S * 4) * 8, false},
         {(void**)&w->xsend, (size_t)w->xcap * 8, false},
         {(void**)&w->xrecv, (size_t)(w->xcap * world) * 8, false},
         {(void**)&w->T, (size_t)(S * n_rows) * 8, false},
@@ -493,6 +492,13 @@ void hard_replay(Run& R, pcx_mat& m, pcx_workspace* w, pcx_result* res, int64_t 
     }
 }
 
+// the selection histograms of a pass over `active` events: hist_n right after hist_w's active
+// rows, hist_max right after hist_min's, so each pass reduces over ranks in one SUM and one MAX
+void sel_layout(pcx_mat& m, int64_t active) {
+    m.hist_n = m.hist_w + active * SEL_NB * 3;
+    m.hist_max = m.hist_min + active * SEL_NB;
+}
+
 // weighted medians of the scaled events (phase 1: interpolation fills, phase 2: outcomes),
 // plus the replay of rounding-decided binary fills (phase 1)
 void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
@@ -509,17 +515,22 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         // its collectives sized for S.  Counting only for reputation=None interpolation medians.
         R.stage(m, M_SEL_INIT);  // (also the sampled windows, k_sel_sample: every rank's samples summed)
         R.allreduce(w->hist_w, (int64_t)S * SEL_NB * 3, PCX_F64, PCX_SUM);
+        sel_layout(m, S);
+        m.sel_imin = m.hist_min + (int64_t)S * SEL_NB * 2;  // right after hist_max's S rows
+        m.sel_imax = m.sel_imin + (int64_t)S * 2;
+        R.hip(hipMemsetAsync(m.sel_imin, 0, (size_t)S * 4 * 8, R.st), "sel_imin");  // (MAX identity)
         m.sel_first = 1;
         R.mark(M_SEL_HIST);
         R.check_err(sel_hist(m, S, R.st), "k_sel_hist");
         R.mark(-1);
         m.sel_first = 0;
-        if (!(phase == 1 && !m.rep_raw)) R.allreduce(w->hist_w, (int64_t)S * SEL_NB * 3, PCX_U64, PCX_SUM);
-        R.allreduce(w->hist_n, (int64_t)S * SEL_NB, PCX_U64, PCX_SUM);
-        R.allreduce(w->hist_min, (int64_t)S * SEL_NB, PCX_U64, PCX_MIN);
-        R.allreduce(w->hist_max, (int64_t)S * SEL_NB, PCX_U64, PCX_MAX);
-        R.allreduce(w->sel_imin, (int64_t)S * 2, PCX_U64, PCX_MIN);
-        R.allreduce(w->sel_imax, (int64_t)S * 2, PCX_U64, PCX_MAX);
+        // two collectives: the counts (and limbs unless every weight is equal), and the (complemented)
+        // minima with the maxima -- bucket keys, then the weights' bit patterns
+        if (!(phase == 1 && !m.rep_raw))
+            R.allreduce(w->hist_w, (int64_t)S * SEL_NB * 4, PCX_U64, PCX_SUM);
+        else
+            R.allreduce(m.hist_n, (int64_t)S * SEL_NB, PCX_U64, PCX_SUM);
+        R.allreduce(w->hist_min, (int64_t)S * SEL_NB * 2 + (int64_t)S * 4, PCX_U64, PCX_MAX);
         R.stage(m, M_SEL_START);
         R.mark(M_SEL_STEP);
         R.check_err(sel_step(m, S, R.st), "k_sel_step");
@@ -543,14 +554,16 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
                 R.err = "weighted selection did not converge";
                 throw Fail{PCX_EINVAL};
             }
+            sel_layout(m, active);
             R.mark(M_SEL_HIST);
             R.check_err(sel_hist(m, (int)active, R.st), "k_sel_hist");
             R.mark(-1);
             // exact integers: order-independent reductions (limbs only when some event walks weights)
-            if (wactive > 0) R.allreduce(w->hist_w, active * SEL_NB * 3, PCX_U64, PCX_SUM);
-            R.allreduce(w->hist_n, active * SEL_NB, PCX_U64, PCX_SUM);
-            R.allreduce(w->hist_min, active * SEL_NB, PCX_U64, PCX_MIN);
-            R.allreduce(w->hist_max, active * SEL_NB, PCX_U64, PCX_MAX);
+            if (wactive > 0)
+                R.allreduce(w->hist_w, active * SEL_NB * 4, PCX_U64, PCX_SUM);
+            else
+                R.allreduce(m.hist_n, active * SEL_NB, PCX_U64, PCX_SUM);
+            R.allreduce(w->hist_min, active * SEL_NB * 2, PCX_U64, PCX_MAX);
             R.mark(M_SEL_STEP);
             R.check_err(sel_step(m, (int)active, R.st), "k_sel_step");
             R.mark(-1);
@@ -882,12 +895,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.info = w->info;
         m.sel_state = w->sel_state;
         m.sel_isum = w->sel_isum;
-        m.sel_imin = w->sel_imin;
-        m.sel_imax = w->sel_imax;
         m.hist_w = w->hist_w;
-        m.hist_n = w->hist_n;
-        m.hist_min = w->hist_min;
-        m.hist_max = w->hist_max;
+        m.hist_min = w->hist_min;  // (hist_n, hist_max, sel_imin, sel_imax: select())
         m.sel_arg = w->sel_arg;
         m.sel_act = w->sel_act;
         m.hard = w->hard;
