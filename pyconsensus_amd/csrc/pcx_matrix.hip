@@ -2044,6 +2044,43 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
     st_dd(pp + 2, a2.get());
 }
 
+// Subset sums of a 16-row group's weights for the grid positions' passes: byte j of a 2-bit code
+// word (zpack layout) holds rows j, j + 4, j + 8, j + 12, so a lane's four code pairs of that byte
+// select a subset of those four rows; entry 16 j + s of the wave's table is the sum of the subset s
+// (bit k: row j + 4 k) in double-double (a two_sum chain: exact to ~2^-106 of the sum).  Lane l
+// builds entry l.  A position then takes four table reads per byte instead of four per-row
+// additions per quantity.
+// (the lane's four weights come in wq[k] = wg[j + 4 k], j = lane / 16: loaded a group ahead by
+// subset_load, so the table waits for no load)
+struct SubW {
+    double w[4];
+};
+__device__ __forceinline__ SubW subset_load(const double* wg) {
+    const int j = (threadIdx.x & (WAVE - 1)) >> 4;
+    return SubW{{wg[j], wg[j + 4], wg[j + 8], wg[j + 12]}};
+}
+__device__ __forceinline__ void subset_table(const SubW& wq, dd* tab) {
+    const int l = threadIdx.x & (WAVE - 1), sb = l & 15;
+    dd a{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const dd t = two_sum(a.hi, (sb >> k) & 1 ? wq.w[k] : 0.0);
+        a = dd{t.hi, a.lo + t.lo};
+    }
+    tab[l] = a;
+}
+// the 4-bit subset index of code byte bits at 0, 2, 4, 6 (x & 0x55)
+__device__ __forceinline__ uint32_t sub4_even(uint32_t x) {
+    x = (x | (x >> 1)) & 0x33u;
+    return (x | (x >> 2)) & 0x0Fu;
+}
+// ... of missing-word bits j, j + 4, j + 8, j + 12
+__device__ __forceinline__ uint32_t sub4_stride4(uint32_t M, int j) {
+    uint32_t v = (M >> j) & 0x1111u;
+    v = (v | (v >> 3)) & 0x0303u;
+    return (v | (v >> 6)) & 0x0Fu;
+}
+
 // M_GEMV2 from the compact sources (m.compact): thread = one wcd position (general positions
 // read the filled values Fg, grid positions F = 1 + z / 2 from the 2-bit codes), 16-row groups;
 // the same per-row products and compensated sums as k_gemv2, into the same partial slots
@@ -2066,32 +2103,90 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
         S1 = chunk_sum_dd(n1, r0, r1);
         S2 = chunk_sum_dd(n2, r0, r1);
     }
-    if (q >= E || (!GRID && q >= gb)) return;
-    const int c = m.cov_perm[q];
-    if (c < 0) return;  // (padding)
+    // (a grid wave keeps every lane until its subset tables are built: one entry per lane)
+    if (GRID ? (q & ~(WAVE - 1)) >= E : (q >= E || q >= gb)) return;
+    const bool live = q < E;
+    const int c = live ? m.cov_perm[q] : -1;
+    if (!GRID && c < 0) return;  // (padding)
     acc2 a1, a2;
     if constexpr (GRID) {
-        const uint32_t* zb = zb_packed(m) + (q - gb);
-        // whole 16-row groups: the group's (uniform) weights as one batch of scalar loads, the
-        // next group's code word in flight during this group's adds; then the ragged tail
+        __shared__ dd tabs[BT / WAVE][2][WAVE];  // per wave: the subset tables of n1 and n2
+        dd* t1 = tabs[threadIdx.x / WAVE][0];
+        dd* t2 = tabs[threadIdx.x / WAVE][1];
+        const uint32_t* zb = zb_packed(m) + (live ? q - gb : 0);
+        // whole 16-row groups (the next group's code word in flight during this group's adds),
+        // then the ragged tail
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Pn = g0 < gf ? zb[g0 * m.zq] : 0u;
-        for (int64_t g = g0; g < gf; g++) {
-            const uint32_t P = Pn;
-            if (g + 1 < gf) Pn = zb[(g + 1) * m.zq];
-            double w1[16], w2[16];
+        if (__builtin_isfinite(S1.hi) && __builtin_isfinite(S2.hi)) {
+            // subset tables (as k_outcomes_c): sum v z = sum over code bytes j of T1 + 2 T2, the
+            // subset sums of the rows whose code is 1 / 2, compensated (a non-finite weight: the
+            // per-row loop, whose NaN x 0 the result keeps)
+            constexpr int GB = 4;  // four groups' loads at once, one accumulator per code byte (as k_outcomes_c)
+            acc2 a1j[4], a2j[4];
+            for (int64_t g = g0; g < gf; g += GB) {
+                uint32_t Pg[GB];
+                SubW wa[GB], wb[GB];
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                w1[r] = n1[g * 16 + r];
-                w2[r] = n2[g * 16 + r];
+                for (int k = 0; k < GB; k++) {
+                    const int64_t gk = g + k < gf ? g + k : gf - 1;
+                    Pg[k] = zb[gk * m.zq];
+                    wa[k] = subset_load(n1 + gk * 16);
+                    wb[k] = subset_load(n2 + gk * 16);
+                }
+#pragma unroll
+                for (int k = 0; k < GB; k++) {
+                    if (g + k >= gf) break;  // (wave-uniform)
+                    const uint32_t P = Pg[k];
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    subset_table(wa[k], t1);
+                    subset_table(wb[k], t2);
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t by = (P >> (8 * j)) & 0xFFu, lo = by & 0x55u, hi = (by >> 1) & 0x55u;
+                        const int i1 = 16 * j + (int)sub4_even(lo & ~hi), i2 = 16 * j + (int)sub4_even(hi & ~lo);
+                        const dd u1 = t1[i1], u2 = t1[i2], v1 = t2[i1], v2 = t2[i2];
+                        a1j[j].add(u1.hi);
+                        a1j[j].c += u1.lo;
+                        a1j[j].add(2.0 * u2.hi);
+                        a1j[j].c += 2.0 * u2.lo;
+                        a2j[j].add(v1.hi);
+                        a2j[j].c += v1.lo;
+                        a2j[j].add(2.0 * v2.hi);
+                        a2j[j].c += 2.0 * v2.lo;
+                    }
+                }
             }
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const double z = (double)zpack_get(P, r);
-                a1.add(w1[r] * z);
-                a2.add(w2[r] * z);
+            for (int j = 0; j < 4; j++) {
+                const dd x1 = a1j[j].get(), x2 = a2j[j].get();
+                a1.add(x1.hi);
+                a1.c += x1.lo;
+                a2.add(x2.hi);
+                a2.c += x2.lo;
+            }
+        } else {
+            for (int64_t g = g0; g < gf; g++) {
+                const uint32_t P = Pn;
+                if (g + 1 < gf) Pn = zb[(g + 1) * m.zq];
+                double w1[16], w2[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    w1[r] = n1[g * 16 + r];
+                    w2[r] = n2[g * 16 + r];
+                }
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const double z = (double)zpack_get(P, r);
+                    a1.add(w1[r] * z);
+                    a2.add(w2[r] * z);
+                }
             }
         }
+        if (!live) return;
         if (r0 < r1 && gf * 16 < r1) {  // (r0 < r1: r0 is 16-aligned; an empty chunk capped at a ragged n_rows has none)
             const uint32_t P = zb[gf * m.zq];
             for (int64_t i = gf * 16; i < r1; i++) {
@@ -2357,14 +2452,17 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
 }
 
 // M_OUTCOMES from the compact sources (m.compact): as k_gemv2_c, with the missing bits nam
-// the general positions' (GRID false) and the grid positions' bodies; S: the chunk's weight total
+// the general positions' (GRID false) and the grid positions' bodies; S: the chunk's weight total.
+// tab: the calling wave's subset table (GRID); live: the lane holds a position (every lane of a
+// grid wave runs the body: the table takes all 64)
 template <bool GRID>
-__device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S) {
+__device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S, dd* tab,
+                                                bool live) {
     const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
     const int E = (int)m.n_events;
     const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
-    const int c = m.cov_perm[q];
-    if (c < 0) return;
+    const int c = live ? m.cov_perm[q] : -1;
+    if (!GRID && live && c < 0) return;  // (padding: none below gb)
     acc2 raw;
     double pc = 0, b1 = 0, b15 = 0, b2 = 0;
     double n1 = 0, n15 = 0, n2 = 0;
@@ -2379,12 +2477,62 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
         n2 += f == 2.0 ? 1.0 : 0.0;
     };
     const bool general = !GRID;
-    if (general && m.scaled && m.scaled[c]) {
+    const int64_t qn = live ? q : 0;  // (a lane past the positions reads a valid word, unused)
+    const bool scl = general && (!live || (m.scaled && m.scaled[c]));
+    if (general && __all(scl)) {  // (a wave of scaled events only: the subset tables need every lane)
         // a scaled event's raw is its weighted median (:520-523) and its certainty comes from
         // the selection (:540-546): only np.dot(smooth_rep, na_mat) (:559) is read here, from
         // the missing bits alone (no filled values), in the same row order and arithmetic
-        // whole 16-row groups: the weights as one batch of loads ahead of the adds (a load per
-        // row waited on in turn left this pass latency-bound), the next missing word in flight
+        // whole 16-row groups, four at a time (words and weights loaded together): the missing
+        // rows' weight from the wave's subset table (four reads per group, four independent
+        // sums); a group with a non-finite weight adds row by row, so that NaN x 0 reaches pc as
+        // in np.dot.  (Row by row with the weights loaded per group this pass took 2.4 of
+        // k_outcomes_c's 3.3 ms at C5 for a quarter of its positions: latency, not issue.)
+        const int64_t g0 = r0 / 16, gf = r1 / 16;
+        constexpr int GB = 4;
+        double pcj[4] = {0, 0, 0, 0};
+        for (int64_t g = g0; g < gf; g += GB) {
+            uint32_t Mg[GB];
+            SubW wg[GB];
+#pragma unroll
+            for (int k = 0; k < GB; k++) {
+                const int64_t gk = g + k < gf ? g + k : gf - 1;
+                Mg[k] = m.nam[gk * ld + qn];
+                wg[k] = subset_load(sm + gk * 16);
+            }
+#pragma unroll
+            for (int k = 0; k < GB; k++) {
+                if (g + k >= gf) break;  // (wave-uniform)
+                const uint32_t M = Mg[k];
+                const bool fin = __builtin_isfinite(wg[k].w[0]) && __builtin_isfinite(wg[k].w[1]) &&
+                                 __builtin_isfinite(wg[k].w[2]) && __builtin_isfinite(wg[k].w[3]);
+                if (__all(fin)) {  // (wave-uniform)
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    subset_table(wg[k], tab);
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int j = 0; j < 4; j++) pcj[j] += tab[16 * j + sub4_stride4(M, j)].hi;
+                } else {
+                    const int64_t gg = g + k;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) pcj[r & 3] += sm[gg * 16 + r] * (((M >> r) & 1u) ? 1.0 : 0.0);
+                }
+            }
+        }
+        pc = (pcj[0] + pcj[1]) + (pcj[2] + pcj[3]);
+        if (!live) return;
+        if (r0 < r1 && gf * 16 < r1) {  // the ragged tail (r0 < r1: r0 is 16-aligned)
+            const uint32_t M = m.nam[gf * ld + q];
+            for (int64_t i = gf * 16; i < r1; i++) pc += sm[i] * (((M >> (i - gf * 16)) & 1u) ? 1.0 : 0.0);
+        }
+        double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+        st_dd(pp + 2, {pc, 0.0});
+        return;
+    }
+    if (scl) {  // a scaled event in a wave with other kinds of position: row by row
+        if (!live) return;
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Mn = g0 < gf ? m.nam[g0 * ld + q] : 0u;
         for (int64_t g = g0; g < gf; g++) {
@@ -2396,7 +2544,7 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
 #pragma unroll
             for (int r = 0; r < 16; r++) pc += w[r] * (((M >> r) & 1u) ? 1.0 : 0.0);
         }
-        if (r0 < r1 && gf * 16 < r1) {  // the ragged tail (r0 < r1: r0 is 16-aligned)
+        if (r0 < r1 && gf * 16 < r1) {
             const uint32_t M = m.nam[gf * ld + q];
             for (int64_t i = gf * 16; i < r1; i++) pc += sm[i] * (((M >> (i - gf * 16)) & 1u) ? 1.0 : 0.0);
         }
@@ -2410,7 +2558,7 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
         // sum per wave) and w z exact, so one compensated add per element replaces the
         // product's; b1 / b15 / b2 are the same plain row-order sums as the general path's
         // and the counts are popcounts of the code bits (code 1 = value 1.5, 2 = value 2)
-        const uint32_t* zb = zb_packed(m) + (q - gb);
+        const uint32_t* zb = zb_packed(m) + (live ? q - gb : 0);
         acc2 zs;
         uint32_t c15 = 0, c2 = 0;
         auto row = [&](uint32_t z, double w, uint32_t ms) {
@@ -2420,28 +2568,94 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
             b15 += z == 1u ? w : 0.0;
             b2 += z == 2u ? w : 0.0;
         };
-        // whole 16-row groups (weights as one batch of scalar loads, the next group's code and
-        // missing words in flight during this group's adds), then the ragged tail
+        // whole 16-row groups (the next group's code and missing words in flight during this
+        // group's adds), then the ragged tail
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Pn = 0, Mn = 0;
         if (g0 < gf) {
             Pn = zb[g0 * m.zq];
-            Mn = m.nam[g0 * ld + q];
+            Mn = m.nam[g0 * ld + qn];
         }
-        for (int64_t g = g0; g < gf; g++) {
-            const uint32_t P = Pn, M = Mn;
-            if (g + 1 < gf) {
-                Pn = zb[(g + 1) * m.zq];
-                Mn = m.nam[(g + 1) * ld + q];
+        if (__builtin_isfinite(S.hi)) {
+            // subset tables (round 5): per code byte j, the weights of the rows whose code is 0, 1
+            // or 2 and of the missing rows are four table reads; Σ w z = Σ_j (T1 + 2 T2) stays
+            // compensated, b1 / b15 / b2 / pc are plain sums of the subset sums (np.dot / the
+            // certainty sums: any order within rounding).  With a non-finite weight in the chunk
+            // the per-row loop below keeps NaN × 0 propagating into pc as np.dot does.
+            // four groups' words and weights loaded at once (one group ahead left every group
+            // waiting on its loads: the pass is latency-bound, not issue-bound)
+            constexpr int GB = 4;
+            // one accumulator per code byte j: four independent chains (one chain of dependent
+            // compensated adds per quantity held every wave on the fp64 latency: SQ_WAIT_INST_ANY
+            // was half the wave cycles)
+            acc2 zj[4];
+            double b1j[4] = {0, 0, 0, 0}, b15j[4] = {0, 0, 0, 0}, b2j[4] = {0, 0, 0, 0}, pcj[4] = {0, 0, 0, 0};
+            for (int64_t g = g0; g < gf; g += GB) {
+                uint32_t Pg[GB], Mg[GB];
+                SubW wg[GB];
+#pragma unroll
+                for (int k = 0; k < GB; k++) {
+                    const int64_t gk = g + k < gf ? g + k : gf - 1;
+                    Pg[k] = zb[gk * m.zq];
+                    Mg[k] = m.nam[gk * ld + qn];
+                    wg[k] = subset_load(sm + gk * 16);
+                }
+#pragma unroll
+                for (int k = 0; k < GB; k++) {
+                    if (g + k >= gf) break;  // (wave-uniform)
+                    const uint32_t P = Pg[k], M = Mg[k];
+                    __builtin_amdgcn_wave_barrier();  // the previous group's reads are done
+                    asm volatile("" ::: "memory");
+                    subset_table(wg[k], tab);
+                    __builtin_amdgcn_wave_barrier();
+                    asm volatile("" ::: "memory");
+                    c15 += __popc(P & 0x55555555u);
+                    c2 += __popc(P & 0xAAAAAAAAu);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t by = (P >> (8 * j)) & 0xFFu, lo = by & 0x55u, hi = (by >> 1) & 0x55u;
+                        const dd T0 = tab[16 * j + sub4_even(0x55u & ~(lo | hi))];
+                        const dd T1 = tab[16 * j + sub4_even(lo & ~hi)];
+                        const dd T2 = tab[16 * j + sub4_even(hi & ~lo)];
+                        const dd TM = tab[16 * j + sub4_stride4(M, j)];
+                        zj[j].add(T1.hi);
+                        zj[j].c += T1.lo;
+                        zj[j].add(2.0 * T2.hi);
+                        zj[j].c += 2.0 * T2.lo;
+                        b1j[j] += T0.hi;
+                        b15j[j] += T1.hi;
+                        b2j[j] += T2.hi;
+                        pcj[j] += TM.hi;
+                    }
+                }
             }
-            c15 += __popc(P & 0x55555555u);
-            c2 += __popc(P & 0xAAAAAAAAu);
-            double w[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) w[r] = sm[g * 16 + r];
+            for (int j = 0; j < 4; j++) {
+                const dd z = zj[j].get();
+                zs.add(z.hi);
+                zs.c += z.lo;
+            }
+            b1 = (b1j[0] + b1j[1]) + (b1j[2] + b1j[3]);
+            b15 = (b15j[0] + b15j[1]) + (b15j[2] + b15j[3]);
+            b2 = (b2j[0] + b2j[1]) + (b2j[2] + b2j[3]);
+            pc = (pcj[0] + pcj[1]) + (pcj[2] + pcj[3]);
+        } else {
+            for (int64_t g = g0; g < gf; g++) {
+                const uint32_t P = Pn, M = Mn;
+                if (g + 1 < gf) {
+                    Pn = zb[(g + 1) * m.zq];
+                    Mn = m.nam[(g + 1) * ld + qn];
+                }
+                c15 += __popc(P & 0x55555555u);
+                c2 += __popc(P & 0xAAAAAAAAu);
+                double w[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) row(zpack_get(P, r), w[r], (M >> r) & 1u);
+                for (int r = 0; r < 16; r++) w[r] = sm[g * 16 + r];
+#pragma unroll
+                for (int r = 0; r < 16; r++) row(zpack_get(P, r), w[r], (M >> r) & 1u);
+            }
         }
+        if (!live) return;
         if (r0 < r1 && gf * 16 < r1) {  // (r0 < r1: r0 is 16-aligned; an empty chunk capped at a ragged n_rows has none)
             const uint32_t P = zb[gf * m.zq], M = m.nam[gf * ld + q];
             for (int64_t i = gf * 16; i < r1; i++) {
@@ -2505,13 +2719,14 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     row_range(m, r0, r1, 16);
     // the chunk's weight total for the grid positions, by every lane of a wave holding one
     // (before any lane leaves: the sum is a wave reduction)
+    __shared__ dd tabs[BT / WAVE][WAVE];  // the grid waves' subset tables
     dd S{0.0, 0.0};
     if ((q | (WAVE - 1)) >= gb) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
-    if (q >= m.n_events) return;
-    if (q >= gb)
-        outcomes_c_body<true>(m, q, r0, r1, S);
+    if ((q & ~(WAVE - 1)) >= m.n_events) return;  // (wave-uniform: a grid wave runs all its lanes)
+    if (q >= gb)  // (gb is a multiple of 128: a wave is all grid or all general)
+        outcomes_c_body<true>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events);
     else
-        outcomes_c_body<false>(m, q, r0, r1, S);
+        outcomes_c_body<false>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events);
 }
 
 // certainty of an event no reporter matched (:542): NaN on the PCA path (smooth_rep is a
