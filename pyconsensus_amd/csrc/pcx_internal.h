@@ -133,7 +133,8 @@ typedef struct {
        PCX_NDIG - 1; k_syrk then runs nothing */
     int32_t  cov_gg8;
     int32_t  ks_gx;               /* k-slices of that product (int32-exact: |d e| <= 127^2 per row)   */
-    int8_t*  zE;                  /* [wcd_rows/16][zd_ld][16] digit s of w at s * 128 cov_jb + q       */
+    int8_t*  zE;                  /* [wcd_rows/16][zd_ld][16] digit s of w at s * 128 cov_jb + q (== zD
+                                     when every token is 1: tok w = w, the same digits and scale)    */
     double*  escale;              /* [wcd_ld] 2^-f per general position                               */
     int32_t* Pgx;                 /* gemm_i8x_slab(ks, i, j, lower tile) x [256][256] int32            */
     /* algorithms other than PCA (enum pcx_algorithm) */
@@ -275,7 +276,7 @@ hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner
 enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
                      INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7, INFO_COV_GENERAL = 8,
-                     INFO_COV_MIXED = 9 };
+                     INFO_COV_MIXED = 9, INFO_COV_TOK1 = 10 };
 hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st);
 
 // pack / unpack of strided dd slot ranges for the slot exchange (runner)

@@ -56,7 +56,7 @@ enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ,
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
-                 IN_COV_GENERAL, IN_COV_MIXED };
+                 IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1 };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -914,7 +914,14 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
         }
     }
     bad = __syncthreads_or(bad);
-    if (tid == 0) m.info[IN_COV_MIXED] = (!big && gb > 0 && gb < E && !bad) ? 1 : 0;
+    if (tid == 0) {
+        m.info[IN_COV_MIXED] = (!big && gb > 0 && gb < E && !bad) ? 1 : 0;
+        // every token of this rank is 1 (and none anywhere above it): tok w = w and both digit
+        // strings coincide, so the general x general product takes zD for both operands
+        // (reputation=None: int(1/N 1e6) = 1 for N <= 1e6)
+        const double tsum = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
+        m.info[IN_COV_TOK1] = (maxtok == 1.0 && tsum == (double)m.n_rows) ? 1 : 0;
+    }
 }
 
 // PCX_M_WCD: wcd = F - mu (:317-322) materialised once, [wcd_rows][wcd_ld] in the
@@ -1248,9 +1255,10 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const bool live = q < gb;
     const int qq = live ? q : 0;
     const double sc = m.dscale[qq];
-    const bool gg = m.cov_gg8 != 0;
+    const bool fg = m.cov_gg8 != 0;            // no wcd written: w = Fg - mu (k_wcd's own op)
+    const bool gg = fg && m.zE != m.zD;       // the digits of w too (the same ones when every token is 1)
     const double esc = gg ? m.escale[qq] : 1.0;
-    const double mu = gg ? m.ev[EV_MU * m.n_events + m.cov_perm[qq]] : 0.0;  // w = Fg - mu (k_wcd's own op)
+    const double mu = fg ? m.ev[EV_MU * m.n_events + m.cov_perm[qq]] : 0.0;
     const int64_t ng = m.wcd_rows / 16;
     const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
     const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
@@ -1266,7 +1274,7 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int64_t i = grp * 16 + 4 * h + u;
-            wr[u] = gg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q];
+            wr[u] = fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q];
             tk[u] = m.tokp[i];  // 0 past n_rows
         }
 #pragma unroll
@@ -1300,6 +1308,56 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
         t += __shfl_xor(t, 2, WAVE);
         if (live && h == 0 && t) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)t);
     }
+}
+
+// The tok w digits alone (no zE to write: no general x general product on int8, or every token 1):
+// one lane per position holding a whole 16-row group (16-byte stores; 2.66 ms at C5 against 3.8
+// ms for the four-lane layout above, whose point is the register room for both strings).
+__global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
+    const int gb = m.cov_jb * CT;
+    const int q = blockIdx.x * BT + threadIdx.x;
+    if (q >= gb) return;
+    const double sc = m.dscale[q];
+    const bool fg = m.cov_gg8 != 0;  // no wcd written: w = Fg - mu (k_wcd's own op)
+    const double mu = fg ? m.ev[EV_MU * m.n_events + m.cov_perm[q]] : 0.0;
+    const int64_t ng = m.wcd_rows / 16;
+    const int64_t per = (ng + gridDim.y - 1) / gridDim.y;
+    const int64_t g0 = blockIdx.y * per, g1 = g0 + per < ng ? g0 + per : ng;
+    const int64_t ldd = zd_ld(gb);
+    int32_t dsum[PCX_NDIG];  // |d| <= 127: int32-exact for any chunk under 16M rows
+#pragma unroll
+    for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
+    for (int64_t grp = g0; grp < g1; grp++) {
+        uint32_t d[PCX_NDIG][4];
+#pragma unroll
+        for (int k = 0; k < PCX_NDIG; k++) d[k][0] = d[k][1] = d[k][2] = d[k][3] = 0;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int64_t i = grp * 16 + r;
+            const double w = (fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q]) * sc;  // exact (power of two)
+            const double tk = m.tokp[i];                                                    // 0 past n_rows
+            double hi = w * tk, lo = fma(w, tk, -hi);  // tok w exactly
+            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv);
+            double X = rint(pv + fma(lo, DIG_SCALE, pe));
+#pragma unroll
+            for (int k = PCX_NDIG - 1; k >= 0; k--) {  // (k_digits: the same digits)
+                double di = X;
+                if (k > 0) {
+                    const double qd = rint(X * (1.0 / PCX_DBASE));
+                    di = fma(-qd, PCX_DBASE, X);
+                    X = qd;
+                }
+                d[k][r >> 2] |= (uint32_t)(uint8_t)(int8_t)(int)di << (8 * (r & 3));
+                dsum[k] += (int)di;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PCX_NDIG; k++)
+            *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
+    }
+#pragma unroll
+    for (int k = 0; k < PCX_NDIG; k++)
+        if (dsum[k]) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)dsum[k]);
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -5166,7 +5224,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
                 const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
                 if (hipMemsetAsync(m.dtok, 0, (size_t)PCX_NDIG * gb * 8, st) != hipSuccess) return hipGetLastError();
-                hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
+                if (m.cov_gg8 && m.zE != m.zD)  // both digit strings
+                    hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
+                else
+                    hipLaunchKernelGGL(k_digits1, dim3((unsigned)((gb + BT - 1) / BT), (unsigned)ng), dim3(BT), 0, st, m);
                 GemmI8 g{m.zD, zd_ld(gb), m.zB, m.zq, m.Pmx, (int64_t)PCX_NDIG * gb, m.zq * PCX_NDIG * gb, PCX_NDIG * gb, np,
                          0, 0, 0, m.ks_mx, rg, 1};
                 g.tp = (PCX_NDIG * gb + GT - 1) / GT;

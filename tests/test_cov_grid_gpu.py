@@ -53,6 +53,8 @@ CASES = {
     # 256 and 512 general positions (1 and 2 whole 256-position tiles)
     "gg_int8_one_tile": (40000, 700, 0.33, None, (), True),
     "gg_int8_int_rep": (40000, 900, 0.5, "int", (), True),
+    # every token int(1/N 1e6) = 1: the general pairs take the tok w digits for both operands
+    "gg_int8_tokens_one": (600000, 300, 0.5, None, (), True),
 }
 
 
