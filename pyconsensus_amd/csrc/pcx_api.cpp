@@ -294,7 +294,6 @@ int pcx_consensus_batched_f64(pcx_ctx* ctx, const pcx_batch* in, pcx_batch_resul
             const size_t need = per * (size_t)chunk;
             if (ctx->mscr_bytes < need) {
                 if (ctx->mscr) (void)hipFree(ctx->mscr);
-    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
                 ctx->mscr = nullptr;
                 ctx->mscr_bytes = 0;
                 e = hipMalloc(&ctx->mscr, need);
