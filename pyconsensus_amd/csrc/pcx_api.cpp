@@ -189,6 +189,9 @@ void pcx_destroy(pcx_ctx* ctx) {
     pcx::rounds_free(ctx);
     if (ctx->mscr) (void)hipFree(ctx->mscr);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->sel_pin) (void)hipHostFree(ctx->sel_pin);
+    for (hipEvent_t ev : ctx->sel_ev)
+        if (ev) (void)hipEventDestroy(ev);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
     delete ctx->comm;

@@ -339,6 +339,9 @@ struct pcx_ctx {
     // pinned staging slots of the host-memory path's large output copies (pcx_runner.cpp)
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // the selection passes' info words, read one pass late (pinned, two slots; pcx_runner.cpp select)
+    int64_t* sel_pin = nullptr;
+    hipEvent_t sel_ev[2] = {nullptr, nullptr};
 };
 
 namespace pcx {

@@ -548,32 +548,62 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
             R.allreduce(w->sel_arg + S, S, PCX_U64, PCX_MAX);
             R.stage(m, M_SEL_VALUE_FINISH);
         }
+        // Later passes, with no host round trip between them: pass p + 1 is launched before the
+        // host has read pass p's active count, sized by the last count it knows (an upper bound:
+        // events only leave; the extra workgroups see info[IN_SEL_ACTIVE] and exit, the extra
+        // collective rows are reduced and ignored, and all ranks size them alike), while pass p's
+        // five info words travel to pinned memory behind it.  When a count comes back 0 the pass
+        // already launched after it finds nothing to do (one empty pass per phase: three short
+        // launches against one host round trip per pass).
         int passes = 1;
-        while (active > 0) {
-            if (passes == MAX_SEL_PASSES) {
-                R.err = "weighted selection did not converge";
-                throw Fail{PCX_EINVAL};
+        if (active > 0) {
+            pcx_ctx* c = R.c;
+            if (!c->sel_pin) {
+                R.hip(hipHostMalloc((void**)&c->sel_pin, 16 * sizeof(int64_t), hipHostMallocDefault), "hipHostMalloc(sel)");
+                for (hipEvent_t& ev : c->sel_ev) R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
             }
-            sel_layout(m, active);
-            R.mark(M_SEL_HIST);
-            R.check_err(sel_hist(m, (int)active, R.st), "k_sel_hist");
-            R.mark(-1);
-            // exact integers: order-independent reductions (limbs only when some event walks weights)
-            if (wactive > 0)
-                R.allreduce(w->hist_w, active * SEL_NB * 4, PCX_U64, PCX_SUM);
-            else
-                R.allreduce(m.hist_n, active * SEL_NB, PCX_U64, PCX_SUM);
-            R.allreduce(w->hist_min, active * SEL_NB * 2, PCX_U64, PCX_MAX);
-            R.mark(M_SEL_STEP);
-            R.check_err(sel_step(m, (int)active, R.st), "k_sel_step");
-            R.mark(-1);
-            R.stage(m, M_SEL_COMPACT);
-            R.hip(hipMemcpyAsync(inf5, m.info + INFO_SEL_ACTIVE, sizeof(inf5), hipMemcpyDeviceToHost, R.st), "D2H");
-            R.sync();
-            active = inf5[0];
-            wactive = inf5[4];
-            known_H = inf5[3];
-            passes++;
+            auto launch_pass = [&](int64_t a_ub, int64_t w_ub, int slot) {
+                if (passes == MAX_SEL_PASSES + 1) {  // (+1: the speculative pass after the last)
+                    R.err = "weighted selection did not converge";
+                    throw Fail{PCX_EINVAL};
+                }
+                sel_layout(m, a_ub);
+                R.mark(M_SEL_HIST);
+                R.check_err(sel_hist(m, (int)a_ub, R.st), "k_sel_hist");
+                R.mark(-1);
+                // exact integers: order-independent reductions (limbs only when some event walks weights)
+                if (w_ub > 0)
+                    R.allreduce(w->hist_w, a_ub * SEL_NB * 4, PCX_U64, PCX_SUM);
+                else
+                    R.allreduce(m.hist_n, a_ub * SEL_NB, PCX_U64, PCX_SUM);
+                R.allreduce(w->hist_min, a_ub * SEL_NB * 2, PCX_U64, PCX_MAX);
+                R.mark(M_SEL_STEP);
+                R.check_err(sel_step(m, (int)a_ub, R.st), "k_sel_step");
+                R.mark(-1);
+                R.stage(m, M_SEL_COMPACT);
+                R.hip(hipMemcpyAsync(c->sel_pin + 8 * slot, m.info + INFO_SEL_ACTIVE, 5 * sizeof(int64_t),
+                                     hipMemcpyDeviceToHost, R.st),
+                      "D2H");
+                R.hip(hipEventRecord(c->sel_ev[slot], R.st), "event record");
+                passes++;
+            };
+            int slot = 0;
+            launch_pass(active, wactive, slot);
+            while (true) {
+                launch_pass(active, wactive, slot ^ 1);  // (speculative: pass `slot`'s count unknown yet)
+                c->progress_wait.store(1, std::memory_order_relaxed);
+                R.hip(hipEventSynchronize(c->sel_ev[slot]), "hipEventSynchronize");
+                c->progress_wait.store(0, std::memory_order_relaxed);
+                const int64_t* r = c->sel_pin + 8 * slot;
+                known_H = r[3];
+                if (r[0] == 0) {
+                    passes--;  // (the pass launched after it had nothing to do)
+                    break;
+                }
+                active = r[0];
+                wactive = r[4];
+                slot ^= 1;
+            }
         }
         res->sel_passes += passes;
     }
