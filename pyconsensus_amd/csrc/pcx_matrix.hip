@@ -46,7 +46,7 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
-constexpr int SEL_HC = 2;  // copies of each k_sel_hist bucket (4: slower, 12.3 vs 9.0 ms at C5)
+constexpr int SEL_HC = 2;  // copies of each k_sel_hist bucket (4: 12.3 vs 9.0 ms at C5; 1: 9.37 vs 8.66 ms, round 5)
 constexpr int SELS = 40;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
 constexpr int CM = 8;            // doubles per column in mpart / cmax
@@ -3252,7 +3252,9 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
 // sums / minima / maxima, so the compacted order does not matter).
 // NT threads per event: 256, or 1,024 when the active events leave CUs idle (C4: 250 events on 256
 // CUs -- one 256-thread workgroup per CU kept four waves streaming each column)
-template <int NT>
+// CM: phase 1 under reputation=None, where every pass counts (every weight is 1 / N): no weight
+// loads, limbs or weight extremes, half the LDS
+template <int NT, bool CM>
 __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
@@ -3262,12 +3264,13 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     // copy threadIdx.x % SEL_HC: lanes of a wave whose keys share a bucket split over the copies
     // (same-address LDS atomics serialise); the copies merge exactly (integer sums, min, max)
     constexpr int HC = SEL_HC;
-    __shared__ unsigned long long ha[NB * HC], hb[NB * HC], hc[NB * HC], hmin[NB * HC], hmax[NB * HC];
+    constexpr int HW = CM ? 1 : NB * HC;
+    __shared__ unsigned long long ha[HW], hb[HW], hc[HW], hmin[NB * HC], hmax[NB * HC];
     typedef unsigned long long hn_t;  // (32-bit LDS counts measured: no faster)
     __shared__ hn_t hn[NB * HC];
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
     for (int b = threadIdx.x; b < NB * HC; b += NT) {
-        ha[b] = hb[b] = hc[b] = 0;
+        if constexpr (!CM) ha[b] = hb[b] = hc[b] = 0;
         hn[b] = 0;
         hmin[b] = ~0ull;
         hmax[b] = 0;
@@ -3282,7 +3285,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     // first pass (sel_first): the weight extremes of every element, and in phase 2 the filled
     // rows (all at the fill value) summed apart and binned once at the end
     const bool first = m.sel_first != 0;
-    const bool gfirst = first && m.sel_phase == 2;
+    const bool gfirst = !CM && first && m.sel_phase == 2;
     uint64_t wlo = ~0ull, whi = 0, ga = 0, gb = 0, gc = 0, gn = 0;
     __shared__ int win_s[2];
     if (first && threadIdx.x == 0) {  // the sampled window (k_sel_sample, all ranks)
@@ -3331,10 +3334,10 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     const bool wgather = first && wb0 <= wb1;
     const uint64_t lo = st[SW_LO], hi = st[SW_HI];
     const int sh = (int)st[SW_SHIFT];
-    const bool wmode = st[SW_MODE] == 0;
+    const bool wmode = !CM && st[SW_MODE] == 0;
     const bool from_buf = st[SW_CMODE] == 1;
     // phase 2: the filled rows all sit at the fill value -- binned once, not per element
-    const bool gties = m.sel_phase == 2 && st[SW_GN] > 0;
+    const bool gties = !CM && m.sel_phase == 2 && st[SW_GN] > 0;
     const uint64_t gk = gties ? dkey(m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]]) : 0;
     const bool gin = gties && gk >= lo && gk <= hi;
     const uint64_t ties_all = gin ? (uint64_t)m.ev[EV_MISS * m.n_events + m.scaled_cols[s]] : 0;  // all ranks
@@ -3348,11 +3351,13 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     const int hcp = HC > 1 ? (int)(threadIdx.x % HC) : 0;
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh) * HC + hcp;
-        if (wmode) {
-            const limbs3 L = to_limbs(w);
-            atomicAdd(&ha[b], (unsigned long long)L.l0);
-            atomicAdd(&hb[b], (unsigned long long)L.l1);
-            atomicAdd(&hc[b], (unsigned long long)L.l2);
+        if constexpr (!CM) {
+            if (wmode) {
+                const limbs3 L = to_limbs(w);
+                atomicAdd(&ha[b], (unsigned long long)L.l0);
+                atomicAdd(&hb[b], (unsigned long long)L.l1);
+                atomicAdd(&hc[b], (unsigned long long)L.l2);
+            }
         }
         atomicAdd(&hn[b], (hn_t)1);
         // (measured: reading the extremes first and skipping the atomics that cannot change them
@@ -3371,12 +3376,21 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
             bin(k, __longlong_as_double(cb[2 * j + 1]));
         }
     } else {
-        rows_strided<ROW_UNROLL>(threadIdx.x, NT, m.n_rows, [&](int64_t i) { return sel_load(m, s, i); },
+        const double* const tcol = m.T + (int64_t)s * m.n_rows;
+        const double wc = 1.0 / (double)m.n_total;  // (CM: sel_load's weight)
+        rows_strided<ROW_UNROLL>(threadIdx.x, NT, m.n_rows, [&](int64_t i) {
+                                     if constexpr (CM) return XW{tcol[i], wc};
+                                     else return sel_load(m, s, i);
+                                 },
                                  [&](int64_t, XW v) {
             double x, w;
             if (gties && __builtin_isnan(v.x)) return;  // a filled row
-            if (!sel_decode(m, s, v, x, w)) return;
-            if (first) {
+            if constexpr (CM) {
+                if (__builtin_isnan(v.x)) return;
+                x = v.x;
+                w = v.w;
+            } else if (!sel_decode(m, s, v, x, w)) return;
+            if (!CM && first) {
                 const uint64_t wb = (uint64_t)__double_as_longlong(w);  // weights >= 0 order like their bits
                 wlo = wb < wlo ? wb : wlo;
                 whi = wb > whi ? wb : whi;
@@ -3415,6 +3429,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
         });
     }
     if (first) {
+        if (CM) wlo = whi = (uint64_t)__double_as_longlong(1.0 / (double)m.n_total);
         atomicMin(&f_wlo, (unsigned long long)wlo);
         atomicMax(&f_whi, (unsigned long long)whi);
         if (gn) {
@@ -3427,17 +3442,19 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
         if (threadIdx.x == 0) {
             m.sel_imin[s * 2 + 1] = ~f_wlo;  // all ranks: (complemented) MAX before k_sel_start
             m.sel_imax[s * 2 + 1] = f_whi;
-            if (f_gn) {  // this rank's filled rows, all at the fill value (inside [lo, hi])
+            if (!CM && f_gn) {  // this rank's filled rows, all at the fill value (inside [lo, hi])
                 st[SW_GN] = f_gn;
                 st[SW_GW0] = f_ga;
                 st[SW_GW1] = f_gb;
                 st[SW_GW2] = f_gc;
                 const uint64_t fk = dkey(m.ev[EV_GUESS * m.n_events + m.scaled_cols[s]]);
                 const int b = (int)((fk - lo) >> sh) * HC;
-                if (wmode) {
-                    atomicAdd(&ha[b], f_ga);
-                    atomicAdd(&hb[b], f_gb);
-                    atomicAdd(&hc[b], f_gc);
+                if constexpr (!CM) {
+                    if (wmode) {
+                        atomicAdd(&ha[b], f_ga);
+                        atomicAdd(&hb[b], f_gb);
+                        atomicAdd(&hc[b], f_gc);
+                    }
                 }
                 atomicAdd(&hn[b], (hn_t)f_gn);
                 atomicMin(&hmin[b], (unsigned long long)fk);
@@ -3447,10 +3464,12 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     }
     if (gin && threadIdx.x == 0) {
         const int b = (int)((gk - lo) >> sh) * HC;
-        if (wmode) {
-            atomicAdd(&ha[b], (unsigned long long)st[SW_GW0]);
-            atomicAdd(&hb[b], (unsigned long long)st[SW_GW1]);
-            atomicAdd(&hc[b], (unsigned long long)st[SW_GW2]);
+        if constexpr (!CM) {
+            if (wmode) {
+                atomicAdd(&ha[b], (unsigned long long)st[SW_GW0]);
+                atomicAdd(&hb[b], (unsigned long long)st[SW_GW1]);
+                atomicAdd(&hc[b], (unsigned long long)st[SW_GW2]);
+            }
         }
         atomicAdd(&hn[b], (hn_t)st[SW_GN]);
         atomicMin(&hmin[b], (unsigned long long)gk);
@@ -3472,9 +3491,11 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
         uint64_t sn = 0;
 #pragma unroll
         for (int c = 0; c < HC; c++) {
-            sa += ha[b * HC + c];
-            sb += hb[b * HC + c];
-            sc += hc[b * HC + c];
+            if constexpr (!CM) {
+                sa += ha[b * HC + c];
+                sb += hb[b * HC + c];
+                sc += hc[b * HC + c];
+            }
             sn += (uint64_t)hn[b * HC + c];
             mn = hmin[b * HC + c] < mn ? hmin[b * HC + c] : mn;
             mx = hmax[b * HC + c] > mx ? hmax[b * HC + c] : mx;
@@ -5534,10 +5555,19 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st) {
             ncu = n;
         if (ncu <= 0) ncu = 256;
     }
-    if (n_active <= ncu)
-        hipLaunchKernelGGL(k_sel_hist<1024>, dim3(n_active), dim3(1024), 0, st, m);
-    else
-        hipLaunchKernelGGL(k_sel_hist<BT>, dim3(n_active), dim3(BT), 0, st, m);
+    const bool cm = m.sel_phase == 1 && !m.rep_raw;  // (every pass of this phase counts)
+    if (n_active <= ncu) {
+        if (cm)
+            hipLaunchKernelGGL((k_sel_hist<1024, true>), dim3(n_active), dim3(1024), 0, st, m);
+        else
+            hipLaunchKernelGGL((k_sel_hist<1024, false>), dim3(n_active), dim3(1024), 0, st, m);
+    } else if (cm) {  // (49 VGPRs: eight waves per SIMD, so 512 threads an event at four events a CU)
+        hipLaunchKernelGGL((k_sel_hist<512, true>), dim3(n_active), dim3(512), 0, st, m);
+    } else {
+        // (weight mode: 107 VGPRs, four waves per SIMD; with 75 VGPRs and 384 threads an event the
+        // weight passes ran 5.1 vs 4.5 ms at C5 -- more waves contend for the LDS atomics)
+        hipLaunchKernelGGL((k_sel_hist<BT, false>), dim3(n_active), dim3(BT), 0, st, m);
+    }
     return hipGetLastError();
 }
 
