@@ -134,7 +134,7 @@ typedef struct {
     int32_t  cov_gg8;
     int32_t  ks_gx;               /* k-slices of that product (int32-exact: |d e| <= 127^2 per row)   */
     int8_t*  zE;                  /* [wcd_rows/16][zd_ld][16] digit s of w at s * 128 cov_jb + q (== zD
-                                     when every token is 1: tok w = w, the same digits and scale)    */
+                                     when every token is 2^k: tok w 2^-e = w 2^-f, the same digits)    */
     double*  escale;              /* [wcd_ld] 2^-f per general position                               */
     int32_t* Pgx;                 /* gemm_i8x_slab(ks, i, j, lower tile) x [256][256] int32            */
     /* algorithms other than PCA (enum pcx_algorithm) */

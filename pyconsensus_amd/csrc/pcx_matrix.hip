@@ -56,7 +56,7 @@ enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ,
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
-                 IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1 };
+                 IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1, IN_SEL_WLIMB };
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -916,11 +916,13 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
     bad = __syncthreads_or(bad);
     if (tid == 0) {
         m.info[IN_COV_MIXED] = (!big && gb > 0 && gb < E && !bad) ? 1 : 0;
-        // every token of this rank is 1 (and none anywhere above it): tok w = w and both digit
-        // strings coincide, so the general x general product takes zD for both operands
-        // (reputation=None: int(1/N 1e6) = 1 for N <= 1e6)
+        // every token of this rank is maxtok = 2^k (the largest anywhere): tok w 2^-e = w 2^-f
+        // exactly (dscale = 2^-k escale above) and both digit strings coincide, so the general x
+        // general product takes zD for both operands (reputation=None: int(1/N 1e6) = 1 for
+        // N <= 1e6; 8 for a 125k-row consensus)
         const double tsum = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
-        m.info[IN_COV_TOK1] = (maxtok == 1.0 && tsum == (double)m.n_rows) ? 1 : 0;
+        const bool pow2 = maxtok >= 1.0 && maxtok < 0x1p52 && maxtok == ldexp(1.0, ilogb(maxtok));
+        m.info[IN_COV_TOK1] = (pow2 && tsum == maxtok * (double)m.n_rows) ? 1 : 0;
     }
 }
 
@@ -2924,6 +2926,7 @@ __device__ __forceinline__ void sel_done(uint64_t* st, double r) {
 __global__ void __launch_bounds__(BT) k_sel_setup(pcx_mat m) {
     const int s = blockIdx.x * BT + threadIdx.x;
     if (s >= m.n_scaled) return;
+    if (s == 0) m.info[IN_SEL_WLIMB] = 0;  // (k_sel_wlimbs ORs this phase's limb use in)
     uint64_t* st = m.sel_state + (int64_t)s * SELS;
     const int c = m.scaled_cols[s];
     const bool need = m.sel_phase == 1 ? m.ev[EV_MISS * m.n_events + c] > 0 : true;
@@ -3197,6 +3200,32 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
     }
 }
 
+// which of the three weight limbs any of this rank's rows uses in this phase (bit 0: L0, bit 2:
+// L2; bit 3: computed) -> info[IN_SEL_WLIMB].  k_sel_hist skips the LDS sums of a limb that is zero
+// for every row (C5's phase-2 weights, ~1e-6, leave L2 empty): a local saving, the histograms
+// and their exchange are unchanged.
+__global__ void __launch_bounds__(BT) k_sel_wlimbs(pcx_mat m) {
+    const double* w = m.sel_phase == 1 ? m.rep : m.rowv + RV_SMOOTH * m.n_rows;
+    uint64_t any0 = 0, any2 = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const limbs3 L = to_limbs(w[i]);
+        any0 |= L.l0;
+        any2 |= L.l2;
+    }
+    __shared__ unsigned long long bits;
+    if (threadIdx.x == 0) bits = 8;
+    __syncthreads();
+    const bool b0 = __ballot(any0 != 0) != 0, b2 = __ballot(any2 != 0) != 0;
+    if (threadIdx.x % WAVE == 0 && (b0 || b2)) atomicOr(&bits, (b0 ? 1ull : 0ull) | (b2 ? 4ull : 0ull));
+    __syncthreads();
+    // one global atomic per block, and only when it adds a bit (thousands of ORs into one word
+    // serialise at its L2 channel: 50 us)
+    if (threadIdx.x == 0) {
+        unsigned long long* f = (unsigned long long*)&m.info[IN_SEL_WLIMB];
+        if ((__atomic_load_n(f, __ATOMIC_RELAXED) & bits) != bits) atomicOr(f, bits);
+    }
+}
+
 // The first pass's window: a sample of the column (1 / SEL_SAMPLE of its rows, all ranks'
 // samples summed) histogrammed in the first pass's buckets; the bucket where the sample's
 // weight crosses half, +- SEL_WIN buckets, is the window the first pass also gathers into cbuf.
@@ -3349,14 +3378,16 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
                         8 * need <= st[SW_COUNT];
     uint64_t* cb = m.cbuf ? m.cbuf + (int64_t)s * m.ccap * 2 : nullptr;
     const int hcp = HC > 1 ? (int)(threadIdx.x % HC) : 0;
+    const int64_t wl = CM ? 0 : m.info[IN_SEL_WLIMB];  // (k_sel_wlimbs: a limb no row uses is not summed)
+    const bool use0 = !(wl & 8) || (wl & 1), use2 = !(wl & 8) || (wl & 4);
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh) * HC + hcp;
         if constexpr (!CM) {
             if (wmode) {
                 const limbs3 L = to_limbs(w);
-                atomicAdd(&ha[b], (unsigned long long)L.l0);
+                if (use0) atomicAdd(&ha[b], (unsigned long long)L.l0);
                 atomicAdd(&hb[b], (unsigned long long)L.l1);
-                atomicAdd(&hc[b], (unsigned long long)L.l2);
+                if (use2) atomicAdd(&hc[b], (unsigned long long)L.l2);
             }
         }
         atomicAdd(&hn[b], (hn_t)1);
@@ -5243,7 +5274,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             if (m.cov_mixed) {
                 // general digits x grid: digits of tok w (A, PCX_NDIG per general position) times z (B);
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
-                const int ng = (int)std::min<int64_t>(4096, (rg + 63) / 64);
+                // (16 row groups a block at least: 64 left a 125k-row shard's k_digits1 with 492 blocks)
+                const int ng = (int)std::min<int64_t>(4096, (rg + 15) / 16);
                 if (hipMemsetAsync(m.dtok, 0, (size_t)PCX_NDIG * gb * 8, st) != hipSuccess) return hipGetLastError();
                 if (m.cov_gg8 && m.zE != m.zD)  // both digit strings
                     hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
@@ -5404,6 +5436,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_SEL_INIT:  // status, key range and the active list of the first histogram pass
             if (m.n_scaled == 0) break;
             hipLaunchKernelGGL(k_sel_setup, dim3(sg), dim3(BT), 0, st, m);
+            if (m.sel_phase == 2 || m.rep_raw) {
+                const int64_t wb = (m.n_rows + BT - 1) / BT;
+                hipLaunchKernelGGL(k_sel_wlimbs, dim3(wb < 512 ? (wb > 0 ? wb : 1) : 512), dim3(BT), 0, st, m);
+            }
             hipLaunchKernelGGL(k_sel_range, dim3(sg), dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_sel_compact, dim3(1), dim3(1024), 0, st, m);
             hipLaunchKernelGGL(k_sel_sample, dim3(m.n_scaled), dim3(BT), 0, st, m);

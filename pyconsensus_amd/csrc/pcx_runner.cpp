@@ -982,7 +982,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.dscale = w->dscale;
                 m.escale = w->dscale + w->wcd_ld;
                 R.stage(m, M_COV_PLAN);
-                int64_t plan[3];  // general events, mixed pairs on int8, every token 1
+                int64_t plan[3];  // general events, mixed pairs on int8, every token the same power of two
                 R.hip(hipMemcpyAsync(plan, m.info + INFO_COV_GENERAL, sizeof(plan), hipMemcpyDeviceToHost, R.st),
                       "D2H plan");
                 R.sync();
@@ -1054,7 +1054,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     // |d e| <= 127^2 per row: int32-exact k-slices of <= 133,143 rows
                     m.ks_gx = ks_for(npair * nt * (nt + 1) / 2, 133120,
                                      4.0 * (double)(npair * nt * (nt + 1) / 2) * 256.0 * 256.0);
-                    // every token 1 (reputation=None): the digits of w are those of tok w (zD)
+                    // every token 2^k (reputation=None: 1 up to 1e6 rows): the digits of w are those of tok w (zD)
                     const bool same = plan[2] != 0;
                     m.cov_gg8 = (same || w->grow(w->ze, (size_t)(w->wcd_rows * zd_ld(gb)))) &&
                                         w->grow(w->pgx, (size_t)(gemm_i8x_slab(m.ks_gx, 0, 0, 0, (int)nt) * 256 * 256 * 4))

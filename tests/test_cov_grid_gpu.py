@@ -55,6 +55,8 @@ CASES = {
     "gg_int8_int_rep": (40000, 900, 0.5, "int", (), True),
     # every token int(1/N 1e6) = 1: the general pairs take the tok w digits for both operands
     "gg_int8_tokens_one": (600000, 300, 0.5, None, (), True),
+    # every token int(1/N 1e6) = 16, a power of two: tok w 2^-e = w 2^-f, the same shortcut
+    "gg_int8_tokens_pow2": (62500, 700, 0.33, None, (), True),
 }
 
 
