@@ -3203,7 +3203,8 @@ __global__ void __launch_bounds__(1024) k_sel_compact(pcx_mat m) {
 // which of the three weight limbs any of this rank's rows uses in this phase (bit 0: L0, bit 2:
 // L2; bit 3: computed) -> info[IN_SEL_WLIMB].  k_sel_hist skips the LDS sums of a limb that is zero
 // for every row (C5's phase-2 weights, ~1e-6, leave L2 empty): a local saving, the histograms
-// and their exchange are unchanged.
+// and their exchange are unchanged.  (Measured, not kept: the counts carried in L0's sums from
+// bit 40 up when both fit, one atomic per element fewer -- 4.16 vs 4.14 ms at C5.)
 __global__ void __launch_bounds__(BT) k_sel_wlimbs(pcx_mat m) {
     const double* w = m.sel_phase == 1 ? m.rep : m.rowv + RV_SMOOTH * m.n_rows;
     uint64_t any0 = 0, any2 = 0;
@@ -3292,7 +3293,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     // SEL_HC copies of every bucket, bucket b's copy c at b SEL_HC + c and a thread binning into
     // copy threadIdx.x % SEL_HC: lanes of a wave whose keys share a bucket split over the copies
     // (same-address LDS atomics serialise); the copies merge exactly (integer sums, min, max)
-    constexpr int HC = SEL_HC;
+    constexpr int HC = CM ? 4 : SEL_HC;  // (count mode, half the arrays: four copies, 2.38 -> 2.26 ms at C5)
     constexpr int HW = CM ? 1 : NB * HC;
     __shared__ unsigned long long ha[HW], hb[HW], hc[HW], hmin[NB * HC], hmax[NB * HC];
     typedef unsigned long long hn_t;  // (32-bit LDS counts measured: no faster)
