@@ -3283,9 +3283,11 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
 // NT threads per event: 256, or 1,024 when the active events leave CUs idle (C4: 250 events on 256
 // CUs -- one 256-thread workgroup per CU kept four waves streaming each column)
 // CM: phase 1 under reputation=None, where every pass counts (every weight is 1 / N): no weight
-// loads, limbs or weight extremes, half the LDS
+// loads, limbs or weight extremes, 32-bit counts (n_rows < 2^32, sel_hist), a 16-row load batch
+// held to 64 VGPRs (eight waves per SIMD: 2.30 -> 2.03 ms at C5 against 8-row batches; 65 VGPRs
+// unforced cost a wave per SIMD)
 template <int NT, bool CM>
-__global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 : 1))) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
@@ -3296,7 +3298,8 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     constexpr int HC = CM ? 4 : SEL_HC;  // (count mode, half the arrays: four copies, 2.38 -> 2.26 ms at C5)
     constexpr int HW = CM ? 1 : NB * HC;
     __shared__ unsigned long long ha[HW], hb[HW], hc[HW], hmin[NB * HC], hmax[NB * HC];
-    typedef unsigned long long hn_t;  // (32-bit LDS counts measured: no faster)
+    // (32-bit LDS counts in the weight-mode kernel measured: no faster)
+    typedef typename std::conditional<CM, unsigned int, unsigned long long>::type hn_t;
     __shared__ hn_t hn[NB * HC];
     __shared__ unsigned long long gcount, f_wlo, f_whi, f_ga, f_gb, f_gc, f_gn;
     for (int b = threadIdx.x; b < NB * HC; b += NT) {
@@ -3410,7 +3413,7 @@ __global__ void __launch_bounds__(NT) k_sel_hist(pcx_mat m) {
     } else {
         const double* const tcol = m.T + (int64_t)s * m.n_rows;
         const double wc = 1.0 / (double)m.n_total;  // (CM: sel_load's weight)
-        rows_strided<ROW_UNROLL>(threadIdx.x, NT, m.n_rows, [&](int64_t i) {
+        rows_strided<(CM ? 16 : ROW_UNROLL)>(threadIdx.x, NT, m.n_rows, [&](int64_t i) {
                                      if constexpr (CM) return XW{tcol[i], wc};
                                      else return sel_load(m, s, i);
                                  },
@@ -5592,7 +5595,7 @@ hipError_t sel_hist(pcx_mat& m, int n_active, hipStream_t st) {
             ncu = n;
         if (ncu <= 0) ncu = 256;
     }
-    const bool cm = m.sel_phase == 1 && !m.rep_raw;  // (every pass of this phase counts)
+    const bool cm = m.sel_phase == 1 && !m.rep_raw && m.n_rows < (1ll << 32);  // (every pass of this phase counts)
     if (n_active <= ncu) {
         if (cm)
             hipLaunchKernelGGL((k_sel_hist<1024, true>), dim3(n_active), dim3(1024), 0, st, m);
