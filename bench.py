@@ -195,6 +195,16 @@ def bench_c5(world, rank, dev, steps, warmup, N=1_000_000, E=4096):
                                 "unit": "TOP/s", "frac": (tops / I8_MFMA_PEAK_TOPS) if tops else None,
                                 "ops_per_launch": i8_ops_rank, "mixed_digits": digits,
                                 "traffic": _sum_traffic(("k_gemm_i8_grid", "k_gemm_i8_mixed", "k_gemm_i8x", "k_digits"))},
+            # the int8 emulation priced as the fp64 covariance it replaces: N E (E + 1) multiply-adds
+            # (every unique pair, two flops each) over the M_COV_I8 stage, against the fp64 MFMA peak
+            "roofline_cov_fp64_equiv": {"kernel": "M_COV_I8 (the whole covariance on int8 digit products)",
+                                        "achieved": (1.0 * cnt * E * (E + 1) / (i8_ms * 1e-3) / 1e12
+                                                     if i8_ms == i8_ms and gg else None),
+                                        "unit": "TFLOP/s (fp64-equivalent)", "fp64_peak": FP64_MFMA_PEAK_TFS},
+            "cov_guard": {"mode": meta.get("cov_guard"), "cols": meta.get("cov_guard_cols"),
+                          "err_bound": meta.get("cov_err_bound"),
+                          "meaning": "bound on |dC_pq| / sqrt(C_pp C_qq) of the int8 emulation (k_cov_guard); "
+                                     "mode 0 = passed (<= 2^-40), 1 = every digit pair recomputed, 2 = fp64"},
             "grid_events": ng, "mixed_int8": mixed, "inplace": inplace,
             "data": "synthetic on-GPU (SURVEY.md 8(d) spec, torch Philox per 125k-row shard, seed 3), "
                     "reputation=None"}
@@ -311,6 +321,78 @@ def bench_c4(dev, steps=3, oracle=True):
                                "sample": "the whole C4 consensus, numpy restatement (oracle/pcx_oracle.py)",
                                "cpu_model": cpu_model()}
         out["smooth_rep_max_rel_diff"] = float(np.max(np.abs(smooth - rs) / np.maximum(np.abs(rs), 1e-300)))
+    return out
+
+
+# config C1: README.rst:28-45 (the reference's own example; scaled + binary events)
+README_REPORTS = [[0.2, 0.7, 1, 1], [0.3, 0.5, 1, 1], [0.1, 0.7, 1, 1], [0.5, 0.7, 2, 1], [0.1, 0.2, 2, 2],
+                  [0.1, 0.2, 2, 2]]
+README_REPUTATION = [1, 2, 10, 9, 4, 2]
+README_BOUNDS = [{"scaled": True, "min": 0.1, "max": 0.5}, {"scaled": True, "min": 0.2, "max": 0.7},
+                 {"scaled": False, "min": 1, "max": 2}, {"scaled": False, "min": 1, "max": 2}]
+
+
+def bench_dropin(dev, which, calls, oracle=True):
+    """Configs C1 / C2 through the drop-in exactly as an unchanged caller of the reference runs them:
+    ``Oracle(reports=<host lists / numpy>, reputation=..., event_bounds=...).consensus()`` per call,
+    nothing cached across calls but libpcx's context.  Median per-call latency, the constructor and
+    the host-side split (Oracle.last_info["timing_ms"]: argument preparation, the GPU call, the copy
+    back, the result dict), for C2 the libpcx per-stage device times of one profiled call, and the
+    numpy restatement of the same call timed beside it."""
+    import numpy as np
+
+    from pyconsensus_amd import Oracle, _abi, _lib, synthetic
+
+    if which == "c1":
+        mk = lambda: dict(reports=[list(r) for r in README_REPORTS], reputation=list(README_REPUTATION),
+                          event_bounds=[dict(b) for b in README_BOUNDS])
+        desc = "README.rst:28-45 example, 6 reporters x 4 events (2 scaled), host lists"
+    else:
+        R, sc, lo, hi, rep = synthetic.matrix(1000, 100, seed=1)
+        b = synthetic.bounds_list(sc, lo, hi)
+        mk = lambda: dict(reports=R.copy(), reputation=rep, event_bounds=b)
+        desc = "1k x 100, 10% NA, 25% scaled, integer reputations (SURVEY.md 8(d), seed 1), numpy arrays"
+    for _ in range(5):
+        Oracle(**mk()).consensus()
+    tot, ctor, split = [], [], []
+    for _ in range(calls):
+        a = mk()  # (the caller's own data; a float64 array is rescaled in place, Q2)
+        t0 = time.perf_counter()
+        o = Oracle(**a)
+        t1 = time.perf_counter()
+        o.consensus()
+        t2 = time.perf_counter()
+        tot.append(t2 - t0)
+        ctor.append(t1 - t0)
+        split.append(o.last_info["timing_ms"])
+    med = lambda v: sorted(v)[len(v) // 2]
+    out = {"metric": "drop-in Oracle(...).consensus() per-call latency (%s)" % which.upper(), "calls": calls,
+           "latency_ms": 1e3 * med(tot), "latency_ms_min": 1e3 * min(tot), "path": o.last_info["path"],
+           "split_ms": {"constructor": 1e3 * med(ctor), **{k: med([d[k] for d in split]) for k in split[0]}},
+           "data": desc}
+    if o.last_info["path"] == "matrix":  # libpcx's own per-stage device time of one call
+        h = _lib.context(o._device_index())
+        _lib.lib().pcx_profile_enable(h, 1)
+        Oracle(**mk()).consensus()
+        import ctypes as C
+
+        ms = (C.c_double * _abi.NSTAGES)()
+        _lib.lib().pcx_profile_read(h, ms)
+        _lib.lib().pcx_profile_enable(h, 0)
+        st = {_lib.lib().pcx_stage_name(k).decode(): ms[k] for k in range(_abi.NSTAGES) if ms[k] > 0}
+        out["libpcx_stage_ms"] = {k: round(v, 4) for k, v in sorted(st.items(), key=lambda kv: -kv[1])[:12]}
+        out["libpcx_device_ms"] = sum(v for k, v in st.items() if k not in ("H2D", "D2H", "EXCHANGE"))
+    if oracle:
+        from oracle.pcx_oracle import OracleCPU
+
+        ts = []
+        for _ in range(3 if which == "c2" else 20):
+            a = mk()
+            t0 = time.perf_counter()
+            OracleCPU(**a).consensus()
+            ts.append(time.perf_counter() - t0)
+        out["cpu_baseline"] = {"value": 1e3 * med(ts), "unit": "ms", "kind": "port", "cores": host_threads(),
+                               "sample": "the same call, numpy restatement (oracle/pcx_oracle.py)"}
     return out
 
 
@@ -592,7 +674,17 @@ def main():
             traceback.print_exc()
             failed.append("medium")
             medium = {"metric": "oracle rounds/sec (batched 100x50)", "error": repr(e)[:400]}
+    dropin = {}
+    if args.c4 and world == 1:
+        for which, calls in (("c1", 200), ("c2", 30)):
+            try:
+                dropin[which] = bench_dropin(dev, which, calls, oracle=not args.no_cpu_baseline)
+            except Exception as e:  # noqa: BLE001
+                traceback.print_exc()
+                failed.append(which)
+                dropin[which] = {"metric": "drop-in per-call latency (%s)" % which.upper(), "error": repr(e)[:400]}
     if rank == 0:
+        line.update(dropin)
         if medium is not None:
             line["medium"] = medium
         if c5 is not None:

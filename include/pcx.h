@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PCX_ABI_VERSION 7
+#define PCX_ABI_VERSION 8
 
 enum pcx_status {
     PCX_OK = 0,
@@ -262,7 +262,10 @@ typedef struct {
      * (__init__.py:121, 266-269, 584: `original` IS the caller's array, rescaled in place): the
      * scaled columns of the reports are then rescaled in place and the other columns are left as
      * they are, which saves writing a copy of the whole matrix (pcx_consensus_f64 and
-     * pcx_interpolate_f64; the reports buffer must then be writable). */
+     * pcx_interpolate_f64; the reports buffer must then be writable).  After a failed call the
+     * buffer's scaled columns are unspecified: with several ranks (pcx_create_devices) each rank
+     * writes its rescaled rows back as it finishes, so a failure elsewhere can leave some rows
+     * rescaled and others not; the reference leaves them rescaled. */
     double *original, *filled;
     /* wpca intermediates (:317-326), optional: [E] weighted_mean, [E][E] covariance_matrix */
     double *weighted_mean, *covariance;
@@ -280,6 +283,14 @@ typedef struct {
                                      their covariance block ran on int8 MFMA */
     int32_t mixed_int8;           /* bit 0: general x grid pairs ran on int8 digit slices too (else fp64 MFMA);
                                      bit 1: and the general x general pairs (digits of tok w x digits of w) */
+    /* the int8 covariance's guard (mixed_int8 != 0): an upper bound, rigorous in exact arithmetic, on
+     * |C_pq - C~_pq| / sqrt(C_pp C_qq) over the entries with a general position, where C~ is the
+     * covariance of the fp64 centred matrix wcd (:322-326) and C the emulation's result.  Above
+     * 2^-40 the covariance is recomputed: cov_guard 1 = the remaining digit pairs (i + j >= NDIG, every
+     * digit product exact), 2 = the general pairs on fp64 MFMA (k_syrk, as without int8).  0 = passed. */
+    int32_t cov_guard;
+    int32_t cov_guard_cols;       /* general events whose own bound (the pair (p, p)) exceeded 2^-40   */
+    double  cov_err_bound;        /* the bound of the emulation that ran first (before any recompute)  */
 } pcx_result;
 
 /* The whole consensus (__init__.py:502-611) on this rank's rows; collective over
@@ -307,7 +318,7 @@ int pcx_nonconformity_f64(pcx_ctx* ctx, const pcx_problem* p, const double* scor
 
 /* Per-stage device time of the last single-matrix call (HIP events on the
  * context's stream) when enabled; names by pcx_stage_name(k), k < PCX_NSTAGES. */
-#define PCX_NSTAGES 48
+#define PCX_NSTAGES 56
 int         pcx_profile_enable(pcx_ctx* ctx, int on);
 int         pcx_profile_read(pcx_ctx* ctx, double* ms /* [PCX_NSTAGES] */);
 const char* pcx_stage_name(int k);

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pcx.h (structs and constants).  Keep in sync with the header."""
 import ctypes as C
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 OK, EINVAL, EHIP, ENOMEM, ECOMM = 0, -1, -2, -3, -4
 BRANCH_SET1, BRANCH_SET2, BRANCH_TIE_SET1, BRANCH_TIE_SET2, BRANCH_NONE = 1, 2, 3, 4, 5
@@ -72,7 +72,7 @@ def out_shape(kind, B, N, E):
 MEM_DEVICE, MEM_HOST = 0, 1
 F64, U64 = 0, 1                  # enum pcx_dtype
 RED_SUM, RED_MIN, RED_MAX = 0, 1, 2  # enum pcx_redop
-NSTAGES = 48                     # PCX_NSTAGES
+NSTAGES = 56                     # PCX_NSTAGES
 
 MAT_OUTPUT_AGENTS = ["old_rep", "this_rep", "smooth_rep", "scores", "na_row", "participation_rows",
                      "relative_part", "reporter_bonus"]
@@ -113,4 +113,5 @@ class Result(C.Structure):
         ("participation", C.c_double), ("avg_certainty", C.c_double),
         ("branch", C.c_int32), ("flags", C.c_int32), ("pi_iters", C.c_int32), ("components", C.c_int32),
         ("n_hard", C.c_int32), ("sel_passes", C.c_int32), ("comm_bytes", C.c_double),
-        ("grid_events", C.c_int32), ("mixed_int8", C.c_int32)]
+        ("grid_events", C.c_int32), ("mixed_int8", C.c_int32),
+        ("cov_guard", C.c_int32), ("cov_guard_cols", C.c_int32), ("cov_err_bound", C.c_double)]

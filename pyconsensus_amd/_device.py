@@ -37,3 +37,7 @@ def ptr(x):
 
 def current_stream_handle(device):
     return torch().cuda.current_stream(device).cuda_stream
+
+
+def synchronize(device):
+    torch().cuda.synchronize(device)

@@ -50,7 +50,7 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
                       catch_tolerance=0.1, alpha=0.1, int_dtype=False, algorithm="PCA",
                       outputs=None, device=None, filled=False, original=False,
                       max_components=5, variance_threshold=0.9, aux_scores=None,
-                      hierarchy_threshold=0.5, kmeans_init=None, cluster_threshold=None):
+                      hierarchy_threshold=0.5, kmeans_init=None, cluster_threshold=None, packed=False):
     """Run B rounds of N x E reports on the GPU.
 
     reports:    (B, N, E) float64, NaN = missing (0.0 is missing too, as in the reference)
@@ -64,6 +64,9 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     kmeans_init: (B, restarts, k) initial code-book rows (default: :func:`kmeans_draws`
                 on numpy's global RandomState, as the reference's scipy call draws them)
     cluster_threshold: clusterfeck's cut (default: the reference's log10(E)/1.77 rule)
+    packed:     numpy inputs travel to the device in ONE copy and every output is a view of ONE
+                device buffer (``out["_packed"]``; :func:`unpack_round` brings it back in one
+                copy) -- the drop-in's per-call path, where each separate small copy costs ~10 us
 
     Returns a dict of torch tensors on the device, named like the ABI fields
     (``smooth_rep``, ``outcomes_final``, ...).  Three regimes:
@@ -75,6 +78,10 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
     """
     t = _device.require_gpu()
     dev = t.device(device) if device is not None else t.device("cuda", t.cuda.current_device())
+    if packed and all(x is None or isinstance(x, np.ndarray) for x in (reports, reputation, scaled, lo, hi)):
+        reports, reputation, scaled, lo, hi = _upload_packed(
+            [(reports, np.float64), (reputation, np.float64), (scaled, np.uint8), (lo, np.float64),
+             (hi, np.float64)], dev)
     R = _device.as_device(reports, t.float64, dev)
     if R.dim() != 3:
         raise ValueError("reports must be (B, N, E)")
@@ -124,16 +131,60 @@ def consensus_batched(reports, reputation=None, scaled=None, lo=None, hi=None,
                      float(hierarchy_threshold), cthr, k, restarts, _device.ptr(kinit))
     res = _abi.BatchResult()
     outs = {}
-    for name, kind, dt in _abi.BATCH_OUTPUTS:
-        if name == "filled" and not filled or name == "original" and not original:
-            continue
-        if outputs is not None and name not in outputs and name not in ("filled", "original"):
-            continue
-        tdt = t.float64 if dt == "f8" else t.int32
-        x = t.empty(_abi.out_shape(kind, B, N, E), dtype=tdt, device=dev)
-        outs[name] = x
-        setattr(res, name, x.data_ptr())
+    want = [(name, kind, dt) for name, kind, dt in _abi.BATCH_OUTPUTS
+            if not (name == "filled" and not filled or name == "original" and not original)
+            and not (outputs is not None and name not in outputs and name not in ("filled", "original"))]
+    if packed:  # one device buffer, one 16-byte-aligned view per output
+        layout, off = [], 0
+        for name, kind, dt in want:
+            shape = _abi.out_shape(kind, B, N, E)
+            nb = int(np.prod(shape)) * (8 if dt == "f8" else 4)
+            layout.append((name, off, nb, dt, shape))
+            off += (nb + 15) // 16 * 16
+        buf = t.empty(max(off, 16), dtype=t.uint8, device=dev)
+        for name, o, nb, dt, shape in layout:
+            x = buf[o:o + nb].view(t.float64 if dt == "f8" else t.int32).view(shape)
+            outs[name] = x
+            setattr(res, name, x.data_ptr())
+        outs["_packed"] = buf
+        outs["_layout"] = layout
+    else:
+        for name, kind, dt in want:
+            tdt = t.float64 if dt == "f8" else t.int32
+            x = t.empty(_abi.out_shape(kind, B, N, E), dtype=tdt, device=dev)
+            outs[name] = x
+            setattr(res, name, x.data_ptr())
     h = _lib.bind_stream(dev.index, _device.current_stream_handle(dev))
     _lib.check(_lib.lib().pcx_consensus_batched_f64(h, C.byref(inp), C.byref(res)))
     outs["_inputs"] = (R, rep, sc, lo_, hi_, aux, kinit)  # keep inputs alive until the caller syncs
     return outs
+
+
+def _upload_packed(items, dev):
+    """numpy arrays (or None) -> device tensors, as views of ONE host-to-device copy."""
+    t = _device.torch()
+    parts, off = [], 0
+    for a, dt in items:
+        if a is None:
+            parts.append(None)
+            continue
+        a = np.ascontiguousarray(a, dtype=dt)
+        parts.append((a, off))
+        off += (a.nbytes + 15) // 16 * 16
+    host = np.empty(max(off, 16), dtype=np.uint8)
+    for p in parts:
+        if p is not None:
+            host[p[1]:p[1] + p[0].nbytes] = p[0].reshape(-1).view(np.uint8)
+    d = t.from_numpy(host).to(dev)
+    tdt = {np.float64: t.float64, np.uint8: t.uint8}
+    return [None if p is None else d[p[1]:p[1] + p[0].nbytes].view(tdt[dt]).view(p[0].shape)
+            for p, (_, dt) in zip(parts, items)]
+
+
+def unpack_round(out, b=0):
+    """Round ``b`` of a ``packed=True`` result as numpy arrays, from ONE device-to-host copy."""
+    host = out["_packed"].cpu().numpy()
+    g = {}
+    for name, o, nb, dt, shape in out["_layout"]:
+        g[name] = host[o:o + nb].view(np.float64 if dt == "f8" else np.int32).reshape(shape)[b]
+    return g

@@ -182,17 +182,32 @@ int pcx_release_workspace(pcx_ctx* ctx) {
     return PCX_OK;
 }
 
+}  // extern "C"
+namespace pcx {
+void ctx_host_free(pcx_ctx* c) {
+    if (c->mscr) (void)hipFree(c->mscr);
+    c->mscr = nullptr;
+    c->mscr_bytes = 0;
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+    if (c->sel_pin) (void)hipHostFree(c->sel_pin);
+    c->sel_pin = nullptr;
+    for (hipEvent_t& ev : c->sel_ev) {
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+    }
+}
+}  // namespace pcx
+extern "C" {
+
 void pcx_destroy(pcx_ctx* ctx) {
     if (!ctx) return;
     for (pcx_ctx* s : ctx->sub) pcx_destroy(s);
     if (ctx->group) pcx::group_destroy(ctx->group);
     pcx::rounds_free(ctx);
-    if (ctx->mscr) (void)hipFree(ctx->mscr);
-    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    if (ctx->sel_pin) (void)hipHostFree(ctx->sel_pin);
-    for (hipEvent_t ev : ctx->sel_ev)
-        if (ev) (void)hipEventDestroy(ev);
     (void)hipSetDevice(ctx->device);
+    pcx::ctx_host_free(ctx);
     pcx::workspace_free(ctx);
     delete ctx->comm;
     delete ctx;

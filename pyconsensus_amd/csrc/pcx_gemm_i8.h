@@ -259,14 +259,22 @@ struct GemmX {
     int gb;      // positions per digit slice, a multiple of 256
     int nt;      // gb / 256 event tiles per side
     int smax, kslices;
+    int smin;  // the pairs smin <= i + j <= smax (0: from the first; the covariance guard's second launch
+               // takes the rest, PCX_NDIG .. 2 PCX_NDIG - 2, pcx_matrix.hip k_cov_guard)
 };
-__host__ __device__ inline int gemm_i8x_pairs(int smax) {  // digit pairs (i, j), i, j < NDIG, i + j <= smax
+// digit j range of digit i among the pairs smin <= i + j <= smax (empty: j1 < j0)
+__host__ __device__ inline int gemm_i8x_j0(int i, int smin) { return smin - i > 0 ? smin - i : 0; }
+__host__ __device__ inline int gemm_i8x_j1(int i, int smax) { return smax - i < PCX_NDIG - 1 ? smax - i : PCX_NDIG - 1; }
+__host__ __device__ inline int gemm_i8x_pairs(int smax, int smin = 0) {  // digit pairs (i, j), i, j < NDIG
     int n = 0;
-    for (int i = 0; i < PCX_NDIG; i++) n += smax - i >= 0 ? (smax - i < PCX_NDIG ? smax - i + 1 : PCX_NDIG) : 0;
+    for (int i = 0; i < PCX_NDIG; i++) {
+        const int nj = gemm_i8x_j1(i, smax) - gemm_i8x_j0(i, smin) + 1;
+        n += nj > 0 ? nj : 0;
+    }
     return n;
 }
 __host__ __device__ inline int64_t gemm_i8x_items(const GemmX& g) {
-    return (int64_t)g.kslices * gemm_i8x_pairs(g.smax) * (g.nt * (g.nt + 1) / 2);
+    return (int64_t)g.kslices * gemm_i8x_pairs(g.smax, g.smin) * (g.nt * (g.nt + 1) / 2);
 }
 // slab of (k-slice, i, j, lower tile)
 __host__ __device__ inline int64_t gemm_i8x_slab(int ks, int i, int j, int tl, int nt) {
@@ -288,7 +296,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8x(GemmX g) {
     static_assert(NBUF >= 2 && NBUF * STAGE <= 163840, "int8 GEMM ring (160 KB of LDS)");
     constexpr int LOADS = 2 * KS * LPP;  // vector-memory ops per wave per stage
     extern __shared__ __attribute__((aligned(16))) char glds[];
-    const int ntri = g.nt * (g.nt + 1) / 2, npair = gemm_i8x_pairs(g.smax);
+    const int ntri = g.nt * (g.nt + 1) / 2, npair = gemm_i8x_pairs(g.smax, g.smin);
     const int item = xcd_remap(blockIdx.x, gridDim.x);
     const int ks = item / (npair * ntri);
     // tile major: every digit pair of one output tile, then the next tile (a, b + 1) -- the items
@@ -297,12 +305,12 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8x(GemmX g) {
     int r = item % (npair * ntri), i = 0;
     const int tl = r / npair;
     r %= npair;
-    for (;; i++) {  // digit i: min(smax - i, NDIG - 1) + 1 digits j
-        const int nj = (g.smax - i < PCX_NDIG - 1 ? g.smax - i : PCX_NDIG - 1) + 1;
+    for (;; i++) {  // digit i: the digits j0 .. j1 of the pair range
+        const int nj = gemm_i8x_j1(i, g.smax) - gemm_i8x_j0(i, g.smin) + 1;
         if (r < nj) break;
-        r -= nj;
+        r -= nj > 0 ? nj : 0;
     }
-    const int j = r;
+    const int j = gemm_i8x_j0(i, g.smin) + r;
     int ta = (int)((__builtin_sqrtf(8.0f * (float)tl + 1.0f) - 1.0f) * 0.5f);  // tl = ta (ta + 1) / 2 + tb
     while (ta * (ta + 1) / 2 > tl) ta--;
     while ((ta + 1) * (ta + 2) / 2 <= tl) ta++;

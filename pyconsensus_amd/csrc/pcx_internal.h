@@ -96,6 +96,7 @@ typedef struct {
     /* covariance operands (M_COV): the centred, filled matrix materialised once */
     double* wcd;                  /* [wcd_rows][wcd_ld] wcd = F - mu (:322), zero padded          */
     double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
+    double* rtokp;                /* [wcd_rows + 64] 1 / tokens (0 for 0; k_wcd, for k_digits)       */
     int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
     int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
     uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
@@ -137,6 +138,13 @@ typedef struct {
                                      when every token is 2^k: tok w 2^-e = w 2^-f, the same digits)    */
     double*  escale;              /* [wcd_ld] 2^-f per general position                               */
     int32_t* Pgx;                 /* gemm_i8x_slab(ks, i, j, lower tile) x [256][256] int32            */
+    int32_t  gg_smax;             /* the digit pairs i + j <= gg_smax in Pgx (PCX_NDIG - 1; all of them,
+                                     2 PCX_NDIG - 2, once the covariance guard asked for the rest)      */
+    /* the int8 covariance's error bound against the entries (k_digits -> k_cov_guard): per general
+       position, [G_NSTAT][128 cov_jb] int64 sums over this rank's rows (gacc), then as doubles over
+       all ranks (gsum, exchanged with the covariance) */
+    int64_t* gacc;
+    double*  gsum;
     /* algorithms other than PCA (enum pcx_algorithm) */
     int32_t max_components;       /* "big-five" component count                                     */
     int32_t components;           /* out ("fixed-variance"): components used, else -1               */
@@ -209,7 +217,7 @@ enum mat_stage_id {
     M_AGENTS, M_MATRICES, M_WCD, M_EIG, M_ZERO_LOADING, M_NC_OUT, M_WMEAN_OUT,
     M_SEL_EXACT, M_SEL_INIT, M_SEL_START, M_SEL_ARGMAX, M_SEL_VALUE, M_SEL_VALUE_FINISH, M_SEL_COMPACT,
     M_SEL_HIST, M_SEL_STEP, M_SEL_FINISH, M_HARD_LIST, M_HARD_GATHER, M_HARD_PREP, M_HARD_SORT, M_HARD_WALK,
-    M_EXCHANGE, M_H2D, M_D2H, M_COV_PLAN, M_COV_I8, M_CLUSTER, M_NSTAGE
+    M_EXCHANGE, M_H2D, M_D2H, M_COV_PLAN, M_COV_I8, M_CLUSTER, M_COV_GUARD, M_COV_REST, M_WCD_REBUILD, M_NSTAGE
 };
 static_assert(M_NSTAGE <= PCX_NSTAGES, "stage table");
 const char* stage_name(int k);
@@ -276,7 +284,12 @@ hipError_t sel_step(pcx_mat& m, int n_active, hipStream_t st);
 // info[] slots read by the runner
 enum info_slot_pub { INFO_BRANCH = 0, INFO_PI_ITERS = 1, INFO_FLAGS = 2, INFO_SEL_ACTIVE = 3, INFO_SEL_ARGMAX = 4,
                      INFO_PICK1 = 5, INFO_HARD = 6, INFO_SEL_WACTIVE = 7, INFO_COV_GENERAL = 8,
-                     INFO_COV_MIXED = 9, INFO_COV_TOK1 = 10 };
+                     INFO_COV_MIXED = 9, INFO_COV_TOK1 = 10, INFO_COV_GUARD = 12, INFO_COV_GUARD_COLS = 13,
+                     INFO_COV_GUARD_BOUND = 14 };
+// the covariance guard's sums per general position (pcx_mat.gacc / gsum rows)
+enum cov_guard_stat { G_L1D = 0, G_L1E, G_SD, G_SD2, G_SE, G_SE2, G_NSTAT };
+// the covariance guard's outcome (info[INFO_COV_GUARD], pcx_result.cov_guard)
+enum cov_guard_mode { COV_GUARD_PASS = 0, COV_GUARD_PAIRS = 1, COV_GUARD_FP64 = 2 };
 hipError_t tri_pack(const double* C, double* buf, int64_t E, int unpack, hipStream_t st);
 
 // pack / unpack of strided dd slot ranges for the slot exchange (runner)
@@ -356,4 +369,7 @@ int check_problem(const pcx_problem* p, int world, int entry, std::string& err);
 // pool of worker contexts with their own streams; synchronous
 int run_rounds(pcx_ctx* c, const pcx_batch* in, pcx_batch_result* out, std::string& err);
 void rounds_free(pcx_ctx* c);
+// a context's host-side resources (pinned staging slots, the selection's pinned info words and
+// events, the workgroup-per-round scratch): pcx_destroy and rounds_free (the pool's worker contexts)
+void ctx_host_free(pcx_ctx* c);
 }  // namespace pcx

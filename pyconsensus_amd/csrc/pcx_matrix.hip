@@ -56,7 +56,11 @@ enum ev_slot { EV_GUESS = 0, EV_MU, EV_OLD, EV_LD, EV_D1, EV_D2, EV_RAW, EV_ADJ,
 enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
-                 IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1, IN_SEL_WLIMB };
+                 IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1, IN_SEL_WLIMB, IN_COV_GUARD, IN_COV_GUARD_COLS,
+                 IN_COV_GUARD_BOUND };
+static_assert((int)IN_COV_GUARD == (int)INFO_COV_GUARD && (int)IN_COV_GUARD_COLS == (int)INFO_COV_GUARD_COLS &&
+                  (int)IN_COV_GUARD_BOUND == (int)INFO_COV_GUARD_BOUND,
+              "info slots");
 
 // ------------------------------------------------------------------ element transform
 struct ColParam {
@@ -920,9 +924,12 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
         // exactly (dscale = 2^-k escale above) and both digit strings coincide, so the general x
         // general product takes zD for both operands (reputation=None: int(1/N 1e6) = 1 for
         // N <= 1e6; 8 for a 125k-row consensus)
-        const double tsum = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
+        // (compared exactly: the token sum is an exact double-double of integers, maxtok n_rows an
+        // exact two-product -- in doubles, a sum above 2^53 a few units short would compare equal)
+        const dd tsum = ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2);
         const bool pow2 = maxtok >= 1.0 && maxtok < 0x1p52 && maxtok == ldexp(1.0, ilogb(maxtok));
-        m.info[IN_COV_TOK1] = (pow2 && tsum == maxtok * (double)m.n_rows) ? 1 : 0;
+        const double pp = maxtok * (double)m.n_rows, pe = fma(maxtok, (double)m.n_rows, -pp);
+        m.info[IN_COV_TOK1] = (pow2 && (tsum.hi - pp) + (tsum.lo - pe) == 0.0) ? 1 : 0;
     }
 }
 
@@ -963,7 +970,11 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     }
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
-        m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
+    {
+        const double t = i < m.n_rows ? m.tok[i] : 0.0;
+        m.tokp[i] = t;
+        m.rtokp[i] = t > 0.0 ? 1.0 / t : 0.0;  // (the covariance guard's sum delta^2 / tok, k_digits)
+    }
     const int64_t per = ((m.wcd_rows + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;
     int64_t r0 = blockIdx.x * per;
     r0 = r0 < m.wcd_rows ? r0 : m.wcd_rows;
@@ -1249,6 +1260,37 @@ __device__ __forceinline__ void balanced_digits(double X, uint32_t (&d)[PCX_NDIG
         if (dsum) dsum[k] += (int)di;
     }
 }
+
+// The covariance guard's sums (k_cov_guard), per general position over this rank's rows, taken by
+// the digit passes beside the digits: with t = (tok w 2^-e) 254^NDIG the exact scaled value and X =
+// rint(t) its digits' value, the residue delta = X - t (|delta| <= 0.52), summed as sum delta and
+// sum delta^2 / tok over the rows with tok > 0 (and for the digits of w, eta = Xe - te: sum tok eta,
+// sum tok eta^2), plus the L1 norm of the digits 1 .. NDIG - 1.  Each thread sums its rows in fp64
+// (error << 2^-24 for the <= 4096 rows of a chunk) and adds the fixed-point value at 2^-24 (the
+// squares rounded up) to int64 slots: exact and order-free, so the guard's decision is the same on
+// every run.
+constexpr double G_FIX = 0x1p24;
+// sum |d| over the packed digits 1 .. NDIG - 1 (two's complement bytes; as offset binary b ^ 0x80 =
+// d + 128, |d| = |(b ^ 0x80) - 128|: one v_sad_u8 per four digits)
+template <int W>
+__device__ __forceinline__ int32_t digit_l1(const uint32_t (&d)[PCX_NDIG][W], int32_t acc) {
+#pragma unroll
+    for (int k = 1; k < PCX_NDIG; k++)
+#pragma unroll
+        for (int j = 0; j < W; j++) acc = (int32_t)__builtin_amdgcn_sad_u8(d[k][j] ^ 0x80808080u, 0x80808080u, (uint32_t)acc);
+    return acc;
+}
+__device__ __forceinline__ int32_t digit_l1(const uint32_t (&d)[PCX_NDIG], int32_t acc) {
+#pragma unroll
+    for (int k = 1; k < PCX_NDIG; k++) acc = (int32_t)__builtin_amdgcn_sad_u8(d[k] ^ 0x80808080u, 0x80808080u, (uint32_t)acc);
+    return acc;
+}
+__device__ __forceinline__ void guard_add(int64_t* slot, double v, bool up) {
+    const double f = v * G_FIX;
+    const long long x = up ? (long long)ceil(f * (1.0 + 0x1p-40)) : (long long)rint(f);
+    if (x) atomicAdd((unsigned long long*)slot, (unsigned long long)x);
+}
+
 constexpr int DG_POS = BT / 4;  // positions per k_digits workgroup
 __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     const int gb = m.cov_jb * CT;
@@ -1268,16 +1310,19 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     int32_t dsum[PCX_NDIG];  // |d| <= 127: int32-exact for any chunk under 16M rows
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
+    int32_t l1d = 0, l1e = 0;                         // the guard's sums (guard_add)
+    double sd = 0.0, sd2 = 0.0, se = 0.0, se2 = 0.0;
     for (int64_t grp = g0; live && grp < g1; grp++) {
         uint32_t d[PCX_NDIG], e[PCX_NDIG];
 #pragma unroll
         for (int k = 0; k < PCX_NDIG; k++) d[k] = e[k] = 0;
-        double wr[4], tk[4];
+        double wr[4], tk[4], rt[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int64_t i = grp * 16 + 4 * h + u;
             wr[u] = fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q];
             tk[u] = m.tokp[i];  // 0 past n_rows
+            rt[u] = m.rtokp[i];  // 1 / tok (0 for 0)
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1288,14 +1333,24 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             // q = rint(X / 254) -- X / 254 is a multiple of 1/254 and X * (1/254) lies within 2^-14 of
             // it, so the rounding is exact but for the 1/2 tie, where either neighbour leaves
             // |d| = 127 -- and d = X - 254 q exactly
-            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv);
-            balanced_digits(rint(pv + fma(lo, DIG_SCALE, pe)), d, u, dsum);
+            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv), pl = fma(lo, DIG_SCALE, pe);
+            const double X = rint(pv + pl);
+            balanced_digits(X, d, u, dsum);
+            const double dl = (X - pv) - pl;  // X - t (X - pv exact)
+            sd += dl;
+            sd2 = fma(dl * dl, rt[u], sd2);
             if (gg) {
-                const double v = wr[u] * esc, uv = v * DIG_SCALE;
-                balanced_digits(rint(uv + fma(v, DIG_SCALE, -uv)), e, u, nullptr);
+                const double v = wr[u] * esc, uv = v * DIG_SCALE, ue = fma(v, DIG_SCALE, -uv);
+                const double Xe = rint(uv + ue);
+                balanced_digits(Xe, e, u, nullptr);
+                const double el = (Xe - uv) - ue;
+                se = fma(tk[u], el, se);
+                se2 = fma(tk[u] * el, el, se2);
             }
         }
         const int64_t o = (grp * ldd + q) * 16 + 4 * h;
+        l1d = digit_l1(d, l1d);
+        if (gg) l1e = digit_l1(e, l1e);
 #pragma unroll
         for (int k = 0; k < PCX_NDIG; k++) *(uint32_t*)(m.zD + o + (int64_t)k * gb * 16) = d[k];
         if (gg) {
@@ -1309,6 +1364,30 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
         t += __shfl_xor(t, 1, WAVE);
         t += __shfl_xor(t, 2, WAVE);
         if (live && h == 0 && t) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)t);
+    }
+    // the guard's sums: the four quarters' fp64 sums added, then one fixed-point atomic each
+    auto q4 = [](double v) {
+        v += __shfl_xor(v, 1, WAVE);
+        return v + __shfl_xor(v, 2, WAVE);
+    };
+    l1d += __shfl_xor(l1d, 1, WAVE);
+    l1d += __shfl_xor(l1d, 2, WAVE);
+    l1e += __shfl_xor(l1e, 1, WAVE);
+    l1e += __shfl_xor(l1e, 2, WAVE);
+    sd = q4(sd);
+    sd2 = q4(sd2);
+    se = q4(se);
+    se2 = q4(se2);
+    if (live && h == 0 && m.gacc) {
+        int64_t* ga = m.gacc + q;
+        if (l1d) atomicAdd((unsigned long long*)&ga[G_L1D * gb], (unsigned long long)(int64_t)l1d);
+        guard_add(&ga[G_SD * gb], sd, false);
+        guard_add(&ga[G_SD2 * gb], sd2, true);
+        if (gg) {
+            if (l1e) atomicAdd((unsigned long long*)&ga[G_L1E * gb], (unsigned long long)(int64_t)l1e);
+            guard_add(&ga[G_SE * gb], se, false);
+            guard_add(&ga[G_SE2 * gb], se2, true);
+        }
     }
 }
 
@@ -1329,6 +1408,8 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
     int32_t dsum[PCX_NDIG];  // |d| <= 127: int32-exact for any chunk under 16M rows
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
+    int32_t l1 = 0;  // the guard's sums (guard_add)
+    double sd = 0.0, sd2 = 0.0;
     for (int64_t grp = g0; grp < g1; grp++) {
         uint32_t d[PCX_NDIG][4];
 #pragma unroll
@@ -1337,10 +1418,13 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
         for (int r = 0; r < 16; r++) {
             const int64_t i = grp * 16 + r;
             const double w = (fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q]) * sc;  // exact (power of two)
-            const double tk = m.tokp[i];                                                    // 0 past n_rows
+            const double tk = m.tokp[i], rt = m.rtokp[i];                                   // 0 past n_rows
             double hi = w * tk, lo = fma(w, tk, -hi);  // tok w exactly
-            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv);
-            double X = rint(pv + fma(lo, DIG_SCALE, pe));
+            const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv), pl = fma(lo, DIG_SCALE, pe);
+            double X = rint(pv + pl);
+            const double dl = (X - pv) - pl;  // X - t (X - pv exact)
+            sd += dl;
+            sd2 = fma(dl * dl, rt, sd2);
 #pragma unroll
             for (int k = PCX_NDIG - 1; k >= 0; k--) {  // (k_digits: the same digits)
                 double di = X;
@@ -1356,10 +1440,17 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
 #pragma unroll
         for (int k = 0; k < PCX_NDIG; k++)
             *(uint4*)(m.zD + ((grp * ldd) + (int64_t)k * gb + q) * 16) = uint4{d[k][0], d[k][1], d[k][2], d[k][3]};
+        l1 = digit_l1(d, l1);
     }
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++)
         if (dsum[k]) atomicAdd((unsigned long long*)&m.dtok[(int64_t)k * gb + q], (unsigned long long)(int64_t)dsum[k]);
+    if (m.gacc) {  // (one digit string: the guard derives the w digits' sums, k_cov_guard)
+        int64_t* ga = m.gacc + q;
+        if (l1) atomicAdd((unsigned long long*)&ga[G_L1D * gb], (unsigned long long)(int64_t)l1);
+        guard_add(&ga[G_SD * gb], sd, false);
+        guard_add(&ga[G_SD2 * gb], sd2, true);
+    }
 }
 
 // plain loader for the Gram product of a symmetric E x E matrix (power-iteration squaring)
@@ -1517,7 +1608,7 @@ __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t 
 // residue (2 x 0.52 x 254^-NDIG x 1/2): ~2e-14 of |tok w_p| |w_q|'s bound, exact sums otherwise
 // (fp64 tiles: a rounding per multiply-add).
 __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
-    constexpr int SMAX = PCX_NDIG - 1;
+    const int SMAX = m.gg_smax;  // PCX_NDIG - 1, or 2 PCX_NDIG - 2 once the guard asked for every pair
     const int nt = (m.cov_jb * CT + GT - 1) / GT;
     const int ta = (int)(p / GT), tb = (int)(q / GT), tl = ta * (ta + 1) / 2 + tb;
     const int64_t within = (p % GT) * GT + (q % GT);
@@ -1527,7 +1618,7 @@ __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
         int64_t t = 0;
         for (int i = 0; i <= sd && i < PCX_NDIG; i++) {
             const int j = sd - i;
-            if (j >= PCX_NDIG) continue;
+            if (j >= PCX_NDIG) continue;  // (i + j = sd: every pair of this weight)
             t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
         }
         a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)t, 0.0});
@@ -1636,6 +1727,165 @@ __global__ void __launch_bounds__(BT) k_cov_finish(pcx_mat m) {
     if (idx >= E * E) return;
     const double denom = dd_to_double(scl(m, SC_TOK)) - 1.0;
     m.C[idx] = m.C[idx] / denom;
+}
+
+// ------------------------------------------------------------------ the int8 covariance's guard
+// The emulation's result for an entry with a general position differs from the covariance of the
+// fp64 centred matrix (C~_pq = sum tok w_p w_q, w = fl(F - mu), :322-326) by, per row, the digit
+// strings' residues and the dropped digit pairs.  With D = (tok w_p + delta) / S_p and E = (w_q +
+// eta) / T_q the digit values (S = 2^e, T = 2^f; |delta| <= 0.52 254^-NDIG S per row):
+//   (a) sum delta w_q: sum tok w_q ~ 0 (mu is the token-weighted mean), so for any c, sum delta w_q =
+//       sum tok (delta / tok - c) w_q + c sum tok w_q; Cauchy-Schwarz with the best c = sum delta / T:
+//       |(a)| <= sqrt(V_p) sqrt(C~_qq) + |c| |sum tok w_q|, V_p = sum delta^2 / tok - (sum delta)^2 / T
+//       -- a constant residue (a column whose rows mostly share one value) cancels here;
+//   (b) sum tok w_p eta: likewise with V'_q = sum tok eta^2 - (sum tok eta)^2 / T;
+//   (c) sum delta eta <= sqrt(sum delta^2 / tok) sqrt(sum tok eta^2);
+//   (d) the dropped pairs i + j > smax: per row sum_{i >= 1} |d_i| 254^-(i+1) |tail of E past digit
+//       smax - i| <= 0.502 254^-(smax+2) S T L1(d) (and the same with L1(e)), so over the rows
+//       <= 0.502 254^-(smax+2) S_p T_q sqrt(L1d_p L1e_q) -- linear in the rows: this is the term a
+//       column of equal values with a few outliers makes large (their digits sit far below the scale
+//       the outliers set);
+//   the mean's rounding: |sum tok w_q| <= min(T (|mu_q| 2^-50 + max|w_q| 2^-52), sqrt(T C~_qq)).
+// Relative to sqrt(C_pp C_qq) each term is a product of per-position factors, so the bound R is a sum
+// of products of their maxima.  (the general x grid block has (a) and the mean term only: z is exact.)
+// R <= 2^-40 passes; otherwise the pairs i + j > smax are computed too (no (d): every digit product
+// exact) when that alone brings R under 2^-40, else the general pairs go to fp64 (k_syrk).
+constexpr double GUARD_EPS = 0x1p-40;
+
+// gacc (int64, this rank) -> gsum (doubles) for the exchange; L1 exact, the others at 2^-24
+__global__ void __launch_bounds__(BT) k_guard_stats(pcx_mat m) {
+    const int64_t gb = (int64_t)m.cov_jb * CT, n = G_NSTAT * gb;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < n; i += (int64_t)gridDim.x * BT) {
+        const double v = (double)m.gacc[i];
+        m.gsum[i] = i < 2 * gb ? v : v * (1.0 / G_FIX);
+    }
+}
+
+__device__ __forceinline__ double blk_max_d(double v, double* lds) {
+    v = wave_max_d(v);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) lds[wv] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) r = fmax(r, lds[k]);
+    return r;
+}
+
+// one workgroup: R over every general position (and the grid positions' mean factor) from the
+// final C (normalised: times sum tok - 1), gsum (all ranks) and the digit scales
+__global__ void __launch_bounds__(1024) k_cov_guard(pcx_mat m) {
+    __shared__ double lds[16];
+    __shared__ int cnt;
+    const int64_t E = m.n_events, gb = (int64_t)m.cov_jb * CT;
+    const double T = dd_to_double(scl(m, SC_TOK)), denom = T - 1.0;
+    const bool gg = m.cov_gg8 != 0, one = m.zE == m.zD;  // one digit string: every token maxtok = 2^k
+    double maxtok = 0.0;
+    for (int w = 0; w < m.world; w++) maxtok = fmax(maxtok, m.scal[((int64_t)w * SS + SC_MAXTOK) * 2]);
+    // (the k_digits row chunks: each adds at most one 2^-24 unit of rounding per sum and rank)
+    const double ferr = (double)m.world * 4096.0 / G_FIX;
+    const double b6 = 1.0 / DIG_SCALE;  // 254^-NDIG
+    if (threadIdx.x == 0) cnt = 0;
+    double rd = 0.0, re = 0.0, gd = 0.0, ge = 0.0, kd = 0.0, ke = 0.0, ad = 0.0, ae = 0.0, bg = 0.0, bq = 0.0;
+    bool bad = !(denom != 0.0 && __builtin_isfinite(denom) && T > 0.0);
+    for (int64_t q = threadIdx.x; !bad && q < E; q += blockDim.x) {
+        const int c = m.cov_perm[q];
+        const double Cqq = m.C[(int64_t)c * E + c] * denom * (1.0 - 0x1p-40);
+        const double mu = m.ev[EV_MU * E + c];
+        if (q >= gb) {  // grid position: |F - mu| <= 1; a constant column's entries are exact zeros
+            if (Cqq > 0.0) bq = fmax(bq, fmin(T * (fabs(mu) * 0x1p-50 + 0x1p-52) / sqrt(Cqq), sqrt(T)));
+            continue;
+        }
+        const double S = 1.0 / m.dscale[q], Tq = gg ? 1.0 / m.escale[q] : 0.0;
+        const double* g = m.gsum + q;
+        const double l1d = g[G_L1D * gb], sd = g[G_SD * gb], sd2 = g[G_SD2 * gb];
+        const double l1e = one ? l1d : g[G_L1E * gb], se = one ? maxtok * sd : g[G_SE * gb],
+                     se2 = one ? maxtok * maxtok * sd2 : g[G_SE2 * gb];
+        const double sdl = fmax(0.0, fabs(sd) - ferr), sel = fmax(0.0, fabs(se) - ferr * (one ? maxtok : 1.0));
+        const double Vd = fmax(0.0, sd2 + ferr - sdl * sdl / T);
+        const double Ve = fmax(0.0, se2 + ferr * (one ? maxtok * maxtok : 1.0) - sel * sel / T);
+        if (!(Cqq > 0.0) || !__builtin_isfinite(Cqq)) {
+            // no spread: exact only when nothing was rounded or dropped
+            if (l1d != 0.0 || sd2 != 0.0 || (gg && (l1e != 0.0 || se2 != 0.0)) || !__builtin_isfinite(Cqq)) bad = true;
+            continue;
+        }
+        const double rC = 1.0 / sqrt(Cqq);
+        const double rdq = b6 * S * sqrt(Vd) * rC, adq = b6 * S * (fabs(sd) + ferr) / T * rC;
+        double own = rdq;
+        rd = fmax(rd, rdq);
+        ad = fmax(ad, adq);
+        const double bgq = fmin(T * (fabs(mu) * 0x1p-50 + (gg ? 0.5 * Tq : 0.5 * S) * 0x1p-52) * rC, sqrt(T));
+        bg = fmax(bg, bgq);
+        own += adq * bgq;
+        if (gg) {
+            const double req = b6 * Tq * sqrt(Ve) * rC, aeq = b6 * Tq * (fabs(se) + ferr) / T * rC;
+            const double gdq = S * sqrt(l1d) * rC, geq = Tq * sqrt(l1e) * rC;
+            const double kdq = S * sqrt(sd2 + ferr) * rC, keq = Tq * sqrt(se2 + ferr) * rC;
+            re = fmax(re, req);
+            ae = fmax(ae, aeq);
+            gd = fmax(gd, gdq);
+            ge = fmax(ge, geq);
+            kd = fmax(kd, kdq);
+            ke = fmax(ke, keq);
+            own += req + aeq * bgq + b6 * b6 * kdq * keq;
+            if (m.gg_smax < 2 * PCX_NDIG - 2) own += 0.502 * pow(PCX_DBASE, -(double)(m.gg_smax + 2)) * gdq * geq;
+        }
+        if (!(own <= GUARD_EPS)) atomicAdd(&cnt, 1);
+    }
+    bad = __syncthreads_or(bad);
+    rd = blk_max_d(rd, lds);
+    re = blk_max_d(re, lds);
+    gd = blk_max_d(gd, lds);
+    ge = blk_max_d(ge, lds);
+    kd = blk_max_d(kd, lds);
+    ke = blk_max_d(ke, lds);
+    ad = blk_max_d(ad, lds);
+    ae = blk_max_d(ae, lds);
+    bg = blk_max_d(bg, lds);
+    bq = blk_max_d(bq, lds);
+    if (threadIdx.x == 0) {
+        // (a) + mean term over general and grid q; (b), (c), (d) over general pairs
+        double R = rd + ad * fmax(bg, bq);
+        double Rd = 0.0;
+        if (gg) {
+            R += re + ae * bg + b6 * b6 * kd * ke;
+            if (m.gg_smax < 2 * PCX_NDIG - 2) Rd = 0.502 * pow(PCX_DBASE, -(double)(m.gg_smax + 2)) * gd * ge;
+        }
+        int mode = COV_GUARD_PASS;
+        if (bad || !(R + Rd <= GUARD_EPS)) mode = (!bad && gg && Rd > 0.0 && R <= GUARD_EPS) ? COV_GUARD_PAIRS : COV_GUARD_FP64;
+        const double bound = bad ? __builtin_inf() : R + Rd;
+        m.info[IN_COV_GUARD] = mode;
+        m.info[IN_COV_GUARD_COLS] = bad ? (int64_t)gb : cnt;
+        m.info[IN_COV_GUARD_BOUND] = (int64_t)__double_as_longlong(bound);
+    }
+}
+
+// PCX_M_WCD_REBUILD (the guard's fp64 fallback): wcd = F - mu wherever the fp64 tiles of the whole
+// trapezoid (general x every position) read what k_wcd did not write -- the general positions from
+// the compact Fg when cov_gg8 ran (k_wcd wrote no wcd), the grid positions from their 2-bit codes
+// (F = 1 + z / 2 exactly, so F - mu is k_wcd's own subtraction); rows past n_rows 0
+__global__ void __launch_bounds__(BT) k_wcd_rebuild(pcx_mat m, int general) {
+    const int64_t E = m.n_events, gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
+    const int64_t p = blockIdx.y * (int64_t)BT + threadIdx.x;
+    if (p >= E || (!general && p < gb)) return;
+    const double mu = m.ev[EV_MU * E + m.cov_perm[p]];
+    const int64_t ng = m.wcd_rows / 16;
+    for (int64_t g = blockIdx.x; g < ng; g += gridDim.x) {
+        if (p < gb) {
+#pragma unroll 4
+            for (int r = 0; r < 16; r++) {
+                const int64_t i = g * 16 + r;
+                m.wcd[i * ld + p] = i < m.n_rows ? m.Fg[i * gb + p] - mu : 0.0;
+            }
+        } else {
+            const uint32_t P = zb_packed(m)[g * m.zq + (p - gb)];
+#pragma unroll 4
+            for (int r = 0; r < 16; r++) {
+                const int64_t i = g * 16 + r;
+                m.wcd[i * ld + p] = i < m.n_rows ? (1.0 + 0.5 * (double)zpack_get(P, r)) - mu : 0.0;
+            }
+        }
+    }
 }
 
 // ================================================================== power iteration
@@ -5090,7 +5340,7 @@ const char* stage_name(int k) {
         "ROWSUMS", "AGENTS", "MATRICES", "WCD", "EIG", "ZERO_LOADING", "NC_OUT", "WMEAN_OUT", "SEL_EXACT",
         "SEL_INIT", "SEL_START", "SEL_ARGMAX", "SEL_VALUE", "SEL_VALUE_FINISH", "SEL_COMPACT", "SEL_HIST",
         "SEL_STEP", "SEL_FINISH", "HARD_LIST", "HARD_GATHER", "HARD_PREP", "HARD_SORT", "HARD_WALK", "EXCHANGE",
-        "H2D", "D2H", "COV_PLAN", "COV_I8", "CLUSTER"};
+        "H2D", "D2H", "COV_PLAN", "COV_I8", "CLUSTER", "COV_GUARD", "COV_REST", "WCD_REBUILD"};
     return (k >= 0 && k < M_NSTAGE) ? names[k] : "";
 }
 
@@ -5280,7 +5530,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 // stored transposed into Pmx [grid position][digit position]; |z d| <= 2 * 127 per row
                 // (16 row groups a block at least: 64 left a 125k-row shard's k_digits1 with 492 blocks)
                 const int ng = (int)std::min<int64_t>(4096, (rg + 15) / 16);
-                if (hipMemsetAsync(m.dtok, 0, (size_t)PCX_NDIG * gb * 8, st) != hipSuccess) return hipGetLastError();
+                // (the digit sums and, past them, the covariance guard's sums)
+                if (hipMemsetAsync(m.dtok, 0, (size_t)(PCX_NDIG + (m.gacc ? G_NSTAT : 0)) * gb * 8, st) != hipSuccess)
+                    return hipGetLastError();
                 if (m.cov_gg8 && m.zE != m.zD)  // both digit strings
                     hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
                 else
@@ -5353,6 +5605,40 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int nt = (int)((E + CV_T - 1) / CV_T);
             hipLaunchKernelGGL(k_cov_assemble, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(CV_T * 8), 0, st, m,
                                (const double*)S, (int)(m.world == 1));
+            // the guard's sums as doubles (the runner exchanges them with the covariance)
+            if (m.cov_mixed && m.gacc && m.gsum && m.cov_jb > 0)
+                hipLaunchKernelGGL(k_guard_stats, dim3((unsigned)((G_NSTAT * m.cov_jb * CT + BT - 1) / BT)), dim3(BT), 0,
+                                   st, m);
+            break;
+        }
+        case M_COV_GUARD:
+            if (!m.cov_mixed || !m.gsum || m.cov_jb < 1) {
+                err = "M_COV_GUARD: no int8 covariance to guard";
+                return hipErrorInvalidValue;
+            }
+            hipLaunchKernelGGL(k_cov_guard, dim3(1), dim3(1024), 0, st, m);
+            break;
+        case M_COV_REST: {  // every digit pair i + j >= NDIG of the general x general product (the guard)
+            if (!m.cov_gg8 || !m.Pgx || m.ks_gx < 1 || m.gg_smax != 2 * PCX_NDIG - 2) {
+                err = "M_COV_REST: no general x general int8 product";
+                return hipErrorInvalidValue;
+            }
+            const int gb = m.cov_jb * CT;
+            const int64_t rg = m.wcd_rows / 16;
+            GemmX g{m.zD, m.zE, zd_ld(gb), zd_ld(gb), m.Pgx, rg, gb, (gb + GT - 1) / GT, 2 * PCX_NDIG - 2, m.ks_gx,
+                    PCX_NDIG};
+            hipLaunchKernelGGL((k_gemm_i8x<GEMM_I8X_WAVES, GEMM_I8X_NBUF>), dim3((unsigned)gemm_i8x_items(g)),
+                               dim3(GEMM_I8X_WAVES * 64), GEMM_I8X_LDS, st, g);
+            break;
+        }
+        case M_WCD_REBUILD: {  // args: m.cov_gg8 still as it ran (general positions from Fg)
+            if (!m.wcd || !m.zB || m.cov_jb < 1 || (m.cov_gg8 && !m.Fg) || m.wcd_rows % 16) {
+                err = "M_WCD_REBUILD: operands missing";
+                return hipErrorInvalidValue;
+            }
+            const int64_t ng = m.wcd_rows / 16;
+            hipLaunchKernelGGL(k_wcd_rebuild, dim3((unsigned)std::min<int64_t>(ng, 2048), (unsigned)((E + BT - 1) / BT)),
+                               dim3(BT), 0, st, m, (int)m.cov_gg8);
             break;
         }
         case M_COV_FINISH: {  // several ranks: the exchanged sum normalised, then the flags
@@ -5564,7 +5850,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             break;
         }
         case M_MATRICES:
-            if (m.original || m.filled)
+            // (in place with no other matrix asked for: the scaled columns still need their rescale)
+            if (m.original || m.filled || (m.orig_inplace && !m.rescaled))
                 hipLaunchKernelGGL(k_matrices, colgrid, dim3(BT), 0, st, m);
             break;
         case M_EIG:

@@ -43,6 +43,7 @@ void rounds_free(pcx_ctx* c) {
     for (pcx_ctx* w : c->pool) {
         (void)hipSetDevice(w->device);
         workspace_free(w);
+        ctx_host_free(w);  // (a round above SEL_EXACT_MAX rows took the pipelined selection's pinned words)
         if (w->stream) (void)hipStreamDestroy(w->stream);
         delete w;
     }

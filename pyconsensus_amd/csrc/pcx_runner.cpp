@@ -280,7 +280,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->C, (size_t)(E * E) * 8, false},
         {(void**)&w->Mw, (size_t)(2 * E * E + 8 * E + 64) * 8, false},
         {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
-        {(void**)&w->tokp, (size_t)(w->wcd_rows + 64) * 8, false},
+        {(void**)&w->tokp, (size_t)(2 * (w->wcd_rows + 64)) * 8, false},  // tokens, then 1 / tokens
         {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
         {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
@@ -377,14 +377,15 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
         R.hip(hipHostMalloc(&c->pinned, need, hipHostMallocDefault), "hipHostMalloc(staging)");
         c->pinned_bytes = need;
     }
-    hipEvent_t ev[STAGE_SLOTS];
-    for (int k = 0; k < STAGE_SLOTS; k++) R.hip(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
-    struct Evs {
+    hipEvent_t ev[STAGE_SLOTS] = {};
+    struct Evs {  // (the guard before the first creation: a failed one leaks none made before it)
         hipEvent_t* e;
         ~Evs() {
-            for (int k = 0; k < STAGE_SLOTS; k++) (void)hipEventDestroy(e[k]);
+            for (int k = 0; k < STAGE_SLOTS; k++)
+                if (e[k]) (void)hipEventDestroy(e[k]);
         }
     } evs{ev};
+    for (int k = 0; k < STAGE_SLOTS; k++) R.hip(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
     char* pin = static_cast<char*>(c->pinned);
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
@@ -558,9 +559,12 @@ void select(Run& R, pcx_mat& m, pcx_workspace* w, int phase, pcx_result* res) {
         int passes = 1;
         if (active > 0) {
             pcx_ctx* c = R.c;
-            if (!c->sel_pin) {
-                R.hip(hipHostMalloc((void**)&c->sel_pin, 16 * sizeof(int64_t), hipHostMallocDefault), "hipHostMalloc(sel)");
-                for (hipEvent_t& ev : c->sel_ev) R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+            if (!c->sel_pin) {  // the events first: sel_pin is published only with both of them made
+                for (hipEvent_t& ev : c->sel_ev)
+                    if (!ev) R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+                int64_t* pin = nullptr;
+                R.hip(hipHostMalloc((void**)&pin, 16 * sizeof(int64_t), hipHostMallocDefault), "hipHostMalloc(sel)");
+                c->sel_pin = pin;
             }
             auto launch_pass = [&](int64_t a_ub, int64_t w_ub, int slot) {
                 if (passes == MAX_SEL_PASSES + 1) {  // (+1: the speculative pass after the last)
@@ -938,6 +942,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.scalars = w->scalars;
         m.wcd = w->wcd;
         m.tokp = w->tokp;
+        m.rtokp = w->tokp + w->wcd_rows + 64;
         m.wcd_rows = w->wcd_rows;
         m.wcd_ld = w->wcd_ld;
         m.rowpart = w->rowpart;
@@ -949,6 +954,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         r->sel_passes = 0;
         r->grid_events = 0;
         r->mixed_int8 = 0;
+        r->cov_guard = 0;
+        r->cov_guard_cols = 0;
+        r->cov_err_bound = 0.0;
 
         const double* cstat = w->cstat;
         (void)cstat;
@@ -1031,12 +1039,17 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 // mixed pairs on int8 digits when the bounds are finite and the memory is there
                 m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * zd_ld(gb))) &&
                                       w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4)) &&
-                                      w->grow(w->dtok, (size_t)(PCX_NDIG * gb * 8))
+                                      w->grow(w->dtok, (size_t)((PCX_NDIG + G_NSTAT) * gb * 8))
                                   ? 1
                                   : 0;
                 r->mixed_int8 = m.cov_mixed;
                 m.zD = (int8_t*)w->zd.p;
                 m.dtok = (int64_t*)w->dtok.p;
+                // the guard's sums follow the digit sums (zeroed with them); as doubles past the
+                // covariance's packed triangle in cslab, so that one SUM exchanges both
+                m.gacc = m.cov_mixed ? m.dtok + PCX_NDIG * gb : nullptr;
+                m.gsum = m.cov_mixed ? w->cslab + E * (E + 1) / 2 : nullptr;
+                m.gg_smax = PCX_NDIG - 1;
                 // mixed: the later full passes (M_GEMV2, M_OUTCOMES) read F compactly -- the general
                 // positions' filled values (Fg, written by k_wcd), the grid ones from the 2-bit codes
                 // and the missing bits (nam) -- instead of the reports (a quarter of the bytes at C5)
@@ -1096,13 +1109,47 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.rescaled = m.orig_inplace;  // later stages read the scaled columns rescaled already
                 R.stage(m, M_COV);
                 R.stage(m, M_COV_I8);
-                R.stage(m, M_COV_REDUCE);
-                if (R.comm) {  // the partial covariance: one SUM of its lower triangle (cslab is free now)
-                    R.hip(tri_pack(w->C, w->cslab, E, 0, R.st), "tri pack");
-                    R.allreduce(w->cslab, E * (E + 1) / 2, PCX_F64, PCX_SUM);
-                    R.hip(tri_pack(w->C, w->cslab, E, 1, R.st), "tri unpack");
+                auto cov_reduce = [&] {
+                    R.stage(m, M_COV_REDUCE);
+                    if (R.comm) {  // the partial covariance: one SUM of its lower triangle (cslab is free now)
+                        R.hip(tri_pack(w->C, w->cslab, E, 0, R.st), "tri pack");
+                        // (and the guard's sums, k_guard_stats wrote them past the triangle)
+                        R.allreduce(w->cslab, E * (E + 1) / 2 + (m.cov_mixed ? G_NSTAT * gb : 0), PCX_F64, PCX_SUM);
+                        R.hip(tri_pack(w->C, w->cslab, E, 1, R.st), "tri unpack");
+                    }
+                    R.stage(m, M_COV_FINISH);
+                };
+                cov_reduce();
+                r->cov_guard = 0;
+                r->cov_guard_cols = 0;
+                r->cov_err_bound = 0.0;
+                if (m.cov_mixed) {
+                    // the int8 emulation's error bound against the entries (k_cov_guard); above 2^-40
+                    // the covariance is recomputed: the remaining digit pairs, or fp64 (k_syrk)
+                    R.stage(m, M_COV_GUARD);
+                    int64_t gi[3];
+                    R.hip(hipMemcpyAsync(gi, m.info + INFO_COV_GUARD, sizeof(gi), hipMemcpyDeviceToHost, R.st),
+                          "D2H guard");
+                    R.sync();
+                    r->cov_guard = (int32_t)gi[0];
+                    r->cov_guard_cols = (int32_t)gi[1];
+                    std::memcpy(&r->cov_err_bound, &gi[2], 8);
+                    if (gi[0] == COV_GUARD_PAIRS) {
+                        m.gg_smax = 2 * PCX_NDIG - 2;
+                        R.stage(m, M_COV_REST);
+                        cov_reduce();
+                    } else if (gi[0] == COV_GUARD_FP64) {
+                        R.stage(m, M_WCD_REBUILD);  // (reads cov_gg8 as it ran)
+                        m.cov_mixed = 0;
+                        m.cov_gg8 = 0;
+                        m.cov_fp_tiles = (int32_t)(jb * nb - jb * (jb - 1) / 2);
+                        m.fp_ld = E;
+                        m.fp_ks = (int32_t)w->cov_kslices;
+                        R.stage(m, M_COV);
+                        cov_reduce();
+                        r->mixed_int8 = 0;
+                    }
                 }
-                R.stage(m, M_COV_FINISH);
                 R.stage(m, M_POWER);
                 // big-five / fixed-variance components (:373-390, :429-451); a non-finite
                 // covariance makes the reference's second svd raise (Oracle: LinAlgError).  (PCA

@@ -17,10 +17,12 @@ There is no CPU fallback: without the library or a GPU, ``consensus()`` raises.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
-from . import _abi
-from .batched import MAX_EVENTS, MAX_REPORTERS, consensus_batched
+from . import _abi, _device
+from .batched import MAX_EVENTS, MAX_REPORTERS, consensus_batched, unpack_round
 
 NO, YES, BAD, NA = 1.0, 2.0, 1.5, 0.0  # __init__.py:65-68
 
@@ -212,6 +214,7 @@ class Oracle(object):
         return sc, lo, hi
 
     def consensus(self):
+        t0 = time.perf_counter()
         if self.algorithm not in _abi.ALGORITHMS:
             raise NotImplementedError("algorithm %r is not on the GPU path (supported: %s)"
                                       % (self.algorithm, ", ".join(sorted(_abi.ALGORITHMS))))
@@ -226,12 +229,16 @@ class Oracle(object):
                   algorithm=self.algorithm, device=self.device if self.devices is None else self.devices[0],
                   max_components=self.max_components, variance_threshold=self.variance_threshold)
         small = N <= MAX_REPORTERS and E <= MAX_EVENTS
+        t1 = time.perf_counter()
         if small:
             out = consensus_batched(self._data[None], None if self._rep_raw is None else self._rep_raw[None],
                                     sc, lo, hi, filled=True, original=True,
                                     aux_scores=None if aux is None else aux[None],
-                                    hierarchy_threshold=self.hierarchy_threshold, **kw)
-            g = {k: v[0].cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+                                    hierarchy_threshold=self.hierarchy_threshold, packed=True, **kw)
+            _device.synchronize(out["_packed"].device)  # (the device work apart from the copy back)
+            t2 = time.perf_counter()
+            g = unpack_round(out)
+            t3 = time.perf_counter()
             participation = float(g["participation"])
             avg_certainty = float(g["avg_certainty"])
             comps = int(g["components"])
@@ -250,13 +257,16 @@ class Oracle(object):
                                      aux_scores=aux, original_inplace=True,
                                      devices=None if self.algorithm in _abi.CLUSTER_ALGORITHMS else self.devices,
                                      **ckw, **{k: v for k, v in kw.items() if k != "device"})
+            t2 = t3 = time.perf_counter()  # (one synchronous call: copies in, stages, copies out)
             participation = float(meta["participation"])
             avg_certainty = float(meta["avg_certainty"])
             comps = int(meta["components"])
             self.last_info = {"branch": meta["branch"], "flags": meta["flags"], "pi_iters": meta["pi_iters"],
                               "n_hard": meta["n_hard"], "sel_passes": meta["sel_passes"], "path": "matrix",
                               "devices": self.devices or [self._device_index()], "comm_bytes": meta["comm_bytes"],
-                              "grid_events": meta["grid_events"], "mixed_int8": meta["mixed_int8"]}
+                              "grid_events": meta["grid_events"], "mixed_int8": meta["mixed_int8"],
+                              "cov_guard": meta["cov_guard"], "cov_guard_cols": meta["cov_guard_cols"],
+                              "cov_err_bound": meta["cov_err_bound"]}
         if self.algorithm in ("big-five", "fixed-variance") and self.last_info["flags"] & _abi.FLAG_SVD_FAIL:
             # the reference's second svd (:375, :431) is outside the try of :329-333
             raise np.linalg.LinAlgError("SVD did not converge (non-finite covariance)")
@@ -266,6 +276,12 @@ class Oracle(object):
         if self.algorithm == "clusterfeck":  # cluster() rewrites zero tokens in the caller's list (:202-204)
             self.reptokens = [0.00001 if t == 0 else t for t in self.reptokens]
         res = self._result(g, participation, avg_certainty)
+        t4 = time.perf_counter()
+        # per-call host timing (bench.py's c1 / c2 entries): argument preparation, the GPU call
+        # (batched: inputs to the device, launch, kernel; matrix: the whole synchronous libpcx call),
+        # the copy back (batched), and the result dict
+        self.last_info["timing_ms"] = {"prepare": 1e3 * (t1 - t0), "gpu_call": 1e3 * (t2 - t1),
+                                       "d2h": 1e3 * (t3 - t2), "assemble": 1e3 * (t4 - t3)}
         if self.verbose:
             self._print_verbose(res)
         return res

@@ -313,7 +313,8 @@ def _meta(res, algorithm):
             "branch": int(res.branch), "pi_iters": int(res.pi_iters), "flags": int(res.flags),
             "components": int(res.components), "n_hard": int(res.n_hard), "sel_passes": int(res.sel_passes),
             "comm_bytes": float(res.comm_bytes), "grid_events": int(res.grid_events),
-            "mixed_int8": int(res.mixed_int8)}
+            "mixed_int8": int(res.mixed_int8), "cov_guard": int(res.cov_guard),
+            "cov_guard_cols": int(res.cov_guard_cols), "cov_err_bound": float(res.cov_err_bound)}
 
 
 # ---------------------------------------------------------------- host-memory entry points

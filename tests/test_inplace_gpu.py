@@ -99,3 +99,29 @@ def test_dropin_rescales_caller_array(gpu_lib):
     cols = np.nonzero(sc)[0]
     assert not np.array_equal(R[:, cols][~np.isnan(raw[:, cols])], raw[:, cols][~np.isnan(raw[:, cols])])
     _same(R[:, ~sc.astype(bool)], raw[:, ~sc.astype(bool)], "binary columns untouched")
+
+
+def test_inplace_without_filled(gpu_lib):
+    """`original` aliased and `filled` NULL: the interpolate entry and a consensus without wpca
+    (no k_wcd pass: M_ZERO_LOADING) must still rescale the scaled columns in place (k_matrices
+    runs for the in-place rescale alone)."""
+    from pyconsensus_amd import _abi, synthetic
+    from pyconsensus_amd.pipeline import _host_call, consensus_host, interpolate_host
+
+    R, sc, lo, hi, rep = synthetic.matrix(5000, 120, seed=52)
+    iref, _ = interpolate_host(R.copy(), rep, sc, lo, hi)
+    X = R.copy()
+    got, _ = _host_call("pcx_interpolate_f64", X, rep, sc, lo, hi, 0, {"original": X.shape}, original_inplace=True)
+    assert got["original"] is X
+    _same(X, iref["original"], "interpolate in place, no filled")
+    n, E = R.shape
+    shapes = {k: (n,) for k in _abi.MAT_OUTPUT_AGENTS}
+    shapes.update({k: (E,) for k in _abi.MAT_OUTPUT_EVENTS})
+    cref, _ = consensus_host(R.copy(), rep, sc, lo, hi, algorithm="absolute")
+    X = R.copy()
+    shapes["original"] = X.shape
+    got, _ = _host_call("pcx_consensus_f64", X, rep, sc, lo, hi, 0, shapes, algorithm="absolute", original_inplace=True)
+    _same(X, cref["original"], "absolute consensus in place, no filled")
+    for k in cref:
+        if k not in ("original", "filled"):
+            _same(got[k], cref[k], k)
