@@ -261,6 +261,8 @@ struct GemmX {
     int smax, kslices;
     int smin;  // the pairs smin <= i + j <= smax (0: from the first; the covariance guard's second launch
                // takes the rest, PCX_NDIG .. 2 PCX_NDIG - 2, pcx_matrix.hip k_cov_guard)
+    int sym;   // A == B (one digit string, every token 2^k): on a diagonal tile (a == b) the pair (i, j)
+               // with i > j is the transpose of (j, i) -- those items exit at once, the reader transposes
 };
 // digit j range of digit i among the pairs smin <= i + j <= smax (empty: j1 < j0)
 __host__ __device__ inline int gemm_i8x_j0(int i, int smin) { return smin - i > 0 ? smin - i : 0; }
@@ -315,6 +317,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) k_gemm_i8x(GemmX g) {
     while (ta * (ta + 1) / 2 > tl) ta--;
     while ((ta + 1) * (ta + 2) / 2 <= tl) ta++;
     const int tb = tl - ta * (ta + 1) / 2;
+    if (g.sym && ta == tb && i > j) return;  // (the workgroup as a whole, before any barrier)
     const int64_t nst = g.rg / (4 * KS);
     const int64_t per = (nst + g.kslices - 1) / g.kslices;
     const int64_t s0 = ks * per < nst ? ks * per : nst;

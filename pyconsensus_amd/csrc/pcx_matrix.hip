@@ -1611,7 +1611,8 @@ __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
     const int SMAX = m.gg_smax;  // PCX_NDIG - 1, or 2 PCX_NDIG - 2 once the guard asked for every pair
     const int nt = (m.cov_jb * CT + GT - 1) / GT;
     const int ta = (int)(p / GT), tb = (int)(q / GT), tl = ta * (ta + 1) / 2 + tb;
-    const int64_t within = (p % GT) * GT + (q % GT);
+    const int64_t within = (p % GT) * GT + (q % GT), within_t = (q % GT) * GT + (p % GT);
+    const bool sym = m.zE == m.zD;
     const int64_t kstride = gemm_i8x_slab(1, 0, 0, 0, nt) * (GT * GT);  // one k-slice's slabs
     dd a{0.0, 0.0};
     for (int sd = SMAX; sd >= 0; sd--) {
@@ -1619,7 +1620,11 @@ __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
         for (int i = 0; i <= sd && i < PCX_NDIG; i++) {
             const int j = sd - i;
             if (j >= PCX_NDIG) continue;  // (i + j = sd: every pair of this weight)
-            t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
+            // (one digit string: a diagonal tile's pair i > j is (j, i) transposed, never computed)
+            if (sym && ta == tb && i > j)
+                t += slab_sum(m.Pgx + gemm_i8x_slab(0, j, i, tl, nt) * (GT * GT) + within_t, kstride, m.ks_gx);
+            else
+                t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
         }
         a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)t, 0.0});
     }
@@ -1978,6 +1983,35 @@ __global__ void __launch_bounds__(BT) k_pi_gemv(pcx_mat m, const double* M, int 
     double acc = 0.0;
     for (int q = lane; q < E; q += WAVE) acc = fma(Cr[q], x[q], acc);
     acc = wave_sum_d(acc);
+    if (lane == 0) pv_y(m)[row] = acc;
+}
+
+// The same for E > 1024 (the early-exit path, no golden pinned to its sum order) with E even:
+// 16-byte loads, four independent chains per lane (the row loop had one dependent fma chain per
+// lane: ~2.7 TB/s over the 134 MB of a 4096-event C)
+__global__ void __launch_bounds__(BT) k_pi_gemv4(pcx_mat m, const double* M, int honor_done) {
+    const int E = (int)m.n_events;
+    const int row = blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE;
+    if (row >= E || (honor_done && pv_s(m)[1] != 0.0) || pi_mode_of(m.info[IN_FLAGS]) != 0) return;
+    const double2* Cr = reinterpret_cast<const double2*>(M + (int64_t)row * E);
+    const double2* x = reinterpret_cast<const double2*>(pv_x(m));
+    const int h = E / 2;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int q = lane;
+    for (; q + 3 * WAVE < h; q += 4 * WAVE) {
+        const double2 c0 = Cr[q], c1 = Cr[q + WAVE], c2 = Cr[q + 2 * WAVE], c3 = Cr[q + 3 * WAVE];
+        const double2 x0 = x[q], x1 = x[q + WAVE], x2 = x[q + 2 * WAVE], x3 = x[q + 3 * WAVE];
+        a0 = fma(c0.y, x0.y, fma(c0.x, x0.x, a0));
+        a1 = fma(c1.y, x1.y, fma(c1.x, x1.x, a1));
+        a2 = fma(c2.y, x2.y, fma(c2.x, x2.x, a2));
+        a3 = fma(c3.y, x3.y, fma(c3.x, x3.x, a3));
+    }
+    for (; q < h; q += WAVE) {
+        const double2 c0 = Cr[q], x0 = x[q];
+        a0 = fma(c0.y, x0.y, fma(c0.x, x0.x, a0));
+    }
+    const double acc = wave_sum_d((a0 + a1) + (a2 + a3));
     if (lane == 0) pv_y(m)[row] = acc;
 }
 
@@ -5558,7 +5592,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_I8X_LDS);
                 });
                 if (x_err != hipSuccess) return x_err;
-                GemmX g{m.zD, m.zE, zd_ld(gb), zd_ld(gb), m.Pgx, rg, gb, (gb + GT - 1) / GT, PCX_NDIG - 1, m.ks_gx};
+                GemmX g{m.zD, m.zE, zd_ld(gb), zd_ld(gb), m.Pgx, rg, gb, (gb + GT - 1) / GT, PCX_NDIG - 1, m.ks_gx, 0,
+                        (int)(m.zE == m.zD)};
                 hipLaunchKernelGGL((k_gemm_i8x<GEMM_I8X_WAVES, GEMM_I8X_NBUF>), dim3((unsigned)gemm_i8x_items(g)),
                                    dim3(GEMM_I8X_WAVES * 64), GEMM_I8X_LDS, st, g);
             }
@@ -5626,7 +5661,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             const int gb = m.cov_jb * CT;
             const int64_t rg = m.wcd_rows / 16;
             GemmX g{m.zD, m.zE, zd_ld(gb), zd_ld(gb), m.Pgx, rg, gb, (gb + GT - 1) / GT, 2 * PCX_NDIG - 2, m.ks_gx,
-                    PCX_NDIG};
+                    PCX_NDIG, (int)(m.zE == m.zD)};
             hipLaunchKernelGGL((k_gemm_i8x<GEMM_I8X_WAVES, GEMM_I8X_NBUF>), dim3((unsigned)gemm_i8x_items(g)),
                                dim3(GEMM_I8X_WAVES * 64), GEMM_I8X_LDS, st, g);
             break;
@@ -5823,7 +5858,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 double ps[3] = {1.0, 0.0, 0.0};  // delta, converged, steps (pv_s)
                 while (iters < maxit) {
                     for (int k = 0; k < poll; k++) {
-                        hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m, M, (int)early);
+                        if (early && E % 2 == 0)
+                            hipLaunchKernelGGL(k_pi_gemv4, dim3(gb), dim3(BT), 0, st, m, M, 1);
+                        else
+                            hipLaunchKernelGGL(k_pi_gemv, dim3(gb), dim3(BT), 0, st, m, M, (int)early);
                         hipLaunchKernelGGL(k_pi_norm, dim3(1), dim3(1024), 0, st, m, (int)early);
                     }
                     e = hipMemcpyAsync(ps, m.pvec + 3 * (E + 64), sizeof(ps), hipMemcpyDeviceToHost, st);
