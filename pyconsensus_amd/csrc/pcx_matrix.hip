@@ -1595,8 +1595,22 @@ __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t 
     const int64_t gb = (int64_t)m.cov_jb * CT, ldm = PCX_NDIG * gb;
     const int32_t* P = m.Pmx + row * ldm + q;
     const int64_t slab = m.zq * ldm;
-    dd a{(double)slab_sum(P + (PCX_NDIG - 1) * gb, slab, m.ks_mx), 0.0};
-    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
+    // k-slices outermost: the NDIG digits' loads of one slice are independent (NDIG in flight;
+    // digit-major with the slices inner waited on each digit's chain)
+    int64_t t[PCX_NDIG];
+#pragma unroll
+    for (int d = 0; d < PCX_NDIG; d++) t[d] = 0;
+    for (int k = 0; k < m.ks_mx; k++) {
+        const int32_t* Pk = P + (int64_t)k * slab;
+        int32_t v[PCX_NDIG];
+#pragma unroll
+        for (int d = 0; d < PCX_NDIG; d++) v[d] = Pk[d * gb];
+#pragma unroll
+        for (int d = 0; d < PCX_NDIG; d++) t[d] += v[d];
+    }
+    dd a{(double)t[PCX_NDIG - 1], 0.0};
+#pragma unroll
+    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)t[d], 0.0});
     return dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q])));  // 2^e
 }
 
@@ -1614,19 +1628,31 @@ __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
     const int64_t within = (p % GT) * GT + (q % GT), within_t = (q % GT) * GT + (p % GT);
     const bool sym = m.zE == m.zD;
     const int64_t kstride = gemm_i8x_slab(1, 0, 0, 0, nt) * (GT * GT);  // one k-slice's slabs
+    // the pairs of each weight i + j = s summed exactly over the pairs and the k-slices (k-slices
+    // outermost: every pair's load of one slice in flight at once)
+    constexpr int SM = 2 * PCX_NDIG - 2;
+    int64_t ts[SM + 1];
+#pragma unroll
+    for (int sd = 0; sd <= SM; sd++) ts[sd] = 0;
+    const bool tr = sym && ta == tb;  // (one digit string: a diagonal tile's pair i > j is (j, i)
+                                      // transposed, never computed)
+    for (int k = 0; k < m.ks_gx; k++) {
+        const int32_t* Pk = m.Pgx + (int64_t)k * kstride;
+#pragma unroll
+        for (int i = 0; i < PCX_NDIG; i++)
+#pragma unroll
+            for (int j = 0; j < PCX_NDIG; j++) {
+                if (i + j > SMAX) continue;
+                const int32_t v = (tr && i > j) ? Pk[gemm_i8x_slab(0, j, i, tl, nt) * (GT * GT) + within_t]
+                                                : Pk[gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within];
+                ts[i + j] += v;
+            }
+    }
     dd a{0.0, 0.0};
-    for (int sd = SMAX; sd >= 0; sd--) {
-        int64_t t = 0;
-        for (int i = 0; i <= sd && i < PCX_NDIG; i++) {
-            const int j = sd - i;
-            if (j >= PCX_NDIG) continue;  // (i + j = sd: every pair of this weight)
-            // (one digit string: a diagonal tile's pair i > j is (j, i) transposed, never computed)
-            if (sym && ta == tb && i > j)
-                t += slab_sum(m.Pgx + gemm_i8x_slab(0, j, i, tl, nt) * (GT * GT) + within_t, kstride, m.ks_gx);
-            else
-                t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
-        }
-        a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)t, 0.0});
+#pragma unroll
+    for (int sd = SM; sd >= 0; sd--) {
+        if (sd > SMAX) continue;
+        a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)ts[sd], 0.0});
     }
     a = dd_div_base(dd_div_base(a));  // the (s + 2): 254^-2 more
     // 2^(e_p + f_q) applied to the rounded value: the product of the two scales alone can overflow
@@ -1667,6 +1693,7 @@ __device__ __forceinline__ double cov_entry(const pcx_mat& m, const double* S, i
     }
     if (q >= gb) {  // grid x grid: P from the int8 products
         const double P = (double)slab_sum(m.Pgg + (p - gb) * m.zq + (q - gb), m.zq * m.zq, m.ks_gg);
+        // (T, mu, Z: per-position loads beside the slab chain)
         const double T = dd_to_double(ld_dd(m.scal + ((int64_t)m.rank * SS + SC_TOK) * 2));
         const double ap = 1.0 - m.ev[EV_MU * E + cp], aq = 1.0 - m.ev[EV_MU * E + cq];
         const double Zp = 0.5 * (double)m.zsum[cp], Zq = 0.5 * (double)m.zsum[cq];
@@ -2399,6 +2426,8 @@ __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
 struct SubW {
     double w[4];
 };
+// row groups whose subset tables a grid block of the compact passes builds at once (two per wave)
+constexpr int SG_NG = 8;
 __device__ __forceinline__ SubW subset_load(const double* wg) {
     const int j = (threadIdx.x & (WAVE - 1)) >> 4;
     return SubW{{wg[j], wg[j + 4], wg[j + 8], wg[j + 12]}};
@@ -2447,47 +2476,46 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
         S1 = chunk_sum_dd(n1, r0, r1);
         S2 = chunk_sum_dd(n2, r0, r1);
     }
-    // (a grid wave keeps every lane until its subset tables are built: one entry per lane)
-    if (GRID ? (q & ~(WAVE - 1)) >= E : (q >= E || q >= gb)) return;
+    // (every wave of a grid block stays to the end: the block builds the subset tables together)
+    if (!GRID && (q >= E || q >= gb)) return;
     const bool live = q < E;
     const int c = live ? m.cov_perm[q] : -1;
     if (!GRID && c < 0) return;  // (padding)
     acc2 a1, a2;
     if constexpr (GRID) {
-        __shared__ dd tabs[BT / WAVE][2][WAVE];  // per wave: the subset tables of n1 and n2
-        dd* t1 = tabs[threadIdx.x / WAVE][0];
-        dd* t2 = tabs[threadIdx.x / WAVE][1];
+        // the subset tables of n1 and n2 for SG_NG row groups at a time, built by the block's four
+        // waves together (the tables depend on the rows only: every wave used to build the same ones,
+        // one group at a time, each behind a wave barrier), read by every wave after one block barrier
+        __shared__ dd tabs[SG_NG][2][WAVE];
+        const int wv = threadIdx.x / WAVE;
         const uint32_t* zb = zb_packed(m) + (live ? q - gb : 0);
-        // whole 16-row groups (the next group's code word in flight during this group's adds),
-        // then the ragged tail
+        // whole 16-row groups, then the ragged tail
         const int64_t g0 = r0 / 16, gf = r1 / 16;
         uint32_t Pn = g0 < gf ? zb[g0 * m.zq] : 0u;
         if (__builtin_isfinite(S1.hi) && __builtin_isfinite(S2.hi)) {
             // subset tables (as k_outcomes_c): sum v z = sum over code bytes j of T1 + 2 T2, the
             // subset sums of the rows whose code is 1 / 2, compensated (a non-finite weight: the
             // per-row loop, whose NaN x 0 the result keeps)
-            constexpr int GB = 4;  // four groups' loads at once, one accumulator per code byte (as k_outcomes_c)
             acc2 a1j[4], a2j[4];
-            for (int64_t g = g0; g < gf; g += GB) {
-                uint32_t Pg[GB];
-                SubW wa[GB], wb[GB];
+            for (int64_t g = g0; g < gf; g += SG_NG) {  // (block-uniform)
+                uint32_t Pg[SG_NG];
 #pragma unroll
-                for (int k = 0; k < GB; k++) {
-                    const int64_t gk = g + k < gf ? g + k : gf - 1;
-                    Pg[k] = zb[gk * m.zq];
-                    wa[k] = subset_load(n1 + gk * 16);
-                    wb[k] = subset_load(n2 + gk * 16);
+                for (int k = 0; k < SG_NG; k++) Pg[k] = zb[(g + k < gf ? g + k : gf - 1) * m.zq];
+#pragma unroll
+                for (int t = 0; t < SG_NG / (BT / WAVE); t++) {
+                    const int kk = wv * (SG_NG / (BT / WAVE)) + t;
+                    if (g + kk < gf) {
+                        subset_table(subset_load(n1 + (g + kk) * 16), tabs[kk][0]);
+                        subset_table(subset_load(n2 + (g + kk) * 16), tabs[kk][1]);
+                    }
                 }
+                __syncthreads();
 #pragma unroll
-                for (int k = 0; k < GB; k++) {
-                    if (g + k >= gf) break;  // (wave-uniform)
+                for (int k = 0; k < SG_NG; k++) {
+                    if (g + k >= gf) break;  // (block-uniform)
                     const uint32_t P = Pg[k];
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                    subset_table(wa[k], t1);
-                    subset_table(wb[k], t2);
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
+                    const dd* t1 = tabs[k][0];
+                    const dd* t2 = tabs[k][1];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const uint32_t by = (P >> (8 * j)) & 0xFFu, lo = by & 0x55u, hi = (by >> 1) & 0x55u;
@@ -2503,6 +2531,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
                         a2j[j].c += 2.0 * v2.lo;
                     }
                 }
+                __syncthreads();  // (the next batch's tables overwrite these)
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -3054,6 +3083,106 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     st_dd(pp + 14, {n2, 0.0});
 }
 
+// A block of grid positions only (the general tiles end at a multiple of 128, so at most one block
+// per row chunk mixes the two): outcomes_c_body<true>'s finite-weight path with the subset tables of
+// SG_NG row groups at a time built by the block's four waves together -- the tables depend on the
+// rows only, and every wave used to build the same ones a group at a time, each behind a wave
+// barrier.  The same reads and adds in the same order: bit-identical.
+__device__ void outcomes_grid_block(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S, bool live) {
+    __shared__ dd tabs[SG_NG][WAVE];
+    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
+    const int E = (int)m.n_events;
+    const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
+    const int wv = threadIdx.x / WAVE;
+    const int c = live ? m.cov_perm[q] : -1;
+    const int64_t qn = live ? q : gb;
+    const uint32_t* zb = zb_packed(m) + (qn - gb);
+    acc2 zs;
+    uint32_t c15 = 0, c2 = 0;
+    double pc = 0, b1 = 0, b15 = 0, b2 = 0;
+    const int64_t g0 = r0 / 16, gf = r1 / 16;
+    acc2 zj[4];
+    double b1j[4] = {0, 0, 0, 0}, b15j[4] = {0, 0, 0, 0}, b2j[4] = {0, 0, 0, 0}, pcj[4] = {0, 0, 0, 0};
+    for (int64_t g = g0; g < gf; g += SG_NG) {  // (block-uniform)
+        uint32_t Pg[SG_NG], Mg[SG_NG];
+#pragma unroll
+        for (int k = 0; k < SG_NG; k++) {
+            const int64_t gk = g + k < gf ? g + k : gf - 1;
+            Pg[k] = zb[gk * m.zq];
+            Mg[k] = m.nam[gk * ld + qn];
+        }
+#pragma unroll
+        for (int t = 0; t < SG_NG / (BT / WAVE); t++) {
+            const int kk = wv * (SG_NG / (BT / WAVE)) + t;
+            if (g + kk < gf) subset_table(subset_load(sm + (g + kk) * 16), tabs[kk]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SG_NG; k++) {
+            if (g + k >= gf) break;  // (block-uniform)
+            const uint32_t P = Pg[k], M = Mg[k];
+            const dd* tab = tabs[k];
+            c15 += __popc(P & 0x55555555u);
+            c2 += __popc(P & 0xAAAAAAAAu);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t by = (P >> (8 * j)) & 0xFFu, lo = by & 0x55u, hi = (by >> 1) & 0x55u;
+                const dd T0 = tab[16 * j + sub4_even(0x55u & ~(lo | hi))];
+                const dd T1 = tab[16 * j + sub4_even(lo & ~hi)];
+                const dd T2 = tab[16 * j + sub4_even(hi & ~lo)];
+                const dd TM = tab[16 * j + sub4_stride4(M, j)];
+                zj[j].add(T1.hi);
+                zj[j].c += T1.lo;
+                zj[j].add(2.0 * T2.hi);
+                zj[j].c += 2.0 * T2.lo;
+                b1j[j] += T0.hi;
+                b15j[j] += T1.hi;
+                b2j[j] += T2.hi;
+                pcj[j] += TM.hi;
+            }
+        }
+        __syncthreads();  // (the next batch's tables overwrite these)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const dd z = zj[j].get();
+        zs.add(z.hi);
+        zs.c += z.lo;
+    }
+    b1 = (b1j[0] + b1j[1]) + (b1j[2] + b1j[3]);
+    b15 = (b15j[0] + b15j[1]) + (b15j[2] + b15j[3]);
+    b2 = (b2j[0] + b2j[1]) + (b2j[2] + b2j[3]);
+    pc = (pcj[0] + pcj[1]) + (pcj[2] + pcj[3]);
+    if (!live) return;
+    if (r0 < r1 && gf * 16 < r1) {  // the ragged tail, row by row (as outcomes_c_body)
+        const uint32_t P = zb[gf * m.zq], M = m.nam[gf * ld + q];
+        for (int64_t i = gf * 16; i < r1; i++) {
+            const int r = (int)(i - gf * 16);
+            const uint32_t z = zpack_get(P, r);
+            const double w = sm[i];
+            c15 += z == 1u;
+            c2 += z == 2u;
+            zs.add(w * (double)z);
+            pc += w * (((M >> r) & 1u) ? 1.0 : 0.0);
+            b1 += z == 0u ? w : 0.0;
+            b15 += z == 1u ? w : 0.0;
+            b2 += z == 2u ? w : 0.0;
+        }
+    }
+    const dd Z = zs.get();
+    const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
+    const double n15 = (double)c15, n2 = (double)c2, n1 = rows - n15 - n2;
+    double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+    st_dd(pp + 0, dd_add(S, dd{0.5 * Z.hi, 0.5 * Z.lo}));
+    st_dd(pp + 2, {pc, 0.0});
+    st_dd(pp + 4, {b1, 0.0});
+    st_dd(pp + 6, {b15, 0.0});
+    st_dd(pp + 8, {b2, 0.0});
+    st_dd(pp + 10, {n1, 0.0});
+    st_dd(pp + 12, {n15, 0.0});
+    st_dd(pp + 14, {n2, 0.0});
+}
+
 // one launch over every position (unlike k_gemv2_c: here the general positions of a scaled event
 // read only their missing bits, and the two ranges' blocks fill the chip together)
 __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
@@ -3066,6 +3195,10 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     __shared__ dd tabs[BT / WAVE][WAVE];  // the grid waves' subset tables
     dd S{0.0, 0.0};
     if ((q | (WAVE - 1)) >= gb) S = chunk_sum_dd(m.rowv + RV_SMOOTH * m.n_rows, r0, r1);
+    if ((int64_t)blockIdx.x * BT >= gb && __builtin_isfinite(S.hi)) {  // (block-uniform)
+        outcomes_grid_block(m, q, r0, r1, S, q < m.n_events);
+        return;
+    }
     if ((q & ~(WAVE - 1)) >= m.n_events) return;  // (wave-uniform: a grid wave runs all its lanes)
     if (q >= gb)  // (gb is a multiple of 128: a wave is all grid or all general)
         outcomes_c_body<true>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events);
