@@ -179,6 +179,7 @@ int pcx_release_workspace(pcx_ctx* ctx) {
     pcx::rounds_free(ctx);
     (void)hipSetDevice(ctx->device);
     pcx::workspace_free(ctx);
+    pcx::io_bufs_free(ctx);
     return PCX_OK;
 }
 
@@ -197,6 +198,12 @@ void ctx_host_free(pcx_ctx* c) {
         if (ev) (void)hipEventDestroy(ev);
         ev = nullptr;
     }
+    io_bufs_free(c);
+}
+void io_bufs_free(pcx_ctx* c) {
+    for (auto& b : c->io_bufs)
+        if (b.first) (void)hipFree(b.first);
+    c->io_bufs.clear();
 }
 }  // namespace pcx
 extern "C" {

@@ -355,6 +355,9 @@ struct pcx_ctx {
     // the selection passes' info words, read one pass late (pinned, two slots; pcx_runner.cpp select)
     int64_t* sel_pin = nullptr;
     hipEvent_t sel_ev[2] = {nullptr, nullptr};
+    // the host-memory path's large device copies (the reports, the matrix outputs), kept between
+    // calls (a hipMalloc / hipFree of 33 GB per call is not free); pcx_release_workspace frees them
+    std::vector<std::pair<void*, size_t>> io_bufs;
 };
 
 namespace pcx {
@@ -372,4 +375,5 @@ void rounds_free(pcx_ctx* c);
 // a context's host-side resources (pinned staging slots, the selection's pinned info words and
 // events, the workgroup-per-round scratch): pcx_destroy and rounds_free (the pool's worker contexts)
 void ctx_host_free(pcx_ctx* c);
+void io_bufs_free(pcx_ctx* c);  // the host path's cached device copies (pcx_ctx.io_bufs)
 }  // namespace pcx

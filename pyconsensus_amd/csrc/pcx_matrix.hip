@@ -1011,7 +1011,9 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                             nz += x == 0.0 ? 1 : 0;
                             const double f = missing(x) ? p[k].guess : x;
                             w[k] = f - p[k].mu;
-                            xo[k] = x;
+                            // (a NaN report keeps its own bits in `original`, as numpy's (r - lo) /
+                            // range does: div_rn's fma(-q0, ..) would return it negated)
+                            xo[k] = __builtin_isnan(x) ? rv[u][k] : x;
                             fo[k] = f;
                             if (m.compact) nb[k] |= missing(x) ? 1u << (4 * h + u) : 0u;
                             if (zc[k]) {
@@ -4809,8 +4811,9 @@ __global__ void __launch_bounds__(BT) k_matrices(pcx_mat m) {
         r0, r1, [&](int64_t i) { return m.reports[i * E + c]; },
         [&](int64_t i, double v) {
             const double x = rescale(v, p, m.int_dtype);
-            if (m.original) m.original[i * E + c] = x;
-            if (m.orig_inplace && p.scaled) const_cast<double*>(m.reports)[i * E + c] = x;
+            const double xo = __builtin_isnan(x) ? v : x;  // (a NaN keeps its own bits, as in k_wcd)
+            if (m.original) m.original[i * E + c] = xo;
+            if (m.orig_inplace && p.scaled) const_cast<double*>(m.reports)[i * E + c] = xo;
             if (m.filled) m.filled[i * E + c] = missing(x) ? p.guess : x;
         });
 }

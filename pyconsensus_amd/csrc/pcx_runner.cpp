@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <thread>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -327,26 +328,44 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
 }
 
 // ------------------------------------------------------------------ host <-> device staging
+// Buffers of at least IO_CACHE_MIN bytes (the reports, `original`, `filled`) come from the context's
+// io_bufs, grown on demand and kept between calls, in call order; smaller ones are allocated per call.
+constexpr size_t IO_CACHE_MIN = (size_t)64 << 20;
 struct Io {
+    pcx_ctx* c;
     std::vector<void*> owned;
+    size_t next = 0;  // the next io_bufs slot
+    explicit Io(pcx_ctx* ctx) : c(ctx) {}
     ~Io() {
         for (void* p : owned) (void)hipFree(p);
+    }
+    void* get(Run& R, size_t bytes, const char* what) {
+        void* p = nullptr;
+        if (bytes >= IO_CACHE_MIN) {
+            if (next == c->io_bufs.size()) c->io_bufs.push_back({nullptr, 0});
+            auto& b = c->io_bufs[next++];
+            if (b.second < bytes) {
+                if (b.first) (void)hipFree(b.first);
+                b = {nullptr, 0};
+                R.hip(hipMalloc(&b.first, bytes), what);
+                b.second = bytes;
+            }
+            return b.first;
+        }
+        R.hip(hipMalloc(&p, bytes), what);
+        owned.push_back(p);
+        return p;
     }
     template <class T>
     T* dev(Run& R, const T* host, int64_t n) {  // device copy of a host input (NULL stays NULL)
         if (!host || n <= 0) return nullptr;
-        void* p = nullptr;
-        R.hip(hipMalloc(&p, n * sizeof(T)), "hipMalloc(input)");
-        owned.push_back(p);
+        void* p = get(R, n * sizeof(T), "hipMalloc(input)");
         R.hip(hipMemcpyAsync(p, host, n * sizeof(T), hipMemcpyHostToDevice, R.st), "H2D");
         return (T*)p;
     }
     double* out(Run& R, double* host, int64_t n) {  // device buffer for a host output
         if (!host || n <= 0) return nullptr;
-        void* p = nullptr;
-        R.hip(hipMalloc(&p, n * 8), "hipMalloc(output)");
-        owned.push_back(p);
-        return (double*)p;
+        return (double*)get(R, n * 8, "hipMalloc(output)");
     }
 };
 
@@ -406,6 +425,50 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
         });
     if (rc) R.hip(hipErrorUnknown, "staged D2H of an output");
 }
+
+// result["original"] in place for host memory: the scaled columns of the caller's array rescaled
+// by host threads, (r - lo) / (hi - lo) as IEEE division (the device's div_rn is that division bit
+// for bit, tests/test_fastdiv.py), truncated for an integer dtype (Q3); NaN cells are left as they
+// are (the device's arithmetic returns the same NaN).  Rows split over host_threads() threads.
+struct HostRescale {
+    std::vector<std::thread> th;
+    void start(double* a, int64_t n_rows, int64_t E, const std::vector<int32_t>& cols, const double* lo,
+               const double* hi, bool int_dtype) {
+        const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n_rows / 1024));
+        auto cl = std::make_shared<std::vector<int32_t>>(cols);
+        auto lr = std::make_shared<std::vector<double>>();
+        for (int32_t c : cols) {
+            lr->push_back(lo[c]);
+            lr->push_back(hi[c] - lo[c]);
+        }
+        const bool inline_ = n_rows * (int64_t)cols.size() < (int64_t)1 << 20;  // small: no threads
+        for (int t = 0; t < (inline_ ? 1 : T); t++) {
+            const int64_t r0 = inline_ ? 0 : n_rows * t / T, r1 = inline_ ? n_rows : n_rows * (t + 1) / T;
+            auto body = [=] {
+                const size_t nc = cl->size();
+                for (int64_t i = r0; i < r1; i++) {
+                    double* row = a + i * E;
+                    for (size_t k = 0; k < nc; k++) {
+                        const double v = row[(*cl)[k]];
+                        if (std::isnan(v)) continue;
+                        double x = (v - (*lr)[2 * k]) / (*lr)[2 * k + 1];
+                        if (int_dtype) x = std::trunc(x);
+                        row[(*cl)[k]] = x;
+                    }
+                }
+            };
+            if (inline_)
+                body();
+            else
+                th.emplace_back(body);
+        }
+    }
+    void join() {
+        for (auto& t : th) t.join();
+        th.clear();
+    }
+    ~HostRescale() { join(); }
+};
 
 int64_t pow2_at_least(int64_t n) {
     int64_t p = 2;
@@ -793,8 +856,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
     c->progress_wait.store(0, std::memory_order_relaxed);
     const bool host = p->mem_kind == PCX_MEM_HOST;
     const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
+    HostRescale host_rescale;  // (joined on every exit path, before the caller's array is returned)
     try {
-        Io io;
+        Io io(c);
         // ---- scaled events (host view)
         std::vector<uint8_t> sc_h;
         const uint8_t* sc_in = filled_input ? nullptr : p->scaled;
@@ -872,7 +936,20 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.original = (cons || entry == 1) && !inplace ? out(r->original, n_rows * E) : nullptr;
         m.orig_inplace = inplace ? 1 : 0;
         m.rescaled = 0;
-        if (inplace && host) outs.push_back({r->original, const_cast<double*>(reports), n_rows * E});
+        // host memory, in place: the caller's array is rescaled by host threads while the device
+        // works (once the reports' H2D has drained), instead of copying the whole device copy back
+        // (33 GB of D2H at C5 for the quarter of the columns that change)
+        if (inplace && host && n_scaled > 0) {
+            hipEvent_t ev = nullptr;
+            R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            struct EvGuard {
+                hipEvent_t e;
+                ~EvGuard() { (void)hipEventDestroy(e); }
+            } evg{ev};
+            R.hip(hipEventRecord(ev, R.st), "hipEventRecord");
+            R.hip(hipEventSynchronize(ev), "hipEventSynchronize(H2D)");
+            host_rescale.start(const_cast<double*>(p->reports), n_rows, E, scols, p->lo, p->hi, p->int_dtype != 0);
+        }
         m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
         m.weighted_mean = entry == 2 ? out(r->weighted_mean, E) : nullptr;
         m.nc_out = entry == 4 ? out(nc_out, n_rows) : nullptr;
@@ -1224,6 +1301,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             if ((size_t)o.n * 8 >= STAGE_MIN) d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
         R.mark(-1);
         R.sync();
+        host_rescale.join();
         r->participation = sc2[0];
         r->avg_certainty = sc2[1];
         const bool branchless = (alg == PCX_ALG_ABSOLUTE && entry != 4) || clustering || entry == 1 || entry == 2;
