@@ -324,6 +324,43 @@ def bench_c4(dev, steps=3, oracle=True):
     return out
 
 
+def bench_cov_fp64(dev, N=1_000_000, E=1024, steps=2):
+    """The covariance on fp64 MFMA (k_syrk), measured where it runs: a 1M x 1024 consensus whose
+    every event is scaled (no grid events, so no int8 block: the general x general pairs are all of
+    C, __init__.py:326).  Inputs generated in HBM (the C5 recipe's scaled columns: clip N(0.6, 0.15)
+    of [lo, hi], 10% NA, reputation=None); M_COV is k_syrk alone.  2 N E (E + 1) / 2 flop."""
+    import torch
+
+    from pyconsensus_amd.pipeline import consensus_matrix
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    lo = torch.rand(E, generator=g, device=dev, dtype=torch.float64) * -100.0
+    hi = lo + 1.0 + 199.0 * torch.rand(E, generator=g, device=dev, dtype=torch.float64)
+    z = (0.6 + 0.15 * torch.randn((N, E), generator=g, device=dev, dtype=torch.float64)).clamp_(0.001, 1.0)
+    R = lo + (hi - lo) * z
+    del z
+    R[torch.rand((N, E), generator=g, device=dev) < 0.1] = float("nan")
+    sc = torch.ones(E, dtype=torch.uint8, device=dev)
+    consensus_matrix(R, None, sc, lo, hi, device=dev, matrices=False)
+    ms = []
+    meta = None
+    for _ in range(steps):
+        p1 = {}
+        _, _, meta = consensus_matrix(R, None, sc, lo, hi, device=dev, matrices=False, profile=p1)
+        ms.append(p1.get("M_COV", float("nan")))
+    del R
+    torch.cuda.empty_cache()
+    cov_ms = sorted(ms)[len(ms) // 2]
+    flops = 2.0 * N * E * (E + 1) / 2
+    tfs = flops / (cov_ms * 1e-3) / 1e12
+    return {"kernel": "k_syrk (fp64 MFMA 16x16x4, 128 x 128 tiles, split-K)", "rows": N, "events": E,
+            "m_cov_ms": cov_ms, "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / FP64_MFMA_PEAK_TFS, "flops_per_launch": flops, "mixed_int8": meta["mixed_int8"],
+            "grid_events": meta["grid_events"],
+            "data": "synthetic on-GPU, every event scaled (no int8 block), 10% NA, reputation=None"}
+
+
 # config C1: README.rst:28-45 (the reference's own example; scaled + binary events)
 README_REPORTS = [[0.2, 0.7, 1, 1], [0.3, 0.5, 1, 1], [0.1, 0.7, 1, 1], [0.5, 0.7, 2, 1], [0.1, 0.2, 2, 2],
                   [0.1, 0.2, 2, 2]]
@@ -676,6 +713,12 @@ def main():
             medium = {"metric": "oracle rounds/sec (batched 100x50)", "error": repr(e)[:400]}
     dropin = {}
     if args.c4 and world == 1:
+        try:
+            dropin["cov_fp64"] = bench_cov_fp64(dev)
+        except Exception as e:  # noqa: BLE001
+            traceback.print_exc()
+            failed.append("cov_fp64")
+            dropin["cov_fp64"] = {"kernel": "k_syrk", "error": repr(e)[:400]}
         for which, calls in (("c1", 200), ("c2", 30)):
             try:
                 dropin[which] = bench_dropin(dev, which, calls, oracle=not args.no_cpu_baseline)

@@ -96,7 +96,6 @@ typedef struct {
     /* covariance operands (M_COV): the centred, filled matrix materialised once */
     double* wcd;                  /* [wcd_rows][wcd_ld] wcd = F - mu (:322), zero padded          */
     double* tokp;                 /* [wcd_rows + 64] tokens, zero past n_rows                       */
-    double* rtokp;                /* [wcd_rows + 64] 1 / tokens (0 for 0; k_wcd, for k_digits)       */
     int64_t wcd_rows;             /* n_rows rounded up to the 16-row stage                          */
     int64_t wcd_ld;               /* E rounded up to the 128-column tile                            */
     uint32_t* rowpart;            /* [ceil(wcd_ld/512)][wcd_rows][2] per-column-block NaN / zero row counts */
@@ -141,8 +140,8 @@ typedef struct {
     int32_t  gg_smax;             /* the digit pairs i + j <= gg_smax in Pgx (PCX_NDIG - 1; all of them,
                                      2 PCX_NDIG - 2, once the covariance guard asked for the rest)      */
     /* the int8 covariance's error bound against the entries (k_digits -> k_cov_guard): per general
-       position, [G_NSTAT][128 cov_jb] int64 sums over this rank's rows (gacc), then as doubles over
-       all ranks (gsum, exchanged with the covariance) */
+       position, [G_NSTAT][128 cov_jb] int64 sums over this rank's rows and then sum tok^2 (gacc), then
+       as doubles over all ranks (gsum, exchanged with the covariance) */
     int64_t* gacc;
     double*  gsum;
     /* algorithms other than PCA (enum pcx_algorithm) */

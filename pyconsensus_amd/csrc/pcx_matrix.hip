@@ -970,11 +970,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     }
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
-    {
-        const double t = i < m.n_rows ? m.tok[i] : 0.0;
-        m.tokp[i] = t;
-        m.rtokp[i] = t > 0.0 ? 1.0 / t : 0.0;  // (the covariance guard's sum delta^2 / tok, k_digits)
-    }
+        m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
     const int64_t per = ((m.wcd_rows + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;
     int64_t r0 = blockIdx.x * per;
     r0 = r0 < m.wcd_rows ? r0 : m.wcd_rows;
@@ -1265,12 +1261,13 @@ __device__ __forceinline__ void balanced_digits(double X, uint32_t (&d)[PCX_NDIG
 
 // The covariance guard's sums (k_cov_guard), per general position over this rank's rows, taken by
 // the digit passes beside the digits: with t = (tok w 2^-e) 254^NDIG the exact scaled value and X =
-// rint(t) its digits' value, the residue delta = X - t (|delta| <= 0.52), summed as sum delta and
-// sum delta^2 / tok over the rows with tok > 0 (and for the digits of w, eta = Xe - te: sum tok eta,
-// sum tok eta^2), plus the L1 norm of the digits 1 .. NDIG - 1.  Each thread sums its rows in fp64
+// rint(t) its digits' value, the residue delta = X - t (|delta| <= 0.52), summed as sum delta tok and
+// sum delta^2 (and for the digits of w, eta = Xe - te: sum tok eta, sum tok eta^2), plus the L1 norm
+// of the digits 1 .. NDIG - 1 and, once per rank, sum tok^2.  Each thread sums its rows in fp64
 // (error << 2^-24 for the <= 4096 rows of a chunk) and adds the fixed-point value at 2^-24 (the
 // squares rounded up) to int64 slots: exact and order-free, so the guard's decision is the same on
-// every run.
+// every run.  (A per-row 1 / tok for sum delta^2 / tok cost k_digits1 35 VGPRs: 4 -> 3 waves per
+// SIMD, 3.5 -> 4.4 ms at C5; the bound takes tok >= 1 instead, below.)
 constexpr double G_FIX = 0x1p24;
 // sum |d| over the packed digits 1 .. NDIG - 1 (two's complement bytes; as offset binary b ^ 0x80 =
 // d + 128, |d| = |(b ^ 0x80) - 128|: one v_sad_u8 per four digits)
@@ -1313,21 +1310,21 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
     int32_t l1d = 0, l1e = 0;                         // the guard's sums (guard_add)
-    double sd = 0.0, sd2 = 0.0, se = 0.0, se2 = 0.0;
+    double sd = 0.0, sd2 = 0.0, se = 0.0, se2 = 0.0, tok2 = 0.0;
     for (int64_t grp = g0; live && grp < g1; grp++) {
         uint32_t d[PCX_NDIG], e[PCX_NDIG];
 #pragma unroll
         for (int k = 0; k < PCX_NDIG; k++) d[k] = e[k] = 0;
-        double wr[4], tk[4], rt[4];
+        double wr[4], tk[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int64_t i = grp * 16 + 4 * h + u;
             wr[u] = fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q];
             tk[u] = m.tokp[i];  // 0 past n_rows
-            rt[u] = m.rtokp[i];  // 1 / tok (0 for 0)
         }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
+#pragma unroll 2
+        for (int u = 0; u < 4; u++) {  // (two rows at a time: the guard's sums beside four rows' digit
+                                       // chains took 139 VGPRs, three waves per SIMD)
             const double w = wr[u] * sc;  // exact (power of two)
             double hi = w * tk[u], lo = fma(w, tk[u], -hi);  // tok w exactly
             // X = rint((tok w 2^-e) 254^NDIG) (|X| <= 254^NDIG / 2 < 2^48, within 0.52 of the
@@ -1339,8 +1336,9 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             const double X = rint(pv + pl);
             balanced_digits(X, d, u, dsum);
             const double dl = (X - pv) - pl;  // X - t (X - pv exact)
-            sd += dl;
-            sd2 = fma(dl * dl, rt[u], sd2);
+            sd = fma(dl, tk[u], sd);
+            sd2 = fma(dl, dl, sd2);
+            tok2 = fma(tk[u], tk[u], tok2);
             if (gg) {
                 const double v = wr[u] * esc, uv = v * DIG_SCALE, ue = fma(v, DIG_SCALE, -uv);
                 const double Xe = rint(uv + ue);
@@ -1380,6 +1378,7 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
     sd2 = q4(sd2);
     se = q4(se);
     se2 = q4(se2);
+    tok2 = q4(tok2);
     if (live && h == 0 && m.gacc) {
         int64_t* ga = m.gacc + q;
         if (l1d) atomicAdd((unsigned long long*)&ga[G_L1D * gb], (unsigned long long)(int64_t)l1d);
@@ -1391,6 +1390,8 @@ __global__ void __launch_bounds__(BT) k_digits(pcx_mat m) {
             guard_add(&ga[G_SE2 * gb], se2, true);
         }
     }
+    if (live && h == 0 && q == 0 && m.gacc && tok2 > 0.0)  // sum tok^2 (exact: integers below 2^53)
+        atomicAdd((unsigned long long*)&m.gacc[G_NSTAT * gb], (unsigned long long)(int64_t)tok2);
 }
 
 // The tok w digits alone (no zE to write: no general x general product on int8, or every token 1):
@@ -1411,7 +1412,7 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
 #pragma unroll
     for (int k = 0; k < PCX_NDIG; k++) dsum[k] = 0;
     int32_t l1 = 0;  // the guard's sums (guard_add)
-    double sd = 0.0, sd2 = 0.0;
+    double sd = 0.0, sd2 = 0.0, tok2 = 0.0;
     for (int64_t grp = g0; grp < g1; grp++) {
         uint32_t d[PCX_NDIG][4];
 #pragma unroll
@@ -1420,13 +1421,14 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
         for (int r = 0; r < 16; r++) {
             const int64_t i = grp * 16 + r;
             const double w = (fg ? m.Fg[i * gb + q] - mu : m.wcd[i * m.wcd_ld + q]) * sc;  // exact (power of two)
-            const double tk = m.tokp[i], rt = m.rtokp[i];                                   // 0 past n_rows
+            const double tk = m.tokp[i];                                                    // 0 past n_rows
             double hi = w * tk, lo = fma(w, tk, -hi);  // tok w exactly
             const double pv = hi * DIG_SCALE, pe = fma(hi, DIG_SCALE, -pv), pl = fma(lo, DIG_SCALE, pe);
             double X = rint(pv + pl);
             const double dl = (X - pv) - pl;  // X - t (X - pv exact)
-            sd += dl;
-            sd2 = fma(dl * dl, rt, sd2);
+            sd = fma(dl, tk, sd);
+            sd2 = fma(dl, dl, sd2);
+            tok2 = fma(tk, tk, tok2);
 #pragma unroll
             for (int k = PCX_NDIG - 1; k >= 0; k--) {  // (k_digits: the same digits)
                 double di = X;
@@ -1452,6 +1454,8 @@ __global__ void __launch_bounds__(BT) k_digits1(pcx_mat m) {
         if (l1) atomicAdd((unsigned long long*)&ga[G_L1D * gb], (unsigned long long)(int64_t)l1);
         guard_add(&ga[G_SD * gb], sd, false);
         guard_add(&ga[G_SD2 * gb], sd2, true);
+        if (q == 0 && tok2 > 0.0)  // sum tok^2 (exact: integers below 2^53)
+            atomicAdd((unsigned long long*)&m.gacc[G_NSTAT * gb], (unsigned long long)(int64_t)tok2);
     }
 }
 
@@ -1597,22 +1601,8 @@ __device__ __forceinline__ dd mixed_comb(const pcx_mat& m, int64_t row, int64_t 
     const int64_t gb = (int64_t)m.cov_jb * CT, ldm = PCX_NDIG * gb;
     const int32_t* P = m.Pmx + row * ldm + q;
     const int64_t slab = m.zq * ldm;
-    // k-slices outermost: the NDIG digits' loads of one slice are independent (NDIG in flight;
-    // digit-major with the slices inner waited on each digit's chain)
-    int64_t t[PCX_NDIG];
-#pragma unroll
-    for (int d = 0; d < PCX_NDIG; d++) t[d] = 0;
-    for (int k = 0; k < m.ks_mx; k++) {
-        const int32_t* Pk = P + (int64_t)k * slab;
-        int32_t v[PCX_NDIG];
-#pragma unroll
-        for (int d = 0; d < PCX_NDIG; d++) v[d] = Pk[d * gb];
-#pragma unroll
-        for (int d = 0; d < PCX_NDIG; d++) t[d] += v[d];
-    }
-    dd a{(double)t[PCX_NDIG - 1], 0.0};
-#pragma unroll
-    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)t[d], 0.0});
+    dd a{(double)slab_sum(P + (PCX_NDIG - 1) * gb, slab, m.ks_mx), 0.0};
+    for (int d = PCX_NDIG - 2; d >= 0; d--) a = dd_add(dd_div_base(a), dd{(double)slab_sum(P + d * gb, slab, m.ks_mx), 0.0});
     return dd_mul_d(dd_div_base(a), ldexp(1.0, -ilogb(m.dscale[q])));  // 2^e
 }
 
@@ -1630,31 +1620,19 @@ __device__ double gg_comb(const pcx_mat& m, int64_t p, int64_t q) {
     const int64_t within = (p % GT) * GT + (q % GT), within_t = (q % GT) * GT + (p % GT);
     const bool sym = m.zE == m.zD;
     const int64_t kstride = gemm_i8x_slab(1, 0, 0, 0, nt) * (GT * GT);  // one k-slice's slabs
-    // the pairs of each weight i + j = s summed exactly over the pairs and the k-slices (k-slices
-    // outermost: every pair's load of one slice in flight at once)
-    constexpr int SM = 2 * PCX_NDIG - 2;
-    int64_t ts[SM + 1];
-#pragma unroll
-    for (int sd = 0; sd <= SM; sd++) ts[sd] = 0;
-    const bool tr = sym && ta == tb;  // (one digit string: a diagonal tile's pair i > j is (j, i)
-                                      // transposed, never computed)
-    for (int k = 0; k < m.ks_gx; k++) {
-        const int32_t* Pk = m.Pgx + (int64_t)k * kstride;
-#pragma unroll
-        for (int i = 0; i < PCX_NDIG; i++)
-#pragma unroll
-            for (int j = 0; j < PCX_NDIG; j++) {
-                if (i + j > SMAX) continue;
-                const int32_t v = (tr && i > j) ? Pk[gemm_i8x_slab(0, j, i, tl, nt) * (GT * GT) + within_t]
-                                                : Pk[gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within];
-                ts[i + j] += v;
-            }
-    }
     dd a{0.0, 0.0};
-#pragma unroll
-    for (int sd = SM; sd >= 0; sd--) {
-        if (sd > SMAX) continue;
-        a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)ts[sd], 0.0});
+    for (int sd = SMAX; sd >= 0; sd--) {
+        int64_t t = 0;
+        for (int i = 0; i <= sd && i < PCX_NDIG; i++) {
+            const int j = sd - i;
+            if (j >= PCX_NDIG) continue;  // (i + j = sd: every pair of this weight)
+            // (one digit string: a diagonal tile's pair i > j is (j, i) transposed, never computed)
+            if (sym && ta == tb && i > j)
+                t += slab_sum(m.Pgx + gemm_i8x_slab(0, j, i, tl, nt) * (GT * GT) + within_t, kstride, m.ks_gx);
+            else
+                t += slab_sum(m.Pgx + gemm_i8x_slab(0, i, j, tl, nt) * (GT * GT) + within, kstride, m.ks_gx);
+        }
+        a = dd_add(sd == SMAX ? a : dd_div_base(a), dd{(double)t, 0.0});
     }
     a = dd_div_base(dd_div_base(a));  // the (s + 2): 254^-2 more
     // 2^(e_p + f_q) applied to the rounded value: the product of the two scales alone can overflow
@@ -1769,11 +1747,14 @@ __global__ void __launch_bounds__(BT) k_cov_finish(pcx_mat m) {
 // strings' residues and the dropped digit pairs.  With D = (tok w_p + delta) / S_p and E = (w_q +
 // eta) / T_q the digit values (S = 2^e, T = 2^f; |delta| <= 0.52 254^-NDIG S per row):
 //   (a) sum delta w_q: sum tok w_q ~ 0 (mu is the token-weighted mean), so for any c, sum delta w_q =
-//       sum tok (delta / tok - c) w_q + c sum tok w_q; Cauchy-Schwarz with the best c = sum delta / T:
-//       |(a)| <= sqrt(V_p) sqrt(C~_qq) + |c| |sum tok w_q|, V_p = sum delta^2 / tok - (sum delta)^2 / T
-//       -- a constant residue (a column whose rows mostly share one value) cancels here;
+//       sum (delta - c tok) w_q + c sum tok w_q, and Cauchy-Schwarz (over the rows with tok >= 1; a row
+//       with tok 0 has delta 0) gives |sum (delta - c tok) w_q| <= sqrt(sum (delta - c tok)^2 / tok)
+//       sqrt(C~_qq) <= sqrt(sum (delta - c tok)^2) sqrt(C~_qq); with the best c = sum delta tok /
+//       sum tok^2: |(a)| <= sqrt(V_p) sqrt(C~_qq) + |c| |sum tok w_q|, V_p = sum delta^2 -
+//       (sum delta tok)^2 / sum tok^2 -- a constant residue (a column whose rows mostly share one
+//       value, equal tokens) cancels here;
 //   (b) sum tok w_p eta: likewise with V'_q = sum tok eta^2 - (sum tok eta)^2 / T;
-//   (c) sum delta eta <= sqrt(sum delta^2 / tok) sqrt(sum tok eta^2);
+//   (c) sum delta eta <= sqrt(sum delta^2) sqrt(sum tok eta^2);
 //   (d) the dropped pairs i + j > smax: per row sum_{i >= 1} |d_i| 254^-(i+1) |tail of E past digit
 //       smax - i| <= 0.502 254^-(smax+2) S T L1(d) (and the same with L1(e)), so over the rows
 //       <= 0.502 254^-(smax+2) S_p T_q sqrt(L1d_p L1e_q) -- linear in the rows: this is the term a
@@ -1788,10 +1769,10 @@ constexpr double GUARD_EPS = 0x1p-40;
 
 // gacc (int64, this rank) -> gsum (doubles) for the exchange; L1 exact, the others at 2^-24
 __global__ void __launch_bounds__(BT) k_guard_stats(pcx_mat m) {
-    const int64_t gb = (int64_t)m.cov_jb * CT, n = G_NSTAT * gb;
+    const int64_t gb = (int64_t)m.cov_jb * CT, n = G_NSTAT * gb + 1;  // (+ sum tok^2)
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < n; i += (int64_t)gridDim.x * BT) {
         const double v = (double)m.gacc[i];
-        m.gsum[i] = i < 2 * gb ? v : v * (1.0 / G_FIX);
+        m.gsum[i] = (i < 2 * gb || i == G_NSTAT * gb) ? v : v * (1.0 / G_FIX);
     }
 }
 
@@ -1818,10 +1799,11 @@ __global__ void __launch_bounds__(1024) k_cov_guard(pcx_mat m) {
     for (int w = 0; w < m.world; w++) maxtok = fmax(maxtok, m.scal[((int64_t)w * SS + SC_MAXTOK) * 2]);
     // (the k_digits row chunks: each adds at most one 2^-24 unit of rounding per sum and rank)
     const double ferr = (double)m.world * 4096.0 / G_FIX;
+    const double tok2 = m.gsum[G_NSTAT * gb];  // sum tok^2 over all rows and ranks (exact)
     const double b6 = 1.0 / DIG_SCALE;  // 254^-NDIG
     if (threadIdx.x == 0) cnt = 0;
     double rd = 0.0, re = 0.0, gd = 0.0, ge = 0.0, kd = 0.0, ke = 0.0, ad = 0.0, ae = 0.0, bg = 0.0, bq = 0.0;
-    bool bad = !(denom != 0.0 && __builtin_isfinite(denom) && T > 0.0);
+    bool bad = !(denom != 0.0 && __builtin_isfinite(denom) && T > 0.0 && tok2 > 0.0);
     for (int64_t q = threadIdx.x; !bad && q < E; q += blockDim.x) {
         const int c = m.cov_perm[q];
         const double Cqq = m.C[(int64_t)c * E + c] * denom * (1.0 - 0x1p-40);
@@ -1832,19 +1814,20 @@ __global__ void __launch_bounds__(1024) k_cov_guard(pcx_mat m) {
         }
         const double S = 1.0 / m.dscale[q], Tq = gg ? 1.0 / m.escale[q] : 0.0;
         const double* g = m.gsum + q;
+        // (one digit string: eta = delta in its units, every token maxtok: sum tok eta = sum delta tok,
+        // sum tok eta^2 = maxtok sum delta^2)
         const double l1d = g[G_L1D * gb], sd = g[G_SD * gb], sd2 = g[G_SD2 * gb];
-        const double l1e = one ? l1d : g[G_L1E * gb], se = one ? maxtok * sd : g[G_SE * gb],
-                     se2 = one ? maxtok * maxtok * sd2 : g[G_SE2 * gb];
-        const double sdl = fmax(0.0, fabs(sd) - ferr), sel = fmax(0.0, fabs(se) - ferr * (one ? maxtok : 1.0));
-        const double Vd = fmax(0.0, sd2 + ferr - sdl * sdl / T);
-        const double Ve = fmax(0.0, se2 + ferr * (one ? maxtok * maxtok : 1.0) - sel * sel / T);
+        const double l1e = one ? l1d : g[G_L1E * gb], se = one ? sd : g[G_SE * gb], se2 = one ? maxtok * sd2 : g[G_SE2 * gb];
+        const double sdl = fmax(0.0, fabs(sd) - ferr), sel = fmax(0.0, fabs(se) - ferr);
+        const double Vd = fmax(0.0, sd2 + ferr - sdl * sdl / tok2);
+        const double Ve = fmax(0.0, se2 + ferr * (one ? maxtok : 1.0) - sel * sel / T);
         if (!(Cqq > 0.0) || !__builtin_isfinite(Cqq)) {
             // no spread: exact only when nothing was rounded or dropped
             if (l1d != 0.0 || sd2 != 0.0 || (gg && (l1e != 0.0 || se2 != 0.0)) || !__builtin_isfinite(Cqq)) bad = true;
             continue;
         }
         const double rC = 1.0 / sqrt(Cqq);
-        const double rdq = b6 * S * sqrt(Vd) * rC, adq = b6 * S * (fabs(sd) + ferr) / T * rC;
+        const double rdq = b6 * S * sqrt(Vd) * rC, adq = b6 * S * (fabs(sd) + ferr) / tok2 * rC;
         double own = rdq;
         rd = fmax(rd, rdq);
         ad = fmax(ad, adq);
@@ -1854,7 +1837,7 @@ __global__ void __launch_bounds__(1024) k_cov_guard(pcx_mat m) {
         if (gg) {
             const double req = b6 * Tq * sqrt(Ve) * rC, aeq = b6 * Tq * (fabs(se) + ferr) / T * rC;
             const double gdq = S * sqrt(l1d) * rC, geq = Tq * sqrt(l1e) * rC;
-            const double kdq = S * sqrt(sd2 + ferr) * rC, keq = Tq * sqrt(se2 + ferr) * rC;
+            const double kdq = S * sqrt(sd2 + ferr) * rC, keq = Tq * sqrt(se2 + ferr * (one ? maxtok : 1.0)) * rC;
             re = fmax(re, req);
             ae = fmax(ae, aeq);
             gd = fmax(gd, gdq);
@@ -4129,56 +4112,82 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
     if (st[SW_STATUS] == 0) return;
     __shared__ double xs[SEL_EXACT_MAX];
     __shared__ double ws[SEL_EXACT_MAX];
+    __shared__ uint32_t pres[SEL_EXACT_MAX / 32];  // the rows' present bits (phase 1: a report; 2: a value)
     __shared__ int cnt;
     __shared__ double mid_s, wmax_s;
     __shared__ int first_s;
     const int tid = threadIdx.x;
     const int n_rows = (int)m.n_rows;
+    // the column's (x, w) in row order into LDS by every thread (coalesced; thread 0 read them one
+    // dependent global load at a time: 0.7 ms of a 1k x 100 consensus), the present bits beside
+    for (int k = tid; k < SEL_EXACT_MAX / 32; k += 1024) pres[k] = 0;
+    __syncthreads();
+    for (int i = tid; i < n_rows; i += 1024) {
+        double x = 0.0, w = 0.0;
+        if (sel_elem(m, s, i, x, w)) atomicOr(&pres[i >> 5], 1u << (i & 31));
+        xs[i] = x;
+        ws[i] = w;
+    }
+    __syncthreads();
     if (tid == 0) {
-        // sequential, row order: present total (phase 1), then the weights and their sum
+        // sequential, row order: present total (phase 1), then the weights and their sum --
+        // compacted in place (k <= i)
         double tot = 0.0;
         if (m.sel_phase == 1)
-            for (int i = 0; i < n_rows; i++) {
-                double x, w;
-                if (sel_elem(m, s, i, x, w)) tot += w;
-            }
+            for (int i = 0; i < n_rows; i++)
+                if ((pres[i >> 5] >> (i & 31)) & 1u) tot += ws[i];
         int k = 0;
         double W = 0.0;
         for (int i = 0; i < n_rows; i++) {
-            double x, w;
-            if (!sel_elem(m, s, i, x, w)) continue;
+            if (!((pres[i >> 5] >> (i & 31)) & 1u)) continue;
+            double w = ws[i];
             if (m.sel_phase == 1) w = w / tot;
-            xs[k] = x;
+            xs[k] = xs[i];
             ws[k] = w;
             W += w;
             k++;
         }
         cnt = k;
         mid_s = 0.5 * W;
+        first_s = n_rows;
+        wmax_s = 0.0;
     }
     __syncthreads();
     const int n = cnt;
     const double mid = mid_s;
-    // dominance: any(w > mid) -> data[first index of max(w)]
-    if (tid == 0) {
-        bool dom = false;
-        double mx = n ? ws[0] : 0.0;
-        for (int k = 0; k < n; k++) {
+    // dominance: any(w > mid) -> data[first index of max(w)]; any positive weight (exact
+    // reductions, spread over the block)
+    {
+        __shared__ double red[1024];
+        __shared__ int dom_s;
+        if (tid == 0) dom_s = 0;
+        double mx = -__builtin_inf();
+        bool dom = false, pos = false;
+        for (int k = tid; k < n; k += 1024) {
+            mx = fmax(mx, ws[k]);
             dom |= ws[k] > mid;
-            if (ws[k] > mx) mx = ws[k];
+            pos |= ws[k] > 0.0;
         }
-        first_s = -1;
+        red[tid] = mx;
+        dom = __syncthreads_or(dom);
+        pos = __syncthreads_or(pos);
+        for (int h = 512; h >= 1; h >>= 1) {
+            if (tid < h) red[tid] = fmax(red[tid], red[tid + h]);
+            __syncthreads();
+        }
+        // (the sequential max of the SPEC starts at ws[0]: a NaN there stays, and nothing equals it)
+        const double mxa = (n > 0 && __builtin_isnan(ws[0])) ? __builtin_nan("") : red[0];
         if (dom)
-            for (int k = 0; k < n; k++)
-                if (ws[k] == mx) {
-                    first_s = k;
-                    break;
-                }
-        bool pos = false;
-        for (int k = 0; k < n; k++) pos |= ws[k] > 0.0;
-        wmax_s = pos ? 1.0 : 0.0;
+            for (int k = tid; k < n; k += 1024)
+                if (ws[k] == mxa) atomicMin(&first_s, k);
+        if (tid == 0) {
+            dom_s = dom ? 1 : 0;
+            wmax_s = pos ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        if (tid == 0 && !dom_s) first_s = -1;
+        __syncthreads();
     }
-    __syncthreads();
     if (first_s >= 0) {
         if (tid == 0) sel_done(st, xs[first_s]);
         return;
@@ -5701,7 +5710,8 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 // (16 row groups a block at least: 64 left a 125k-row shard's k_digits1 with 492 blocks)
                 const int ng = (int)std::min<int64_t>(4096, (rg + 15) / 16);
                 // (the digit sums and, past them, the covariance guard's sums)
-                if (hipMemsetAsync(m.dtok, 0, (size_t)(PCX_NDIG + (m.gacc ? G_NSTAT : 0)) * gb * 8, st) != hipSuccess)
+                if (hipMemsetAsync(m.dtok, 0, ((size_t)(PCX_NDIG + (m.gacc ? G_NSTAT : 0)) * gb + (m.gacc ? 1 : 0)) * 8, st) !=
+                    hipSuccess)
                     return hipGetLastError();
                 if (m.cov_gg8 && m.zE != m.zD)  // both digit strings
                     hipLaunchKernelGGL(k_digits, dim3((unsigned)((gb + DG_POS - 1) / DG_POS), (unsigned)ng), dim3(BT), 0, st, m);
@@ -5778,7 +5788,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                                (const double*)S, (int)(m.world == 1));
             // the guard's sums as doubles (the runner exchanges them with the covariance)
             if (m.cov_mixed && m.gacc && m.gsum && m.cov_jb > 0)
-                hipLaunchKernelGGL(k_guard_stats, dim3((unsigned)((G_NSTAT * m.cov_jb * CT + BT - 1) / BT)), dim3(BT), 0,
+                hipLaunchKernelGGL(k_guard_stats, dim3((unsigned)((G_NSTAT * m.cov_jb * CT + BT) / BT)), dim3(BT), 0,
                                    st, m);
             break;
         }

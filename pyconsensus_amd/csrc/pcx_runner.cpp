@@ -281,7 +281,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->C, (size_t)(E * E) * 8, false},
         {(void**)&w->Mw, (size_t)(2 * E * E + 8 * E + 64) * 8, false},
         {(void**)&w->wcd, (size_t)(w->wcd_rows * w->wcd_ld) * 8, false},
-        {(void**)&w->tokp, (size_t)(2 * (w->wcd_rows + 64)) * 8, false},  // tokens, then 1 / tokens
+        {(void**)&w->tokp, (size_t)(w->wcd_rows + 64) * 8, false},
         {(void**)&w->rowpart, (size_t)(((w->wcd_ld + 511) / 512) * w->wcd_rows * 2) * 4, false},
         {(void**)&w->zA, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
         {(void**)&w->zB, (size_t)(w->wcd_rows * (w->wcd_ld + 256)), false},
@@ -1019,7 +1019,6 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.scalars = w->scalars;
         m.wcd = w->wcd;
         m.tokp = w->tokp;
-        m.rtokp = w->tokp + w->wcd_rows + 64;
         m.wcd_rows = w->wcd_rows;
         m.wcd_ld = w->wcd_ld;
         m.rowpart = w->rowpart;
@@ -1116,7 +1115,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 // mixed pairs on int8 digits when the bounds are finite and the memory is there
                 m.cov_mixed = plan[1] && np > 0 && gb > 0 && w->grow(w->zd, (size_t)(w->wcd_rows * zd_ld(gb))) &&
                                       w->grow(w->pmx, (size_t)(m.ks_mx * m.zq * PCX_NDIG * gb * 4)) &&
-                                      w->grow(w->dtok, (size_t)((PCX_NDIG + G_NSTAT) * gb * 8))
+                                      w->grow(w->dtok, (size_t)(((PCX_NDIG + G_NSTAT) * gb + 1) * 8))
                                   ? 1
                                   : 0;
                 r->mixed_int8 = m.cov_mixed;
@@ -1191,7 +1190,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                     if (R.comm) {  // the partial covariance: one SUM of its lower triangle (cslab is free now)
                         R.hip(tri_pack(w->C, w->cslab, E, 0, R.st), "tri pack");
                         // (and the guard's sums, k_guard_stats wrote them past the triangle)
-                        R.allreduce(w->cslab, E * (E + 1) / 2 + (m.cov_mixed ? G_NSTAT * gb : 0), PCX_F64, PCX_SUM);
+                        R.allreduce(w->cslab, E * (E + 1) / 2 + (m.cov_mixed ? G_NSTAT * gb + 1 : 0), PCX_F64, PCX_SUM);
                         R.hip(tri_pack(w->C, w->cslab, E, 1, R.st), "tri unpack");
                     }
                     R.stage(m, M_COV_FINISH);
