@@ -943,7 +943,13 @@ __global__ void __launch_bounds__(1024) k_cov_plan(pcx_mat m) {
 constexpr int WCD_COLS = 2 * BT;  // columns per block (2 per thread)
 // 4096 blocks, halved until each has at least WCD_MIN_ROWS rows: a C5 shard (125k rows) on ~1k
 // blocks of ~1k rows ran k_wcd 3.49 -> 3.30 ms against 4096 of 256 (1M rows: 4096 either way)
-constexpr int64_t WCD_MIN_ROWS = 768;
+#ifndef PCX_WCD_MIN_ROWS  // (a build parameter for A/B runs, tools/ab_variant.sh)
+#define PCX_WCD_MIN_ROWS 768
+#endif
+#ifndef PCX_WCD_MIN_WG
+#define PCX_WCD_MIN_WG 1024
+#endif
+constexpr int64_t WCD_MIN_ROWS = PCX_WCD_MIN_ROWS;
 
 // Blocks own a contiguous row range (a multiple of 64 rows) of a 512-event block; each
 // wave also counts the NaN / zero rescaled reports of its 128 events per row (ballots),
@@ -5762,7 +5768,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 int64_t rb = std::max(1, 4096 / ncb);
                 // (but keep >= 1,024 workgroups: at C4's 1,000 events -- two column blocks -- the
                 // 768-row floor left 256 workgroups, one per CU: k_wcd 1.03 ms at 2.5 TB/s)
-                while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS && (rb / 2) * ncb >= 1024) rb /= 2;
+                while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS && (rb / 2) * ncb >= PCX_WCD_MIN_WG) rb /= 2;
                 hipLaunchKernelGGL(k_wcd, dim3((unsigned)rb, ncb),
                                    dim3(BT), 0, st, m);
                 break;
