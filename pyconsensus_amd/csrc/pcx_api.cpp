@@ -194,6 +194,9 @@ void ctx_host_free(pcx_ctx* c) {
     c->pinned_bytes = 0;
     if (c->sel_pin) (void)hipHostFree(c->sel_pin);
     c->sel_pin = nullptr;
+    if (c->pin_small) (void)hipHostFree(c->pin_small);
+    c->pin_small = nullptr;
+    c->pin_small_bytes = 0;
     for (hipEvent_t& ev : c->sel_ev) {
         if (ev) (void)hipEventDestroy(ev);
         ev = nullptr;

@@ -357,6 +357,9 @@ struct pcx_ctx {
     // the host-memory path's large device copies (the reports, the matrix outputs), kept between
     // calls (a hipMalloc / hipFree of 33 GB per call is not free); pcx_release_workspace frees them
     std::vector<std::pair<void*, size_t>> io_bufs;
+    // pinned buffer of the host path's small outputs (one copy back per call)
+    void* pin_small = nullptr;
+    size_t pin_small_bytes = 0;
 };
 
 namespace pcx {
