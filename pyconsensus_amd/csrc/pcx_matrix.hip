@@ -4125,34 +4125,41 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
     const int tid = threadIdx.x;
     const int n_rows = (int)m.n_rows;
     // the column's (x, w) in row order into LDS by every thread (coalesced; thread 0 read them one
-    // dependent global load at a time: 0.7 ms of a 1k x 100 consensus), the present bits beside
+    // dependent global load at a time: 0.7 ms of a 1k x 100 consensus), the present bits beside;
+    // an absent row holds (+inf, +inf), which the sort puts after every present pair, so nothing is
+    // compacted (an in-place compaction by one thread waited on its own LDS stores)
+    const bool ph1 = m.sel_phase == 1;
     for (int k = tid; k < SEL_EXACT_MAX / 32; k += 1024) pres[k] = 0;
     __syncthreads();
     for (int i = tid; i < n_rows; i += 1024) {
         double x = 0.0, w = 0.0;
-        if (sel_elem(m, s, i, x, w)) atomicOr(&pres[i >> 5], 1u << (i & 31));
-        xs[i] = x;
-        ws[i] = w;
+        const bool ok = sel_elem(m, s, i, x, w);
+        if (ok) atomicOr(&pres[i >> 5], 1u << (i & 31));
+        xs[i] = ok ? x : __builtin_inf();
+        ws[i] = ok ? w : __builtin_inf();
     }
     __syncthreads();
-    if (tid == 0) {
-        // sequential, row order: present total (phase 1), then the weights and their sum --
-        // compacted in place (k <= i)
+    auto present = [&](int i) { return ((pres[i >> 5] >> (i & 31)) & 1u) != 0; };
+    __shared__ double tot_s;
+    if (ph1 && tid == 0) {  // the present total, sequential in row order (read only: the loads pipeline)
         double tot = 0.0;
-        if (m.sel_phase == 1)
-            for (int i = 0; i < n_rows; i++)
-                if ((pres[i >> 5] >> (i & 31)) & 1u) tot += ws[i];
+        for (int i = 0; i < n_rows; i++)
+            if (present(i)) tot += ws[i];
+        tot_s = tot;
+    }
+    __syncthreads();
+    if (ph1)  // rep_j / tot, each its own division
+        for (int i = tid; i < n_rows; i += 1024)
+            if (present(i)) ws[i] = ws[i] / tot_s;
+    __syncthreads();
+    if (tid == 0) {
         int k = 0;
         double W = 0.0;
-        for (int i = 0; i < n_rows; i++) {
-            if (!((pres[i >> 5] >> (i & 31)) & 1u)) continue;
-            double w = ws[i];
-            if (m.sel_phase == 1) w = w / tot;
-            xs[k] = xs[i];
-            ws[k] = w;
-            W += w;
-            k++;
-        }
+        for (int i = 0; i < n_rows; i++)
+            if (present(i)) {
+                W += ws[i];
+                k++;
+            }
         cnt = k;
         mid_s = 0.5 * W;
         first_s = n_rows;
@@ -4162,17 +4169,22 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
     const int n = cnt;
     const double mid = mid_s;
     // dominance: any(w > mid) -> data[first index of max(w)]; any positive weight (exact
-    // reductions, spread over the block)
+    // reductions over the present rows, spread over the block)
     {
         __shared__ double red[1024];
-        __shared__ int dom_s;
-        if (tid == 0) dom_s = 0;
+        __shared__ int dom_s, first_p;
+        if (tid == 0) {
+            dom_s = 0;
+            first_p = n_rows;
+        }
         double mx = -__builtin_inf();
         bool dom = false, pos = false;
-        for (int k = tid; k < n; k += 1024) {
-            mx = fmax(mx, ws[k]);
-            dom |= ws[k] > mid;
-            pos |= ws[k] > 0.0;
+        for (int i = tid; i < n_rows; i += 1024) {
+            if (!present(i)) continue;
+            mx = fmax(mx, ws[i]);
+            dom |= ws[i] > mid;
+            pos |= ws[i] > 0.0;
+            atomicMin(&first_p, i);
         }
         red[tid] = mx;
         dom = __syncthreads_or(dom);
@@ -4181,11 +4193,12 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
             if (tid < h) red[tid] = fmax(red[tid], red[tid + h]);
             __syncthreads();
         }
-        // (the sequential max of the SPEC starts at ws[0]: a NaN there stays, and nothing equals it)
-        const double mxa = (n > 0 && __builtin_isnan(ws[0])) ? __builtin_nan("") : red[0];
+        // (the sequential max of the SPEC starts at the first present weight: a NaN there stays,
+        // and nothing equals it)
+        const double mxa = (n > 0 && __builtin_isnan(ws[first_p])) ? __builtin_nan("") : red[0];
         if (dom)
-            for (int k = tid; k < n; k += 1024)
-                if (ws[k] == mxa) atomicMin(&first_s, k);
+            for (int i = tid; i < n_rows; i += 1024)
+                if (present(i) && ws[i] == mxa) atomicMin(&first_s, i);
         if (tid == 0) {
             dom_s = dom ? 1 : 0;
             wmax_s = pos ? 1.0 : 0.0;
@@ -4202,10 +4215,10 @@ __global__ void __launch_bounds__(1024) k_sel_exact(pcx_mat m) {
         if (tid == 0) sel_done(st, __builtin_nan(""));
         return;
     }
-    // bitonic sort of (x, w) pairs, padded to a power of two with +inf
+    // bitonic sort of (x, w) pairs, padded to a power of two with +inf (the absent rows are too)
     int P = 1;
-    while (P < n) P <<= 1;
-    for (int k = n + tid; k < P; k += 1024) {
+    while (P < n_rows) P <<= 1;
+    for (int k = n_rows + tid; k < P; k += 1024) {
         xs[k] = __builtin_inf();
         ws[k] = __builtin_inf();
     }

@@ -457,48 +457,62 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
     if (rc) R.hip(hipErrorUnknown, "staged D2H of an output");
 }
 
-// result["original"] in place for host memory: the scaled columns of the caller's array rescaled
-// by host threads, (r - lo) / (hi - lo) as IEEE division (the device's div_rn is that division bit
-// for bit, tests/test_fastdiv.py), truncated for an integer dtype (Q3); NaN cells are left as they
-// are (the device's arithmetic returns the same NaN).  Rows split over host_threads() threads.
-struct HostRescale {
+// result["original"] / result["filled"] for host memory, built by host threads from the caller's
+// reports instead of copied back (2 x 33 GB of D2H at C5): x = (r - lo) / (hi - lo) for a scaled
+// event as IEEE division -- the device's div_rn is that division bit for bit, tests/test_fastdiv.py --
+// truncated for an integer dtype (Q3), r itself otherwise; `original` = x (a NaN report keeps its
+// bits, as the device's does), written into the caller's array when it is the reports (in place,
+// Q2: only the scaled columns change); `filled` = x, or the event's fill where x is NaN or 0.0
+// (:278, :310-312) -- the fills are the device's (the interpolation's guesses, EV_GUESS).  Rows split
+// over host_threads() threads; a small matrix runs on the calling thread.
+struct HostMatrices {
     std::vector<std::thread> th;
-    void start(double* a, int64_t n_rows, int64_t E, const std::vector<int32_t>& cols, const double* lo,
-               const double* hi, bool int_dtype) {
-        const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n_rows / 1024));
-        auto cl = std::make_shared<std::vector<int32_t>>(cols);
-        auto lr = std::make_shared<std::vector<double>>();
-        for (int32_t c : cols) {
-            lr->push_back(lo[c]);
-            lr->push_back(hi[c] - lo[c]);
+    void run(const double* rep_in, double* original, double* filled, int64_t n_rows, int64_t E,
+             const std::vector<uint8_t>& scaled, const double* lo, const double* hi, const std::vector<double>& guess,
+             bool int_dtype) {
+        struct Col {
+            bool sc;
+            double lo, range;
+        };
+        auto cols = std::make_shared<std::vector<Col>>(E);
+        for (int64_t j = 0; j < E; j++) {
+            const bool sc = !scaled.empty() && scaled[j];
+            (*cols)[j] = {sc, sc ? lo[j] : 0.0, sc ? hi[j] - lo[j] : 1.0};
         }
-        const bool inline_ = n_rows * (int64_t)cols.size() < (int64_t)1 << 20;  // small: no threads
-        for (int t = 0; t < (inline_ ? 1 : T); t++) {
-            const int64_t r0 = inline_ ? 0 : n_rows * t / T, r1 = inline_ ? n_rows : n_rows * (t + 1) / T;
-            auto body = [=] {
-                const size_t nc = cl->size();
-                for (int64_t i = r0; i < r1; i++) {
-                    double* row = a + i * E;
-                    for (size_t k = 0; k < nc; k++) {
-                        const double v = row[(*cl)[k]];
-                        if (std::isnan(v)) continue;
-                        double x = (v - (*lr)[2 * k]) / (*lr)[2 * k + 1];
+        auto g = std::make_shared<std::vector<double>>(guess);
+        const bool inplace = original == rep_in;
+        auto body = [=](int64_t r0, int64_t r1) {
+            const Col* cl = cols->data();
+            const double* gv = g->data();
+            for (int64_t i = r0; i < r1; i++) {
+                const double* in = rep_in + i * E;
+                double* o = original ? original + i * E : nullptr;
+                double* f = filled ? filled + i * E : nullptr;
+                for (int64_t j = 0; j < E; j++) {
+                    const double r = in[j];
+                    double x = r;
+                    if (cl[j].sc) {
+                        x = (r - cl[j].lo) / cl[j].range;
                         if (int_dtype) x = std::trunc(x);
-                        row[(*cl)[k]] = x;
                     }
+                    if (f) f[j] = (std::isnan(x) || x == 0.0) ? gv[j] : x;
+                    if (o && (!inplace || cl[j].sc)) o[j] = std::isnan(x) ? r : x;
                 }
-            };
-            if (inline_)
-                body();
-            else
-                th.emplace_back(body);
+            }
+        };
+        const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n_rows / 1024));
+        if (T <= 1 || n_rows * E < ((int64_t)1 << 20)) {
+            body(0, n_rows);
+            return;
         }
+        for (int t = 0; t < T; t++) th.emplace_back(body, n_rows * t / T, n_rows * (t + 1) / T);
+        join();
     }
     void join() {
         for (auto& t : th) t.join();
         th.clear();
     }
-    ~HostRescale() { join(); }
+    ~HostMatrices() { join(); }
 };
 
 int64_t pow2_at_least(int64_t n) {
@@ -887,7 +901,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
     c->progress_wait.store(0, std::memory_order_relaxed);
     const bool host = p->mem_kind == PCX_MEM_HOST;
     const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
-    HostRescale host_rescale;  // (joined on every exit path, before the caller's array is returned)
+    HostMatrices host_mats;  // (joined on every exit path, before the caller's arrays are returned)
     try {
         Io io(c);
         // ---- scaled events (host view)
@@ -967,24 +981,14 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         // device copy of the reports is rescaled and copied back into the caller's array)
         const bool inplace = (cons || entry == 1) && r->original &&
                              (const void*)r->original == (const void*)p->reports;
-        m.original = (cons || entry == 1) && !inplace ? out(r->original, n_rows * E) : nullptr;
-        m.orig_inplace = inplace ? 1 : 0;
+        // host memory: `original` and `filled` are built on the host from the caller's reports and
+        // the device's fills once the device is done (HostMatrices), not written by the device and
+        // copied back -- the device then writes neither (k_wcd: 65 GB fewer bytes at C5)
+        const bool host_mats_on = host && (cons || entry == 1) && (r->original || r->filled);
+        m.original = (cons || entry == 1) && !inplace && !host_mats_on ? out(r->original, n_rows * E) : nullptr;
+        m.orig_inplace = inplace ? 1 : 0;  // (host: the device copy of the reports, for later stages)
         m.rescaled = 0;
-        // host memory, in place: the caller's array is rescaled by host threads while the device
-        // works (once the reports' H2D has drained), instead of copying the whole device copy back
-        // (33 GB of D2H at C5 for the quarter of the columns that change)
-        if (inplace && host && n_scaled > 0) {
-            hipEvent_t ev = nullptr;
-            R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-            struct EvGuard {
-                hipEvent_t e;
-                ~EvGuard() { (void)hipEventDestroy(e); }
-            } evg{ev};
-            R.hip(hipEventRecord(ev, R.st), "hipEventRecord");
-            R.hip(hipEventSynchronize(ev), "hipEventSynchronize(H2D)");
-            host_rescale.start(const_cast<double*>(p->reports), n_rows, E, scols, p->lo, p->hi, p->int_dtype != 0);
-        }
-        m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
+        m.filled = (cons || entry == 1) && !host_mats_on ? out(r->filled, n_rows * E) : nullptr;
         m.weighted_mean = entry == 2 ? out(r->weighted_mean, E) : nullptr;
         m.nc_out = entry == 4 ? out(nc_out, n_rows) : nullptr;
         double* cov_out = entry == 2 ? out(r->covariance, E * E) : nullptr;
@@ -1339,13 +1343,20 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         }
         for (auto& o : outs)
             if ((size_t)o.n * 8 >= STAGE_MIN) d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
+        std::vector<double> guess_h;
+        if (host_mats_on) {  // the fills (:310-312), for the host-built `filled`
+            guess_h.resize(E);
+            R.hip(hipMemcpyAsync(guess_h.data(), w->ev, E * 8, hipMemcpyDeviceToHost, R.st), "D2H fills");
+        }
         R.mark(-1);
         R.sync();
+        if (host_mats_on)  // (host time: in the caller's wall clock, not in the device stage times)
+            host_mats.run(p->reports, r->original, r->filled, n_rows, E, sc_h, p->lo, p->hi, guess_h, p->int_dtype != 0);
         if (arena_pin)
             for (auto& o : outs)
                 if ((char*)o.dev >= io.arena && (char*)o.dev < io.arena + io.arena_cap)
                     memcpy(o.user, (char*)c->pin_small + ((char*)o.dev - io.arena), (size_t)o.n * 8);
-        host_rescale.join();
+
         r->participation = sc2[0];
         r->avg_certainty = sc2[1];
         const bool branchless = (alg == PCX_ALG_ABSOLUTE && entry != 4) || clustering || entry == 1 || entry == 2;
