@@ -80,6 +80,10 @@ def cpu_baseline(seconds=12.0):
            "sample": "%d rounds of the C3 workload (50x20, seed %d) in %.1f s, C oracle, %d OpenMP threads"
                      % (done, SEED, el, threads),
            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+    # SURVEY.md 8(d) asks for the box's whole host; this job may use `threads` of its cores (the
+    # pool's share, OMP_NUM_THREADS), so the whole-host figure is an estimate: rounds are
+    # independent, so the rate scales with cores at best linearly -- an upper bound, not measured
+    out["value_all_host_cpus_linear_bound"] = out["value"] * (os.cpu_count() or threads) / threads
     # the numpy restatement (same per-round structure as the reference) for context
     from oracle.pcx_oracle import OracleCPU
     bl = synthetic.bounds_list

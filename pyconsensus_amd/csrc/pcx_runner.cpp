@@ -457,46 +457,44 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
     if (rc) R.hip(hipErrorUnknown, "staged D2H of an output");
 }
 
-// result["original"] / result["filled"] for host memory, built by host threads from the caller's
-// reports instead of copied back (2 x 33 GB of D2H at C5): x = (r - lo) / (hi - lo) for a scaled
-// event as IEEE division -- the device's div_rn is that division bit for bit, tests/test_fastdiv.py --
-// truncated for an integer dtype (Q3), r itself otherwise; `original` = x (a NaN report keeps its
-// bits, as the device's does), written into the caller's array when it is the reports (in place,
-// Q2: only the scaled columns change); `filled` = x, or the event's fill where x is NaN or 0.0
-// (:278, :310-312) -- the fills are the device's (the interpolation's guesses, EV_GUESS).  Rows split
-// over host_threads() threads; a small matrix runs on the calling thread.
-struct HostMatrices {
+// result["original"] for host memory, built by host threads from the caller's reports while the
+// device works (started once the reports' H2D has drained), instead of copied back (33 GB of D2H at
+// C5): x = (r - lo) / (hi - lo) for a scaled event as IEEE division -- the device's div_rn is that
+// division bit for bit, tests/test_fastdiv.py -- truncated for an integer dtype (Q3), r itself
+// otherwise; a NaN report keeps its bits (as the device's `original` does).  In place (Q2: original
+// IS the caller's reports) only the scaled columns are written.  `filled` still comes from the
+// device (its fills are known only at the end): its D2H runs beside this pass, which overlaps it.
+// (Building `filled` here too, after the device, measured slower: 1.58-1.66 s against 1.47-1.51 s
+// in place at C5 -- the host's memory bandwidth, not PCIe, bound it.)  Rows split over
+// host_threads() threads; a small matrix runs on the calling thread.
+struct HostOriginal {
     std::vector<std::thread> th;
-    void run(const double* rep_in, double* original, double* filled, int64_t n_rows, int64_t E,
-             const std::vector<uint8_t>& scaled, const double* lo, const double* hi, const std::vector<double>& guess,
-             bool int_dtype) {
-        struct Col {
-            bool sc;
-            double lo, range;
-        };
-        auto cols = std::make_shared<std::vector<Col>>(E);
-        for (int64_t j = 0; j < E; j++) {
-            const bool sc = !scaled.empty() && scaled[j];
-            (*cols)[j] = {sc, sc ? lo[j] : 0.0, sc ? hi[j] - lo[j] : 1.0};
-        }
-        auto g = std::make_shared<std::vector<double>>(guess);
+    void start(const double* rep_in, double* original, int64_t n_rows, int64_t E, const std::vector<uint8_t>& scaled,
+               const double* lo, const double* hi, bool int_dtype) {
+        std::vector<int32_t> sc;
+        std::vector<double> lr;
+        for (int64_t j = 0; j < (int64_t)scaled.size(); j++)
+            if (scaled[j]) {
+                sc.push_back((int32_t)j);
+                lr.push_back(lo[j]);
+                lr.push_back(hi[j] - lo[j]);
+            }
+        auto scp = std::make_shared<std::vector<int32_t>>(std::move(sc));
+        auto lrp = std::make_shared<std::vector<double>>(std::move(lr));
         const bool inplace = original == rep_in;
         auto body = [=](int64_t r0, int64_t r1) {
-            const Col* cl = cols->data();
-            const double* gv = g->data();
+            const int32_t* cl = scp->data();
+            const double* l = lrp->data();
+            const size_t nc = scp->size();
             for (int64_t i = r0; i < r1; i++) {
                 const double* in = rep_in + i * E;
-                double* o = original ? original + i * E : nullptr;
-                double* f = filled ? filled + i * E : nullptr;
-                for (int64_t j = 0; j < E; j++) {
-                    const double r = in[j];
-                    double x = r;
-                    if (cl[j].sc) {
-                        x = (r - cl[j].lo) / cl[j].range;
-                        if (int_dtype) x = std::trunc(x);
-                    }
-                    if (f) f[j] = (std::isnan(x) || x == 0.0) ? gv[j] : x;
-                    if (o && (!inplace || cl[j].sc)) o[j] = std::isnan(x) ? r : x;
+                double* o = original + i * E;
+                if (!inplace) memcpy(o, in, (size_t)E * 8);
+                for (size_t k = 0; k < nc; k++) {
+                    const double r = in[cl[k]];
+                    double x = (r - l[2 * k]) / l[2 * k + 1];
+                    if (int_dtype) x = std::trunc(x);
+                    o[cl[k]] = std::isnan(x) ? r : x;
                 }
             }
         };
@@ -506,13 +504,12 @@ struct HostMatrices {
             return;
         }
         for (int t = 0; t < T; t++) th.emplace_back(body, n_rows * t / T, n_rows * (t + 1) / T);
-        join();
     }
     void join() {
         for (auto& t : th) t.join();
         th.clear();
     }
-    ~HostMatrices() { join(); }
+    ~HostOriginal() { join(); }
 };
 
 int64_t pow2_at_least(int64_t n) {
@@ -901,7 +898,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
     c->progress_wait.store(0, std::memory_order_relaxed);
     const bool host = p->mem_kind == PCX_MEM_HOST;
     const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
-    HostMatrices host_mats;  // (joined on every exit path, before the caller's arrays are returned)
+    HostOriginal host_orig;  // (joined on every exit path, before the caller's arrays are returned)
     try {
         Io io(c);
         // ---- scaled events (host view)
@@ -981,14 +978,24 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         // device copy of the reports is rescaled and copied back into the caller's array)
         const bool inplace = (cons || entry == 1) && r->original &&
                              (const void*)r->original == (const void*)p->reports;
-        // host memory: `original` and `filled` are built on the host from the caller's reports and
-        // the device's fills once the device is done (HostMatrices), not written by the device and
-        // copied back -- the device then writes neither (k_wcd: 65 GB fewer bytes at C5)
-        const bool host_mats_on = host && (cons || entry == 1) && (r->original || r->filled);
-        m.original = (cons || entry == 1) && !inplace && !host_mats_on ? out(r->original, n_rows * E) : nullptr;
+        // host memory: `original` is built on the host from the caller's reports while the device
+        // works (HostOriginal), not written by the device and copied back
+        const bool host_orig_on = host && (cons || entry == 1) && r->original;
+        m.original = (cons || entry == 1) && !inplace && !host_orig_on ? out(r->original, n_rows * E) : nullptr;
         m.orig_inplace = inplace ? 1 : 0;  // (host: the device copy of the reports, for later stages)
         m.rescaled = 0;
-        m.filled = (cons || entry == 1) && !host_mats_on ? out(r->filled, n_rows * E) : nullptr;
+        m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
+        if (host_orig_on) {  // once the reports' H2D has drained (the caller's array is rewritten in place)
+            hipEvent_t ev = nullptr;
+            R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            struct EvGuard {
+                hipEvent_t e;
+                ~EvGuard() { (void)hipEventDestroy(e); }
+            } evg{ev};
+            R.hip(hipEventRecord(ev, R.st), "hipEventRecord");
+            R.hip(hipEventSynchronize(ev), "hipEventSynchronize(H2D)");
+            host_orig.start(p->reports, r->original, n_rows, E, sc_h, p->lo, p->hi, p->int_dtype != 0);
+        }
         m.weighted_mean = entry == 2 ? out(r->weighted_mean, E) : nullptr;
         m.nc_out = entry == 4 ? out(nc_out, n_rows) : nullptr;
         double* cov_out = entry == 2 ? out(r->covariance, E * E) : nullptr;
@@ -1343,15 +1350,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         }
         for (auto& o : outs)
             if ((size_t)o.n * 8 >= STAGE_MIN) d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
-        std::vector<double> guess_h;
-        if (host_mats_on) {  // the fills (:310-312), for the host-built `filled`
-            guess_h.resize(E);
-            R.hip(hipMemcpyAsync(guess_h.data(), w->ev, E * 8, hipMemcpyDeviceToHost, R.st), "D2H fills");
-        }
         R.mark(-1);
         R.sync();
-        if (host_mats_on)  // (host time: in the caller's wall clock, not in the device stage times)
-            host_mats.run(p->reports, r->original, r->filled, n_rows, E, sc_h, p->lo, p->hi, guess_h, p->int_dtype != 0);
+        host_orig.join();
         if (arena_pin)
             for (auto& o : outs)
                 if ((char*)o.dev >= io.arena && (char*)o.dev < io.arena + io.arena_cap)
