@@ -201,6 +201,8 @@ void ctx_host_free(pcx_ctx* c) {
         if (ev) (void)hipEventDestroy(ev);
         ev = nullptr;
     }
+    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
+    c->side_stream = nullptr;
     io_bufs_free(c);
 }
 void io_bufs_free(pcx_ctx* c) {

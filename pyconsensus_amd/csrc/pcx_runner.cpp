@@ -18,7 +18,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <thread>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <memory>
 #include <new>
 #include <string>
@@ -79,7 +81,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx, clw, fg, nam, dtok, ze, pgx;
+    } pgg, zd, pmx, clw, fg, nam, dtok, ze, pgx, wdig;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -93,7 +95,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok, &ze, &pgx})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok, &ze, &pgx, &wdig})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -417,16 +419,23 @@ int host_threads() {
     return std::max(1, std::min(t, 16));
 }
 
-void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
-    pcx_ctx* c = R.c;
+// pinned staging slots for d2h_staged (grown once, kept in the context)
+bool stage_slots(pcx_ctx* c) {
     const size_t need = STAGE_CHUNK * STAGE_SLOTS;
-    if (c->pinned_bytes < need) {
-        if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->pinned_bytes >= need) return true;
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+    if (hipHostMalloc(&c->pinned, need, hipHostMallocDefault) != hipSuccess) {
         c->pinned = nullptr;
-        c->pinned_bytes = 0;
-        R.hip(hipHostMalloc(&c->pinned, need, hipHostMallocDefault), "hipHostMalloc(staging)");
-        c->pinned_bytes = need;
+        return false;
     }
+    c->pinned_bytes = need;
+    return true;
+}
+
+// the staged copy on stream `st` through the context's slots (stage_slots first); 0 or PCX_EHIP
+int d2h_staged_on(pcx_ctx* c, hipStream_t st, void* dst, const void* src, size_t bytes) {
     hipEvent_t ev[STAGE_SLOTS] = {};
     struct Evs {  // (the guard before the first creation: a failed one leaks none made before it)
         hipEvent_t* e;
@@ -435,18 +444,19 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
                 if (e[k]) (void)hipEventDestroy(e[k]);
         }
     } evs{ev};
-    for (int k = 0; k < STAGE_SLOTS; k++) R.hip(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
+    for (int k = 0; k < STAGE_SLOTS; k++)
+        if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) return PCX_EHIP;
     char* pin = static_cast<char*>(c->pinned);
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
     const int64_t nchunks = (int64_t)((bytes + STAGE_CHUNK - 1) / STAGE_CHUNK);
     auto len_of = [&](int64_t k) { return std::min(STAGE_CHUNK, bytes - (size_t)k * STAGE_CHUNK); };
-    const int rc = chunked_copy(
+    return chunked_copy(
         nchunks, STAGE_SLOTS, host_threads(),
         [&](int64_t k, int slot) -> int {
             hipError_t e = hipMemcpyAsync(pin + slot * STAGE_CHUNK, s + k * STAGE_CHUNK, len_of(k),
-                                          hipMemcpyDeviceToHost, R.st);
-            if (e == hipSuccess) e = hipEventRecord(ev[slot], R.st);
+                                          hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipEventRecord(ev[slot], st);
             return e == hipSuccess ? 0 : PCX_EHIP;
         },
         [&](int slot) { return hipEventSynchronize(ev[slot]) == hipSuccess ? 0 : PCX_EHIP; },
@@ -454,8 +464,74 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
             const size_t len = len_of(k), a = len * t / T, b = len * (t + 1) / T;
             if (b > a) memcpy(d + k * STAGE_CHUNK + a, pin + slot * STAGE_CHUNK + a, b - a);
         });
-    if (rc) R.hip(hipErrorUnknown, "staged D2H of an output");
 }
+
+void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
+    if (!stage_slots(R.c)) R.hip(hipErrorOutOfMemory, "hipHostMalloc(staging)");
+    if (d2h_staged_on(R.c, R.st, dst, src, bytes)) R.hip(hipErrorUnknown, "staged D2H of an output");
+}
+
+// The host path's `filled` is complete once k_wcd has run (M_WCD); its copy back (33 GB at C5)
+// then runs on the context's side stream, behind an event on the main one, while the device
+// computes the covariance and the rest -- instead of after all of it.  Joined before the call
+// returns (the destructor too, on a failure path: the main stream has drained by then).
+struct EarlyD2H {
+    std::thread th;
+    hipEvent_t ready = nullptr;
+    int rc = 0;
+    void start(Run& R, void* dst, const void* src, size_t bytes) {
+        pcx_ctx* c = R.c;
+        if (!c->side_stream) R.hip(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking), "side stream");
+        if (!stage_slots(c)) R.hip(hipErrorOutOfMemory, "hipHostMalloc(staging)");
+        R.hip(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "hipEventCreate");
+        R.hip(hipEventRecord(ready, R.st), "hipEventRecord");
+        R.hip(hipStreamWaitEvent(c->side_stream, ready, 0), "hipStreamWaitEvent");
+        th = std::thread([this, c, dst, src, bytes] { rc = d2h_staged_on(c, c->side_stream, dst, src, bytes); });
+    }
+    int join() {
+        if (th.joinable()) th.join();
+        if (ready) (void)hipEventDestroy(ready);
+        ready = nullptr;
+        return rc;
+    }
+    ~EarlyD2H() { join(); }
+};
+
+// the reports' H2D in row chunks, each followed by an event, so that host threads can rewrite the
+// chunks already copied (the in-place `original`) while the later ones are in flight.  A thread
+// waits until chunk k's event has been recorded (an unrecorded event reads as complete), then on
+// the event; abort() (a failure while issuing) releases the waiters.
+struct ChunkGate {
+    std::vector<hipEvent_t> ev;
+    std::vector<int64_t> row0;  // chunk k: rows [row0[k], row0[k + 1])
+    std::mutex mu;
+    std::condition_variable cv;
+    int recorded = 0;
+    bool aborted = false;
+    int nchunks() const { return (int)ev.size(); }
+    void mark(int k) {
+        std::lock_guard<std::mutex> lk(mu);
+        recorded = k + 1;
+        cv.notify_all();
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
+    }
+    bool wait(int k) {  // false: aborted
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return recorded > k || aborted; });
+            if (recorded <= k) return false;
+        }
+        return hipEventSynchronize(ev[k]) == hipSuccess;
+    }
+    ~ChunkGate() {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
 
 // result["original"] for host memory, built by host threads from the caller's reports while the
 // device works (started once the reports' H2D has drained), instead of copied back (33 GB of D2H at
@@ -469,8 +545,9 @@ void d2h_staged(Run& R, void* dst, const void* src, size_t bytes) {
 // host_threads() threads; a small matrix runs on the calling thread.
 struct HostOriginal {
     std::vector<std::thread> th;
+    // gate: the reports' H2D chunks (in place: a chunk is rewritten only once it has been copied)
     void start(const double* rep_in, double* original, int64_t n_rows, int64_t E, const std::vector<uint8_t>& scaled,
-               const double* lo, const double* hi, bool int_dtype) {
+               const double* lo, const double* hi, bool int_dtype, ChunkGate* gate = nullptr) {
         std::vector<int32_t> sc;
         std::vector<double> lr;
         for (int64_t j = 0; j < (int64_t)scaled.size(); j++)
@@ -499,6 +576,17 @@ struct HostOriginal {
             }
         };
         const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n_rows / 1024));
+        if (gate) {  // every thread takes its share of each chunk as the chunk lands
+            for (int t = 0; t < T; t++)
+                th.emplace_back([=] {
+                    for (int k = 0; k < gate->nchunks(); k++) {
+                        if (!gate->wait(k)) return;  // (the call fails: the array is unspecified)
+                        const int64_t a = gate->row0[k], n = gate->row0[k + 1] - a;
+                        body(a + n * t / T, a + n * (t + 1) / T);
+                    }
+                });
+            return;
+        }
         if (T <= 1 || n_rows * E < ((int64_t)1 << 20)) {
             body(0, n_rows);
             return;
@@ -898,7 +986,9 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
     c->progress_wait.store(0, std::memory_order_relaxed);
     const bool host = p->mem_kind == PCX_MEM_HOST;
     const bool filled_input = entry >= 2;  // wpca / lie_detector / nonconformity: reports already filled
+    ChunkGate gate;          // (outlives host_orig: its threads wait on it)
     HostOriginal host_orig;  // (joined on every exit path, before the caller's arrays are returned)
+    EarlyD2H early_filled;
     try {
         Io io(c);
         // ---- scaled events (host view)
@@ -927,10 +1017,52 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         if (n_scaled) R.hip(hipMemcpyAsync(w->scols, scols.data(), n_scaled * 4, hipMemcpyHostToDevice, R.st), "H2D");
         R.hip(hipMemcpyAsync(w->sidx, sidx.data(), E * 4, hipMemcpyHostToDevice, R.st), "H2D");
 
+        // ---- result["original"] on the host (HostOriginal): a new array is built from the caller's
+        // reports (only read) beside their H2D; in place, once the H2D has drained (below)
+        const bool cons = entry == 0, lie = entry == 3;
+        const bool inplace = (cons || entry == 1) && r->original &&
+                             (const void*)r->original == (const void*)p->reports;
+        const bool host_orig_on = host && (cons || entry == 1) && r->original;
+#ifndef PCX_ORIG_EARLY
+#define PCX_ORIG_EARLY 1
+#endif
+        if (host_orig_on && !inplace && PCX_ORIG_EARLY)
+            host_orig.start(p->reports, r->original, n_rows, E, sc_h, p->lo, p->hi, p->int_dtype != 0);
+        // in place: the reports copied in row chunks, each rewritten by the host threads once it
+        // has landed (the whole H2D drained first measured 1.44 s against 1.33 s for a new array)
+        const bool gated = host_orig_on && inplace && PCX_ORIG_EARLY && (size_t)(n_rows * E) * 8 >= STAGE_MIN;
+        if (gated) {
+            const int K = 16;
+            gate.ev.assign(K, nullptr);
+            for (int k = 0; k <= K; k++) gate.row0.push_back(n_rows * k / K);
+            for (auto& e : gate.ev) R.hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+            host_orig.start(p->reports, r->original, n_rows, E, sc_h, p->lo, p->hi, p->int_dtype != 0, &gate);
+        }
+
         // ---- inputs / outputs on the device
         pcx_mat m{};
         R.mark(M_H2D);
-        const double* reports = host ? io.dev(R, p->reports, n_rows * E) : p->reports;
+        const double* reports = p->reports;
+        if (host && gated) {
+            double* d = (double*)io.get(R, (size_t)(n_rows * E) * 8, "hipMalloc(input)");
+            struct Abort {  // a failure while issuing releases the waiting threads
+                ChunkGate& g;
+                bool done = false;
+                ~Abort() {
+                    if (!done) g.abort();
+                }
+            } ab{gate};
+            for (int k = 0; k < gate.nchunks(); k++) {
+                const int64_t a = gate.row0[k] * E, n = gate.row0[k + 1] * E - a;
+                R.hip(hipMemcpyAsync(d + a, p->reports + a, n * 8, hipMemcpyHostToDevice, R.st), "H2D");
+                R.hip(hipEventRecord(gate.ev[k], R.st), "hipEventRecord");
+                gate.mark(k);
+            }
+            ab.done = true;
+            reports = d;
+        } else if (host) {
+            reports = io.dev(R, p->reports, n_rows * E);
+        }
         const double* rep_raw = host ? io.dev(R, p->reputation, N) : p->reputation;
         const uint8_t* scaled = host ? io.dev(R, sc_in, E) : sc_in;
         const double* lo = sc_in ? (host ? io.dev(R, p->lo, E) : p->lo) : nullptr;
@@ -954,7 +1086,6 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             outs.push_back({user, d, n});
             return d;
         };
-        const bool cons = entry == 0, lie = entry == 3;
         m.old_rep = (cons || lie) ? out(r->old_rep, n_rows) : nullptr;
         m.this_rep = (cons || lie) ? out(r->this_rep, n_rows) : nullptr;
         m.smooth_rep = (cons || lie) ? out(r->smooth_rep, n_rows) : nullptr;
@@ -976,16 +1107,13 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         // the caller's array rescaled in place (__init__.py:121, 266-269, 584, Q2) -- rescale the
         // scaled columns in place instead of writing a copy of every column (host memory: the
         // device copy of the reports is rescaled and copied back into the caller's array)
-        const bool inplace = (cons || entry == 1) && r->original &&
-                             (const void*)r->original == (const void*)p->reports;
         // host memory: `original` is built on the host from the caller's reports while the device
         // works (HostOriginal), not written by the device and copied back
-        const bool host_orig_on = host && (cons || entry == 1) && r->original;
         m.original = (cons || entry == 1) && !inplace && !host_orig_on ? out(r->original, n_rows * E) : nullptr;
         m.orig_inplace = inplace ? 1 : 0;  // (host: the device copy of the reports, for later stages)
         m.rescaled = 0;
         m.filled = (cons || entry == 1) ? out(r->filled, n_rows * E) : nullptr;
-        if (host_orig_on) {  // once the reports' H2D has drained (the caller's array is rewritten in place)
+        if (host_orig_on && !gated && (inplace || !PCX_ORIG_EARLY)) {  // once the reports' H2D has drained (the caller's array is rewritten in place)
             hipEvent_t ev = nullptr;
             R.hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
             struct EvGuard {
@@ -1180,6 +1308,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                                 : 0;
                 m.Fg = m.compact ? (double*)w->fg.p : nullptr;
                 m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
+                // the row weights' balanced base-256 digits for the int8-MFMA outcome sums (M_OUTCOMES)
+                m.wdig = m.compact && w->grow(w->wdig, (size_t)w->wcd_rows * 16) ? (int8_t*)w->wdig.p : nullptr;
                 // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
                 // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
                 // (it reads the general positions' F - mu from the compact Fg, so k_wcd writes no wcd)
@@ -1227,6 +1357,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 }
                 R.stage(m, M_WCD);
                 mats_written = true;
+                if (host && cons && m.filled && (size_t)(n_rows * E) * 8 >= STAGE_MIN)
+                    early_filled.start(R, r->filled, m.filled, (size_t)(n_rows * E) * 8);
                 m.rescaled = m.orig_inplace;  // later stages read the scaled columns rescaled already
                 R.stage(m, M_COV);
                 R.stage(m, M_COV_I8);
@@ -1348,8 +1480,11 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
             if ((size_t)o.n * 8 < STAGE_MIN)
                 R.hip(hipMemcpyAsync(o.user, o.dev, o.n * 8, hipMemcpyDeviceToHost, R.st), "D2H output");
         }
+        const bool early = early_filled.th.joinable();
+        if (early && early_filled.join()) R.hip(hipErrorUnknown, "staged D2H of filled");
         for (auto& o : outs)
-            if ((size_t)o.n * 8 >= STAGE_MIN) d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
+            if ((size_t)o.n * 8 >= STAGE_MIN && !(early && o.user == r->filled))
+                d2h_staged(R, o.user, o.dev, (size_t)o.n * 8);
         R.mark(-1);
         R.sync();
         host_orig.join();

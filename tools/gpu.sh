@@ -125,6 +125,12 @@ for STEP in "$@"; do
         PCX_LIB=$L timeout -k 10 200 python -u tools/c5_shard_latency.py 8 5 > $O/abs.json 2> $O/abs.err || { echo "ab_shard rc=$? ($L)"; tail -3 $O/abs.err; exit 28; }
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('%-24s shard %.2f ms; ' % (sys.argv[2], d['latency_ms']) + ' '.join('%s %.2f' % (k[2:], v) for k, v in list(d.get('stage_ms', {}).items())[:10]))" $O/abs.json "$L"
       done; done ;;
+    ab_host=*)  # the host-memory path's latency (tools/c5_host_latency.py) of several libpcx builds
+      IFS=, read -ra LIBS <<< "${STEP#ab_host=}"
+      for L in "${LIBS[@]}"; do
+        PCX_LIB=$L timeout -k 10 300 python -u tools/c5_host_latency.py 2 > $O/abh.json 2> $O/abh.err || { echo "ab_host rc=$? ($L)"; tail -5 $O/abh.err; exit 32; }
+        echo "== $L"; grep '"mode"' $O/abh.err | cut -c1-220
+      done ;;
     i8bench)
       timeout -k 10 300 tools/i8bench/i8bench 5 > $O/i8bench.txt 2>&1 || { echo "i8bench rc=$?"; tail -20 $O/i8bench.txt; exit 24; }
       cat $O/i8bench.txt ;;
