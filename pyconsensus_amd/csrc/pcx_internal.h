@@ -114,6 +114,7 @@ typedef struct {
     double*  Fg;                  /* [wcd_rows][128 cov_jb] the filled F of the general positions (or NULL) */
     uint16_t* nam;                /* [wcd_rows/16][wcd_ld] missing-report bits of 16 rows per position */
     int32_t  compact;             /* M_GEMV2 / M_OUTCOMES read Fg, zB and nam, not the reports      */
+    int8_t*  wdig;                /* [wcd_rows/16][16 digits][16 rows] a row weight's base-256 digits (or NULL) */
     int32_t  orig_inplace;        /* result.original aliases the reports: rescale the scaled columns
                                      in place (k_wcd / k_matrices), nothing else written (Q2)       */
     int32_t  rescaled;            /* set once that ran: later readers take the scaled columns as
@@ -360,6 +361,8 @@ struct pcx_ctx {
     // pinned buffer of the host path's small outputs (one copy back per call)
     void* pin_small = nullptr;
     size_t pin_small_bytes = 0;
+    // the host path's copy of `filled` back, run beside the device work that follows k_wcd
+    hipStream_t side_stream = nullptr;
 };
 
 namespace pcx {
