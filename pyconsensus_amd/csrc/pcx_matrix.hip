@@ -28,6 +28,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -2445,6 +2446,21 @@ __device__ __forceinline__ uint32_t sub4_stride4(uint32_t M, int j) {
     return (v | (v >> 6)) & 0x0Fu;
 }
 
+// m.wdig: a 256-byte header (the largest |w| bits of weight vector v at word v, zeroed before each
+// pass), then vector v's digits at 256 + v wcd_rows 16 bytes
+__device__ __forceinline__ uint64_t* wdig_max(const pcx_mat& m) { return reinterpret_cast<uint64_t*>(m.wdig); }
+__device__ __forceinline__ int8_t* wdig_vec(const pcx_mat& m, int v) { return m.wdig + 256 + (int64_t)v * m.wcd_rows * 16; }
+__device__ __forceinline__ double wdig_maxabs(const pcx_mat& m, int v) {
+    return __longlong_as_double((long long)wdig_max(m)[v]);
+}
+// the digit passes ran (m.wdig set by the host) and every weight of vectors 0 .. nv - 1 is finite
+__device__ __forceinline__ bool wdig_ok(const pcx_mat& m, int nv) {
+    if (!m.wdig) return false;
+    bool ok = true;
+    for (int v = 0; v < nv; v++) ok = ok && __builtin_isfinite(wdig_maxabs(m, v));
+    return ok;
+}
+
 // M_GEMV2 from the compact sources (m.compact): thread = one wcd position (general positions
 // read the filled values Fg, grid positions F = 1 + z / 2 from the 2-bit codes), 16-row groups;
 // the same per-row products and compensated sums as k_gemv2, into the same partial slots
@@ -2455,6 +2471,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = (GRID ? (int)gb : 0) + blockIdx.x * BT + threadIdx.x;
     const int E = (int)m.n_events;
+    if (GRID && wdig_ok(m, 2)) return;  // (k_gemv2_mf summed them)
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     const double* n1 = m.rowv + RV_N1 * m.n_rows;
@@ -2821,7 +2838,7 @@ __global__ void __launch_bounds__(BT) k_outcomes(pcx_mat m) {
 // grid wave runs the body: the table takes all 64)
 template <bool GRID>
 __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t r0, int64_t r1, dd S, dd* tab,
-                                                bool live) {
+                                                bool live, bool mf = false) {
     const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
     const int E = (int)m.n_events;
     const double* sm = m.rowv + RV_SMOOTH * m.n_rows;
@@ -2843,6 +2860,7 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     const bool general = !GRID;
     const int64_t qn = live ? q : 0;  // (a lane past the positions reads a valid word, unused)
     const bool scl = general && (!live || (m.scaled && m.scaled[c]));
+    if (mf && scl) return;  // (k_outcomes_mf summed its missing rows' weight)
     if (general && __all(scl)) {  // (a wave of scaled events only: the subset tables need every lane)
         // a scaled event's raw is its weighted median (:520-523) and its certainty comes from
         // the selection (:540-546): only np.dot(smooth_rep, na_mat) (:559) is read here, from
@@ -3179,6 +3197,9 @@ __device__ void outcomes_grid_block(const pcx_mat& m, int q, int64_t r0, int64_t
 __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
+    // k_outcomes_mf ran (finite weights): what is left are the general binary positions
+    const bool mf = wdig_ok(m, 1);
+    if (mf && (q & ~(WAVE - 1)) >= gb) return;  // (wave-uniform)
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     // the chunk's weight total for the grid positions, by every lane of a wave holding one
@@ -3194,7 +3215,233 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     if (q >= gb)  // (gb is a multiple of 128: a wave is all grid or all general)
         outcomes_c_body<true>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events);
     else
-        outcomes_c_body<false>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events);
+        outcomes_c_body<false>(m, q, r0, r1, S, tabs[threadIdx.x / WAVE], q < m.n_events, mf);
+}
+
+// ---- M_OUTCOMES on int8 MFMA.  Every sum of the pass over a grid position is a weighted count --
+// sum w [z = 1] (b15), sum w [z = 2] (b2), sum w [missing] (pc) and the chunk's sum w (S), whence
+// b1 = S - b15 - b2 and raw = S + (b15 + 2 b2) / 2 -- and a general scaled position needs pc only:
+// a 0/1 matrix (positions x rows) times the weight vector.  The weights are held as fixed-point
+// integers round(w 2^s) (|w| 2^s < 2^125: s from the rank's largest |w|), sixteen balanced base-256
+// digits each (k_wdigits), so every 0/1 x digit product is an exact v_mfma_i32_16x16x64_i8 (16
+// positions x 16 digits x 64 rows) and a chunk's sums are exact integers per digit (|sum| <= 128 x
+// rows < 2^31: chunks of at most 2^24 rows), then one double-double per quantity.  Against the
+// fp64 subset tables: the same sums to ~2^-100 of the largest weight (those were plain fp64 sums,
+// raw a compensated one), the 0/1 operands unpacked from the 2-bit codes and the missing bits
+// beside the MFMAs.  A non-finite weight (NaN x 0 must reach the sums as in np.dot) leaves the pass
+// to k_outcomes_c.
+__global__ void __launch_bounds__(BT) k_wmax(pcx_mat m, const double* w, int v) {
+    uint64_t mx = 0;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
+        const uint64_t b = (uint64_t)__double_as_longlong(fabs(w[i]));  // (a NaN's bits exceed inf's)
+        mx = b > mx ? b : mx;
+    }
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)mx, d, WAVE);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & (WAVE - 1)) == 0 && mx) atomicMax((unsigned long long*)&wdig_max(m)[v], (unsigned long long)mx);
+}
+
+__device__ __forceinline__ int wdig_scale(double mxw) { return mxw > 0.0 ? 124 - ilogb(mxw) : 0; }
+
+// digits n = 0..15 of row i at wdig_vec(v)[(i / 16) 256 + 16 n + i % 16]: one 16-byte MFMA B fragment
+// per (16 rows, digit); rows past n_rows (to the next multiple of 16) zero
+__global__ void __launch_bounds__(BT) k_wdigits(pcx_mat m, const double* w, int v) {
+    const double mxw = wdig_maxabs(m, v);
+    if (!__builtin_isfinite(mxw)) return;
+    const int s = wdig_scale(mxw);
+    int8_t* dst = wdig_vec(m, v);
+    const int64_t rows = (m.n_rows + 15) / 16 * 16;
+    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < rows; i += (int64_t)gridDim.x * BT) {
+        double t = i < m.n_rows ? rint(ldexp(w[i], s)) : 0.0;  // an integer, |t| < 2^125
+        int8_t* o = dst + (i >> 4) * 256 + (i & 15);
+        // t = sum d_n 256^n, d_n in [-128, 127]: every step exact (t mod 256 and (t - d) / 256 are
+        // integers a double holds)
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const double r = t - 256.0 * floor(t * (1.0 / 256.0));  // [0, 256)
+            const double d = r >= 128.0 ? r - 256.0 : r;
+            o[16 * n] = (int8_t)(int)d;
+            t = (t - d) * (1.0 / 256.0);
+        }
+    }
+}
+
+// digit sums (lane: digit lc of four positions) -> the double-double of sum_n v_n 256^n 2^-s over
+// the 16 lanes of the lane's row of the wave (every lane of that row gets it)
+__device__ __forceinline__ dd wdig_value(int64_t v, int lc, int s) {
+    dd a{ldexp((double)v, 8 * lc - s), 0.0};  // exact (|v| < 2^53)
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) a = dd_add(a, dd{__shfl_xor(a.hi, d, WAVE), __shfl_xor(a.lo, d, WAVE)});
+    return a;
+}
+
+// the 0/1 fragment of a lane's 16 missing bits (byte r = bit r)
+__device__ __forceinline__ v4i wdig_bits16(uint32_t M) {
+    v4i z;
+#pragma unroll
+    for (int k = 0; k < 4; k++) z[k] = (int)((((M >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u);
+    return z;
+}
+
+// one wave per 16 positions and row chunk (the chunks of k_outcomes_c / k_col_finish); gb is a
+// multiple of 128, so a wave's positions are all general or all grid
+__global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
+    if (!wdig_ok(m, 1)) return;
+    const int sc = wdig_scale(wdig_maxabs(m, 0));
+    const int E = (int)m.n_events;
+    const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
+    const int lane = threadIdx.x & (WAVE - 1), lc = lane & 15, lg = lane >> 4;
+    const int q0 = (blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE) * 16;
+    if (q0 >= E) return;  // (wave-uniform)
+    const bool grid = q0 >= gb;
+    const int qa = q0 + lc;  // this lane's A row (position); lg: its 16-row group of the 64-row k-step
+    const bool alive = qa < E;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    // (an empty trailing chunk is [n_rows, n_rows): no group, also when n_rows % 16 != 0)
+    const int64_t g0 = r0 / 16, gf = r0 < r1 ? (r1 + 15) / 16 : g0;
+    const uint32_t* zb = zb_packed(m) + (grid && alive ? qa - gb : 0);
+    const uint16_t* nm = m.nam + (alive ? qa : 0);
+    const v4i* wd = reinterpret_cast<const v4i*>(wdig_vec(m, 0)) + lc;  // + 16 group: digit lc of 16 rows
+    constexpr uint32_t O = 0x01010101u, M2 = 0x03030303u;
+    const v4i ones{(int)O, (int)O, (int)O, (int)O};
+    v4i a1{0, 0, 0, 0}, a2{0, 0, 0, 0}, am{0, 0, 0, 0}, a0{0, 0, 0, 0};
+    uint32_t c15 = 0, c2 = 0;
+    // U k-steps' loads issued together, then their MFMAs (the loads' latency, not the MFMAs, is
+    // the chain here)
+    constexpr int U = 4;
+    for (int64_t gs = g0; gs < gf; gs += 4 * U) {
+        v4i B[U];
+        uint32_t P[U], M[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t g = gs + 4 * u + lg;
+            const bool in = g < gf;
+            B[u] = in ? wd[g * 16] : v4i{0, 0, 0, 0};
+            M[u] = in && alive ? (uint32_t)nm[g * ld] : 0u;
+            P[u] = in && alive && grid ? zb[g * m.zq] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (gs + 4 * u >= gf) break;  // (wave-uniform)
+            am = __builtin_amdgcn_mfma_i32_16x16x64_i8(wdig_bits16(M[u]), B[u], am, 0, 0, 0);
+            if (grid) {
+                v4i z1, z2;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t zk = (P[u] >> (2 * k)) & M2;
+                    z1[k] = (int)(zk & O);
+                    z2[k] = (int)((zk >> 1) & O);
+                }
+                a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(z1, B[u], a1, 0, 0, 0);
+                a2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(z2, B[u], a2, 0, 0, 0);
+                a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, B[u], a0, 0, 0, 0);
+                c15 += __popc(P[u] & 0x55555555u);
+                c2 += __popc(P[u] & 0xAAAAAAAAu);
+            }
+        }
+    }
+    // counts of position lc over the four row groups
+    c15 += __shfl_xor(c15, 16, WAVE);
+    c15 += __shfl_xor(c15, 32, WAVE);
+    c2 += __shfl_xor(c2, 16, WAVE);
+    c2 += __shfl_xor(c2, 32, WAVE);
+    // D layout: lane (lc, lg) element r = position 4 lg + r, digit lc
+    const double rows = (double)(r1 > r0 ? r1 - r0 : 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int p = 4 * lg + r, q = q0 + p;
+        const dd pc = wdig_value(am[r], lc, sc);
+        dd raw{0.0, 0.0}, b1{0.0, 0.0}, b15{0.0, 0.0}, b2{0.0, 0.0};
+        uint32_t n15 = 0, n2 = 0;
+        if (grid) {  // (wave-uniform)
+            const int64_t S = a0[r], v15 = a1[r], v2 = a2[r];
+            raw = wdig_value(2 * S + v15 + 2 * v2, lc, sc + 1);  // (S + (b15 + 2 b2) / 2)
+            b1 = wdig_value(S - v15 - v2, lc, sc);
+            b15 = wdig_value(v15, lc, sc);
+            b2 = wdig_value(v2, lc, sc);
+            n15 = (uint32_t)__shfl((int)c15, p, WAVE);
+            n2 = (uint32_t)__shfl((int)c2, p, WAVE);
+        }
+        if (lc != 0 || q >= E) continue;
+        const int c = m.cov_perm[q];
+        double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
+        if (!grid) {
+            if (m.scaled && m.scaled[c]) st_dd(pp + 2, {dd_to_double(pc), 0.0});
+            continue;
+        }
+        st_dd(pp + 0, raw);
+        st_dd(pp + 2, {dd_to_double(pc), 0.0});
+        st_dd(pp + 4, {dd_to_double(b1), 0.0});
+        st_dd(pp + 6, {dd_to_double(b15), 0.0});
+        st_dd(pp + 8, {dd_to_double(b2), 0.0});
+        st_dd(pp + 10, {rows - (double)n15 - (double)n2, 0.0});
+        st_dd(pp + 12, {(double)n15, 0.0});
+        st_dd(pp + 14, {(double)n2, 0.0});
+    }
+}
+
+// M_GEMV2's grid positions on int8 MFMA (as k_outcomes_mf): sum v F = S_v + (sum v z) / 2 for the
+// weight vectors v = normalize(set1), normalize(set2) -- the 2-bit codes z in {0, 1, 2} are the A
+// operand as they are, the weights' digits (vectors 0 and 1) the B operands, and all-ones A rows give
+// the chunk totals S_v
+__global__ void __launch_bounds__(BT) k_gemv2_mf(pcx_mat m) {
+    if (!wdig_ok(m, 2)) return;
+    const int s1 = wdig_scale(wdig_maxabs(m, 0)), s2 = wdig_scale(wdig_maxabs(m, 1));
+    const int E = (int)m.n_events;
+    const int64_t gb = (int64_t)m.cov_jb * CT;
+    const int lane = threadIdx.x & (WAVE - 1), lc = lane & 15, lg = lane >> 4;
+    const int q0 = (int)gb + (blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE) * 16;
+    if (q0 >= E) return;  // (wave-uniform)
+    const int qa = q0 + lc;
+    const bool alive = qa < E;
+    int64_t r0, r1;
+    row_range(m, r0, r1, 16);
+    // (an empty trailing chunk is [n_rows, n_rows): no group, also when n_rows % 16 != 0)
+    const int64_t g0 = r0 / 16, gf = r0 < r1 ? (r1 + 15) / 16 : g0;
+    const uint32_t* zb = zb_packed(m) + (alive ? qa - gb : 0);
+    const v4i* w1 = reinterpret_cast<const v4i*>(wdig_vec(m, 0)) + lc;
+    const v4i* w2 = reinterpret_cast<const v4i*>(wdig_vec(m, 1)) + lc;
+    constexpr uint32_t O = 0x01010101u, M2 = 0x03030303u;
+    const v4i ones{(int)O, (int)O, (int)O, (int)O};
+    v4i z1{0, 0, 0, 0}, z2{0, 0, 0, 0}, t1{0, 0, 0, 0}, t2{0, 0, 0, 0};
+    constexpr int U = 4;
+    for (int64_t gs = g0; gs < gf; gs += 4 * U) {
+        v4i B1[U], B2[U];
+        uint32_t P[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t g = gs + 4 * u + lg;
+            const bool in = g < gf;
+            B1[u] = in ? w1[g * 16] : v4i{0, 0, 0, 0};
+            B2[u] = in ? w2[g * 16] : v4i{0, 0, 0, 0};
+            P[u] = in && alive ? zb[g * m.zq] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (gs + 4 * u >= gf) break;  // (wave-uniform)
+            v4i z;
+#pragma unroll
+            for (int k = 0; k < 4; k++) z[k] = (int)((P[u] >> (2 * k)) & M2);
+            z1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(z, B1[u], z1, 0, 0, 0);
+            z2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(z, B2[u], z2, 0, 0, 0);
+            t1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, B1[u], t1, 0, 0, 0);
+            t2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, B2[u], t2, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int q = q0 + 4 * lg + r;
+        const dd d1 = wdig_value(2 * (int64_t)t1[r] + z1[r], lc, s1 + 1);
+        const dd d2 = wdig_value(2 * (int64_t)t2[r] + z2[r], lc, s2 + 1);
+        if (lc != 0 || q >= E) continue;
+        double* pp = m.part + ((int64_t)blockIdx.y * E + m.cov_perm[q]) * 16;
+        st_dd(pp + 0, d1);
+        st_dd(pp + 2, d2);
+    }
 }
 
 // certainty of an event no reporter matched (:542): NaN on the PCA path (smooth_rep is a
@@ -5659,6 +5906,25 @@ static void launch_compact(KG kgen, KR kgrid, const pcx_mat& m, hipStream_t st) 
     if (E > gb) hipLaunchKernelGGL(kgrid, dim3((unsigned)((E - gb + BT - 1) / BT), m.col_blocks), dim3(BT), 0, st, m);
 }
 
+// the int8-MFMA weighted counts (k_outcomes_mf, k_gemv2_mf) need row chunks of at most 2^24 rows:
+// their int32 digit sums are then exact
+static bool wdig_fits(const pcx_mat& m) {
+    if (!m.wdig) return false;
+    const int64_t per = ((m.n_rows + m.col_blocks - 1) / m.col_blocks + 15) / 16 * 16;
+    return per <= ((int64_t)1 << 24);
+}
+// the largest |w| and then the digits of each weight vector (vector v = the v-th of ws)
+static void wdig_prepare(const pcx_mat& m, std::initializer_list<const double*> ws, hipStream_t st) {
+    (void)hipMemsetAsync(m.wdig, 0, 256, st);
+    const int64_t rb = std::max<int64_t>(1, (m.n_rows + BT - 1) / BT);
+    int v = 0;
+    for (const double* w : ws) {
+        hipLaunchKernelGGL(k_wmax, dim3((unsigned)std::min<int64_t>(rb, 1024)), dim3(BT), 0, st, m, w, v);
+        hipLaunchKernelGGL(k_wdigits, dim3((unsigned)std::min<int64_t>(rb + 1, 4096)), dim3(BT), 0, st, m, w, v);
+        v++;
+    }
+}
+
 hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
     const int E = (int)m.n_events;
     const int ceb = (E + BT - 1) / BT;
@@ -5871,7 +6137,16 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
         case M_GEMV2:
             hipLaunchKernelGGL(k_nweights, dim3(rg), dim3(BT), 0, st, m);
             if (m.compact && m.Fg && m.nam && m.zB)
-                launch_compact(k_gemv2_c<false>, k_gemv2_c<true>, m, st);
+            {
+                pcx_mat mm = m;
+                if (!wdig_fits(m)) mm.wdig = nullptr;
+                const int64_t gbp = std::min<int64_t>((int64_t)m.cov_jb * CT, E);
+                if (mm.wdig && E > gbp) {  // the grid positions on int8 MFMA (k_gemv2_c<true> then exits)
+                    wdig_prepare(mm, {m.rowv + RV_N1 * m.n_rows, m.rowv + RV_N2 * m.n_rows}, st);
+                    hipLaunchKernelGGL(k_gemv2_mf, dim3((unsigned)((E - gbp + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
+                }
+                launch_compact(k_gemv2_c<false>, k_gemv2_c<true>, mm, st);
+            }
             else
                 hipLaunchKernelGGL(k_gemv2, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 2, 4, 0);
@@ -5895,9 +6170,16 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
             hipLaunchKernelGGL(k_smooth, dim3(rg), dim3(BT), 0, st, m);
             break;
         case M_OUTCOMES:
-            if (m.compact && m.Fg && m.nam && m.zB)
-                hipLaunchKernelGGL(k_outcomes_c, colgrid, dim3(BT), 0, st, m);
-            else
+            if (m.compact && m.Fg && m.nam && m.zB) {
+                // the int8-MFMA sums when the chunks keep them int32-exact (<= 2^24 rows)
+                pcx_mat mm = m;
+                if (!wdig_fits(m)) mm.wdig = nullptr;
+                if (mm.wdig) {
+                    wdig_prepare(mm, {m.rowv + RV_SMOOTH * m.n_rows}, st);
+                    hipLaunchKernelGGL(k_outcomes_mf, dim3((unsigned)((E + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
+                }
+                hipLaunchKernelGGL(k_outcomes_c, colgrid, dim3(BT), 0, st, mm);
+            } else
                 hipLaunchKernelGGL(k_outcomes, colgrid, dim3(BT), 0, st, m);
             hipLaunchKernelGGL(k_col_finish, dim3((E + BT / WAVE - 1) / (BT / WAVE)), dim3(BT), 0, st, m, m.col_blocks, 8, 6, 0);
             break;

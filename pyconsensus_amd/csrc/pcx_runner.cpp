@@ -1309,7 +1309,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.Fg = m.compact ? (double*)w->fg.p : nullptr;
                 m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
                 // the row weights' balanced base-256 digits for the int8-MFMA outcome sums (M_OUTCOMES)
-                m.wdig = m.compact && w->grow(w->wdig, (size_t)w->wcd_rows * 16) ? (int8_t*)w->wdig.p : nullptr;
+                // (a 256-byte header, then two vectors' digits: pcx_matrix.hip wdig_vec)
+                m.wdig = m.compact && w->grow(w->wdig, 256 + (size_t)w->wcd_rows * 32) ? (int8_t*)w->wdig.p : nullptr;
                 // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
                 // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
                 // (it reads the general positions' F - mu from the compact Fg, so k_wcd writes no wcd)
