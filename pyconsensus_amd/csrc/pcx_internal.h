@@ -114,6 +114,7 @@ typedef struct {
     double*  Fg;                  /* [wcd_rows][128 cov_jb] the filled F of the general positions (or NULL) */
     uint16_t* nam;                /* [wcd_rows/16][wcd_ld] missing-report bits of 16 rows per position */
     int32_t  compact;             /* M_GEMV2 / M_OUTCOMES read Fg, zB and nam, not the reports      */
+    uint32_t* zbg;                /* [wcd_rows/16][128] 2-bit codes of the grid events in the general tiles */
     int8_t*  wdig;                /* row weights' base-256 digits, [wcd_rows/16][16][16] per vector (or NULL) */
     int32_t  orig_inplace;        /* result.original aliases the reports: rescale the scaled columns
                                      in place (k_wcd / k_matrices), nothing else written (Q2)       */

@@ -58,7 +58,7 @@ enum row_slot { RV_S = 0, RV_U, RV_THIS, RV_SMOOTH, RV_N1, RV_N2 };
 enum scal_slot { SC_TOK = 0, SC_REP, SC_A1, SC_A1P, SC_A2, SC_A2P, SC_U, SC_UP, SC_AR, SC_ARP, SC_BIGTOK, SC_MAXTOK };
 enum info_slot { IN_BRANCH = 0, IN_PI_ITERS, IN_FLAGS, IN_SEL_ACTIVE, IN_SEL_ARGMAX, IN_PICK1, IN_HARD, IN_SEL_WACTIVE,
                  IN_COV_GENERAL, IN_COV_MIXED, IN_COV_TOK1, IN_SEL_WLIMB, IN_COV_GUARD, IN_COV_GUARD_COLS,
-                 IN_COV_GUARD_BOUND };
+                 IN_COV_GUARD_BOUND };  // (word 15: M_POWER's squaring scratch)
 static_assert((int)IN_COV_GUARD == (int)INFO_COV_GUARD && (int)IN_COV_GUARD_COLS == (int)INFO_COV_GUARD_COLS &&
                   (int)IN_COV_GUARD_BOUND == (int)INFO_COV_GUARD_BOUND,
               "info slots");
@@ -484,6 +484,11 @@ __device__ __forceinline__ double max_nn(double a, double b) {
     return r;
 }
 
+// ---------------------------------------------------------------- covariance operands
+// z in {0, 1, 2} of 16 rows packed into one uint32 (the B operand of k_gemm_i8): row r at bit
+// 8 (r % 4) + 2 (r / 4); zpack_bit(r) is the bit of value 1
+__device__ __forceinline__ uint32_t zpack_bit(int r) { return 1u << (8 * (r & 3) + 2 * (r >> 2)); }
+
 // PCX_M_COLSTATS: present count, sum rep, sum rep*x, zero count, max rep (first row),
 // min/max present value; writes the scaled columns (column-major) into T.  A lane owns a column
 // and walks the rows, so its T column is one contiguous run; the lanes' values go through a
@@ -813,10 +818,6 @@ __device__ __forceinline__ void store_tile(double* out, int64_t ld, int64_t E, i
             }
 }
 
-// ---------------------------------------------------------------- covariance operands
-// z in {0, 1, 2} of 16 rows packed into one uint32 (the B operand of k_gemm_i8): row r at bit
-// 8 (r % 4) + 2 (r / 4); zpack_bit(r) is the bit of value 1
-__device__ __forceinline__ uint32_t zpack_bit(int r) { return 1u << (8 * (r & 3) + 2 * (r >> 2)); }
 __device__ __forceinline__ uint32_t zpack_get(uint32_t P, int r) { return (P >> (8 * (r & 3) + 2 * (r >> 2))) & 3u; }
 __device__ __forceinline__ uint32_t* zb_packed(const pcx_mat& m) { return reinterpret_cast<uint32_t*>(m.zB); }
 
@@ -975,6 +976,12 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
         pos[k] = ok[k] ? m.cov_pos[c] : (c < ld ? c : -1);  // padding positions keep their index
         zc[k] = ok[k] && pos[k] >= gb;
     }
+    // the grid events the general tiles hold (positions [n_general, gb), gb - n_general < 128): their
+    // codes too, into zbg [row / 16][128] (k_outcomes_mf, k_gemv2_mf)
+    const int64_t ngen = m.info[IN_COV_GENERAL];
+    bool zg[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) zg[k] = m.zbg && ok[k] && pos[k] < gb && pos[k] >= ngen && pos[k] >= gb - 128;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
         m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
@@ -987,7 +994,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int64_t g0 = r0; g0 < r1; g0 += 64) {
         const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;  // a multiple of 16 (wcd_rows % 16 == 0)
         for (int q0 = 0; q0 < gn; q0 += 16) {
-            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0}, nb[2] = {0, 0};
+            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0}, nb[2] = {0, 0}, zgw[2] = {0, 0};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
                 double rv[4][2];
@@ -1025,6 +1032,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                                 zb[k] |= (uint32_t)z * zpack_bit(4 * h + u);
                                 zs[k] += tk * z;
                             }
+                            if (zg[k]) zgw[k] |= (uint32_t)(int)((f - 1.0) * 2.0) * zpack_bit(4 * h + u);
                         }
                     }
 #pragma unroll
@@ -1084,6 +1092,8 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     const int64_t o = grp * m.zq + (pos[k] - gb);
                     *(uint4*)(m.zA + o * 16) = uint4{za[k][0], za[k][1], za[k][2], za[k][3]};
                     zb_packed(m)[o] = zb[k];
+                } else if (zg[k]) {
+                    m.zbg[grp * 128 + (pos[k] - (gb - 128))] = zgw[k];
                 }
         }
         __syncthreads();
@@ -2446,6 +2456,9 @@ __device__ __forceinline__ uint32_t sub4_stride4(uint32_t M, int j) {
     return (v | (v >> 6)) & 0x0Fu;
 }
 
+#ifndef PCX_MF_ZBG  // (a build parameter for A/B runs: bit 0 the outcome sums, bit 1 the GEMV2 sums take zbg)
+#define PCX_MF_ZBG 3
+#endif
 // m.wdig: a 256-byte header (the largest |w| bits of weight vector v at word v, zeroed before each
 // pass), then vector v's digits at 256 + v wcd_rows 16 bytes
 __device__ __forceinline__ uint64_t* wdig_max(const pcx_mat& m) { return reinterpret_cast<uint64_t*>(m.wdig); }
@@ -2486,6 +2499,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
     }
     // (every wave of a grid block stays to the end: the block builds the subset tables together)
     if (!GRID && (q >= E || q >= gb)) return;
+    if (!GRID && (PCX_MF_ZBG & 2) && q >= m.info[IN_COV_GENERAL] && m.zbg && wdig_ok(m, 2)) return;  // (k_gemv2_mf: zbg)
     const bool live = q < E;
     const int c = live ? m.cov_perm[q] : -1;
     if (!GRID && c < 0) return;  // (padding)
@@ -2860,7 +2874,8 @@ __device__ __forceinline__ void outcomes_c_body(const pcx_mat& m, int q, int64_t
     const bool general = !GRID;
     const int64_t qn = live ? q : 0;  // (a lane past the positions reads a valid word, unused)
     const bool scl = general && (!live || (m.scaled && m.scaled[c]));
-    if (mf && scl) return;  // (k_outcomes_mf summed its missing rows' weight)
+    // (k_outcomes_mf took the scaled positions' missing rows and the grid events of the general tiles)
+    if (mf && (scl || q >= ((PCX_MF_ZBG & 1) ? m.info[IN_COV_GENERAL] : gb))) return;
     if (general && __all(scl)) {  // (a wave of scaled events only: the subset tables need every lane)
         // a scaled event's raw is its weighted median (:520-523) and its certainty comes from
         // the selection (:540-546): only np.dot(smooth_rep, na_mat) (:559) is read here, from
@@ -3303,9 +3318,15 @@ __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
     row_range(m, r0, r1, 16);
     // (an empty trailing chunk is [n_rows, n_rows): no group, also when n_rows % 16 != 0)
     const int64_t g0 = r0 / 16, gf = r0 < r1 ? (r1 + 15) / 16 : g0;
-    const uint32_t* zb = zb_packed(m) + (grid && alive ? qa - gb : 0);
     const uint16_t* nm = m.nam + (alive ? qa : 0);
     const v4i* wd = reinterpret_cast<const v4i*>(wdig_vec(m, 0)) + lc;  // + 16 group: digit lc of 16 rows
+    // positions [n_general, gb) of the general tiles hold grid events too (the general tiles end at a
+    // multiple of 128): their codes come from zbg (k_wcd)
+    const int64_t ngen = (PCX_MF_ZBG & 1) ? m.info[IN_COV_GENERAL] : gb;
+    const bool lbin = !grid && alive && qa >= ngen;
+    const bool full = grid || q0 + 15 >= ngen;  // (wave-uniform: the code sums run)
+    const uint32_t* zsrc = grid && alive ? zb_packed(m) + (qa - gb) : (lbin ? m.zbg + (qa - (gb - 128)) : nullptr);
+    const int64_t zst = grid ? m.zq : 128;
     constexpr uint32_t O = 0x01010101u, M2 = 0x03030303u;
     const v4i ones{(int)O, (int)O, (int)O, (int)O};
     v4i a1{0, 0, 0, 0}, a2{0, 0, 0, 0}, am{0, 0, 0, 0}, a0{0, 0, 0, 0};
@@ -3322,13 +3343,13 @@ __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
             const bool in = g < gf;
             B[u] = in ? wd[g * 16] : v4i{0, 0, 0, 0};
             M[u] = in && alive ? (uint32_t)nm[g * ld] : 0u;
-            P[u] = in && alive && grid ? zb[g * m.zq] : 0u;
+            P[u] = in && zsrc ? zsrc[g * zst] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (gs + 4 * u >= gf) break;  // (wave-uniform)
             am = __builtin_amdgcn_mfma_i32_16x16x64_i8(wdig_bits16(M[u]), B[u], am, 0, 0, 0);
-            if (grid) {
+            if (full) {
                 v4i z1, z2;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -3357,7 +3378,7 @@ __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
         const dd pc = wdig_value(am[r], lc, sc);
         dd raw{0.0, 0.0}, b1{0.0, 0.0}, b15{0.0, 0.0}, b2{0.0, 0.0};
         uint32_t n15 = 0, n2 = 0;
-        if (grid) {  // (wave-uniform)
+        if (full) {  // (wave-uniform)
             const int64_t S = a0[r], v15 = a1[r], v2 = a2[r];
             raw = wdig_value(2 * S + v15 + 2 * v2, lc, sc + 1);  // (S + (b15 + 2 b2) / 2)
             b1 = wdig_value(S - v15 - v2, lc, sc);
@@ -3369,7 +3390,7 @@ __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
         if (lc != 0 || q >= E) continue;
         const int c = m.cov_perm[q];
         double* pp = m.part + ((int64_t)blockIdx.y * E + c) * 16;
-        if (!grid) {
+        if (!grid && q < ngen) {  // (general off-grid binary positions: k_outcomes_c)
             if (m.scaled && m.scaled[c]) st_dd(pp + 2, {dd_to_double(pc), 0.0});
             continue;
         }
@@ -3394,15 +3415,18 @@ __global__ void __launch_bounds__(BT) k_gemv2_mf(pcx_mat m) {
     const int E = (int)m.n_events;
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int lane = threadIdx.x & (WAVE - 1), lc = lane & 15, lg = lane >> 4;
-    const int q0 = (int)gb + (blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE) * 16;
+    // from the first 16 positions holding a grid event (the general tiles' tail [n_general, gb): zbg)
+    const int64_t ngen = (PCX_MF_ZBG & 2) ? m.info[IN_COV_GENERAL] : gb;
+    const int q0 = (int)(gb > ngen ? ngen / 16 * 16 : gb) + (blockIdx.x * (BT / WAVE) + threadIdx.x / WAVE) * 16;
     if (q0 >= E) return;  // (wave-uniform)
     const int qa = q0 + lc;
-    const bool alive = qa < E;
+    const bool alive = qa < E && qa >= ngen;
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     // (an empty trailing chunk is [n_rows, n_rows): no group, also when n_rows % 16 != 0)
     const int64_t g0 = r0 / 16, gf = r0 < r1 ? (r1 + 15) / 16 : g0;
-    const uint32_t* zb = zb_packed(m) + (alive ? qa - gb : 0);
+    const uint32_t* zb = !alive ? nullptr : (qa >= gb ? zb_packed(m) + (qa - gb) : m.zbg + (qa - (gb - 128)));
+    const int64_t zst = qa >= gb ? m.zq : 128;
     const v4i* w1 = reinterpret_cast<const v4i*>(wdig_vec(m, 0)) + lc;
     const v4i* w2 = reinterpret_cast<const v4i*>(wdig_vec(m, 1)) + lc;
     constexpr uint32_t O = 0x01010101u, M2 = 0x03030303u;
@@ -3418,7 +3442,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_mf(pcx_mat m) {
             const bool in = g < gf;
             B1[u] = in ? w1[g * 16] : v4i{0, 0, 0, 0};
             B2[u] = in ? w2[g * 16] : v4i{0, 0, 0, 0};
-            P[u] = in && alive ? zb[g * m.zq] : 0u;
+            P[u] = in && alive ? zb[g * zst] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -3437,7 +3461,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_mf(pcx_mat m) {
         const int q = q0 + 4 * lg + r;
         const dd d1 = wdig_value(2 * (int64_t)t1[r] + z1[r], lc, s1 + 1);
         const dd d2 = wdig_value(2 * (int64_t)t2[r] + z2[r], lc, s2 + 1);
-        if (lc != 0 || q >= E) continue;
+        if (lc != 0 || q >= E || q < ngen) continue;
         double* pp = m.part + ((int64_t)blockIdx.y * E + m.cov_perm[q]) * 16;
         st_dd(pp + 0, d1);
         st_dd(pp + 2, d2);
@@ -6143,7 +6167,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 const int64_t gbp = std::min<int64_t>((int64_t)m.cov_jb * CT, E);
                 if (mm.wdig && E > gbp) {  // the grid positions on int8 MFMA (k_gemv2_c<true> then exits)
                     wdig_prepare(mm, {m.rowv + RV_N1 * m.n_rows, m.rowv + RV_N2 * m.n_rows}, st);
-                    hipLaunchKernelGGL(k_gemv2_mf, dim3((unsigned)((E - gbp + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
+                    // (from n_general, a device value > gb - 128: the waves past E exit)
+                    const int64_t from = std::max<int64_t>(0, gbp - 128);
+                    hipLaunchKernelGGL(k_gemv2_mf, dim3((unsigned)((E - from + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
                 }
                 launch_compact(k_gemv2_c<false>, k_gemv2_c<true>, mm, st);
             }
@@ -6268,7 +6294,9 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 // between the two working matrices (the same leading eigenvector, gap ratio squared)
                 const double* M = m.C;
                 double* Tm = m.Mw;
-                unsigned long long* mxb = (unsigned long long*)&m.info[8];
+                // (info word 15: free -- word 8 holds the plan's general count, which the compact
+                // passes after this stage read)
+                unsigned long long* mxb = (unsigned long long*)&m.info[15];
                 const int64_t* fl = &m.info[IN_FLAGS];
                 // split-K squaring for E >= 512 when the slabs fit the covariance's (free by now);
                 // smaller E keeps the single pass (the goldens' arithmetic)

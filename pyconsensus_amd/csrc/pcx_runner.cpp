@@ -81,7 +81,7 @@ struct pcx_workspace {
     struct Grow {
         void* p = nullptr;
         size_t bytes = 0;
-    } pgg, zd, pmx, clw, fg, nam, dtok, ze, pgx, wdig;
+    } pgg, zd, pmx, clw, fg, nam, dtok, ze, pgx, wdig, zbg;
     bool grow(Grow& g, size_t need) {
         if (g.bytes >= need) return true;
         if (g.p) (void)hipFree(g.p);
@@ -95,7 +95,7 @@ struct pcx_workspace {
 
     ~pcx_workspace() {
         for (void* p : blocks) (void)hipFree(p);
-        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok, &ze, &pgx, &wdig})
+        for (Grow* g : {&pgg, &zd, &pmx, &clw, &fg, &nam, &dtok, &ze, &pgx, &wdig, &zbg})
             if (g->p) (void)hipFree(g->p);
     }
 };
@@ -1310,7 +1310,13 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.nam = m.compact ? (uint16_t*)w->nam.p : nullptr;
                 // the row weights' balanced base-256 digits for the int8-MFMA outcome sums (M_OUTCOMES)
                 // (a 256-byte header, then two vectors' digits: pcx_matrix.hip wdig_vec)
-                m.wdig = m.compact && w->grow(w->wdig, 256 + (size_t)w->wcd_rows * 32) ? (int8_t*)w->wdig.p : nullptr;
+                // (and the codes of the grid events the general tiles end with, positions [n_general, gb))
+                m.zbg = m.compact && gb >= 128 && w->grow(w->zbg, (size_t)(w->wcd_rows / 16) * 128 * 4)
+                            ? (uint32_t*)w->zbg.p
+                            : nullptr;
+                m.wdig = m.compact && (gb == 0 || m.zbg) && w->grow(w->wdig, 256 + (size_t)w->wcd_rows * 32)
+                             ? (int8_t*)w->wdig.p
+                             : nullptr;
                 // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
                 // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
                 // (it reads the general positions' F - mu from the compact Fg, so k_wcd writes no wcd)

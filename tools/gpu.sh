@@ -117,7 +117,7 @@ for STEP in "$@"; do
         i=$((i+1))
         PCX_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt$i -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --c5-steps 1 --no-c4 > $O/kt$i.log 2>&1 || { echo "kt_c5 rc=$? ($L)"; tail -5 $O/kt$i.log; exit 30; }
         echo "== $L"
-        python3 tools/kt_top.py $(find $O/kt$i -name "kt_kernel_trace.csv" | head -1) -1 14 ${KT_LAUNCHES:-k_sel_hist} || exit 31
+        python3 tools/kt_top.py $(find $O/kt$i -name "kt_kernel_trace.csv" | head -1) -1 ${KT_TOP:-14} ${KT_LAUNCHES:-k_sel_hist} || exit 31
       done ;;
     ab_shard=*)
       IFS=, read -ra LIBS <<< "${STEP#ab_shard=}"
