@@ -976,12 +976,6 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
         pos[k] = ok[k] ? m.cov_pos[c] : (c < ld ? c : -1);  // padding positions keep their index
         zc[k] = ok[k] && pos[k] >= gb;
     }
-    // the grid events the general tiles hold (positions [n_general, gb), gb - n_general < 128): their
-    // codes too, into zbg [row / 16][128] (k_outcomes_mf, k_gemv2_mf)
-    const int64_t ngen = m.info[IN_COV_GENERAL];
-    bool zg[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) zg[k] = m.zbg && ok[k] && pos[k] < gb && pos[k] >= ngen && pos[k] >= gb - 128;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; blockIdx.y == 0 && i < m.wcd_rows + 64;
          i += (int64_t)gridDim.x * BT)
         m.tokp[i] = i < m.n_rows ? m.tok[i] : 0.0;
@@ -994,7 +988,7 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
     for (int64_t g0 = r0; g0 < r1; g0 += 64) {
         const int gn = r1 - g0 < 64 ? (int)(r1 - g0) : 64;  // a multiple of 16 (wcd_rows % 16 == 0)
         for (int q0 = 0; q0 < gn; q0 += 16) {
-            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0}, nb[2] = {0, 0}, zgw[2] = {0, 0};
+            uint32_t za[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, zb[2] = {0, 0}, nb[2] = {0, 0};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
                 double rv[4][2];
@@ -1032,7 +1026,6 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                                 zb[k] |= (uint32_t)z * zpack_bit(4 * h + u);
                                 zs[k] += tk * z;
                             }
-                            if (zg[k]) zgw[k] |= (uint32_t)(int)((f - 1.0) * 2.0) * zpack_bit(4 * h + u);
                         }
                     }
 #pragma unroll
@@ -1092,8 +1085,6 @@ __global__ void __launch_bounds__(BT) k_wcd(pcx_mat m) {
                     const int64_t o = grp * m.zq + (pos[k] - gb);
                     *(uint4*)(m.zA + o * 16) = uint4{za[k][0], za[k][1], za[k][2], za[k][3]};
                     zb_packed(m)[o] = zb[k];
-                } else if (zg[k]) {
-                    m.zbg[grp * 128 + (pos[k] - (gb - 128))] = zgw[k];
                 }
         }
         __syncthreads();
@@ -3299,6 +3290,26 @@ __device__ __forceinline__ v4i wdig_bits16(uint32_t M) {
 #pragma unroll
     for (int k = 0; k < 4; k++) z[k] = (int)((((M >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u);
     return z;
+}
+
+// The grid events the general tiles end with (positions [n_general, gb), fewer than 128: gb is the
+// next multiple of 128) as 2-bit codes in zbg [row / 16][128] (the zpack layout of zB), from their
+// filled values Fg -- on the grid by the plan -- for k_outcomes_mf / k_gemv2_mf.  Thread = (position,
+// 16-row group); the lanes of a wave read consecutive positions of a row.  (Written inside k_wcd:
+// the same C5 time on one box, 20.5 vs 20.2-20.6 ms, with two more VGPRs and 14 more scalar spills in
+// its row loop; this pass reads 1 GB at C5.)
+__global__ void __launch_bounds__(BT) k_zbg(pcx_mat m) {
+    const int64_t gb = (int64_t)m.cov_jb * CT, ngen = m.info[IN_COV_GENERAL];
+    const int64_t p = (gb - 128) + (threadIdx.x & 127), g = (int64_t)blockIdx.x * (BT / 128) + (threadIdx.x >> 7);
+    if (p < ngen || p >= gb || g * 16 >= m.n_rows) return;
+    uint32_t P = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int64_t i = g * 16 + r;
+        const double F = i < m.n_rows ? m.Fg[i * gb + p] : 1.0;
+        P |= (F == 2.0 ? 2u : (F == 1.5 ? 1u : 0u)) * zpack_bit(r);
+    }
+    m.zbg[g * 128 + (p - (gb - 128))] = P;
 }
 
 // one wave per 16 positions and row chunk (the chunks of k_outcomes_c / k_col_finish); gb is a
@@ -6074,6 +6085,10 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 while (rb > 1 && m.wcd_rows / rb < WCD_MIN_ROWS && (rb / 2) * ncb >= PCX_WCD_MIN_WG) rb /= 2;
                 hipLaunchKernelGGL(k_wcd, dim3((unsigned)rb, ncb),
                                    dim3(BT), 0, st, m);
+                if (m.zbg && m.Fg && m.cov_jb * CT >= 128) {  // the general tiles' grid events as codes
+                    const int64_t groups = (m.n_rows + 15) / 16;
+                    hipLaunchKernelGGL(k_zbg, dim3((unsigned)((groups + 1) / 2)), dim3(BT), 0, st, m);
+                }
                 break;
             }
             static std::once_flag lds_once;
