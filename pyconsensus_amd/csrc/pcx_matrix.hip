@@ -5943,10 +5943,13 @@ static void launch_compact(KG kgen, KR kgrid, const pcx_mat& m, hipStream_t st) 
 
 // the int8-MFMA weighted counts (k_outcomes_mf, k_gemv2_mf) need row chunks of at most 2^24 rows:
 // their int32 digit sums are then exact
+// (and only on a large grid block: at C4's 100k x 743 grid events the subset-table kernels take
+// 0.15 / 0.18 ms against 0.19 / 0.20 with the digit passes' launches)
 static bool wdig_fits(const pcx_mat& m) {
     if (!m.wdig) return false;
     const int64_t per = ((m.n_rows + m.col_blocks - 1) / m.col_blocks + 15) / 16 * 16;
-    return per <= ((int64_t)1 << 24);
+    const int64_t ng = m.n_events - std::min<int64_t>((int64_t)m.cov_jb * CT, m.n_events);
+    return per <= ((int64_t)1 << 24) && m.n_rows * ng >= ((int64_t)1 << 27);
 }
 // the largest |w| and then the digits of each weight vector (vector v = the v-th of ws)
 static void wdig_prepare(const pcx_mat& m, std::initializer_list<const double*> ws, hipStream_t st) {

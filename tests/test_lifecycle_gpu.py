@@ -7,7 +7,8 @@ then a workgroup-per-round batch larger than the context's scratch, then another
 pcx_destroy freed the slots twice.  This runs exactly that sequence -- plus a batched round above
 the one-block selection limit, which takes the pipelined selection's pinned info words on a worker
 context of the round scheduler (freed by rounds_free) -- in a fresh process, twice over with
-pcx_release_workspace between, and requires a clean exit with every result still correct.
+pcx_release_workspace between, and requires a clean exit with every result still correct.  Each
+cycle also runs the host path in place (the chunked H2D with its host rewrite threads, round 6).
 """
 import os
 import subprocess
@@ -39,6 +40,13 @@ SCRIPT = textwrap.dedent(r"""
         out = consensus_batched(Rb, repb, scb, lob, hib)
         assert np.isfinite(out["smooth_rep"].cpu().numpy()).all()
         got, _ = consensus_host(R.copy(), rep, sc, lo, hi)
+        for k in ref:
+            assert np.array_equal(got[k].view(np.int64), ref[k].view(np.int64)), k
+        # in place (the reports' H2D in row chunks, each rewritten by host threads as it lands;
+        # `filled` copied back on the context's side stream): the same bits
+        X = R.copy()
+        got, _ = consensus_host(X, rep, sc, lo, hi, original_inplace=True)
+        assert got["original"] is X
         for k in ref:
             assert np.array_equal(got[k].view(np.int64), ref[k].view(np.int64)), k
         if cycle == 0:

@@ -1,11 +1,12 @@
 """`original` keeps the caller's bits of every missing report, and the compact passes agree with
-the oracle, on a matrix large enough for every int8 block.
+the oracle, on a matrix large enough for every int8 block and the int8-MFMA weighted counts
+(DESIGN.md 5.1, round 6).
 
 `original` is the rescaled reports (__init__.py:266-269), so an unscaled column's cells -- a NaN,
 a negative NaN, a NaN with a payload, a zero (missing by the reference's own rule, :278), a -0.0
--- come back bit for bit.  1024 events, 283 of them scaled: the general tiles end at 384, so 101
+-- come back bit for bit.  1024 events, 265 of them scaled: the general tiles end at 384, so 119
 grid events sit in them (positions [n_general, gb)), whose outcome / GEMV2 sums take the 2-bit codes
-k_wcd keeps for them (zbg) on int8 MFMA.  E <= 1024 also runs the power iteration's presquaring,
+k_zbg keeps for them on int8 MFMA.  E <= 1024 also runs the power iteration's presquaring,
 whose scratch once overwrote the plan's general count that those passes read (a C4 failure at
 world 1).  Checked at one rank (the drop-in, host arrays) and two (device arrays).
 """
@@ -19,28 +20,26 @@ pytestmark = pytest.mark.gpu
 
 
 def _matrix(N, E, seed):
-    rng = np.random.default_rng(seed)
-    R = rng.choice([1.0, 1.5, 2.0], size=(N, E), p=[0.45, 0.1, 0.45])
-    sc = rng.random(E) < 0.25
-    lo = np.where(sc, rng.uniform(-10.0, 0.0, E), 1.0)
-    hi = np.where(sc, lo + rng.uniform(1.0, 20.0, E), 2.0)
-    R[:, sc] = lo[sc] + (hi[sc] - lo[sc]) * np.clip(rng.normal(0.6, 0.15, (N, int(sc.sum()))), 0.001, 1.0)
-    R[rng.random((N, E)) < 0.1] = np.nan
+    """The synthetic recipe (truth per event, 10 % NaN, 25 % scaled) with three
+    grid columns' missing reports re-encoded: zeros (+0.0 and -0.0), negative NaNs, NaNs with a
+    payload."""
+    from pyconsensus_amd import synthetic
+
+    R, sc, lo, hi, _ = synthetic.matrix(N, E, seed=seed)
+    sc = np.asarray(sc, dtype=bool)
+    rng = np.random.default_rng(seed + 1)
     grid = np.flatnonzero(~sc)
     odd = {}
-    # a grid column with zeros among its missing reports, one with negative NaNs, one with a payload
     c_zero, c_neg, c_pay = grid[3], grid[7], grid[11]
-    rows = rng.choice(N, 40, replace=False)
-    R[rows, c_zero] = 0.0
-    R[rows[:20], c_zero] = -0.0
+    m = np.isnan(R[:, c_zero])
+    z = np.where(m)[0]
+    R[z, c_zero] = np.where(rng.random(z.size) < 0.5, 0.0, -0.0)
     odd["zero"] = c_zero
     u = R[:, c_neg].view(np.uint64)
-    m = np.isnan(R[:, c_neg])
-    u[m] = np.uint64(0xFFF8000000000000)  # -NaN
+    u[np.isnan(R[:, c_neg])] = np.uint64(0xFFF8000000000000)  # -NaN
     odd["neg"] = c_neg
     u = R[:, c_pay].view(np.uint64)
-    m = np.isnan(R[:, c_pay])
-    u[m] = np.uint64(0x7FF8000000000123)  # quiet NaN with a payload
+    u[np.isnan(R[:, c_pay])] = np.uint64(0x7FF8000000000123)  # quiet NaN with a payload
     odd["payload"] = c_pay
     return R, sc, lo, hi, odd
 
@@ -53,7 +52,7 @@ def test_grid_codes_original_bits_and_oracle(gpu_lib, world):
 
     from test_matrix_gpu import _sharded
 
-    N, E = 16400, 1024  # 16.8M cells >= 2^24: the codes path
+    N, E = 220_000, 1024  # N x 640 grid positions >= 2^27: the int8-MFMA weighted counts (wdig_fits)
     R, sc, lo, hi, odd = _matrix(N, E, seed=11)
     b = synthetic.bounds_list(sc, lo, hi)
     ref = G.flat_result(OracleCPU(reports=R.copy(), event_bounds=b, reputation=None).consensus())
