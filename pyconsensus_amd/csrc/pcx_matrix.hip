@@ -2370,16 +2370,38 @@ __device__ __forceinline__ double nweight(double v, double S, double Sp) {
 // PCX_M_GEMV2: d1 = normalize(set1) . F, d2 = normalize(set2) . F  (:492-493)
 // row weights of the two candidate sets, normalize(set1) and normalize(set2) (:488-493),
 // computed once per row (k_gemv2 reads them instead of dividing per element)
+// the largest |w| of a weight vector as it is written (bits: a NaN's exceed inf's), for the int8-MFMA
+// weighted counts' fixed-point scale: m.wdig's header word `slot` (zeroed once per call by the
+// runner; 0: normalize(set1), 1: normalize(set2), 2: smooth_rep), one atomic per wave.  Every lane
+// of the wave calls it.
+enum wdig_slot { WD_N1 = 0, WD_N2, WD_SMOOTH };
+__device__ __forceinline__ void wdig_note(const pcx_mat& m, int slot, uint64_t mx) {
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)mx, d, WAVE);
+        mx = o > mx ? o : mx;
+    }
+    if (m.wdig && (threadIdx.x & (WAVE - 1)) == 0 && mx)
+        atomicMax(reinterpret_cast<unsigned long long*>(m.wdig) + slot, (unsigned long long)mx);
+}
+__device__ __forceinline__ uint64_t abs_bits(double w) { return (uint64_t)__double_as_longlong(fabs(w)); }
+
 __global__ void __launch_bounds__(BT) k_nweights(pcx_mat m) {
     double mn, mx;
     score_minmax(m, mn, mx);
     const double S1 = dd_to_double(scl(m, SC_A1)), S1p = dd_to_double(scl(m, SC_A1P));
     const double S2 = dd_to_double(scl(m, SC_A2)), S2p = dd_to_double(scl(m, SC_A2P));
+    uint64_t m1 = 0, m2 = 0;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         const double s = m.rowv[RV_S * m.n_rows + i];
-        m.rowv[RV_N1 * m.n_rows + i] = nweight(fabs(s + fabs(mn)), S1, S1p);
-        m.rowv[RV_N2 * m.n_rows + i] = nweight(fabs(s - mx), S2, S2p);
+        const double a = nweight(fabs(s + fabs(mn)), S1, S1p), b = nweight(fabs(s - mx), S2, S2p);
+        m.rowv[RV_N1 * m.n_rows + i] = a;
+        m.rowv[RV_N2 * m.n_rows + i] = b;
+        m1 = abs_bits(a) > m1 ? abs_bits(a) : m1;
+        m2 = abs_bits(b) > m2 ? abs_bits(b) : m2;
     }
+    wdig_note(m, WD_N1, m1);
+    wdig_note(m, WD_N2, m2);
 }
 
 __global__ void __launch_bounds__(BT) k_gemv2(pcx_mat m) {
@@ -2450,19 +2472,18 @@ __device__ __forceinline__ uint32_t sub4_stride4(uint32_t M, int j) {
 #ifndef PCX_MF_ZBG  // (a build parameter for A/B runs: bit 0 the outcome sums, bit 1 the GEMV2 sums take zbg)
 #define PCX_MF_ZBG 3
 #endif
-// m.wdig: a 256-byte header (the largest |w| bits of weight vector v at word v, zeroed before each
-// pass), then vector v's digits at 256 + v wcd_rows 16 bytes
+// m.wdig: a 256-byte header (the largest |w| bits of each weight vector, wdig_slot, written by the
+// kernels that write the weights), then vector v's digits at 256 + v wcd_rows 16 bytes
 __device__ __forceinline__ uint64_t* wdig_max(const pcx_mat& m) { return reinterpret_cast<uint64_t*>(m.wdig); }
 __device__ __forceinline__ int8_t* wdig_vec(const pcx_mat& m, int v) { return m.wdig + 256 + (int64_t)v * m.wcd_rows * 16; }
 __device__ __forceinline__ double wdig_maxabs(const pcx_mat& m, int v) {
     return __longlong_as_double((long long)wdig_max(m)[v]);
 }
-// the digit passes ran (m.wdig set by the host) and every weight of vectors 0 .. nv - 1 is finite
-__device__ __forceinline__ bool wdig_ok(const pcx_mat& m, int nv) {
+// the digit passes ran (m.wdig set by the host) and every weight of the vectors in header words s0, s1
+// is finite
+__device__ __forceinline__ bool wdig_ok(const pcx_mat& m, int s0, int s1 = -1) {
     if (!m.wdig) return false;
-    bool ok = true;
-    for (int v = 0; v < nv; v++) ok = ok && __builtin_isfinite(wdig_maxabs(m, v));
-    return ok;
+    return __builtin_isfinite(wdig_maxabs(m, s0)) && (s1 < 0 || __builtin_isfinite(wdig_maxabs(m, s1)));
 }
 
 // M_GEMV2 from the compact sources (m.compact): thread = one wcd position (general positions
@@ -2475,7 +2496,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = (GRID ? (int)gb : 0) + blockIdx.x * BT + threadIdx.x;
     const int E = (int)m.n_events;
-    if (GRID && wdig_ok(m, 2)) return;  // (k_gemv2_mf summed them)
+    if (GRID && wdig_ok(m, WD_N1, WD_N2)) return;  // (k_gemv2_mf summed them)
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
     const double* n1 = m.rowv + RV_N1 * m.n_rows;
@@ -2490,7 +2511,7 @@ __global__ void __launch_bounds__(BT) k_gemv2_c(pcx_mat m) {
     }
     // (every wave of a grid block stays to the end: the block builds the subset tables together)
     if (!GRID && (q >= E || q >= gb)) return;
-    if (!GRID && (PCX_MF_ZBG & 2) && q >= m.info[IN_COV_GENERAL] && m.zbg && wdig_ok(m, 2)) return;  // (k_gemv2_mf: zbg)
+    if (!GRID && (PCX_MF_ZBG & 2) && q >= m.info[IN_COV_GENERAL] && m.zbg && wdig_ok(m, WD_N1, WD_N2)) return;  // (k_gemv2_mf: zbg)
     const bool live = q < E;
     const int c = live ? m.cov_perm[q] : -1;
     if (!GRID && c < 0) return;  // (padding)
@@ -2790,11 +2811,15 @@ __global__ void __launch_bounds__(BT) k_repu(pcx_mat m) {
 __global__ void __launch_bounds__(BT) k_smooth(pcx_mat m) {
     const double S = dd_to_double(scl(m, SC_U)), Sp = dd_to_double(scl(m, SC_UP));
     const double a = m.alpha, oma = 1.0 - m.alpha;
+    uint64_t ms = 0;
     for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
         const double t = nweight(m.rowv[RV_U * m.n_rows + i], S, Sp);
+        const double w = a * t + oma * m.rep[i];
         m.rowv[RV_THIS * m.n_rows + i] = t;
-        m.rowv[RV_SMOOTH * m.n_rows + i] = a * t + oma * m.rep[i];
+        m.rowv[RV_SMOOTH * m.n_rows + i] = w;
+        ms = abs_bits(w) > ms ? abs_bits(w) : ms;
     }
+    wdig_note(m, WD_SMOOTH, ms);
 }
 
 // PCX_M_OUTCOMES: smooth . F (:510), smooth . na (:559), certainty bins for binary events
@@ -3204,7 +3229,7 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int q = blockIdx.x * BT + threadIdx.x;
     // k_outcomes_mf ran (finite weights): what is left are the general binary positions
-    const bool mf = wdig_ok(m, 1);
+    const bool mf = wdig_ok(m, WD_SMOOTH);
     if (mf && (q & ~(WAVE - 1)) >= gb) return;  // (wave-uniform)
     int64_t r0, r1;
     row_range(m, r0, r1, 16);
@@ -3236,26 +3261,12 @@ __global__ void __launch_bounds__(BT) k_outcomes_c(pcx_mat m) {
 // raw a compensated one), the 0/1 operands unpacked from the 2-bit codes and the missing bits
 // beside the MFMAs.  A non-finite weight (NaN x 0 must reach the sums as in np.dot) leaves the pass
 // to k_outcomes_c.
-__global__ void __launch_bounds__(BT) k_wmax(pcx_mat m, const double* w, int v) {
-    uint64_t mx = 0;
-    for (int64_t i = blockIdx.x * (int64_t)BT + threadIdx.x; i < m.n_rows; i += (int64_t)gridDim.x * BT) {
-        const uint64_t b = (uint64_t)__double_as_longlong(fabs(w[i]));  // (a NaN's bits exceed inf's)
-        mx = b > mx ? b : mx;
-    }
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) {
-        const uint64_t o = (uint64_t)__shfl_xor((long long)mx, d, WAVE);
-        mx = o > mx ? o : mx;
-    }
-    if ((threadIdx.x & (WAVE - 1)) == 0 && mx) atomicMax((unsigned long long*)&wdig_max(m)[v], (unsigned long long)mx);
-}
-
 __device__ __forceinline__ int wdig_scale(double mxw) { return mxw > 0.0 ? 124 - ilogb(mxw) : 0; }
 
 // digits n = 0..15 of row i at wdig_vec(v)[(i / 16) 256 + 16 n + i % 16]: one 16-byte MFMA B fragment
 // per (16 rows, digit); rows past n_rows (to the next multiple of 16) zero
-__global__ void __launch_bounds__(BT) k_wdigits(pcx_mat m, const double* w, int v) {
-    const double mxw = wdig_maxabs(m, v);
+__global__ void __launch_bounds__(BT) k_wdigits(pcx_mat m, const double* w, int v, int slot) {
+    const double mxw = wdig_maxabs(m, slot);
     if (!__builtin_isfinite(mxw)) return;
     const int s = wdig_scale(mxw);
     int8_t* dst = wdig_vec(m, v);
@@ -3315,8 +3326,8 @@ __global__ void __launch_bounds__(BT) k_zbg(pcx_mat m) {
 // one wave per 16 positions and row chunk (the chunks of k_outcomes_c / k_col_finish); gb is a
 // multiple of 128, so a wave's positions are all general or all grid
 __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
-    if (!wdig_ok(m, 1)) return;
-    const int sc = wdig_scale(wdig_maxabs(m, 0));
+    if (!wdig_ok(m, WD_SMOOTH)) return;
+    const int sc = wdig_scale(wdig_maxabs(m, WD_SMOOTH));
     const int E = (int)m.n_events;
     const int64_t gb = (int64_t)m.cov_jb * CT, ld = m.wcd_ld;
     const int lane = threadIdx.x & (WAVE - 1), lc = lane & 15, lg = lane >> 4;
@@ -3421,8 +3432,8 @@ __global__ void __launch_bounds__(BT) k_outcomes_mf(pcx_mat m) {
 // operand as they are, the weights' digits (vectors 0 and 1) the B operands, and all-ones A rows give
 // the chunk totals S_v
 __global__ void __launch_bounds__(BT) k_gemv2_mf(pcx_mat m) {
-    if (!wdig_ok(m, 2)) return;
-    const int s1 = wdig_scale(wdig_maxabs(m, 0)), s2 = wdig_scale(wdig_maxabs(m, 1));
+    if (!wdig_ok(m, WD_N1, WD_N2)) return;
+    const int s1 = wdig_scale(wdig_maxabs(m, WD_N1)), s2 = wdig_scale(wdig_maxabs(m, WD_N2));
     const int E = (int)m.n_events;
     const int64_t gb = (int64_t)m.cov_jb * CT;
     const int lane = threadIdx.x & (WAVE - 1), lc = lane & 15, lg = lane >> 4;
@@ -5951,15 +5962,16 @@ static bool wdig_fits(const pcx_mat& m) {
     const int64_t ng = m.n_events - std::min<int64_t>((int64_t)m.cov_jb * CT, m.n_events);
     return per <= ((int64_t)1 << 24) && m.n_rows * ng >= ((int64_t)1 << 27);
 }
-// the largest |w| and then the digits of each weight vector (vector v = the v-th of ws)
-static void wdig_prepare(const pcx_mat& m, std::initializer_list<const double*> ws, hipStream_t st) {
-    (void)hipMemsetAsync(m.wdig, 0, 256, st);
+// the digits of each weight vector (vector v = the v-th of ws, its largest |w| in header word slots[v])
+static void wdig_prepare(const pcx_mat& m, std::initializer_list<const double*> ws, std::initializer_list<int> slots,
+                         hipStream_t st) {
     const int64_t rb = std::max<int64_t>(1, (m.n_rows + BT - 1) / BT);
     int v = 0;
+    auto sl = slots.begin();
     for (const double* w : ws) {
-        hipLaunchKernelGGL(k_wmax, dim3((unsigned)std::min<int64_t>(rb, 1024)), dim3(BT), 0, st, m, w, v);
-        hipLaunchKernelGGL(k_wdigits, dim3((unsigned)std::min<int64_t>(rb + 1, 4096)), dim3(BT), 0, st, m, w, v);
+        hipLaunchKernelGGL(k_wdigits, dim3((unsigned)std::min<int64_t>(rb + 1, 4096)), dim3(BT), 0, st, m, w, v, *sl);
         v++;
+        sl++;
     }
 }
 
@@ -6184,7 +6196,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 if (!wdig_fits(m)) mm.wdig = nullptr;
                 const int64_t gbp = std::min<int64_t>((int64_t)m.cov_jb * CT, E);
                 if (mm.wdig && E > gbp) {  // the grid positions on int8 MFMA (k_gemv2_c<true> then exits)
-                    wdig_prepare(mm, {m.rowv + RV_N1 * m.n_rows, m.rowv + RV_N2 * m.n_rows}, st);
+                    wdig_prepare(mm, {m.rowv + RV_N1 * m.n_rows, m.rowv + RV_N2 * m.n_rows}, {(int)WD_N1, (int)WD_N2}, st);
                     // (from n_general, a device value > gb - 128: the waves past E exit)
                     const int64_t from = std::max<int64_t>(0, gbp - 128);
                     hipLaunchKernelGGL(k_gemv2_mf, dim3((unsigned)((E - from + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
@@ -6219,7 +6231,7 @@ hipError_t mat_stage(pcx_mat& m, int stage, hipStream_t st, std::string& err) {
                 pcx_mat mm = m;
                 if (!wdig_fits(m)) mm.wdig = nullptr;
                 if (mm.wdig) {
-                    wdig_prepare(mm, {m.rowv + RV_SMOOTH * m.n_rows}, st);
+                    wdig_prepare(mm, {m.rowv + RV_SMOOTH * m.n_rows}, {(int)WD_SMOOTH}, st);
                     hipLaunchKernelGGL(k_outcomes_mf, dim3((unsigned)((E + 63) / 64), m.col_blocks), dim3(BT), 0, st, mm);
                 }
                 hipLaunchKernelGGL(k_outcomes_c, colgrid, dim3(BT), 0, st, mm);

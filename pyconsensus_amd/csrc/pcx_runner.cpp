@@ -221,7 +221,10 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
     const int64_t S = std::max(1, n_scaled);
     const int64_t ceb = (E + BT - 1) / BT;
     // enough row chunks to give ~2048 column-pass blocks, at least 32 rows each
-    w->col_blocks = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(1, 2048 / ceb),
+#ifndef PCX_COL_TARGET  // (a build parameter for A/B runs: column-pass blocks aimed at)
+#define PCX_COL_TARGET 2048
+#endif
+    w->col_blocks = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(1, PCX_COL_TARGET / ceb),
                                                                              (n_rows + 31) / 32),
                                                            4096));
     const int64_t nb = (E + COV_TILE - 1) / COV_TILE;
@@ -1317,6 +1320,8 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
                 m.wdig = m.compact && (gb == 0 || m.zbg) && w->grow(w->wdig, 256 + (size_t)w->wcd_rows * 32)
                              ? (int8_t*)w->wdig.p
                              : nullptr;
+                // (its header: the weight vectors' largest |w|, noted by k_nweights / k_smooth)
+                if (m.wdig) R.hip(hipMemsetAsync(m.wdig, 0, 256, R.st), "hipMemset(wdig)");
                 // general x general pairs on int8 digits too (k_gemm_i8x) when the memory is there:
                 // 21 digit-pair products on int8 MFMA instead of k_syrk's fp64 tiles
                 // (it reads the general positions' F - mu from the compact Fg, so k_wcd writes no wcd)
