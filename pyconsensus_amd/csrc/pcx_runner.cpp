@@ -548,6 +548,7 @@ struct ChunkGate {
 // host_threads() threads; a small matrix runs on the calling thread.
 struct HostOriginal {
     std::vector<std::thread> th;
+    ChunkGate* gate_ = nullptr;  // (released on destruction: a failure before every chunk was issued)
     // gate: the reports' H2D chunks (in place: a chunk is rewritten only once it has been copied)
     void start(const double* rep_in, double* original, int64_t n_rows, int64_t E, const std::vector<uint8_t>& scaled,
                const double* lo, const double* hi, bool int_dtype, ChunkGate* gate = nullptr) {
@@ -580,6 +581,7 @@ struct HostOriginal {
         };
         const int T = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n_rows / 1024));
         if (gate) {  // every thread takes its share of each chunk as the chunk lands
+            gate_ = gate;
             for (int t = 0; t < T; t++)
                 th.emplace_back([=] {
                     for (int k = 0; k < gate->nchunks(); k++) {
@@ -600,7 +602,12 @@ struct HostOriginal {
         for (auto& t : th) t.join();
         th.clear();
     }
-    ~HostOriginal() { join(); }
+    ~HostOriginal() {
+        // a call that failed before marking every chunk (a hipMalloc of the device copy, an H2D)
+        // leaves threads waiting on the gate: release them (after a normal join this does nothing)
+        if (gate_) gate_->abort();
+        join();
+    }
 };
 
 int64_t pow2_at_least(int64_t n) {
