@@ -382,11 +382,11 @@ __device__ __noinline__ double wave_wmedian(double x, double w, bool sel, double
 //    left to right, eight broadcast loads per step group, stopping at the first
 //    cum > mid: the SPEC's sequential sums bit for bit; `before` is the same subtraction.
 // NaN keys have no total order: rounds with a NaN among the selected pairs take
-// wave_wmedian.  NR = compile-time row count bound (64 when the shape is dynamic).
-// scr: med_scr(NR) doubles of LDS: sx | sw | ox [NR] | ow [med_ow(NR)] | NR int counters
+// wave_wmedian (in ox / ow).  NR = compile-time row count bound (64 when the shape is dynamic).
+// scr: med_scr(NR) doubles of LDS: ox [NR] | ow [med_ow(NR)] | NR int counters
 // (ow holds the zero-padded walk groups: every prefetched group of eight).
 __host__ __device__ constexpr int med_ow(int NR) { return (NR + 7) / 8 * 8 + 8; }
-__host__ __device__ constexpr int med_scr(int NR) { return 3 * NR + med_ow(NR) + (NR + 1) / 2; }
+__host__ __device__ constexpr int med_scr(int NR) { return NR + med_ow(NR) + (NR + 1) / 2; }
 
 // top 32 bits of the order-preserving key of a double (-0.0 folded onto +0.0)
 __device__ __forceinline__ uint32_t key_hi32(double x) {
@@ -406,19 +406,16 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
                                                     long long* prof = nullptr, bool use_rank = false, int rank = 0,
                                                     int* rank_out = nullptr, bool wlazy = false) {
     const int l = lane_id();
-    double *sx = scr, *sw = scr + NR, *ox = scr + 2 * NR, *ow = scr + 3 * NR;
-    int* cnt = reinterpret_cast<int*>(scr + 3 * NR + med_ow(NR));
+    double *ox = scr, *ow = scr + NR;
+    int* cnt = reinterpret_cast<int*>(scr + NR + med_ow(NR));
     const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
     double slack = 0.0;
-    // the exact total, through sx (free before the rank loop and after the scatter)
+    // the exact total (row order, an absent row adding +0.0), read lane by lane: a near tie or
+    // NaN data only, so it needs no LDS of its own (the sorted pairs may already fill ox / ow)
     auto exact_total = [&]() {
-        wsync();
-        if (l < N) sx[l] = sel ? w : 0.0;
-        wsync();
+        const double v = sel ? w : 0.0;
         double t = 0.0;
-#pragma unroll 8
-        for (int i = 0; i < N; i++) t = t + sx[i];
-        wsync();
+        for (int i = 0; i < N; i++) t = t + readlane_d(v, i);
         slack = 0.0;
         return t;
     };
@@ -435,7 +432,7 @@ __device__ PCX_OUTLINE double wave_wmedian_rank(double x, double w, bool sel, do
     if (!ballot(sel && w > 0.0)) return __builtin_nan("");
     if (ballot(sel && (__builtin_isnan(x) || __builtin_isnan(w)))) {
         if (slack != 0.0) Wtot = exact_total();
-        return wave_wmedian(x, w, sel, Wtot, sx, sw);
+        return wave_wmedian(x, w, sel, Wtot, ox, ow);
     }
     const int n = popc(ballot(sel));
     // rank by the top 32 bits of x's order-preserving key (one 32-bit compare per row,
@@ -627,55 +624,63 @@ struct Smem {
     double* F;      // [N][ES] rescaled, then filled reports
     double* C;      // [E][ES] covariance (phase aliases: see carve)
     double* M;      // [max(E*ES, MED_SCR)] power-iteration / Jacobi working matrix
-    double* rep;    // [N]
+    double* rep;    // [N] (aliases C: dead once the covariance has its tokens)
     double* n1;     // [N] normalize(set1) (aliases C)
     double* n2;     // [N] normalize(set2) (aliases C)
     double* smooth; // [N] (aliases C)
-    double* mu;     // [E]
+    double* mu;     // [E] full layout only (the clusterings' mean; the rest read lane registers)
+    double* tot;    // [E] present-reputation totals of the interpolation medians (aliases M)
     double* guess;  // [E] (aliases C)
-    double* x;      // [E] power-iteration vector
-    double* ld;     // [E] loading
+    double* x;      // [E] full layout only: the Jacobi rotations' cos
+    double* ld;     // [E] full layout only: the Jacobi rotations' sin
     double* old;    // [E] (aliases C)
     double* nv1;    // [E] (aliases M)
     double* nv2;    // [E] (aliases M)
     double* adj;    // [E] (aliases C)
-    uint64_t* nanm; // [E] bit i = report (i, j) is NaN
-    uint64_t* zerm; // [E] bit i = report (i, j) == 0.0
+    uint64_t* miss; // [E] bit i = report (i, j) is NaN or 0.0 (the per-row / per-column counts
+                    // of each kind are lane registers)
 };
 
 // LDS per round, by phase.  The kernel is latency bound: throughput scales with the
 // rounds resident per CU (tools/occupancy_batched.py), and LDS is what bounds them, so
 // vectors whose lifetimes do not overlap the matrices' share their space:
 //   C  (covariance, Jacobi V) is live from the covariance to the scores only; before
-//      it holds guess (interpolation), after it n1 | n2 | smooth | adj | old;
+//      it holds guess | rep (load to fill | load to the covariance's tokens), after it
+//      n1 | n2 | smooth | adj | old;
 //   M  (squared matrix, Jacobi A) is dead in both median phases, where the median
-//      scratch (MED_SCR doubles) lives, and after the eigenpairs, where nv1 | nv2 live;
-//   x | ld (power iteration, loading) are dead in the Jacobi sweeps: rotation cos | sin.
+//      scratch (med_scr doubles) lives, and after the eigenpairs, where nv1 | nv2 live;
+//   the power-iteration vector, the loading and the weighted mean are lane registers, read
+//      by other lanes through readlane / ds_bpermute (no LDS); the full layout keeps mu
+//      (the clusterings read it) and x | ld as the Jacobi rotations' cos | sin.
 // The integer tokens are recomputed from rep where the covariance needs them.  Per-row
-// vectors hold N entries, per-event vectors E (rounded up to even).  50 x 20: 16.3 KB,
-// ten rounds per CU.
+// vectors hold N entries, per-event vectors E (rounded up to even).  LDS is allocated in
+// 1,280-byte units (160 KiB / 128; measured with PCX_BATCHED_LDS_PAD: a 50 x 20 round of
+// 12,800 bytes ran twelve to a CU, one of 13,192 eleven).
 __host__ __device__ inline int smem_rows(int N) { return (N + 1) & ~1; }
-// F also holds the certainty phase's compacted hit lists, [E][N | 1]
+// F also holds the certainty phase's compacted hit lists, [E][cert_stride] (an odd stride with
+// the odd row pitch; the even pitch of PCX_BATCHED_ES_EVEN keeps N)
+__host__ __device__ inline int cert_stride(int N, int ES) { return (ES & 1) ? (N | 1) : N; }
 __host__ __device__ inline int smem_f_size(int N, int E, int ES) {
-    return N * ES > E * (N | 1) ? N * ES : E * (N | 1);
+    return N * ES > E * cert_stride(N, ES) ? N * ES : E * cert_stride(N, ES);
 }
 __host__ __device__ inline int smem_evs(int E) { return (E + 1) & ~1; }
 // C and M: full [E][ES] (the Jacobi eigenpairs of big-five / fixed-variance need a
 // general V), or -- every other algorithm -- packed lower triangles (both are symmetric:
-// the squared M bitwise too), which brings a 50 x 20 round to 13.2 KB, twelve per CU.
+// the squared M bitwise too).
 __host__ __device__ inline int smem_mat(int E, int ES, bool pk) { return pk ? E * (E + 1) / 2 : E * ES; }
 __host__ __device__ inline int smem_c_size(int N, int E, int ES, bool pk) {
     const int need = 3 * smem_rows(N) + 2 * smem_evs(E);
     return smem_mat(E, ES, pk) > need ? smem_mat(E, ES, pk) : need;
 }
 __host__ __device__ inline int smem_m_size(int E, int ES, int NR, bool pk) {
-    const int need = med_scr(NR) > 2 * smem_evs(E) ? med_scr(NR) : 2 * smem_evs(E);
+    const int scr = med_scr(NR) + smem_evs(E);  // the median scratch and the totals beside it
+    const int need = scr > 2 * smem_evs(E) ? scr : 2 * smem_evs(E);
     return smem_mat(E, ES, pk) > need ? smem_mat(E, ES, pk) : need;
 }
 
 __host__ __device__ inline size_t smem_doubles(int N, int E, int ES, int NR, bool pk) {
-    return (size_t)smem_f_size(N, E, ES) + smem_c_size(N, E, ES, pk) + smem_m_size(E, ES, NR, pk) + smem_rows(N) +
-           5 * (size_t)smem_evs(E);
+    return (size_t)smem_f_size(N, E, ES) + smem_c_size(N, E, ES, pk) + smem_m_size(E, ES, NR, pk) +
+           (pk ? 1 : 4) * (size_t)smem_evs(E);
 }
 
 // entry (j, k) of the symmetric C / M
@@ -694,13 +699,16 @@ __device__ Smem carve(double* base, int N, int E, int ES, int NR, bool pk) {
     s.F = p; p += smem_f_size(N, E, ES);
     s.C = p; p += smem_c_size(N, E, ES, pk);
     s.M = p; p += smem_m_size(E, ES, NR, pk);
-    s.rep = p; p += nr;
-    s.mu = p; p += ne;
-    s.x = p; p += ne;
-    s.ld = p; p += ne;
-    s.nanm = reinterpret_cast<uint64_t*>(p); p += ne;
-    s.zerm = reinterpret_cast<uint64_t*>(p); p += ne;
+    s.miss = reinterpret_cast<uint64_t*>(p); p += ne;
+    s.mu = s.x = s.ld = nullptr;
+    if (!pk) {
+        s.mu = p; p += ne;
+        s.x = p; p += ne;
+        s.ld = p; p += ne;
+    }
     // phase aliases (see above)
+    s.tot = s.M + med_scr(NR);
+    s.rep = s.C + ne;  // (beside guess, C[0, E))
     s.guess = s.C;
     s.n1 = s.C;
     s.n2 = s.C + nr;
@@ -712,16 +720,13 @@ __device__ Smem carve(double* base, int N, int E, int ES, int NR, bool pk) {
     return s;
 }
 
-// y = normalize(M x) for lane j < E, x in LDS; returns y_j (0 on other lanes)
+// y = normalize(M x) for lane j < E, x_k on lane k; returns y_j (0 on other lanes)
 template <bool PK>
-__device__ PCX_OUTLINE double matvec_unit(const double* M, int ES, const double* x, int E) {
-    const int l = lane_id();
-    double y = 0.0;
-    if (l < E) {
-        double acc = 0.0;
-        for (int k = 0; k < E; k++) acc = fma(M[sym_at<PK>(l, k, ES)], x[k], acc);
-        y = acc;
-    }
+__device__ PCX_OUTLINE double matvec_unit(const double* M, int ES, double xv, int E) {
+    const int l = lane_id(), r = l < E ? l : 0;  // (every lane runs the chain: readlane is wave-wide)
+    double acc = 0.0;
+    for (int k = 0; k < E; k++) acc = fma(M[sym_at<PK>(r, k, ES)], lane_value(xv, k), acc);
+    const double y = l < E ? acc : 0.0;
     const double nrm = sqrt(tree_sum(l < E ? y * y : 0.0));
     return l < E ? y / nrm : 0.0;
 }
@@ -1259,14 +1264,26 @@ __device__ __noinline__ double feck_nc(const BatchArgs& a, const double* F, int 
 
 }  // namespace
 
+// The compiled shapes' row pitch: E (1) or E | 1 (0).  The odd pitch spreads a row-phase column
+// read over the banks, but 50 x 20 rounds at the even one fit nine LDS units instead of ten -- 14
+// rounds a CU instead of 12 with the 128-VGPR budget below (C3: 1.53 -> 1.46 ms, 42.5 -> 44.6 M
+// rounds/s; the odd pitch at 128 VGPRs, still 12 a CU, ran 1.55 ms).  (Build parameters for A/B runs.)
+#ifndef PCX_BATCHED_ES_EVEN
+#define PCX_BATCHED_ES_EVEN 1
+#endif
+__host__ __device__ constexpr int compiled_es(int E) { return PCX_BATCHED_ES_EVEN ? E : (E | 1); }
+#ifndef PCX_BATCHED_WAVES  // waves per SIMD the compiled packed shapes' VGPR budget is sized for (4: 128 VGPRs)
+#define PCX_BATCHED_WAVES 4
+#endif
+
 // NT/ET > 0: the round shape is a compile-time constant (the Monte Carlo shapes the
 // launcher specialises, e.g. the 50 x 20 of config C3): every loop bound is known, so
 // the sequential column/row loops unroll and their LDS reads issue ahead of the
 // dependent adds.  NT = ET = 0: any N <= 64, E <= 32 at run time.  Same arithmetic.
 template <int NT, int ET, bool CLUS, bool PK>
-__global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
+__global__ void __launch_bounds__(64, (NT > 0 && PK) ? PCX_BATCHED_WAVES : 3) batched_round_kernel(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? (ET | 1) : a.ES;
+    const int N = NT > 0 ? NT : a.N, E = ET > 0 ? ET : a.E, ES = ET > 0 ? compiled_es(ET) : a.ES;
     const int l = lane_id();
     const int64_t b = blockIdx.x;
     constexpr int NRM = NT > 0 ? NT : 64;  // median scratch rows
@@ -1330,6 +1347,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     // (the next column's value is loaded before this column's stores: a load after a store to
     // the same LDS array would otherwise wait for it)
     double xnext = row ? S.F[l * ES] : 0.0;
+    // per-lane counts, 7 bits each: row l's zeros (bits 0-7) and NaNs (8-15), column l's zeros (16-23)
+    uint32_t nacnt = 0;
     for (int j = 0; j < E; j++) {
         const bool sc = (scaled_mask >> j) & 1;
         const double lo = bcast(loj, j), hi = bcast(hij, j);
@@ -1344,10 +1363,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         }
         const uint64_t nm = ballot(row && __builtin_isnan(x));
         const uint64_t zm = ballot(row && x == 0.0);
-        if (l == 0) {
-            S.nanm[j] = nm;
-            S.zerm[j] = zm;
-        }
+        nacnt += (uint32_t)((zm >> l) & 1) + ((uint32_t)((nm >> l) & 1) << 8) + (l == j ? (uint32_t)popc(zm) << 16 : 0u);
+        if (l == 0) S.miss[j] = nm | zm;
     }
     wsync();
     // result["original"] (the rescaled reports), from LDS in row-major order: every store
@@ -1357,7 +1374,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(2);
     // ---- a3: interpolation guesses (:284-313), column phase ----------------
     uint64_t miss_j = 0;
-    if (col) miss_j = S.nanm[l] | S.zerm[l];
+    if (col) miss_j = S.miss[l];
     constexpr int RKW = (ET > 0 ? ET + 3 : EMAX) / 4;  // interpolation-median ranks, a byte per column
     uint32_t rkq[RKW];
 #pragma unroll
@@ -1406,7 +1423,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             if (a.int_dtype) g = trunc(g);
             S.guess[l] = g;
         }
-        if (col && miss_j) S.mu[l] = tot;  // the present-reputation total, for the median phase
+        if (col && miss_j) S.tot[l] = tot;  // the present-reputation total, for the median phase
     }
     wsync();
     STAMP(13);
@@ -1417,9 +1434,9 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         // Wsum = weightedstats' sum(weights), sequential in row order (absent rows add +0.0,
         // which leaves a sum from +0.0 unchanged)
         auto pair_of = [&](int j, double& x, double& w, bool& present, double& Wsum) {
-            const uint64_t mj = S.nanm[j] | S.zerm[j];
+            const uint64_t mj = S.miss[j];
             present = row && !((mj >> l) & 1);
-            const double tot = S.mu[j];
+            const double tot = S.tot[j];
             x = row ? S.F[l * ES + j] : 0.0;
             w = present ? S.rep[l] / tot : 0.0;
             Wsum = 0.0;  // (formed inside the median only where a decision needs it: wlazy)
@@ -1452,13 +1469,13 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     STAMP(14);
     // fill (row phase; the next column's masks and fill loaded ahead of this column's store)
     if (row) {
-        uint64_t mn = S.nanm[0] | S.zerm[0];
+        uint64_t mn = S.miss[0];
         double gn = S.guess[0];
         for (int j = 0; j < E; j++) {
             const uint64_t mj = mn;
             const double g = gn;
             if (j + 1 < E) {
-                mn = S.nanm[j + 1] | S.zerm[j + 1];
+                mn = S.miss[j + 1];
                 gn = S.guess[j + 1];
             }
             if ((mj >> l) & 1) S.F[l * ES + j] = g;
@@ -1488,9 +1505,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             for (int i = 1; i < N; i++) acc = acc + S.F[i * ES + l] * S.rep[i];
             muj = acc / den;
         }
-        wsync();
-        if (col) S.mu[l] = muj;
-        wsync();
+        if constexpr (!PK) {  // (the clusterings and big-five read it from LDS)
+            wsync();
+            if (col) S.mu[l] = muj;
+            wsync();
+        }
 
         STAMP(4);
         // ---- a6: token-weighted covariance (:326), lower triangle ----------
@@ -1502,7 +1521,8 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             constexpr int NR = NT > 0 ? NT : 64;
             const int ml = l & 15, kq = l >> 4;
             const bool two = E > 16;
-            const double mu0 = ml < E ? S.mu[ml] : 0.0, mu1 = 16 + ml < E ? S.mu[16 + ml] : 0.0;
+            const double m0 = __shfl(muj, ml), m1 = __shfl(muj, 16 + ml);  // column ml's / 16 + ml's mean
+            const double mu0 = ml < E ? m0 : 0.0, mu1 = 16 + ml < E ? m1 : 0.0;
             d4v c00 = {0, 0, 0, 0}, c10 = {0, 0, 0, 0}, c11 = {0, 0, 0, 0};
 #pragma unroll
             for (int i0 = 0; i0 < NR; i0 += 4) {
@@ -1562,16 +1582,11 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             xv = col ? x0 / n0 : 0.0;
             int sqn = 0;
             for (; sqn < PI_PRESQUARE; sqn++) square_scaled<PK>(S.M, ES, E);
-            if (col) S.x[l] = xv;
-            wsync();
             int it = 0, since = 0;
             for (;;) {
-                const double y = matvec_unit<PK>(S.M, ES, S.x, E);
+                const double y = matvec_unit<PK>(S.M, ES, xv, E);
                 const double d = wave_max(col ? fabs(y - xv) : 0.0);
                 xv = y;
-                wsync();
-                if (col) S.x[l] = xv;
-                wsync();
                 it++;
                 since++;
                 if (d <= PI_TOL) break;
@@ -1585,12 +1600,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
                     since = 0;
                 }
             }
-            for (int p = 0; p < PI_POLISH; p++) {
-                xv = matvec_unit<PK>(S.C, ES, S.x, E);
-                wsync();
-                if (col) S.x[l] = xv;
-                wsync();
-            }
+            for (int p = 0; p < PI_POLISH; p++) xv = matvec_unit<PK>(S.C, ES, xv, E);
             // SPEC sign: first nonzero component negative; a unit vector e_k is +e_k
             const uint64_t nzm = ballot(col && xv != 0.0);
             if (nzm) {
@@ -1604,17 +1614,14 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
         const double nv = sqrt(wave_pw_sum(xv * xv, col));
         ld_j = col ? xv / nv : 0.0;
         wsync();
-        if (col) S.ld[l] = ld_j;
-        wsync();
         if (clus) {
             // the loading only: scores stay zeros (:357)
         } else if (alg == 0) {
-            // scores s = wcd . loading (:337), row phase
-            if (row) {
-                double acc = 0.0;
-                for (int j = 0; j < E; j++) acc = fma(S.F[l * ES + j] - S.mu[j], S.ld[j], acc);
-                sc_i = acc;
-            }
+            // scores s = wcd . loading (:337), row phase (column j's mean and loading from lane j)
+            const int r = row ? l : 0;
+            double acc = 0.0;
+            for (int j = 0; j < E; j++) acc = fma(S.F[r * ES + j] - lane_value(muj, j), lane_value(ld_j, j), acc);
+            if (row) sc_i = acc;
         } else if (flags & 2) {
             sc_i = __builtin_nan("");  // the reference's second svd raises (:375, :431)
         } else if constexpr (!PK) {  // (the packed layout is never launched for these)
@@ -1778,7 +1785,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             const bool reuse = (rk_valid >> j) & 1;
             int rk = 0;
             if (reuse) {
-                const uint64_t mj = S.nanm[j] | S.zerm[j];
+                const uint64_t mj = S.miss[j];
                 const bool ms = (mj >> l) & 1;
                 const uint32_t key = key_hi32(x0);
                 const uint32_t kg = (uint32_t)__builtin_amdgcn_readlane((int)key, __builtin_ctzll(mj));
@@ -1828,7 +1835,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             if (l == 0) hitm[j] = hm;
         }
         wsync();
-        const int NS = N | 1;  // odd stride: lane-per-column reads spread over the banks
+        const int NS = cert_stride(N, ES);  // odd stride: lane-per-column reads spread over the banks
         double* comp = S.F;    // [E][NS]
         for (int j = 0; j < E; j++) {
             const uint64_t hm = hitm[j];
@@ -1874,7 +1881,7 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
     // (s, c) bit for bit as they were (neither is ever -0.0), so only the missing rows are visited
     const bool smooth_finite = !ballot(row && !__builtin_isfinite(smooth_i));
     if (col) {
-        const uint64_t nam = S.nanm[l] | S.zerm[l];
+        const uint64_t nam = S.miss[l];
         // dot2(smooth, na) with na in {0,1}
         double s = 0.0, c = 0.0;
         auto step = [&](double x, double y) {
@@ -1892,17 +1899,13 @@ __global__ void __launch_bounds__(64, 3) batched_round_kernel(BatchArgs a) {
             for (int i = 0; i < N; i++) step(S.smooth[i], ((nam >> i) & 1) ? 1.0 : 0.0);
         }
         pcj = 1.0 - (s + c);
-        nzj = (double)popc(S.zerm[l]);
+        nzj = (double)((nacnt >> 16) & 0xffu);
     }
     double narow = 0.0;
     int nnan = 0;
     if (row) {
-        int nz = 0;
-        for (int j = 0; j < E; j++) {
-            nz += (S.zerm[j] >> l) & 1;
-            nnan += (S.nanm[j] >> l) & 1;
-        }
-        narow = (double)nz;
+        narow = (double)(nacnt & 0xffu);
+        nnan = (int)((nacnt >> 8) & 0xffu);
     }
     const bool rowmasked = row && nnan == E;
     const double pr = 1.0 - narow / (double)E;
@@ -1969,8 +1972,9 @@ static bool shape_50x20(int N, int E, int ES) { return N == 50 && E == 20 && ES 
 static bool packed_alg(int alg) { return alg == 0 || alg == 1 || alg == 4; }
 
 size_t batched_lds_bytes(int N, int E, int alg) {
-    const int ES = E | 1;
-    const int NR = shape_50x20(N, E, ES) && alg < 5 ? 50 : 64;
+    const bool c50 = shape_50x20(N, E, E | 1) && alg < 5;  // the <50, 20> instantiation
+    const int ES = c50 ? compiled_es(E) : E | 1;
+    const int NR = c50 ? 50 : 64;
     return smem_doubles(N, E, ES, NR, packed_alg(alg)) * sizeof(double);
 }
 
