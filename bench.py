@@ -655,7 +655,7 @@ def main():
                          "traffic": traffic, "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bpl,
                          "limiter": ("latency / instruction issue, not HBM: one wave64 per LDS-resident "
-                                     "round, 12 rounds per CU (DESIGN.md 5.2)"),
+                                     "round, 14 rounds per CU (DESIGN.md 5.2)"),
                          "valu": {"insts_per_launch": valu, "issue_ms": valu_ms,
                                   "frac": (valu_ms / kern_ms) if valu_ms else None,
                                   "note": "VALU issue time of the launch's instructions (SQ_INSTS_VALU, "
