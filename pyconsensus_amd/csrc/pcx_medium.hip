@@ -615,7 +615,10 @@ __host__ __device__ __forceinline__ int medium_work(int N, int E, int alg) {
         }                                                                         \
     } while (0)
 
-__global__ void __launch_bounds__(MT, 3) medium_round_kernel(BatchArgs a, int64_t b0, double* Fscr, double* Cscr) {
+#ifndef PCX_MEDIUM_WAVES  // waves per SIMD the VGPR budget is sized for (a build parameter for A/B runs)
+#define PCX_MEDIUM_WAVES 3
+#endif
+__global__ void __launch_bounds__(MT, PCX_MEDIUM_WAVES) medium_round_kernel(BatchArgs a, int64_t b0, double* Fscr, double* Cscr) {
     extern __shared__ __attribute__((aligned(16))) double mlds[];
     __shared__ double sh[MT];
     __shared__ double scal[16];

@@ -17,6 +17,7 @@
 #   dist         the 2-process tests and bench.py as the driver launches N=2 (gloo: both ranks on cuda:0)
 #   selfdist     bench.py --gpus 2 with no launcher (bench.py starts the ranks itself; gloo on cuda:0)
 #   ab_c3=L1,L2  C3 bench of several libpcx builds (PCX_LIB), alternating twice
+#   ab_med=L1,L2 the medium-round (100 x 50) line of several libpcx builds, alternating twice
 #   ab_c5=L1,L2  C5 latency of several libpcx builds, alternating twice
 #   ab_shard=L1,L2  one C5 shard's latency of several libpcx builds, alternating twice
 #   kt_c5=L1,L2  rocprofv3 kernel trace of one C5 consensus per libpcx build, per-kernel times (tools/kt_top.py)
@@ -103,6 +104,12 @@ for STEP in "$@"; do
       for i in 1 2; do for L in "${LIBS[@]}"; do
         PCX_LIB=$L timeout -k 10 120 python bench.py --no-cpu-baseline --c5-steps 0 --no-c4 --steps 30 > $O/ab.json 2> $O/ab.err || { echo "ab rc=$? ($L)"; tail -3 $O/ab.err; exit 22; }
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('%-36s %.3f ms  %.2fM rounds/s' % (sys.argv[2], d['roofline']['kernel_ms'], d['value']/1e6))" $O/ab.json "$L"
+      done; done ;;
+    ab_med=*)  # the medium-round (100 x 50) line of several libpcx builds, alternating twice
+      IFS=, read -ra LIBS <<< "${STEP#ab_med=}"
+      for i in 1 2; do for L in "${LIBS[@]}"; do
+        PCX_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --c5-steps 0 --steps 5 > $O/abm.json 2> $O/abm.err || { echo "ab_med rc=$? ($L)"; tail -3 $O/abm.err; exit 33; }
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); m=d['medium']; print('%-28s medium %.3f ms  %.3fM rounds/s' % (sys.argv[2], m['ms'], m['rounds_per_s']/1e6))" $O/abm.json "$L"
       done; done ;;
     ab_c5=*)
       IFS=, read -ra LIBS <<< "${STEP#ab_c5=}"
