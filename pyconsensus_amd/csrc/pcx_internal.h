@@ -83,6 +83,10 @@ typedef struct {
     uint64_t* cbuf;               /* [n_scaled][ccap][2] compacted (key, weight bits) of the range (k_sel_hist) */
     int64_t*  ccount;             /* [n_scaled] compacted elements of this rank                    */
     int64_t   ccap;               /* compaction capacity per event (0: none)                       */
+    uint64_t* vsave;              /* [n_scaled][256][3] this rank's first-pass bucket counts, min and max
+                                     keys of phase 1, then [n_scaled][4] (lo, hi, shift, 1) of their
+                                     range: phase 2's first pass over the same range takes them
+                                     instead of recounting (zeroed per call; k_sel_hist) */
     /* outputs ([E] events, [n_rows] agents of this rank) */
     double *old_rep, *this_rep, *smooth_rep, *scores, *na_row, *participation_rows, *relative_part,
         *reporter_bonus;

@@ -47,6 +47,17 @@ namespace {
 constexpr int CS = 16;           // dd slots per column in cstat
 constexpr int SS = 16;           // dd slots in scal
 constexpr int NB = SEL_NB;       // selection buckets
+// rows per load batch of the weight-mode column passes, and the minimum waves per SIMD their
+// registers are held to (build parameters for A/B runs).  Measured at C5 (round 6, the phase-2
+// first pass): 8 rows, 107 VGPRs, 3.85-3.98 ms; 12 rows (139 VGPRs, 3 waves) 7.44 ms; 16 rows
+// (171 VGPRs, 2 waves) 7.77 ms, or held to 4 waves (58 VGPRs spilled) 7.65 ms.
+#ifndef PCX_SEL_WUNROLL
+#define PCX_SEL_WUNROLL 8
+#endif
+constexpr int SEL_WUNROLL = PCX_SEL_WUNROLL;
+#ifndef PCX_SEL_WWAVES
+#define PCX_SEL_WWAVES 1
+#endif
 constexpr int SEL_HC = 2;  // copies of each k_sel_hist bucket (4: 12.3 vs 9.0 ms at C5; 1: 9.37 vs 8.66 ms, round 5)
 constexpr int SELS = 40;         // sel_state words per scaled event
 constexpr int BT = 256;          // threads per block for row/column passes
@@ -3988,7 +3999,7 @@ __global__ void __launch_bounds__(BT) k_sel_sample(pcx_mat m) {
 // held to 64 VGPRs (eight waves per SIMD: 2.30 -> 2.03 ms at C5 against 8-row batches; 65 VGPRs
 // unforced cost a wave per SIMD)
 template <int NT, bool CM>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 : 1))) k_sel_hist(pcx_mat m) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 : PCX_SEL_WWAVES))) k_sel_hist(pcx_mat m) {
     const int a = blockIdx.x;
     if (a >= (int)m.info[IN_SEL_ACTIVE]) return;  // the first pass is launched for every scaled event
     const int s = m.sel_act[a];
@@ -4085,6 +4096,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 
     const int hcp = HC > 1 ? (int)(threadIdx.x % HC) : 0;
     const int64_t wl = CM ? 0 : m.info[IN_SEL_WLIMB];  // (k_sel_wlimbs: a limb no row uses is not summed)
     const bool use0 = !(wl & 8) || (wl & 1), use2 = !(wl & 8) || (wl & 4);
+    // Phase 2's first pass bins the present values of phase 1's first pass (the same rows, the
+    // same keys) plus the filled rows, which it bins apart: over the same range and shift the
+    // buckets' counts and key extremes of the present values are the ones phase 1 counted.  Phase
+    // 1's first pass keeps them (this rank's, before the reduction: vsave), and phase 2's takes
+    // them instead of three LDS atomics per element -- the weight limbs are new, the rest is not.
+    // (A filled row's fill value may lie outside phase 1's range, int_dtype truncating it: a
+    // changed range recounts.)
+    uint64_t* const vkey = m.vsave ? m.vsave + (int64_t)m.n_scaled * NB * 3 + (int64_t)s * 4 : nullptr;
+    const bool vput = first && m.sel_phase == 1 && vkey;
+    const bool vreuse = !CM && first && m.sel_phase == 2 && vkey && vkey[3] == 1 && vkey[0] == lo &&
+                        vkey[1] == hi && vkey[2] == (uint64_t)sh;
     auto bin = [&](uint64_t k, double w) {
         const int b = (int)((k - lo) >> sh) * HC + hcp;
         if constexpr (!CM) {
@@ -4095,6 +4117,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 
                 if (use2) atomicAdd(&hc[b], (unsigned long long)L.l2);
             }
         }
+        if (!CM && vreuse) return;
         atomicAdd(&hn[b], (hn_t)1);
         // (measured: reading the extremes first and skipping the atomics that cannot change them
         // is slower, 9.4 -> 12.0 ms at C5 -- the read's latency sits in every element's path,
@@ -4114,7 +4137,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 
     } else {
         const double* const tcol = m.T + (int64_t)s * m.n_rows;
         const double wc = 1.0 / (double)m.n_total;  // (CM: sel_load's weight)
-        rows_strided<(CM ? 16 : ROW_UNROLL)>(threadIdx.x, NT, m.n_rows, [&](int64_t i) {
+        rows_strided<(CM ? 16 : SEL_WUNROLL)>(threadIdx.x, NT, m.n_rows, [&](int64_t i) {
                                      if constexpr (CM) return XW{tcol[i], wc};
                                      else return sel_load(m, s, i);
                                  },
@@ -4221,6 +4244,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 
         m.ccount[s] = fits ? (int64_t)gcount : 0;
         st[SW_CMODE] = fits ? 2 : 0;
     }
+    if (vput && threadIdx.x == 0) {
+        vkey[0] = lo;
+        vkey[1] = hi;
+        vkey[2] = (uint64_t)sh;
+        vkey[3] = 1;
+    }
     const int64_t o = (int64_t)a * NB;
     for (int b = threadIdx.x; b < NB; b += NT) {
         unsigned long long sa = 0, sb = 0, sc = 0, mn = ~0ull, mx = 0;
@@ -4235,6 +4264,16 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(CM ? 8 
             sn += (uint64_t)hn[b * HC + c];
             mn = hmin[b * HC + c] < mn ? hmin[b * HC + c] : mn;
             mx = hmax[b * HC + c] > mx ? hmax[b * HC + c] : mx;
+        }
+        uint64_t* const vs = m.vsave ? m.vsave + ((int64_t)s * NB + b) * 3 : nullptr;
+        if (vput) {  // this rank's present values of the range (before the reduction over ranks)
+            vs[0] = sn;
+            vs[1] = mn;
+            vs[2] = mx;
+        } else if (vreuse) {
+            sn += vs[0];
+            mn = vs[1] < mn ? vs[1] : mn;
+            mx = vs[2] > mx ? vs[2] : mx;
         }
         if (wmode) {
             m.hist_w[(o + b) * 3 + 0] = sa;

@@ -75,6 +75,7 @@ struct pcx_workspace {
     int64_t* zsum;
     double* dscale;
     uint64_t* cbuf;
+    uint64_t* vsave;
     int64_t* ccount;
     int64_t ccap = 0;
     // sized by the data (the grid / general split), grown on demand
@@ -270,6 +271,7 @@ pcx_workspace* workspace(pcx_ctx* c, int64_t n_rows, int64_t E, int64_t n_total,
         {(void**)&w->hard, (size_t)E * 4, true},
         {(void**)&w->ccount, (size_t)S * 8, true},
         {(void**)&w->cbuf, (size_t)(S * w->ccap * 2) * 8, false},
+        {(void**)&w->vsave, (size_t)(S * (SEL_NB * 3 + 4)) * 8, true},
         {(void**)&w->hard_cols, (size_t)E * 4, true},
         {(void**)&w->hard_modes, (size_t)E * 4, true},
         {(void**)&w->scols, (size_t)S * 4, false},
@@ -1197,6 +1199,7 @@ int run_matrix(pcx_ctx* c, const pcx_problem* p, pcx_result* r, int entry, const
         m.hard_cols = w->hard_cols;
         m.hard_modes = w->hard_modes;
         m.cbuf = w->ccap > 0 ? w->cbuf : nullptr;
+        m.vsave = w->vsave;
         m.ccount = w->ccount;
         m.ccap = w->ccap;
         m.scalars = w->scalars;
