@@ -1267,7 +1267,8 @@ __device__ __noinline__ double feck_nc(const BatchArgs& a, const double* F, int 
 // The compiled shapes' row pitch: E (1) or E | 1 (0).  The odd pitch spreads a row-phase column
 // read over the banks, but 50 x 20 rounds at the even one fit nine LDS units instead of ten -- 14
 // rounds a CU instead of 12 with the 128-VGPR budget below (C3: 1.53 -> 1.46 ms, 42.5 -> 44.6 M
-// rounds/s; the odd pitch at 128 VGPRs, still 12 a CU, ran 1.55 ms).  (Build parameters for A/B runs.)
+// rounds/s; the even pitch under the three-wave budget, 12 a CU, ran 1.534-1.546 ms against the odd
+// pitch's 1.530-1.540: its bank conflicts cost little).  (Build parameters for A/B runs.)
 #ifndef PCX_BATCHED_ES_EVEN
 #define PCX_BATCHED_ES_EVEN 1
 #endif
