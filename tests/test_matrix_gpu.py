@@ -106,6 +106,14 @@ def _big_case(name):
         R, sc, lo, hi, rep = synthetic.matrix(N, E, seed=N + E)
         if len(name) == 3 and name[2] is None:
             rep = None
+        elif len(name) == 3 and name[2] == "nomiss":
+            # a few scaled events with no missing report: phase 1 selects nothing for them, so phase
+            # 2's first pass over them counts every element itself while the others take phase 1's
+            # bucket counts (k_sel_hist, vsave) -- both kinds in one launch
+            idx = np.flatnonzero(sc)[:3]
+            for j in idx:
+                col = R[:, j]
+                col[np.isnan(col) | (col == 0.0)] = 0.5 * (lo[j] + hi[j])
         elif len(name) == 3:
             rep = _signed_reputation(rep, name[2], seed=N)
     b = synthetic.bounds_list(sc, lo, hi)
@@ -197,9 +205,11 @@ def _abi_events():
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), (20000, 80, "neg"), "C4", "C5r", "C5r_1M", "C5w"],
+@pytest.mark.parametrize("case", [(3000, 150), (20000, 400), (20008, 400), (16648, 2048, None), (20000, 80, "neg"),
+                                  (12000, 60, "nomiss"), "C4", "C5r", "C5r_1M", "C5w"],
                          ids=["3000x150", "20000x400", "20008x400_ragged16",
                               "16648x2048_repNone_ragged16_empty_chunks", "20000x80_negative_rep",
+                              "12000x60_scaled_without_missing",
                               "C4_100k_x_1k_intrep",
                               "C5recipe_250k_x_1024_repNone",
                               "C5r_1M_x_1024_repNone", "C5width_250k_x_4096_repNone"])
